@@ -1,0 +1,234 @@
+"""Contrastive pre-training throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+
+A step is the reference's hot-loop iteration (molclr.py:108-128): two
+encoder forwards of augmented views, F.normalize, NT-Xent, backward, Adam —
+including the per-batch graph build (the reference's add_self_loops work).
+Inputs: NB distinct pre-built synthetic batches per rank, resident in HBM
+before the timed region (SURVEY.md §8d generator; rank r uses seed r*10^6),
+rotated every step so repeated steps do not re-read one batch.
+
+Workloads: c2 = GIN 5x300, feat 512, batch 512 per GPU, fp32 (default; the
+config the metric is quoted on); c3 = GCN 5x300.  N > 1 runs under torchrun,
+one rank per GPU over RCCL: the NT-Xent batch is global (512 N), weak scaling.
+
+The JSON line adds:
+  roofline      — the GIN scatter-add (molclr_gine_aggregate_fwd), HBM-bound:
+                  algorithmic bytes per launch / HIP-event launch time in the
+                  timed region, against 8.0 TB/s.
+  roofline_mfma — all fp32 MFMA GEMM launches in the timed region, against
+                  157.3 TF/s (fp32 dense MFMA peak).
+  cpu_baseline  — the oracle (CPU restatement of the reference step, incl.
+                  the broadcast-cosine NT-Xent) on this host, rank 0, N=1 only,
+                  a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+METRIC = "contrastive pre-train molecules/sec at batch 512, 1/2/4/8 MI355X; HBM GB/s on scatter_add"
+HBM_PEAK_GBS = 8000.0
+FP32_MFMA_PEAK_TFS = 157.3
+
+CONFIGS = {
+    "c2": dict(model_type="gin", num_layer=5, emb_dim=300, feat_dim=512, batch=512,
+               shape="uniform", desc="c2: GIN 5x300 feat 512, batch 512/GPU, 10-50 atom graphs"),
+    "c3": dict(model_type="gcn", num_layer=5, emb_dim=300, feat_dim=512, batch=512,
+               shape="uniform", desc="c3: GCN 5x300 feat 512, batch 512/GPU, 10-50 atom graphs"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--batches", type=int, default=16, help="distinct resident batches per rank")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--no-kernel-timing", action="store_true")
+    return p.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg, batches_cpu, steps):
+    """Oracle step (reference restatement) timed on this host's cores."""
+    import torch
+
+    from oracle.reference_cpu import RefGCN, RefGINet, RefNTXentLoss, ref_train_step
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    M = RefGINet if cfg["model_type"] == "gin" else RefGCN
+    model = M(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"])
+    crit = RefNTXentLoss("cpu", cfg["batch"], 0.1, True)
+    opt = torch.optim.Adam(model.parameters(), 5e-4, weight_decay=1e-5)
+    times = []
+    for i in range(steps + 1):  # first step is warm-up
+        xi, xj = batches_cpu[i % len(batches_cpu)]
+        t0 = time.perf_counter()
+        ref_train_step(model, crit, opt, xi, xj)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": round(cfg["batch"] / med, 2), "unit": "molecules/s", "cores": threads,
+            "kind": "port", "ms_per_step": round(med * 1e3, 1),
+            "sample": f"{steps} steps (+1 warm-up) of {cfg['desc']}, oracle/reference_cpu.py, "
+                      f"torch CPU fp32, {threads} threads, median step"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    from molclr_amd import distributed as mdist
+    from molclr_amd import ops
+    from molclr_amd.dataset import SyntheticPairBatches
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.optim import FusedAdam
+
+    rank, world, dev = mdist.init()
+    if world != args.gpus:
+        log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    cfg = CONFIGS[args.config]
+    B = cfg["batch"]
+
+    # ---- inputs: NB distinct batches, resident on the device -----------------
+    t0 = time.perf_counter()
+    gen = SyntheticPairBatches(B, seed=rank * 10**6, shape=cfg["shape"])
+    batches_cpu = gen.take(args.batches)
+    batches = [(a.to(dev), b.to(dev)) for a, b in batches_cpu]
+    n_nodes = sum(a.x.shape[0] + b.x.shape[0] for a, b in batches_cpu) / (2 * len(batches_cpu))
+    n_edges = sum(a.edge_index.shape[1] + b.edge_index.shape[1]
+                  for a, b in batches_cpu) / (2 * len(batches_cpu))
+    log(rank, f"built {args.batches} batches in {time.perf_counter() - t0:.1f}s "
+              f"(mean N={n_nodes:.0f}, E={n_edges:.0f} per view)")
+
+    # ---- model / optimiser / loss ---------------------------------------------
+    torch.manual_seed(0)
+    if cfg["model_type"] == "gin":
+        from molclr_amd.ginet_molclr import GINet as M
+    else:
+        from molclr_amd.gcn_molclr import GCN as M
+    model = M(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"]).to(dev)
+    opt = FusedAdam(model.parameters(), 5e-4, weight_decay=1e-5)
+    mdist.broadcast_params(opt.flat)
+    group = torch.distributed.group.WORLD if world > 1 else None
+    crit = NTXentLoss(dev, B * world, 0.1, True, group=group)
+
+    def step(i):
+        xi, xj = batches[i % len(batches)]
+        for g in (xi, xj):  # rebuild the graph every step: it is part of the work
+            g.__dict__.pop("_molclr_graph", None)
+        opt.zero_grad()
+        _, zi = model(xi)
+        _, zj = model(xj)
+        loss = crit(ops.l2_normalize(zi), ops.l2_normalize(zj))
+        loss.backward()
+        if world > 1:
+            mdist.allreduce_grads(opt.flat_grad)
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    log(rank, f"warm-up done, loss {loss.item():.4f}")
+
+    timer = None if args.no_kernel_timing else ops.KernelTimer()
+    ops.set_kernel_timer(timer)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    elapsed = mdist.max_over_ranks(elapsed, dev)
+    final_loss = float(loss.item())
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+
+    roofline = roofline_mfma = None
+    if timer is not None:
+        s = timer.summary()
+        agg = s.get("gine_aggregate_fwd")
+        if agg:
+            per_launch_s = agg["ms"] / agg["launches"] / 1e3
+            per_launch_bytes = agg["work"] / agg["launches"]
+            achieved = per_launch_bytes / per_launch_s / 1e9
+            roofline = {"kernel": "molclr_gine_aggregate_fwd (k_gine_agg_fwd)", "bound": "hbm",
+                        "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": load_pmc_traffic(),
+                        "bytes_per_launch": int(per_launch_bytes),
+                        "us_per_launch": round(per_launch_s * 1e6, 2),
+                        "launches": agg["launches"]}
+        gm = s.get("gemm_f32")
+        if gm:
+            tfs = gm["work"] / (gm["ms"] / 1e3) / 1e12
+            roofline_mfma = {"kernel": "molclr_gemm_f32 (all launches)", "bound": "mfma",
+                             "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
+                             "unit": "TFLOP/s", "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
+                             "traffic": None, "launches": gm["launches"],
+                             "ms_per_step": round(gm["ms"] / args.steps, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(rank, "timing the CPU baseline (oracle) ...")
+        cpu = cpu_baseline(cfg, batches_cpu, args.cpu_steps)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "molecules/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic: {args.batches} resident pre-built batch pairs per rank "
+                    f"(SURVEY §8d generator, node-mask views), random-init weights",
+            "config": {"workload": cfg["desc"], "model": f"{cfg['model_type']} "
+                       f"{cfg['num_layer']}x{cfg['emb_dim']} feat {cfg['feat_dim']}",
+                       "global_batch": B * world, "per_gpu_batch": B,
+                       "mean_nodes_per_view": round(n_nodes), "mean_edges_per_view": round(n_edges),
+                       "parallelism": f"dp{world}"},
+            "final_loss": round(final_loss, 5),
+            "roofline": roofline, "roofline_mfma": roofline_mfma, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def load_pmc_traffic():
+    """HBM bytes per aggregation launch from the committed PMC summary
+    (profiles/*pmc_gine_agg*.json, written by tools/pmc_traffic.py), or None."""
+    cands = sorted((ROOT / "profiles").glob("*pmc_gine_agg*.json"))
+    if not cands:
+        return None
+    try:
+        return json.loads(cands[-1].read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

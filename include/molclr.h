@@ -1,0 +1,251 @@
+/*
+ * molclr.h — C ABI of the MI355X-native MolCLR pre-training hot path.
+ *
+ * This is the drop-in boundary: every entry point is `extern "C"`, takes plain
+ * device pointers, element counts and an opaque HIP stream (`void*`, a
+ * `hipStream_t`), and returns 0 on success or a non-zero status
+ * (MOLCLR_ERR_* below, or a positive hipError_t).  `molclr_last_error()` gives
+ * a thread-local message for the last failure.  No entry point allocates,
+ * synchronises the device, or keeps state between calls: the caller owns
+ * every buffer (including the `workspace` scratch, sized by the matching
+ * `*_workspace_bytes` query) and all work is stream-ordered, so a caller may
+ * capture any sequence of these calls into a HIP graph.
+ *
+ * Reference interfaces replaced (CameronDiao/MolCLR @ /root/reference):
+ *   - PyG 1.6.3 `add_self_loops` + self-loop edge attr, done per layer in
+ *       models/ginet_molclr.py:31-37 and models/gcn_molclr.py:64-70
+ *       -> molclr_graph_build (once per batch, self loops implicit)
+ *   - atom embedding   models/ginet_molclr.py:103, models/gcn_molclr.py:144
+ *       -> molclr_atom_embed_fwd / _bwd
+ *   - GINEConv edge embedding + message + PyG aggr='add'
+ *       models/ginet_molclr.py:39-44        -> molclr_gine_aggregate_fwd / _bwd
+ *   - GCNConv message + aggr='add' + bias
+ *       models/gcn_molclr.py:72-88          -> molclr_gcn_aggregate_fwd / _bwd
+ *   - nn.Linear (GIN MLP ginet_molclr.py:19-23, heads :90-96), GCN `x @ W`
+ *       (gcn_molclr.py:76) and their autograd -> molclr_gemm_f32, molclr_colsum_f32
+ *   - BatchNorm1d(train/eval) + ReLU + dropout(p=0)
+ *       models/ginet_molclr.py:107-111     -> molclr_batchnorm_fwd / _bwd
+ *   - global_mean_pool / global_add_pool  ginet_molclr.py:113
+ *                                           -> molclr_segment_pool_fwd / _bwd
+ *   - F.normalize(dim=1)                  molclr.py:63-64 -> molclr_l2norm_fwd / _bwd
+ *   - NTXentLoss.forward (cosine / dot)   utils/nt_xent.py:33-65
+ *                                           -> molclr_ntxent_fwd / _bwd
+ *   - torch.optim.Adam(weight_decay=L2)   molclr.py:84-87,127 -> molclr_adam_step
+ */
+#ifndef MOLCLR_H_
+#define MOLCLR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* molclr_stream_t; /* a hipStream_t; NULL = legacy default stream */
+
+enum {
+  MOLCLR_OK = 0,
+  MOLCLR_ERR_ARG = -1,       /* bad shape / pointer / size argument */
+  MOLCLR_ERR_WORKSPACE = -2, /* workspace too small */
+  MOLCLR_ERR_UNSUPPORTED = -3
+};
+
+/* Vocabulary of the reference (models/ginet_molclr.py:9-13). */
+#define MOLCLR_NUM_ATOM_TYPE 119     /* 118 elements + mask token 118 */
+#define MOLCLR_NUM_CHIRALITY 3
+#define MOLCLR_NUM_BOND_TYPE 5       /* 4 bond types + self-loop type 4 */
+#define MOLCLR_NUM_BOND_DIR 3
+#define MOLCLR_SELF_LOOP_BOND_TYPE 4 /* ginet_molclr.py:35 */
+#define MOLCLR_ECOUNT_STRIDE 8       /* per-node counts: 5 bond types, 3 dirs */
+
+const char* molclr_version(void);
+const char* molclr_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Graph build (once per batch and view).
+ * Inputs are the PyG Batch fields exactly as the reference collates them
+ * (dataset/dataset.py:86-147 + PyG collate): edge_index int64 [2,E]
+ * (row 0 = source j, row 1 = destination i, flow source_to_target),
+ * edge_attr int64 [E,2] (bond type 0..4, bond dir 0..2), batch int64 [N]
+ * (ascending, graphs contiguous).
+ * Outputs (device, caller-allocated):
+ *   rowptr [N+1] i32, col [E] i32, ecode [E] u8 : in-edges of every node
+ *       sorted stably by destination (edge order kept inside a row) — the
+ *       order in which PyG's scatter-add accumulates them; the self loop PyG
+ *       appends at the end of the edge list is implicit (applied last).
+ *       ecode = bond_type | bond_dir << 3.
+ *   rowptr_t [N+1] i32, col_t [E] i32 : out-edges sorted stably by source
+ *       (the accumulation order of index_select's backward).
+ *   ecount [N*8] i32 : per destination, counts of in-edge bond types 0..4
+ *       and bond dirs 0..2, self loop included.
+ *   graph_ptr [G+1] i32 : node range of every graph.
+ *   status [1] i32 : bit 0 edge index out of range, bit 1 edge attr out of
+ *       range, bit 2 batch not ascending / out of range.  Offending entries
+ *       are clamped so no later kernel reads out of bounds.
+ * ------------------------------------------------------------------------ */
+size_t molclr_graph_build_workspace_bytes(int64_t num_nodes, int64_t num_edges);
+int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
+                       const int64_t* batch, int64_t num_nodes, int64_t num_edges,
+                       int64_t num_graphs, int32_t* rowptr, int32_t* col,
+                       uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t,
+                       int32_t* ecount, int32_t* graph_ptr, int32_t* status,
+                       void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
+/* Atom embedding: h[i] = X1[x[i,0]] + X2[x[i,1]]  (ginet_molclr.py:103).
+ * x int64 [N,2]; X1 [n1,D], X2 [n2,D]; h [N,D] f32.  Indices are clamped. */
+int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
+                          float* h, int64_t num_nodes, int64_t dim, int64_t n1,
+                          int64_t n2, molclr_stream_t stream);
+/* dX1 [n1,D], dX2 [n2,D] = Σ over nodes of each type of dh (deterministic). */
+size_t molclr_atom_embed_bwd_workspace_bytes(int64_t num_nodes, int64_t dim, int64_t n1,
+                                             int64_t n2);
+int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
+                          int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,
+                          void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
+/* GINE aggregation (ginet_molclr.py:39-44 + PyG aggr='add'):
+ *   out[i] = Σ_{k in in(i), edge order} (x[src_k] + (E1[bt_k] + E2[bd_k]))
+ *            + (x[i] + (E1[4] + E2[0]))                    (self loop last)
+ * Same operation order as the reference CPU path, so results are
+ * bit-identical to it.  x, out [N,D] f32; E1 [5,D]; E2 [3,D]. */
+int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32_t* col,
+                              const uint8_t* ecode, const float* E1, const float* E2,
+                              float* out, int64_t num_nodes, int64_t dim,
+                              molclr_stream_t stream);
+/* Backward: dx[j] = Σ_{k in out(j), edge order} g[dst_k] + g[j];
+ * dE1[t] = Σ_i ecount[i][t] g[i], dE2[d] = Σ_i ecount[i][5+d] g[i].
+ * dx may be NULL (first layer input needs no grad); dE1/dE2 may be NULL. */
+size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
+int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
+                              const int32_t* ecount, float* dx, float* dE1, float* dE2,
+                              int64_t num_nodes, int64_t dim, void* workspace,
+                              size_t workspace_bytes, molclr_stream_t stream);
+
+/* GCN aggregation (gcn_molclr.py:72-88; gcn_norm at :74 is computed and
+ * discarded by the reference, so it is not computed here):
+ *   out[i] = Σ_{k in in(i)} (e_k + xw[src_k]) + (e_self + xw[i]) + bias
+ * with scalar e = E1[bt][0] + E2[bd][0] (tables [5,1], [3,1]). */
+int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr, const int32_t* col,
+                             const uint8_t* ecode, const float* E1, const float* E2,
+                             const float* bias, float* out, int64_t num_nodes,
+                             int64_t dim, molclr_stream_t stream);
+/* Backward: dxw[j] = Σ_{out(j)} g[dst] + g[j]; dE1[t] = Σ_i ecount[i][t]·Σ_d g[i][d];
+ * dE2 likewise; dbias = Σ_i g[i].  Any output pointer may be NULL. */
+size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
+int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
+                             const int32_t* ecount, float* dxw, float* dE1, float* dE2,
+                             float* dbias, int64_t num_nodes, int64_t dim, void* workspace,
+                             size_t workspace_bytes, molclr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * FP32 GEMM on the gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 FMA
+ * chains, no TF32-style truncation).
+ *   C[m,n] = Σ_k A(m,k) B(k,n)  (+ epilogue)
+ *   A(m,k) = a_kmajor ? A[k*lda + m] : A[m*lda + k]
+ *   B(k,n) = b_kmajor ? B[k*ldb + n] : B[n*ldb + k]
+ * so nn.Linear forward (x W^T) is a_kmajor=0, b_kmajor=0; dX = dY W is
+ * a_kmajor=0, b_kmajor=1; dW = dY^T X is a_kmajor=1, b_kmajor=1.
+ * Epilogues: MOLCLR_EPI_NONE, _BIAS (C += bias[n]), _BIAS_RELU,
+ * _RELU_MASK (C *= (aux[m*ldaux+n] > 0), the ReLU backward).
+ * Requires K, lda, ldb, ldc and the contiguous dims to be multiples of 4.
+ * Split-K (for the weight-gradient shape, K = number of nodes) runs when the
+ * workspace is large enough: molclr_gemm_f32_workspace_bytes(M,N,K). */
+enum { MOLCLR_EPI_NONE = 0, MOLCLR_EPI_BIAS = 1, MOLCLR_EPI_BIAS_RELU = 2,
+       MOLCLR_EPI_RELU_MASK = 3 };
+size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K);
+int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
+                    int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                    int b_kmajor, int epilogue, const float* bias, const float* aux,
+                    int64_t ldaux, void* workspace, size_t workspace_bytes,
+                    molclr_stream_t stream);
+
+/* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
+size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
+int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
+                      void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * BatchNorm1d over the rows of z [N,D] (+ ReLU), ginet_molclr.py:107-111.
+ * training != 0: batch statistics (biased variance for normalising),
+ *   running_mean/var updated in place with `momentum` and the unbiased
+ *   variance, exactly as torch.nn.BatchNorm1d; save_mean / save_invstd [D]
+ *   receive the statistics for the backward.
+ * training == 0: running statistics are used and nothing is updated.
+ * relu != 0 applies max(y, 0) to the output. */
+size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t dim);
+int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
+                         float* running_mean, float* running_var, float* y,
+                         float* save_mean, float* save_invstd, int64_t rows, int64_t dim,
+                         double momentum, double eps, int training, int relu,
+                         void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+/* dy is the gradient w.r.t. the (ReLU'd) output; dz/dgamma/dbeta out. */
+int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
+                         const float* beta, const float* save_mean,
+                         const float* save_invstd, float* dz, float* dgamma, float* dbeta,
+                         int64_t rows, int64_t dim, int relu, void* workspace,
+                         size_t workspace_bytes, molclr_stream_t stream);
+
+/* Segment pooling over graph_ptr (PyG global_mean_pool / global_add_pool):
+ * mode 0 = mean (sum / max(count,1)), 1 = add. */
+int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr, float* out,
+                            int64_t num_graphs, int64_t dim, int mode,
+                            molclr_stream_t stream);
+int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_ptr, float* dh,
+                            int64_t num_nodes, int64_t num_graphs, int64_t dim, int mode,
+                            molclr_stream_t stream);
+
+/* F.normalize(z, dim=1, eps): y = z / max(||z||, eps); norm [rows] saved. */
+int molclr_l2norm_fwd(const float* z, float* y, float* norm, int64_t rows, int64_t dim,
+                      double eps, molclr_stream_t stream);
+int molclr_l2norm_bwd(const float* dy, const float* y, const float* norm, float* dz,
+                      int64_t rows, int64_t dim, double eps, molclr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * NT-Xent (utils/nt_xent.py:47-65), row-sharded so it also serves the
+ * data-parallel global batch.
+ *   R = [zj ; zi] in the global order (nt_xent.py:48), 2B rows of width C.
+ *   cosine != 0: rows are first scaled by 1/max(||r||, 1e-8)
+ *       (torch CosineSimilarity, nt_xent.py:40-45); cosine == 0: dot.
+ *   loss = (1/2B) Σ_r [ log Σ_{c≠r} exp(S_rc/T) − S_{r,(r+B) mod 2B}/T ].
+ * This process owns `nrows` rows of R: `rows` [nrows,C] with global indices
+ * row_gidx [nrows]; `cols` [2B,C] is the full (gathered) R.
+ * ntxent_prep: rhat = scaled rows of a [n,C] matrix, norm [n] (clamped denominators).
+ * ntxent_fwd:  lse_rows [nrows] (needed by every rank's backward) and
+ *              loss_rows [nrows] = per-row loss / 2B.
+ * ntxent_bwd:  drhat_rows [nrows,C] = dL/d(rhat rows) given the full
+ *              lse_cols [2B] and the upstream scalar gradient *grad_loss.
+ * ntxent_prep_bwd: chain rule through the row scaling. */
+int molclr_ntxent_prep(const float* r, float* rhat, float* norm, int64_t n, int64_t C,
+                       int cosine, molclr_stream_t stream);
+int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, const float* norm,
+                           float* dr, int64_t n, int64_t C, int cosine,
+                           molclr_stream_t stream);
+size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C);
+int molclr_ntxent_fwd(const float* rhat_rows, const int32_t* row_gidx, const float* rhat_cols,
+                      int64_t nrows, int64_t ncols, int64_t C, int64_t batch_size,
+                      double temperature, float* lse_rows, float* loss_rows,
+                      void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+int molclr_ntxent_bwd(const float* rhat_rows, const int32_t* row_gidx, const float* rhat_cols,
+                      const float* lse_cols, const float* grad_loss, int64_t nrows,
+                      int64_t ncols, int64_t C, int64_t batch_size, double temperature,
+                      float* drhat_rows, void* workspace, size_t workspace_bytes,
+                      molclr_stream_t stream);
+/* loss = Σ loss_rows (deterministic single-block sum). */
+int molclr_sum_f32(const float* x, float* out, int64_t n, molclr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Adam with coupled L2 weight decay over one flat fp32 parameter buffer
+ * (torch.optim.Adam semantics, molclr.py:84-87,127):
+ *   g += wd·p; m = b1·m + (1−b1)·g; v = b2·v + (1−b2)·g²;
+ *   p −= lr/(1−b1^t) · m / (sqrt(v)/sqrt(1−b2^t) + eps)
+ * lr and step live in device memory so a captured step replays with the
+ * current learning rate; *step is incremented by the kernel. */
+int molclr_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                     int64_t n, const float* lr, int32_t* step, double beta1, double beta2,
+                     double eps, double weight_decay, molclr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOLCLR_H_ */

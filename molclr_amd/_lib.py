@@ -1,0 +1,121 @@
+"""ctypes binding of the C-ABI library ``libmolclr_hip.so`` (include/molclr.h).
+
+This is the only way the Python side reaches the GPU kernels.  Loading fails
+loudly if the library has not been built (``python -m molclr_amd.build``);
+there is no CPU or eager-PyTorch fallback for any op.
+
+``torch`` is imported first on purpose: torch ships its own HIP runtime
+(SONAME ``libamdhip64.so.7``) and the dynamic loader then resolves the
+library's HIP dependency to that same runtime, so streams and device pointers
+handed over from torch are valid in the kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_size_t, c_void_p
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = Path(os.environ.get("MOLCLR_LIB", Path(__file__).resolve().parent / "libmolclr_hip.so"))
+
+_P = c_void_p
+_I64 = c_int64
+
+# name -> (restype, argtypes); mirrors include/molclr.h exactly
+SIGNATURES = {
+    "molclr_version": (c_char_p, []),
+    "molclr_last_error": (c_char_p, []),
+    "molclr_graph_build_workspace_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_graph_build": (c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
+                                   _P, c_size_t, _P]),
+    "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "molclr_atom_embed_bwd_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64]),
+    "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, c_size_t, _P]),
+    "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, c_size_t,
+                                          _P]),
+    "molclr_gcn_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_gcn_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_gcn_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, c_size_t,
+                                         _P]),
+    "molclr_gemm_f32_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_gemm_f32": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, c_int, c_int, c_int,
+                                _P, _P, _I64, _P, c_size_t, _P]),
+    "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, _P, c_size_t, _P]),
+    "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_batchnorm_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_double, c_double,
+                                     c_int, c_int, _P, c_size_t, _P]),
+    "molclr_batchnorm_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
+                                     c_size_t, _P]),
+    "molclr_segment_pool_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_segment_pool_bwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
+    "molclr_l2norm_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_double, _P]),
+    "molclr_l2norm_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, c_double, _P]),
+    "molclr_ntxent_prep": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_ntxent_prep_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_ntxent_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_ntxent_fwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P, _P, _P,
+                                  c_size_t, _P]),
+    "molclr_ntxent_bwd": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P, _P,
+                                  c_size_t, _P]),
+    "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
+    "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
+                                 c_double, _P]),
+}
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+
+
+class MolclrError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load and type the library (once).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} not found: the MolCLR HIP kernels are not built. "
+            "Run `python -m molclr_amd.build` (hipcc, gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    return (load().molclr_last_error() or b"").decode()
+
+
+def call(name: str, *args) -> None:
+    """Call an int-returning entry point and raise on a non-zero status."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise MolclrError(f"{name} failed (status {rc}): {last_error()}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

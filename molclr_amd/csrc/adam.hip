@@ -1,0 +1,79 @@
+// Adam with coupled L2 weight decay over one flat parameter buffer, and the
+// library's error/version plumbing.
+//
+// Reference: torch.optim.Adam(model.parameters(), init_lr,
+// weight_decay=eval(config['weight_decay'])) stepped once per batch
+// (molclr.py:84-87,127).  torch's Adam adds weight_decay * param to the
+// gradient before the moments (coupled L2, not AdamW).
+#include "common.h"
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+namespace molclr {
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+}  // namespace molclr
+
+namespace {
+
+__global__ void k_adam_step(float4* __restrict__ p, const float4* __restrict__ g,
+                            float4* __restrict__ m, float4* __restrict__ v, int64_t n4,
+                            const float* __restrict__ lr_ptr, const int32_t* __restrict__ step_ptr,
+                            float b1, float b2, float eps, float wd) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n4) return;
+  const int step = *step_ptr + 1;  // the counter is advanced by k_adam_tick afterwards
+  const float lr = *lr_ptr;
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(b2, (float)step));
+  const float step_size = lr / bc1;
+  float4 pp = p[t], gg = g[t], mm = m[t], vv = v[t];
+#define MOLCLR_ADAM_LANE(c)                                   \
+  {                                                           \
+    float gr = gg.c + wd * pp.c;                              \
+    mm.c = b1 * mm.c + (1.f - b1) * gr;                       \
+    vv.c = b2 * vv.c + (1.f - b2) * gr * gr;                  \
+    float den = sqrtf(vv.c) / bc2s + eps;                     \
+    pp.c = pp.c - step_size * (mm.c / den);                   \
+  }
+  MOLCLR_ADAM_LANE(x)
+  MOLCLR_ADAM_LANE(y)
+  MOLCLR_ADAM_LANE(z)
+  MOLCLR_ADAM_LANE(w)
+#undef MOLCLR_ADAM_LANE
+  p[t] = pp;
+  m[t] = mm;
+  v[t] = vv;
+}
+
+__global__ void k_adam_tick(int32_t* step) { *step += 1; }
+
+}  // namespace
+
+MOLCLR_API const char* molclr_version(void) { return "molclr_amd 0.1.0 gfx950"; }
+MOLCLR_API const char* molclr_last_error(void) { return molclr::g_err; }
+
+MOLCLR_API int molclr_adam_step(float* param, const float* grad, float* exp_avg,
+                                float* exp_avg_sq, int64_t n, const float* lr, int32_t* step,
+                                double beta1, double beta2, double eps, double weight_decay,
+                                molclr_stream_t stream) {
+  MOLCLR_REQUIRE(n % 4 == 0, "adam_step: flat buffer length %lld must be a multiple of 4",
+                 (long long)n);
+  MOLCLR_REQUIRE(lr && step, "adam_step: lr and step must be device pointers");
+  hipStream_t s = molclr::as_stream(stream);
+  int64_t n4 = n / 4;
+  if (n4 > 0)
+    hipLaunchKernelGGL(k_adam_step, dim3(molclr::ceil_div(n4, 256)), dim3(256), 0, s,
+                       (float4*)param, (const float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
+                       n4, lr, step, (float)beta1, (float)beta2, (float)eps, (float)weight_decay);
+  hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}

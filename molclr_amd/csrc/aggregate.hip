@@ -1,0 +1,423 @@
+// Neighbour aggregation kernels: atom embedding, GINE and GCN message passing.
+//
+// Reference semantics (CameronDiao/MolCLR):
+//   atom embedding   models/ginet_molclr.py:103  h = X1[x0] + X2[x1]
+//   GINEConv         models/ginet_molclr.py:29-47 with PyG 1.6.3 propagate
+//                    (aggr='add', flow source_to_target): message x_j + e_k,
+//                    e_k = E1[bt_k] + E2[bd_k], scatter-add at edge_index[1],
+//                    self loop (bt=4, bd=0) appended after the real edges.
+//   GCNConv          models/gcn_molclr.py:62-91: message e_k + (xW)_j with a
+//                    scalar e_k, then `out += bias`.
+//
+// Layout: node features are row-major [N, D] fp32, D % 4 == 0.  One thread
+// owns one float4 column of one destination row; consecutive threads cover a
+// row and then the next, so every neighbour-row gather is a contiguous
+// 16*D-byte read by D/4 consecutive lanes, and the output write is fully
+// coalesced.  The per-row neighbour loop is a segmented reduction over the
+// CSR built by graph.hip — no atomics, deterministic, and in the reference's
+// accumulation order (in-edges in edge order, self loop last), so the sums
+// are bit-identical to the reference CPU path.
+#include "common.h"
+
+namespace {
+
+constexpr int kT = 256;
+
+// ---------------------------------------------------------------------------
+// atom embedding
+// ---------------------------------------------------------------------------
+__global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __restrict__ X1,
+                                 const float4* __restrict__ X2, float4* __restrict__ h, int64_t N,
+                                 int d4, int64_t n1, int64_t n2) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t i = t / d4;
+  int c = (int)(t - i * d4);
+  int64_t a = x[2 * i], b = x[2 * i + 1];
+  a = a < 0 ? 0 : (a >= n1 ? n1 - 1 : a);
+  b = b < 0 ? 0 : (b >= n2 ? n2 - 1 : b);
+  h[t] = f4add(X1[a * d4 + c], X2[b * d4 + c]);
+}
+
+// Partial per-type column sums of dh.  grid = (P partitions, ceil(D/64)),
+// block = 64 threads (one column each), LDS table [n1+n2][64].
+__global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
+    const int64_t* __restrict__ x, const float* __restrict__ dh, int64_t N, int64_t D,
+    int64_t n1, int64_t n2, int64_t rows_per_part, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float tab[];  // [(n1+n2)][64]
+  const int lane = threadIdx.x;
+  const int64_t nt = n1 + n2;
+  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.f;
+  const int64_t c = (int64_t)blockIdx.y * 64 + lane;
+  const bool active = c < D;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
+  int64_t end = beg + rows_per_part;
+  if (end > N) end = N;
+  int64_t i = beg;
+  for (; i + 4 <= end; i += 4) {
+    float v[4];
+    int64_t a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = x[2 * (i + u)];
+      b[u] = x[2 * (i + u) + 1];
+      v[u] = active ? dh[(i + u) * D + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int64_t aa = a[u] < 0 ? 0 : (a[u] >= n1 ? n1 - 1 : a[u]);
+      int64_t bb = b[u] < 0 ? 0 : (b[u] >= n2 ? n2 - 1 : b[u]);
+      tab[aa * 64 + lane] += v[u];
+      tab[(n1 + bb) * 64 + lane] += v[u];
+    }
+  }
+  for (; i < end; ++i) {
+    int64_t aa = x[2 * i], bb = x[2 * i + 1];
+    aa = aa < 0 ? 0 : (aa >= n1 ? n1 - 1 : aa);
+    bb = bb < 0 ? 0 : (bb >= n2 ? n2 - 1 : bb);
+    float v = active ? dh[i * D + c] : 0.f;
+    tab[aa * 64 + lane] += v;
+    tab[(n1 + bb) * 64 + lane] += v;
+  }
+  if (!active) return;
+  float* out = partial + (int64_t)blockIdx.x * nt * D;
+  for (int64_t r = 0; r < nt; ++r) out[r * D + c] = tab[r * 64 + lane];
+}
+
+// out[r][c] = Σ_p partial[p][r][c], rows [0,n1) -> dX1, [n1,n1+n2) -> dX2.
+__global__ void k_reduce_partials_split(const float* __restrict__ partial, int64_t P,
+                                        int64_t rows, int64_t D, int64_t split,
+                                        float* __restrict__ outA, float* __restrict__ outB) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * D) return;
+  float acc = 0.f;
+  for (int64_t p = 0; p < P; ++p) acc += partial[p * rows * D + t];
+  int64_t r = t / D;
+  if (r < split) {
+    if (outA) outA[t] = acc;
+  } else {
+    if (outB) outB[t - split * D] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// GINE aggregation
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kT) void k_gine_agg_fwd(
+    const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+    const float4* __restrict__ E1, const float4* __restrict__ E2, float4* __restrict__ out,
+    int64_t N, int d4) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t i = t / d4;
+  int c = (int)(t - i * d4);
+  int32_t k = rowptr[i];
+  const int32_t end = rowptr[i + 1];
+  float4 acc = f4zero();
+  // two neighbours per step: both gathers are issued before the ordered adds
+  for (; k + 2 <= end; k += 2) {
+    int32_t j0 = col[k], j1 = col[k + 1];
+    uint8_t q0 = ecode[k], q1 = ecode[k + 1];
+    float4 x0 = x[(int64_t)j0 * d4 + c];
+    float4 x1 = x[(int64_t)j1 * d4 + c];
+    float4 e0 = f4add(E1[(q0 & 7) * d4 + c], E2[(q0 >> 3) * d4 + c]);
+    float4 e1 = f4add(E1[(q1 & 7) * d4 + c], E2[(q1 >> 3) * d4 + c]);
+    acc = f4add(acc, f4add(x0, e0));
+    acc = f4add(acc, f4add(x1, e1));
+  }
+  if (k < end) {
+    int32_t j0 = col[k];
+    uint8_t q0 = ecode[k];
+    float4 e0 = f4add(E1[(q0 & 7) * d4 + c], E2[(q0 >> 3) * d4 + c]);
+    acc = f4add(acc, f4add(x[(int64_t)j0 * d4 + c], e0));
+  }
+  // self loop: bond type 4, bond dir 0, appended last (ginet_molclr.py:31-37)
+  float4 es = f4add(E1[MOLCLR_SELF_LOOP_BOND_TYPE * d4 + c], E2[c]);
+  acc = f4add(acc, f4add(x[t], es));
+  out[t] = acc;
+}
+
+// dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]
+__global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restrict__ g,
+                                                         const int32_t* __restrict__ rowptr_t,
+                                                         const int32_t* __restrict__ col_t,
+                                                         float4* __restrict__ dx, int64_t N,
+                                                         int d4) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t j = t / d4;
+  int c = (int)(t - j * d4);
+  int32_t k = rowptr_t[j];
+  const int32_t end = rowptr_t[j + 1];
+  float4 acc = f4zero();
+  for (; k + 2 <= end; k += 2) {
+    int32_t i0 = col_t[k], i1 = col_t[k + 1];
+    float4 g0 = g[(int64_t)i0 * d4 + c];
+    float4 g1 = g[(int64_t)i1 * d4 + c];
+    acc = f4add(acc, g0);
+    acc = f4add(acc, g1);
+  }
+  if (k < end) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+  acc = f4add(acc, g[t]);
+  dx[t] = acc;
+}
+
+// Edge-table gradient partials: partial[p][s][c4] = Σ_{i in part p} ecount[i][s] * g[i][c4]
+// grid (P, ceil(d4/64)), block 64.
+__global__ __launch_bounds__(64) void k_ecount_weighted_partial(
+    const float4* __restrict__ g, const int32_t* __restrict__ ecount, int64_t N, int d4,
+    int64_t rows_per_part, float4* __restrict__ partial) {
+  const int c = blockIdx.y * 64 + threadIdx.x;
+  if (c >= d4) return;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
+  int64_t end = beg + rows_per_part;
+  if (end > N) end = N;
+  float4 acc[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc[s] = f4zero();
+  for (int64_t i = beg; i < end; ++i) {
+    const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
+    int4 lo = ec[0], hi = ec[1];
+    float4 v = g[i * d4 + c];
+    int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      float w = (float)cnt[s];
+      acc[s].x += w * v.x;
+      acc[s].y += w * v.y;
+      acc[s].z += w * v.z;
+      acc[s].w += w * v.w;
+    }
+  }
+  float4* out = partial + (int64_t)blockIdx.x * 8 * d4;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) out[s * d4 + c] = acc[s];
+}
+
+// ---------------------------------------------------------------------------
+// GCN aggregation (scalar edge embedding, bias)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kT) void k_gcn_agg_fwd(
+    const float4* __restrict__ xw, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+    const float* __restrict__ E1, const float* __restrict__ E2, const float4* __restrict__ bias,
+    float4* __restrict__ out, int64_t N, int d4) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t i = t / d4;
+  int c = (int)(t - i * d4);
+  int32_t k = rowptr[i];
+  const int32_t end = rowptr[i + 1];
+  float4 acc = f4zero();
+  for (; k < end; ++k) {
+    int32_t j = col[k];
+    uint8_t q = ecode[k];
+    float e = E1[q & 7] + E2[q >> 3];
+    float4 v = xw[(int64_t)j * d4 + c];
+    acc = f4add(acc, make_float4(e + v.x, e + v.y, e + v.z, e + v.w));
+  }
+  float es = E1[MOLCLR_SELF_LOOP_BOND_TYPE] + E2[0];
+  float4 v = xw[t];
+  acc = f4add(acc, make_float4(es + v.x, es + v.y, es + v.z, es + v.w));
+  out[t] = f4add(acc, bias[c]);
+}
+
+// One wave per row: rowsum(g_i) weighted by ecount[i][0..8); per-wave partials.
+__global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __restrict__ g,
+                                                               const int32_t* __restrict__ ecount,
+                                                               int64_t N, int d4,
+                                                               float* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t i = wave; i < N; i += nwaves) {
+    float s = 0.f;
+    for (int c = lane; c < d4; c += 64) {
+      float4 v = g[i * d4 + c];
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    s = wave_sum(s);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += (float)ecount[i * 8 + q] * s;
+  }
+  if (lane < 8) {
+    float v = acc[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q)
+      if (lane == q) v = acc[q];
+    partial[wave * 8 + lane] = v;
+  }
+}
+
+__global__ void k_reduce_rowsum_partial(const float* __restrict__ partial, int64_t nparts,
+                                        float* __restrict__ dE1, float* __restrict__ dE2) {
+  int q = threadIdx.x;
+  if (q >= 8) return;
+  float acc = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) acc += partial[p * 8 + q];
+  if (q < 5) {
+    if (dE1) dE1[q] = acc;
+  } else {
+    if (dE2) dE2[q - 5] = acc;
+  }
+}
+
+int64_t atom_parts(int64_t N) {
+  int64_t P = molclr::ceil_div(N, 128);
+  if (P > 128) P = 128;
+  if (P < 1) P = 1;
+  return P;
+}
+int64_t ecount_parts(int64_t N) {
+  int64_t P = molclr::ceil_div(N, 64);
+  if (P > 256) P = 256;
+  if (P < 1) P = 1;
+  return P;
+}
+constexpr int64_t kRowsumBlocks = 128;
+
+}  // namespace
+
+// Column sums shared with norm.hip (declared there).
+int molclr_colsum_impl(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
+                       molclr::Workspace& w, hipStream_t s);
+size_t molclr_colsum_ws(int64_t rows, int64_t cols);
+
+MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
+                                     float* h, int64_t N, int64_t D, int64_t n1, int64_t n2,
+                                     molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "atom_embed_fwd: dim %lld must be a positive multiple of 4",
+                 (long long)D);
+  MOLCLR_REQUIRE(n1 > 0 && n2 > 0, "atom_embed_fwd: empty table");
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && X1 && X2 && h, "atom_embed_fwd: null pointer");
+  int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_atom_embed_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2,
+                     (float4*)h, N, d4, n1, n2);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_atom_embed_bwd_workspace_bytes(int64_t N, int64_t D, int64_t n1,
+                                                        int64_t n2) {
+  return (size_t)atom_parts(N) * (n1 + n2) * D * sizeof(float) + 256;
+}
+
+MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
+                                     int64_t N, int64_t D, int64_t n1, int64_t n2,
+                                     void* workspace, size_t workspace_bytes,
+                                     molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd: bad sizes");
+  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd: tables too large");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
+  hipStream_t s = molclr::as_stream(stream);
+  int64_t P = atom_parts(N);
+  int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
+  float* partial = (float*)workspace;
+  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
+  hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
+                     x, dh, N, D, n1, n2, rpp, partial);
+  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, kT)), dim3(kT),
+                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
+                                         const int32_t* col, const uint8_t* ecode,
+                                         const float* E1, const float* E2, float* out,
+                                         int64_t N, int64_t D, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_fwd: dim %lld must be a multiple of 4",
+                 (long long)D);
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && rowptr && E1 && E2 && out, "gine_aggregate_fwd: null pointer");
+  int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_gine_agg_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), (const float4*)x, rowptr, col, ecode,
+                     (const float4*)E1, (const float4*)E2, (float4*)out, N, d4);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t N, int64_t D) {
+  return (size_t)ecount_parts(N) * 8 * D * sizeof(float) + 256;
+}
+
+MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t,
+                                         const int32_t* col_t, const int32_t* ecount, float* dx,
+                                         float* dE1, float* dE2, int64_t N, int64_t D,
+                                         void* workspace, size_t workspace_bytes,
+                                         molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_bwd: dim must be a multiple of 4");
+  hipStream_t s = molclr::as_stream(stream);
+  int d4 = (int)(D / 4);
+  if (dx && N > 0) {
+    hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
+                       (const float4*)g, rowptr_t, col_t, (float4*)dx, N, d4);
+  }
+  if (dE1 || dE2) {
+    MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
+    int64_t P = ecount_parts(N);
+    int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
+    float* partial = (float*)workspace;
+    hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P, molclr::ceil_div(d4, 64)), dim3(64), 0,
+                       s, (const float4*)g, ecount, N, d4, rpp, (float4*)partial);
+    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, kT)), dim3(kT), 0, s,
+                       partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2);
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr,
+                                        const int32_t* col, const uint8_t* ecode,
+                                        const float* E1, const float* E2, const float* bias,
+                                        float* out, int64_t N, int64_t D,
+                                        molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gcn_aggregate_fwd: dim must be a multiple of 4");
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(xw && rowptr && E1 && E2 && bias && out, "gcn_aggregate_fwd: null pointer");
+  int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_gcn_agg_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), (const float4*)xw, rowptr, col, ecode, E1, E2,
+                     (const float4*)bias, (float4*)out, N, d4);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t N, int64_t D) {
+  size_t a = (size_t)kRowsumBlocks * 4 * 8 * sizeof(float) + 256;
+  return a + molclr_colsum_ws(N, D);
+}
+
+MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
+                                        const int32_t* col_t, const int32_t* ecount, float* dxw,
+                                        float* dE1, float* dE2, float* dbias, int64_t N,
+                                        int64_t D, void* workspace, size_t workspace_bytes,
+                                        molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gcn_aggregate_bwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gcn_aggregate_bwd_workspace_bytes(N, D));
+  hipStream_t s = molclr::as_stream(stream);
+  int d4 = (int)(D / 4);
+  if (dxw && N > 0) {
+    hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
+                       (const float4*)g, rowptr_t, col_t, (float4*)dxw, N, d4);
+  }
+  molclr::Workspace w(workspace, workspace_bytes);
+  float* partial = w.take<float>(kRowsumBlocks * 4 * 8);
+  if (dE1 || dE2) {
+    hipLaunchKernelGGL(k_rowsum_ecount_partial, dim3(kRowsumBlocks), dim3(256), 0, s,
+                       (const float4*)g, ecount, N, d4, partial);
+    hipLaunchKernelGGL(k_reduce_rowsum_partial, dim3(1), dim3(64), 0, s, partial,
+                       kRowsumBlocks * 4, dE1, dE2);
+  }
+  MOLCLR_LAUNCHED();
+  if (dbias) {
+    int rc = molclr_colsum_impl(g, dbias, N, D, D, w, s);
+    if (rc) return rc;
+  }
+  return MOLCLR_OK;
+}

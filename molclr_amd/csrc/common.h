@@ -1,0 +1,103 @@
+// Shared helpers for the MolCLR gfx950 kernels (see include/molclr.h for the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/molclr.h"
+
+#define MOLCLR_API extern "C" __attribute__((visibility("default")))
+
+namespace molclr {
+
+// Thread-local error text for molclr_last_error().
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
+inline hipStream_t as_stream(molclr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Carves sub-buffers out of a caller-provided workspace, 256-byte aligned.
+struct Workspace {
+  char* base;
+  size_t size;
+  size_t used = 0;
+  Workspace(void* p, size_t n) : base(static_cast<char*>(p)), size(n) {}
+  template <typename T>
+  T* take(size_t count) {
+    used = align_up(used, 256);
+    T* p = reinterpret_cast<T*>(base + used);
+    used += count * sizeof(T);
+    return p;
+  }
+  bool ok() const { return used <= size && (used == 0 || base != nullptr); }
+};
+
+// Row-band geometry for [rows, D] kernels that own one float4 column per thread:
+// a block covers `band` consecutive rows x all D/4 float4 columns, so each
+// wave reads contiguous 1 KiB of the row-major matrix (rows are contiguous).
+struct Band {
+  int d4;       // float4 columns
+  int band;     // rows per block iteration
+  int threads;  // band * d4, rounded up to a multiple of 64
+};
+inline Band make_band(int64_t dim) {
+  Band b;
+  b.d4 = (int)(dim / 4);
+  int band = 256 / b.d4;
+  if (band < 1) band = 1;
+  if (band * b.d4 < 192 && (band + 1) * b.d4 <= 1024) band += 1;
+  while (band * b.d4 > 1024) band--;
+  b.band = band;
+  b.threads = (band * b.d4 + 63) / 64 * 64;
+  return b;
+}
+
+}  // namespace molclr
+
+#define MOLCLR_REQUIRE(cond, ...)        \
+  do {                                   \
+    if (!(cond)) {                       \
+      molclr::set_error(__VA_ARGS__);    \
+      return MOLCLR_ERR_ARG;             \
+    }                                    \
+  } while (0)
+
+#define MOLCLR_REQUIRE_WS(ws, need)                                                   \
+  do {                                                                                \
+    if ((ws) < (need)) {                                                              \
+      molclr::set_error("%s: workspace %zu bytes < required %zu", __func__,           \
+                        (size_t)(ws), (size_t)(need));                                \
+      return MOLCLR_ERR_WORKSPACE;                                                    \
+    }                                                                                 \
+  } while (0)
+
+#define MOLCLR_LAUNCHED()                                                             \
+  do {                                                                                \
+    hipError_t e_ = hipGetLastError();                                                \
+    if (e_ != hipSuccess) {                                                           \
+      molclr::set_error("%s: launch failed: %s", __func__, hipGetErrorString(e_));    \
+      return (int)e_;                                                                 \
+    }                                                                                 \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}

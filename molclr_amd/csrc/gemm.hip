@@ -1,0 +1,366 @@
+// FP32 GEMM on the gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Serves every dense product of the pre-training step:
+//   GIN MLP  Linear(D,2D) -> ReLU -> Linear(2D,D)   models/ginet_molclr.py:19-23
+//   heads    feat_lin / out_lin                     models/ginet_molclr.py:90-96
+//   GCN      x @ W                                  models/gcn_molclr.py:76
+// and their backward products (dX = dY W, dW = dY^T X).  The f32 MFMA is an
+// exact f32 FMA chain (no TF32-style rounding), so results stay within the
+// fp32 tolerance of the reference CPU path.
+//
+// Structure: a workgroup of WM x WN waves owns a BM x BN output tile
+// (BM = WM*TM*32, BN = WN*TN*32); each wave owns TM x TN 32x32 MFMA tiles.
+// A and B K-slices (BK = 32) are staged in LDS as [row][k] images with a
+// 36-float row pitch; the next slice is prefetched into registers while the
+// current one is consumed.  The K order inside a slice is permuted so that a
+// lane half h consumes k = 16h .. 16h+15: one ds_read_b128 then feeds four
+// MFMAs and the image stays conflict-free (pitch 36 -> distinct 4-bank groups
+// across a 16-lane read group).  A K-major operand (X^T / dY^T of a weight
+// gradient) is transposed while staging: 4 coalesced scalar loads per lane
+// (64 consecutive m per wave instruction) then one ds_write_b128.
+//
+// Workgroups are remapped so that the tiles sharing an A row-slab land on the
+// same XCD (blocks b and b+8 share an L2): the A slab is then read from HBM
+// once per XCD rather than once per column tile.
+#include "common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;  // LDS row pitch (floats)
+
+template <bool KMAJOR, int ROWS, int T>
+struct Stager {
+  // non-K-major: ROWS x BK floats as float4 along k
+  // K-major: ROWS x BK, source stored [k][row]; each item = 4 consecutive k of one row
+  static constexpr int ITEMS = ROWS * BK / 4;
+  static constexpr int PER_THREAD = (ITEMS + T - 1) / T;
+  float4 r[PER_THREAD];
+
+  __device__ __forceinline__ void load(const float* __restrict__ src, int64_t ld, int64_t row0,
+                                       int64_t rows, int64_t k0, int64_t K, int tid) {
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+      int idx = tid + j * T;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < ITEMS) {
+        if (!KMAJOR) {
+          int row = idx / (BK / 4), k4 = idx % (BK / 4);
+          int64_t gr = row0 + row, gk = k0 + 4 * k4;
+          if (gr < rows && gk < K) v = *reinterpret_cast<const float4*>(src + gr * ld + gk);
+        } else {
+          int row = idx % ROWS, k4 = idx / ROWS;
+          int64_t gr = row0 + row, gk = k0 + 4 * k4;
+          if (gr < rows) {
+            const float* p = src + gk * ld + gr;
+            if (gk + 0 < K) v.x = p[0];
+            if (gk + 1 < K) v.y = p[ld];
+            if (gk + 2 < K) v.z = p[2 * ld];
+            if (gk + 3 < K) v.w = p[3 * ld];
+          }
+        }
+      }
+      r[j] = v;
+    }
+  }
+
+  __device__ __forceinline__ void store(float* __restrict__ lds, int tid) const {
+#pragma unroll
+    for (int j = 0; j < PER_THREAD; ++j) {
+      int idx = tid + j * T;
+      if (idx < ITEMS) {
+        int row, k4;
+        if (!KMAJOR) {
+          row = idx / (BK / 4);
+          k4 = idx % (BK / 4);
+        } else {
+          row = idx % ROWS;
+          k4 = idx / ROWS;
+        }
+        *reinterpret_cast<float4*>(lds + row * LDK + 4 * k4) = r[j];
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  // bijective: XCD x (= bid % 8) receives a contiguous range of tile ids
+  int q = nwg / 8, r = nwg % 8;
+  int x = bid % 8, pos = bid / 8;
+  int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + pos;
+}
+
+template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
+__global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
+    const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
+    int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
+    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split) {
+  constexpr int T = WM * WN * 64;
+  constexpr int BM = WM * TM * 32;
+  constexpr int BN = WN * TN * 32;
+  __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * LDK];
+  float* As = lds;
+  float* Bs = lds + BM * LDK;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
+  const int nk_total = (int)((K + BK - 1) / BK);
+  const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
+  int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
+  if (kt_end > nk_total) kt_end = nk_total;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  Stager<AK, BM, T> sa;
+  Stager<BKM, BN, T> sb;
+  if (kt_beg < kt_end) {
+    sa.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid);
+    sb.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tid);
+  }
+  for (int kt = kt_beg; kt < kt_end; ++kt) {
+    __syncthreads();  // previous slice fully consumed
+    sa.store(As, tid);
+    sb.store(Bs, tid);
+    __syncthreads();
+    if (kt + 1 < kt_end) {  // prefetch the next slice into registers
+      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * BK, K, tid);
+      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * BK, K, tid);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 af[TM], bf[TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[a] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + a * 32 + li) * LDK + lh * 16 + 4 * q);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bf[b] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + b * 32 + li) * LDK + lh * 16 + 4 * q);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].x, bf[b].x, acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].y, bf[b].y, acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].z, bf[b].z, acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].w, bf[b].w, acc[a][b], 0, 0, 0);
+        }
+    }
+  }
+
+  // epilogue: acc register r of lane (li, lh) -> row (r&3) + 8*(r>>2) + 4*lh, col li
+  float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
+  const int64_t ldo = SPLIT ? N : ldc;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= M) continue;
+        float v = acc[a][b][r];
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
+          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+        }
+        Cout[m * ldo + n] = v;
+      }
+    }
+  }
+}
+
+// C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
+template <int EPI>
+__global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
+                                float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                const float* __restrict__ aux, int64_t ldaux) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * N) return;
+  int64_t m = t / N, n = t - m * N;
+  float v = 0.f;
+  for (int z = 0; z < splits; ++z) v += partial[(int64_t)z * M * N + t];
+  if (EPI == MOLCLR_EPI_BIAS) v = v + bias[n];
+  if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bias[n], 0.f);
+  if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+  C[m * ldc + n] = v;
+}
+
+struct Cfg {
+  int wm, wn, tm, tn;
+  int bm() const { return wm * tm * 32; }
+  int bn() const { return wn * tn * 32; }
+};
+
+Cfg pick_cfg(int64_t M, int64_t N) {
+  if (M <= 1024 && N <= 1024) return {2, 2, 1, 1};  // 64 x 64: small (heads, NT-Xent-sized)
+  // prefer the wide 128 x 128 tile unless it wastes > 12% of the N extent
+  int64_t pad128 = (N + 127) / 128 * 128, pad64 = (N + 63) / 64 * 64;
+  if ((double)pad128 / N <= 1.12 * (double)pad64 / N) return {2, 2, 2, 2};
+  return {4, 1, 1, 2};  // 128 x 64
+}
+
+int pick_splits(const Cfg& c, int64_t M, int64_t N, int64_t K) {
+  int64_t tiles = ((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn());
+  int64_t nk = (K + BK - 1) / BK;
+  if (tiles >= 256 || nk < 8) return 1;
+  int64_t s = (512 + tiles - 1) / tiles;
+  if (s > nk / 4) s = nk / 4;  // keep >= 4 K-slices per split
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : (int)s;
+}
+
+template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
+void launch_t(dim3 grid, hipStream_t s, const float* A, const float* B, float* C, int64_t M,
+              int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
+              const float* aux, int64_t ldaux, int kps) {
+  hipLaunchKernelGGL((k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
+                     0, s, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, kps);
+}
+
+template <int WM, int WN, int TM, int TN, bool SPLIT>
+int dispatch_layout(int ak, int bk, int epi, dim3 grid, hipStream_t s, const float* A,
+                    const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                    int64_t ldb, int64_t ldc, const float* bias, const float* aux, int64_t ldaux,
+                    int kps) {
+#define MOLCLR_GEMM_CASE(AKV, BKV, EPV)                                                        \
+  if (ak == AKV && bk == BKV && (SPLIT || epi == EPV)) {                                       \
+    launch_t<WM, WN, TM, TN, AKV, BKV, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(                  \
+        grid, s, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, kps);                      \
+    return 0;                                                                                  \
+  }
+#define MOLCLR_GEMM_EPIS(AKV, BKV)                \
+  MOLCLR_GEMM_CASE(AKV, BKV, MOLCLR_EPI_NONE)      \
+  MOLCLR_GEMM_CASE(AKV, BKV, MOLCLR_EPI_BIAS)      \
+  MOLCLR_GEMM_CASE(AKV, BKV, MOLCLR_EPI_BIAS_RELU) \
+  MOLCLR_GEMM_CASE(AKV, BKV, MOLCLR_EPI_RELU_MASK)
+  if (SPLIT) {
+    MOLCLR_GEMM_CASE(false, false, MOLCLR_EPI_NONE)
+    MOLCLR_GEMM_CASE(false, true, MOLCLR_EPI_NONE)
+    MOLCLR_GEMM_CASE(true, false, MOLCLR_EPI_NONE)
+    MOLCLR_GEMM_CASE(true, true, MOLCLR_EPI_NONE)
+  } else {
+    MOLCLR_GEMM_EPIS(false, false)
+    MOLCLR_GEMM_EPIS(false, true)
+    MOLCLR_GEMM_EPIS(true, false)
+    MOLCLR_GEMM_EPIS(true, true)
+  }
+#undef MOLCLR_GEMM_EPIS
+#undef MOLCLR_GEMM_CASE
+  return -1;
+}
+
+template <bool SPLIT>
+int dispatch_cfg(const Cfg& c, int ak, int bk, int epi, dim3 grid, hipStream_t s, const float* A,
+                 const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                 int64_t ldb, int64_t ldc, const float* bias, const float* aux, int64_t ldaux,
+                 int kps) {
+  if (c.wm == 2 && c.wn == 2 && c.tm == 2 && c.tn == 2)
+    return dispatch_layout<2, 2, 2, 2, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb,
+                                              ldc, bias, aux, ldaux, kps);
+  if (c.wm == 4 && c.wn == 1 && c.tm == 1 && c.tn == 2)
+    return dispatch_layout<4, 1, 1, 2, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb,
+                                              ldc, bias, aux, ldaux, kps);
+  return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb, ldc,
+                                            bias, aux, ldaux, kps);
+}
+
+}  // namespace
+
+MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
+  Cfg c = pick_cfg(M, N);
+  int sp = pick_splits(c, M, N, K);
+  return sp > 1 ? (size_t)sp * M * N * sizeof(float) + 256 : 0;
+}
+
+MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
+                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                               int b_kmajor, int epilogue, const float* bias, const float* aux,
+                               int64_t ldaux, void* workspace, size_t workspace_bytes,
+                               molclr_stream_t stream) {
+  MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32: negative size");
+  MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
+                 "gemm_f32: bad epilogue %d", epilogue);
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU || bias,
+                 "gemm_f32: bias epilogue needs bias");
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux, "gemm_f32: relu-mask epilogue needs aux");
+  MOLCLR_REQUIRE(K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0,
+                 "gemm_f32: K (%lld), lda, ldb must be multiples of 4", (long long)K);
+  MOLCLR_REQUIRE(!a_kmajor || M % 4 == 0 || true, "");
+  MOLCLR_REQUIRE(ldc >= N && (a_kmajor ? lda >= M : lda >= K) && (b_kmajor ? ldb >= N : ldb >= K),
+                 "gemm_f32: leading dimension too small");
+  if (M == 0 || N == 0) return MOLCLR_OK;
+  hipStream_t s = molclr::as_stream(stream);
+  if (K == 0) {
+    // empty reduction: C = epilogue(0)
+    molclr::set_error("gemm_f32: K == 0 unsupported");
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  Cfg c = pick_cfg(M, N);
+  int64_t tiles = ((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn());
+  MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
+  int sp = pick_splits(c, M, N, K);
+  if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
+  int rc;
+  if (sp == 1) {
+    rc = dispatch_cfg<false>(c, a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, A,
+                             B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0);
+  } else {
+    int64_t nk = (K + BK - 1) / BK;
+    int kps = (int)((nk + sp - 1) / sp);
+    sp = (int)((nk + kps - 1) / kps);
+    float* partial = (float*)workspace;
+    rc = dispatch_cfg<true>(c, a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
+                            dim3((unsigned)tiles, sp), s, A, B, partial, M, N, K, lda, ldb, N,
+                            nullptr, nullptr, 0, kps);
+    if (rc == 0) {
+      dim3 g((unsigned)molclr::ceil_div(M * N, 256));
+      switch (epilogue) {
+        case MOLCLR_EPI_NONE:
+          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s, partial, sp, M,
+                             N, C, ldc, bias, aux, ldaux);
+          break;
+        case MOLCLR_EPI_BIAS:
+          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s, partial, sp, M,
+                             N, C, ldc, bias, aux, ldaux);
+          break;
+        case MOLCLR_EPI_BIAS_RELU:
+          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0, s, partial, sp,
+                             M, N, C, ldc, bias, aux, ldaux);
+          break;
+        default:
+          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0, s, partial, sp,
+                             M, N, C, ldc, bias, aux, ldaux);
+      }
+    }
+  }
+  if (rc != 0) {
+    molclr::set_error("gemm_f32: no kernel for this layout");
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}

@@ -1,0 +1,230 @@
+// Graph build: PyG Batch (edge_index / edge_attr / batch) -> destination CSR,
+// source CSC, per-node bond-type counts and graph offsets.
+//
+// Replaces the per-layer `add_self_loops` + host-built self-loop attribute of
+// the reference (models/ginet_molclr.py:31-37, models/gcn_molclr.py:64-70):
+// here it is done once per batch and the self loop (bond type 4, dir 0,
+// appended LAST by PyG) is implicit in the aggregation kernels.
+//
+// The CSR keeps, inside every destination row, the original edge order — the
+// order in which PyG's scatter-add (torch_scatter 2.0.6 on CPU) accumulates
+// messages — so the aggregation reproduces the reference's rounding exactly.
+// Slots are claimed with integer atomics and each (short) row is then sorted by
+// edge id, so the result is deterministic.
+#include "common.h"
+
+namespace {
+
+constexpr int kScanThreads = 1024;
+
+__global__ void k_graph_init(int32_t* __restrict__ ecount, int32_t* __restrict__ counters,
+                             int64_t n_counters, int64_t N, int32_t* __restrict__ status) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) *status = 0;
+  if (t < n_counters) counters[t] = 0;
+  if (t < N * MOLCLR_ECOUNT_STRIDE) {
+    int j = (int)(t % MOLCLR_ECOUNT_STRIDE);
+    // implicit self loop: bond type 4 (slot 4) and bond dir 0 (slot 5)
+    ecount[t] = (j == MOLCLR_SELF_LOOP_BOND_TYPE || j == 5) ? 1 : 0;
+  }
+}
+
+__global__ void k_graph_count(const int64_t* __restrict__ ei, const int64_t* __restrict__ ea,
+                              int64_t N, int64_t E, int32_t* __restrict__ src32,
+                              int32_t* __restrict__ dst32, uint8_t* __restrict__ code8,
+                              int32_t* __restrict__ indeg, int32_t* __restrict__ outdeg,
+                              int32_t* __restrict__ ecount, int32_t* __restrict__ status) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E) return;
+  int64_t s = ei[k], d = ei[E + k];
+  int64_t bt = ea[2 * k], bd = ea[2 * k + 1];
+  int bad = 0;
+  if (s < 0 || s >= N || d < 0 || d >= N) {
+    bad |= 1;
+    s = s < 0 ? 0 : (s >= N ? N - 1 : s);
+    d = d < 0 ? 0 : (d >= N ? N - 1 : d);
+  }
+  if (bt < 0 || bt >= MOLCLR_NUM_BOND_TYPE || bd < 0 || bd >= MOLCLR_NUM_BOND_DIR) {
+    bad |= 2;
+    bt = bt < 0 ? 0 : (bt >= MOLCLR_NUM_BOND_TYPE ? MOLCLR_NUM_BOND_TYPE - 1 : bt);
+    bd = bd < 0 ? 0 : (bd >= MOLCLR_NUM_BOND_DIR ? MOLCLR_NUM_BOND_DIR - 1 : bd);
+  }
+  if (bad) atomicOr(status, bad);
+  src32[k] = (int32_t)s;
+  dst32[k] = (int32_t)d;
+  code8[k] = (uint8_t)(bt | (bd << 3));
+  atomicAdd(&indeg[d], 1);
+  atomicAdd(&outdeg[s], 1);
+  atomicAdd(&ecount[d * MOLCLR_ECOUNT_STRIDE + bt], 1);
+  atomicAdd(&ecount[d * MOLCLR_ECOUNT_STRIDE + 5 + bd], 1);
+}
+
+// Exclusive scan of deg[0..n) into ptr[0..n]; blockIdx.x selects one of two arrays.
+__global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ degA,
+                                                        int32_t* __restrict__ ptrA,
+                                                        const int32_t* __restrict__ degB,
+                                                        int32_t* __restrict__ ptrB, int64_t n) {
+  const int32_t* deg = blockIdx.x == 0 ? degA : degB;
+  int32_t* ptr = blockIdx.x == 0 ? ptrA : ptrB;
+  __shared__ int32_t wsum[kScanThreads / 64];
+  int tid = threadIdx.x;
+  int64_t per = (n + kScanThreads - 1) / kScanThreads;
+  int64_t beg = tid * per, end = beg + per < n ? beg + per : n;
+  int32_t local = 0;
+  for (int64_t i = beg; i < end; ++i) local += deg[i];
+  // inclusive scan of `local` across the block
+  int lane = tid & 63, wid = tid >> 6;
+  int32_t v = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int32_t u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[wid] = v;
+  __syncthreads();
+  if (wid == 0) {
+    int32_t w = lane < kScanThreads / 64 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int32_t u = __shfl_up(w, o, 64);
+      if (lane >= o) w += u;
+    }
+    if (lane < kScanThreads / 64) wsum[lane] = w;
+  }
+  __syncthreads();
+  int32_t run = v - local + (wid > 0 ? wsum[wid - 1] : 0);
+  for (int64_t i = beg; i < end; ++i) {
+    ptr[i] = run;
+    run += deg[i];
+  }
+  if (tid == kScanThreads - 1) ptr[n] = run;
+}
+
+__global__ void k_graph_fill(const int32_t* __restrict__ src32, const int32_t* __restrict__ dst32,
+                             int64_t E, const int32_t* __restrict__ rowptr,
+                             const int32_t* __restrict__ rowptr_t, int32_t* __restrict__ cur,
+                             int32_t* __restrict__ cur_t, int32_t* __restrict__ perm,
+                             int32_t* __restrict__ perm_t) {
+  int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= E) return;
+  int32_t s = src32[k], d = dst32[k];
+  perm[rowptr[d] + atomicAdd(&cur[d], 1)] = (int32_t)k;
+  perm_t[rowptr_t[s] + atomicAdd(&cur_t[s], 1)] = (int32_t)k;
+}
+
+// Threads [0,N) finish CSR row i, threads [N,2N) finish CSC row i: sort the
+// row's edge ids (insertion sort; molecular degrees are tiny) and gather.
+__global__ void k_graph_rows(int64_t N, const int32_t* __restrict__ src32,
+                             const int32_t* __restrict__ dst32, const uint8_t* __restrict__ code8,
+                             const int32_t* __restrict__ rowptr, const int32_t* __restrict__ rowptr_t,
+                             int32_t* __restrict__ perm, int32_t* __restrict__ perm_t,
+                             int32_t* __restrict__ col, uint8_t* __restrict__ ecode,
+                             int32_t* __restrict__ col_t) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * N) return;
+  bool csc = t >= N;
+  int64_t i = csc ? t - N : t;
+  const int32_t* ptr = csc ? rowptr_t : rowptr;
+  int32_t* p = csc ? perm_t : perm;
+  int32_t beg = ptr[i], end = ptr[i + 1];
+  for (int32_t a = beg + 1; a < end; ++a) {
+    int32_t key = p[a];
+    int32_t b = a - 1;
+    while (b >= beg && p[b] > key) {
+      p[b + 1] = p[b];
+      --b;
+    }
+    p[b + 1] = key;
+  }
+  if (!csc) {
+    for (int32_t a = beg; a < end; ++a) {
+      int32_t k = p[a];
+      col[a] = src32[k];
+      ecode[a] = code8[k];
+    }
+  } else {
+    for (int32_t a = beg; a < end; ++a) col_t[a] = dst32[p[a]];
+  }
+}
+
+__global__ void k_graph_ptr(const int64_t* __restrict__ batch, int64_t N, int64_t G,
+                            int32_t* __restrict__ graph_ptr, int32_t* __restrict__ status) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < N) {
+    int64_t b = batch[t];
+    if (b < 0 || b >= G || (t > 0 && batch[t - 1] > b)) atomicOr(status, 4);
+  }
+  if (t <= G) {
+    // lower_bound(batch, t)
+    int64_t lo = 0, hi = N;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (batch[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    graph_ptr[t] = (int32_t)(t == G ? N : lo);
+  }
+}
+
+}  // namespace
+
+MOLCLR_API size_t molclr_graph_build_workspace_bytes(int64_t N, int64_t E) {
+  molclr::Workspace w(nullptr, 0);
+  w.take<int32_t>(E);      // src32
+  w.take<int32_t>(E);      // dst32
+  w.take<uint8_t>(E);      // code8
+  w.take<int32_t>(4 * N);  // indeg, outdeg, cur, cur_t
+  w.take<int32_t>(E);      // perm
+  w.take<int32_t>(E);      // perm_t
+  return w.used + 256;
+}
+
+MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
+                                  const int64_t* batch, int64_t N, int64_t E, int64_t G,
+                                  int32_t* rowptr, int32_t* col, uint8_t* ecode,
+                                  int32_t* rowptr_t, int32_t* col_t, int32_t* ecount,
+                                  int32_t* graph_ptr, int32_t* status, void* workspace,
+                                  size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(N >= 0 && E >= 0 && G >= 0, "graph_build: negative size");
+  MOLCLR_REQUIRE(N < (int64_t)1 << 31 && E < (int64_t)1 << 31, "graph_build: N/E exceed int32");
+  MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status, "graph_build: null output");
+  MOLCLR_REQUIRE(E == 0 || (edge_index && edge_attr && col && ecode && col_t),
+                 "graph_build: null edge buffer");
+  MOLCLR_REQUIRE(N == 0 || batch, "graph_build: null batch");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_graph_build_workspace_bytes(N, E));
+  hipStream_t s = molclr::as_stream(stream);
+  molclr::Workspace w(workspace, workspace_bytes);
+  int32_t* src32 = w.take<int32_t>(E);
+  int32_t* dst32 = w.take<int32_t>(E);
+  uint8_t* code8 = w.take<uint8_t>(E);
+  int32_t* counters = w.take<int32_t>(4 * N);
+  int32_t* indeg = counters;
+  int32_t* outdeg = counters + N;
+  int32_t* cur = counters + 2 * N;
+  int32_t* cur_t = counters + 3 * N;
+  int32_t* perm = w.take<int32_t>(E);
+  int32_t* perm_t = w.take<int32_t>(E);
+
+  const int T = 256;
+  int64_t n_init = 8 * N > 4 * N ? 8 * N : 4 * N;
+  if (n_init < 1) n_init = 1;
+  hipLaunchKernelGGL(k_graph_init, dim3(molclr::ceil_div(n_init, T)), dim3(T), 0, s, ecount,
+                     counters, 4 * N, N, status);
+  if (E > 0) {
+    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, edge_index,
+                       edge_attr, N, E, src32, dst32, code8, indeg, outdeg, ecount, status);
+  }
+  hipLaunchKernelGGL(k_scan2, dim3(2), dim3(kScanThreads), 0, s, indeg, rowptr, outdeg, rowptr_t,
+                     N);
+  if (E > 0) {
+    hipLaunchKernelGGL(k_graph_fill, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, src32, dst32, E,
+                       rowptr, rowptr_t, cur, cur_t, perm, perm_t);
+    hipLaunchKernelGGL(k_graph_rows, dim3(molclr::ceil_div(2 * N, T)), dim3(T), 0, s, N, src32,
+                       dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t);
+  }
+  int64_t n_ptr = N > G + 1 ? N : G + 1;
+  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, batch, N, G,
+                     graph_ptr, status);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}

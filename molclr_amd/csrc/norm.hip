@@ -1,0 +1,602 @@
+// Row-band reductions and normalisations: column sums (bias gradients),
+// BatchNorm1d(+ReLU) forward/backward, segment mean/add pooling, F.normalize.
+//
+// Reference: models/ginet_molclr.py:107-113 (BatchNorm1d in train mode, ReLU on
+// all but the last layer, dropout p = drop_ratio = 0, global_mean_pool),
+// molclr.py:63-64 (F.normalize).  Column statistics are reduced in a fixed
+// order (per-thread Welford -> per-block Chan merge -> per-column merge over
+// blocks), so every result is run-to-run deterministic.
+//
+// Band layout (molclr::make_band): a block covers `band` consecutive rows x all
+// D/4 float4 columns, each wave reading 1 KiB of contiguous memory.
+#include "common.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr int kT = 256;
+
+int64_t band_parts(int64_t rows, int band) {
+  // ~16 row-iterations per thread, at most 1024 partitions
+  int64_t P = molclr::ceil_div(rows, (int64_t)band * 16);
+  if (P > 1024) P = 1024;
+  if (P < 1) P = 1;
+  return P;
+}
+
+// ---------------------------------------------------------------------------
+// column sums
+// ---------------------------------------------------------------------------
+__global__ void k_colsum_partial(const float4* __restrict__ X, int64_t rows, int d4, int64_t ld4,
+                                 int band, int64_t rows_per_part, float4* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float4 red[];  // [band][d4]
+  const int tid = threadIdx.x;
+  const bool live = tid < band * d4;
+  const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
+  int64_t end = beg + rows_per_part;
+  if (end > rows) end = rows;
+  float4 acc = f4zero();
+  if (live)
+    for (int64_t i = beg + r; i < end; i += band) acc = f4add(acc, X[i * ld4 + c]);
+  if (live) red[r * d4 + c] = acc;
+  __syncthreads();
+  if (live && r == 0) {
+    float4 s = red[c];
+    for (int q = 1; q < band; ++q) s = f4add(s, red[q * d4 + c]);
+    partial[(int64_t)blockIdx.x * d4 + c] = s;
+  }
+}
+
+__global__ void k_colsum_final(const float* __restrict__ partial, int64_t P, int64_t cols,
+                               float* __restrict__ out) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float acc = 0.f;
+  for (int64_t p = 0; p < P; ++p) acc += partial[p * cols + c];
+  out[c] = acc;
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm
+// ---------------------------------------------------------------------------
+struct Welford4 {
+  float n;
+  float4 mean, m2;
+};
+
+__device__ __forceinline__ void chan_merge(float& na, float4& ma, float4& qa, float nb, float4 mb,
+                                           float4 qb) {
+  if (nb == 0.f) return;
+  if (na == 0.f) {
+    na = nb;
+    ma = mb;
+    qa = qb;
+    return;
+  }
+  float n = na + nb;
+  float wb = nb / n, wab = na * nb / n;
+  float4 d = make_float4(mb.x - ma.x, mb.y - ma.y, mb.z - ma.z, mb.w - ma.w);
+  ma = make_float4(ma.x + d.x * wb, ma.y + d.y * wb, ma.z + d.z * wb, ma.w + d.w * wb);
+  qa = make_float4(qa.x + qb.x + d.x * d.x * wab, qa.y + qb.y + d.y * d.y * wab,
+                   qa.z + qb.z + d.z * d.z * wab, qa.w + qb.w + d.w * d.w * wab);
+  na = n;
+}
+
+// partial layout: mean [P][d4] float4, m2 [P][d4] float4, n [P]
+__global__ void k_bn_stats_partial(const float4* __restrict__ z, int64_t rows, int d4, int band,
+                                   int64_t rows_per_part, float4* __restrict__ pmean,
+                                   float4* __restrict__ pm2, float* __restrict__ pn) {
+  extern __shared__ __attribute__((aligned(16))) float4 red[];  // [2][band][d4]
+  const int tid = threadIdx.x;
+  const bool live = tid < band * d4;
+  const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
+  int64_t end = beg + rows_per_part;
+  if (end > rows) end = rows;
+  float n = 0.f;
+  float4 mean = f4zero(), m2 = f4zero();
+  if (live) {
+    for (int64_t i = beg + r; i < end; i += band) {
+      float4 x = z[i * d4 + c];
+      n += 1.f;
+      float inv = 1.f / n;
+      float4 d = make_float4(x.x - mean.x, x.y - mean.y, x.z - mean.z, x.w - mean.w);
+      mean = make_float4(mean.x + d.x * inv, mean.y + d.y * inv, mean.z + d.z * inv,
+                         mean.w + d.w * inv);
+      m2 = make_float4(m2.x + d.x * (x.x - mean.x), m2.y + d.y * (x.y - mean.y),
+                       m2.z + d.z * (x.z - mean.z), m2.w + d.w * (x.w - mean.w));
+    }
+    red[r * d4 + c] = mean;
+    red[(band + r) * d4 + c] = m2;
+  }
+  __syncthreads();
+  if (live && r == 0) {
+    // rows handled by lane-row q: ceil((cnt - q) / band)
+    int64_t cnt = end > beg ? end - beg : 0;
+    float na = (float)(cnt > 0 ? (cnt + band - 1) / band : 0);
+    float4 ma = red[c], qa = red[band * d4 + c];
+    for (int q = 1; q < band; ++q) {
+      float nb = (float)(cnt > q ? (cnt - q + band - 1) / band : 0);
+      chan_merge(na, ma, qa, nb, red[q * d4 + c], red[(band + q) * d4 + c]);
+    }
+    pmean[(int64_t)blockIdx.x * d4 + c] = ma;
+    pm2[(int64_t)blockIdx.x * d4 + c] = qa;
+    if (c == 0) pn[blockIdx.x] = (float)cnt;
+  }
+}
+
+__device__ __forceinline__ void bn_coeffs(float gamma, float beta, float mean, float invstd,
+                                          float& scale, float& shift) {
+  scale = gamma * invstd;
+  shift = beta - mean * scale;
+}
+
+// One thread per column: merge partials in order, update running stats,
+// write save_mean/save_invstd and the apply coefficients.
+__global__ void k_bn_stats_final(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                 const float* __restrict__ pn, int64_t P, int64_t D,
+                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 float* __restrict__ running_mean, float* __restrict__ running_var,
+                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                 float* __restrict__ scale, float* __restrict__ shift,
+                                 float momentum, float eps) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int64_t p = 0; p < P; ++p) {
+    float nb = pn[p];
+    if (nb == 0.f) continue;
+    float mb = pmean[p * D + c], qb = pm2[p * D + c];
+    if (n == 0.f) {
+      n = nb;
+      mean = mb;
+      m2 = qb;
+      continue;
+    }
+    float nn = n + nb;
+    float d = mb - mean;
+    mean = mean + d * (nb / nn);
+    m2 = m2 + qb + d * d * (n * nb / nn);
+    n = nn;
+  }
+  float var = m2 / n;
+  float invstd = 1.0f / sqrtf(var + eps);
+  save_mean[c] = mean;
+  save_invstd[c] = invstd;
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+  if (running_var) {
+    float unbiased = n > 1.f ? m2 / (n - 1.f) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+  float sc, sh;
+  bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
+  scale[c] = sc;
+  shift[c] = sh;
+}
+
+__global__ void k_bn_eval_coeffs(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 const float* __restrict__ running_mean,
+                                 const float* __restrict__ running_var, int64_t D, float eps,
+                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                                 float* __restrict__ scale, float* __restrict__ shift) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float mean = running_mean[c];
+  float invstd = 1.0f / sqrtf(running_var[c] + eps);
+  if (save_mean) save_mean[c] = mean;
+  if (save_invstd) save_invstd[c] = invstd;
+  float sc, sh;
+  bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
+  scale[c] = sc;
+  shift[c] = sh;
+}
+
+__global__ void k_bn_saved_coeffs(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  const float* __restrict__ save_mean,
+                                  const float* __restrict__ save_invstd, int64_t D,
+                                  float* __restrict__ scale, float* __restrict__ shift) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float sc, sh;
+  bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, save_mean[c], save_invstd[c], sc, sh);
+  scale[c] = sc;
+  shift[c] = sh;
+}
+
+__device__ __forceinline__ float bn_apply1(float z, float sc, float sh) { return z * sc + sh; }
+
+__global__ __launch_bounds__(kT) void k_bn_apply(const float4* __restrict__ z,
+                                                 const float4* __restrict__ scale,
+                                                 const float4* __restrict__ shift,
+                                                 float4* __restrict__ y, int64_t total4, int d4,
+                                                 int relu) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total4) return;
+  int c = (int)(t % d4);
+  float4 v = z[t], sc = scale[c], sh = shift[c];
+  float4 o = make_float4(bn_apply1(v.x, sc.x, sh.x), bn_apply1(v.y, sc.y, sh.y),
+                         bn_apply1(v.z, sc.z, sh.z), bn_apply1(v.w, sc.w, sh.w));
+  if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+  y[t] = o;
+}
+
+// BN backward pass 1: per-column Σ dyr and Σ dyr * xhat (fixed order).
+__global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __restrict__ z,
+                                 const float4* __restrict__ mean, const float4* __restrict__ invstd,
+                                 const float4* __restrict__ scale, const float4* __restrict__ shift,
+                                 int64_t rows, int d4, int band, int64_t rows_per_part, int relu,
+                                 float4* __restrict__ p1, float4* __restrict__ p2) {
+  extern __shared__ __attribute__((aligned(16))) float4 red[];  // [2][band][d4]
+  const int tid = threadIdx.x;
+  const bool live = tid < band * d4;
+  const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
+  int64_t end = beg + rows_per_part;
+  if (end > rows) end = rows;
+  float4 s1 = f4zero(), s2 = f4zero();
+  if (live) {
+    float4 mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+    for (int64_t i = beg + r; i < end; i += band) {
+      float4 g = dy[i * d4 + c], x = z[i * d4 + c];
+      if (relu) {
+        g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
+        g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
+        g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
+        g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
+      }
+      s1 = f4add(s1, g);
+      s2.x += g.x * ((x.x - mu.x) * is.x);
+      s2.y += g.y * ((x.y - mu.y) * is.y);
+      s2.z += g.z * ((x.z - mu.z) * is.z);
+      s2.w += g.w * ((x.w - mu.w) * is.w);
+    }
+    red[r * d4 + c] = s1;
+    red[(band + r) * d4 + c] = s2;
+  }
+  __syncthreads();
+  if (live && r == 0) {
+    float4 a = red[c], b = red[band * d4 + c];
+    for (int q = 1; q < band; ++q) {
+      a = f4add(a, red[q * d4 + c]);
+      b = f4add(b, red[(band + q) * d4 + c]);
+    }
+    p1[(int64_t)blockIdx.x * d4 + c] = a;
+    p2[(int64_t)blockIdx.x * d4 + c] = b;
+  }
+}
+
+__global__ void k_bn_bwd_final(const float* __restrict__ p1, const float* __restrict__ p2,
+                               int64_t P, int64_t D, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta, float* __restrict__ k1,
+                               float* __restrict__ k2, float inv_rows) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= D) return;
+  float a = 0.f, b = 0.f;
+  for (int64_t p = 0; p < P; ++p) {
+    a += p1[p * D + c];
+    b += p2[p * D + c];
+  }
+  if (dbeta) dbeta[c] = a;
+  if (dgamma) dgamma[c] = b;
+  k1[c] = a * inv_rows;
+  k2[c] = b * inv_rows;
+}
+
+__global__ __launch_bounds__(kT) void k_bn_bwd_apply(
+    const float4* __restrict__ dy, const float4* __restrict__ z, const float4* __restrict__ mean,
+    const float4* __restrict__ invstd, const float4* __restrict__ scale,
+    const float4* __restrict__ shift, const float4* __restrict__ k1,
+    const float4* __restrict__ k2, float4* __restrict__ dz, int64_t total4, int d4, int relu) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total4) return;
+  int c = (int)(t % d4);
+  float4 g = dy[t], x = z[t], mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+  float4 a = k1[c], b = k2[c];
+  if (relu) {
+    g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
+    g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
+    g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
+    g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
+  }
+  // dz = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat))  (torch CPU BN backward)
+  float4 o;
+  o.x = (g.x - a.x - ((x.x - mu.x) * is.x) * b.x) * sc.x;
+  o.y = (g.y - a.y - ((x.y - mu.y) * is.y) * b.y) * sc.y;
+  o.z = (g.z - a.z - ((x.z - mu.z) * is.z) * b.z) * sc.z;
+  o.w = (g.w - a.w - ((x.w - mu.w) * is.w) * b.w) * sc.w;
+  dz[t] = o;
+}
+
+// ---------------------------------------------------------------------------
+// segment pooling over graph_ptr
+// ---------------------------------------------------------------------------
+__global__ void k_pool_fwd(const float4* __restrict__ h, const int32_t* __restrict__ ptr,
+                           float4* __restrict__ out, int64_t G, int d4, int mode) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= G * d4) return;
+  int64_t g = t / d4;
+  int c = (int)(t - g * d4);
+  int32_t beg = ptr[g], end = ptr[g + 1];
+  float4 acc = f4zero();
+  for (int32_t i = beg; i < end; ++i) acc = f4add(acc, h[(int64_t)i * d4 + c]);
+  if (mode == 0) {
+    float cnt = (float)(end - beg > 1 ? end - beg : 1);
+    acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
+  }
+  out[t] = acc;
+}
+
+__global__ void k_pool_bwd(const float4* __restrict__ dout, const int32_t* __restrict__ ptr,
+                           float4* __restrict__ dh, int64_t G, int d4, int mode) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= G * d4) return;
+  int64_t g = t / d4;
+  int c = (int)(t - g * d4);
+  int32_t beg = ptr[g], end = ptr[g + 1];
+  float4 v = dout[t];
+  if (mode == 0) {
+    float cnt = (float)(end - beg > 1 ? end - beg : 1);
+    v = make_float4(v.x / cnt, v.y / cnt, v.z / cnt, v.w / cnt);
+  }
+  for (int32_t i = beg; i < end; ++i) dh[(int64_t)i * d4 + c] = v;
+}
+
+// ---------------------------------------------------------------------------
+// F.normalize (one wave per row)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_l2norm_fwd(const float* __restrict__ z,
+                                                    float* __restrict__ y,
+                                                    float* __restrict__ norm, int64_t rows,
+                                                    int64_t D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= rows) return;
+  const float* zr = z + r * D;
+  float ss = 0.f;
+  for (int64_t c = lane; c < D; c += 64) ss += zr[c] * zr[c];
+  ss = wave_sum(ss);
+  float nrm = sqrtf(ss);
+  float den = fmaxf(nrm, eps);
+  if (lane == 0) norm[r] = nrm;
+  for (int64_t c = lane; c < D; c += 64) y[r * D + c] = zr[c] / den;
+}
+
+__global__ __launch_bounds__(256) void k_l2norm_bwd(const float* __restrict__ dy,
+                                                    const float* __restrict__ y,
+                                                    const float* __restrict__ norm,
+                                                    float* __restrict__ dz, int64_t rows,
+                                                    int64_t D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= rows) return;
+  float nrm = norm[r];
+  if (nrm > eps) {
+    float dot = 0.f;
+    for (int64_t c = lane; c < D; c += 64) dot += dy[r * D + c] * y[r * D + c];
+    dot = wave_sum(dot);
+    for (int64_t c = lane; c < D; c += 64)
+      dz[r * D + c] = (dy[r * D + c] - dot * y[r * D + c]) / nrm;
+  } else {
+    for (int64_t c = lane; c < D; c += 64) dz[r * D + c] = dy[r * D + c] / eps;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_sum(const float* __restrict__ x, float* __restrict__ out,
+                                              int64_t n) {
+  __shared__ float ws[16];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) acc += x[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += ws[w];
+    *out = s;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// shared with aggregate.hip
+// ---------------------------------------------------------------------------
+size_t molclr_colsum_ws(int64_t rows, int64_t cols) {
+  molclr::Band b = molclr::make_band(cols);
+  return (size_t)band_parts(rows, b.band) * cols * sizeof(float) + 256;
+}
+
+int molclr_colsum_impl(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
+                       molclr::Workspace& w, hipStream_t s) {
+  MOLCLR_REQUIRE(cols > 0 && cols % 4 == 0 && ld % 4 == 0, "colsum: cols/ld must be multiples of 4");
+  molclr::Band b = molclr::make_band(cols);
+  int64_t P = band_parts(rows, b.band);
+  float* partial = w.take<float>(P * cols);
+  if (!w.ok()) {
+    molclr::set_error("colsum: workspace too small");
+    return MOLCLR_ERR_WORKSPACE;
+  }
+  int64_t rpp = molclr::ceil_div(rows > 0 ? rows : 1, P);
+  size_t lds = (size_t)b.band * b.d4 * sizeof(float4);
+  hipLaunchKernelGGL(k_colsum_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)X, rows,
+                     b.d4, ld / 4, b.band, rpp, (float4*)partial);
+  hipLaunchKernelGGL(k_colsum_final, dim3(molclr::ceil_div(cols, kT)), dim3(kT), 0, s, partial, P,
+                     cols, out);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols) {
+  return molclr_colsum_ws(rows, cols);
+}
+
+MOLCLR_API int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols,
+                                 int64_t ld, void* workspace, size_t workspace_bytes,
+                                 molclr_stream_t stream) {
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_colsum_ws(rows, cols));
+  molclr::Workspace w(workspace, workspace_bytes);
+  return molclr_colsum_impl(X, out, rows, cols, ld, w, molclr::as_stream(stream));
+}
+
+MOLCLR_API size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t D) {
+  molclr::Band b = molclr::make_band(D);
+  int64_t P = band_parts(rows, b.band);
+  molclr::Workspace w(nullptr, 0);
+  w.take<float>(P * D);  // partial mean / s1
+  w.take<float>(P * D);  // partial m2 / s2
+  w.take<float>(P);      // partial n
+  w.take<float>(D);      // scale
+  w.take<float>(D);      // shift
+  w.take<float>(D);      // k1
+  w.take<float>(D);      // k2
+  return w.used + 256;
+}
+
+MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
+                                    float* running_mean, float* running_var, float* y,
+                                    float* save_mean, float* save_invstd, int64_t rows,
+                                    int64_t D, double momentum, double eps, int training,
+                                    int relu, void* workspace, size_t workspace_bytes,
+                                    molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_fwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(!training || rows > 1, "batchnorm_fwd: need more than 1 row when training");
+  MOLCLR_REQUIRE(training || (running_mean && running_var), "batchnorm_fwd: eval needs running stats");
+  MOLCLR_REQUIRE(save_mean && save_invstd && y && z, "batchnorm_fwd: null pointer");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_batchnorm_workspace_bytes(rows, D));
+  hipStream_t s = molclr::as_stream(stream);
+  molclr::Band b = molclr::make_band(D);
+  int64_t P = band_parts(rows, b.band);
+  molclr::Workspace w(workspace, workspace_bytes);
+  float* pmean = w.take<float>(P * D);
+  float* pm2 = w.take<float>(P * D);
+  float* pn = w.take<float>(P);
+  float* scale = w.take<float>(D);
+  float* shift = w.take<float>(D);
+  if (training) {
+    int64_t rpp = molclr::ceil_div(rows, P);
+    size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
+    hipLaunchKernelGGL(k_bn_stats_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)z, rows,
+                       b.d4, b.band, rpp, (float4*)pmean, (float4*)pm2, pn);
+    hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, pmean, pm2,
+                       pn, P, D, gamma, beta, running_mean, running_var, save_mean, save_invstd,
+                       scale, shift, (float)momentum, (float)eps);
+  } else {
+    hipLaunchKernelGGL(k_bn_eval_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma,
+                       beta, running_mean, running_var, D, (float)eps, save_mean, save_invstd,
+                       scale, shift);
+  }
+  int64_t total4 = rows * (D / 4);
+  if (total4 > 0)
+    hipLaunchKernelGGL(k_bn_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
+                       (const float4*)z, (const float4*)scale, (const float4*)shift, (float4*)y,
+                       total4, (int)(D / 4), relu);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
+                                    const float* beta, const float* save_mean,
+                                    const float* save_invstd, float* dz, float* dgamma,
+                                    float* dbeta, int64_t rows, int64_t D, int relu,
+                                    void* workspace, size_t workspace_bytes,
+                                    molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_bwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(rows > 0 && dy && z && save_mean && save_invstd && dz, "batchnorm_bwd: bad args");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_batchnorm_workspace_bytes(rows, D));
+  hipStream_t s = molclr::as_stream(stream);
+  molclr::Band b = molclr::make_band(D);
+  int64_t P = band_parts(rows, b.band);
+  molclr::Workspace w(workspace, workspace_bytes);
+  float* p1 = w.take<float>(P * D);
+  float* p2 = w.take<float>(P * D);
+  w.take<float>(P);
+  float* scale = w.take<float>(D);
+  float* shift = w.take<float>(D);
+  float* k1 = w.take<float>(D);
+  float* k2 = w.take<float>(D);
+  // the same coefficients as the forward (same expression -> same ReLU mask)
+  hipLaunchKernelGGL(k_bn_saved_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma, beta,
+                     save_mean, save_invstd, D, scale, shift);
+  int64_t rpp = molclr::ceil_div(rows, P);
+  size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
+  hipLaunchKernelGGL(k_bn_bwd_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)dy,
+                     (const float4*)z, (const float4*)save_mean, (const float4*)save_invstd,
+                     (const float4*)scale, (const float4*)shift, rows, b.d4, b.band, rpp, relu,
+                     (float4*)p1, (float4*)p2);
+  hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, p1, p2, P, D,
+                     dgamma, dbeta, k1, k2, 1.0f / (float)rows);
+  int64_t total4 = rows * (D / 4);
+  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
+                     (const float4*)dy, (const float4*)z, (const float4*)save_mean,
+                     (const float4*)save_invstd, (const float4*)scale, (const float4*)shift,
+                     (const float4*)k1, (const float4*)k2, (float4*)dz, total4, (int)(D / 4), relu);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr, float* out,
+                                       int64_t G, int64_t D, int mode, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_fwd: dim must be a multiple of 4");
+  if (mode != 0 && mode != 1) {
+    molclr::set_error("segment_pool_fwd: mode %d unsupported (0 mean, 1 add)", mode);
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  if (G == 0) return MOLCLR_OK;
+  int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_pool_fwd, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), (const float4*)h, graph_ptr, (float4*)out, G, d4,
+                     mode);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_ptr, float* dh,
+                                       int64_t N, int64_t G, int64_t D, int mode,
+                                       molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_bwd: dim must be a multiple of 4");
+  if (mode != 0 && mode != 1) {
+    molclr::set_error("segment_pool_bwd: mode %d unsupported (0 mean, 1 add)", mode);
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  hipStream_t s = molclr::as_stream(stream);
+  // nodes outside every segment get zero gradient
+  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * sizeof(float), s) != hipSuccess) {
+    molclr::set_error("segment_pool_bwd: memset failed");
+    return MOLCLR_ERR_ARG;
+  }
+  if (G == 0) return MOLCLR_OK;
+  int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_pool_bwd, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
+                     (const float4*)dout, graph_ptr, (float4*)dh, G, d4, mode);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_l2norm_fwd(const float* z, float* y, float* norm, int64_t rows, int64_t D,
+                                 double eps, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0, "l2norm_fwd: bad dim");
+  if (rows == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_l2norm_fwd, dim3(molclr::ceil_div(rows * 64, 256)), dim3(256), 0,
+                     molclr::as_stream(stream), z, y, norm, rows, D, (float)eps);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_l2norm_bwd(const float* dy, const float* y, const float* norm, float* dz,
+                                 int64_t rows, int64_t D, double eps, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0, "l2norm_bwd: bad dim");
+  if (rows == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_l2norm_bwd, dim3(molclr::ceil_div(rows * 64, 256)), dim3(256), 0,
+                     molclr::as_stream(stream), dy, y, norm, dz, rows, D, (float)eps);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_sum_f32(const float* x, float* out, int64_t n, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(out && (n == 0 || x), "sum_f32: null pointer");
+  hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, molclr::as_stream(stream), x, out, n);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}

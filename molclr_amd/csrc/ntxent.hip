@@ -1,0 +1,327 @@
+// Fused NT-Xent (utils/nt_xent.py:47-65) on the f32 MFMA.
+//
+// The reference materialises the cosine broadcast (2B,2B,C), the mask gather
+// and the cross entropy.  Here, with R = [zj; zi] (nt_xent.py:48) scaled to
+// unit rows (CosineSimilarity, eps 1e-8; nt_xent.py:40-45):
+//   S      = R R^T, logits S/T
+//   lse_r  = log Σ_{c≠r} exp(S_rc/T)           (positive + masked negatives)
+//   loss   = (1/2B) Σ_r (lse_r − S_{r,p(r)}/T),  p(r) = (r + B) mod 2B
+// and the gradient is dR = W R with the SYMMETRIC
+//   W_rc = g/(2B·T) · (P_rc + P_cr − 2·[c = p(r)]),  c ≠ r,  P_rc = exp(S_rc/T − lse_r)
+// (S_rc enters loss rows r and c).  A rank that owns a subset of the rows only
+// needs the gathered R and the gathered lse to produce the exact gradient of
+// its rows: no reduce-scatter of column gradients is required.
+//
+// Tiles are computed transposed, S'[c][r] (rows c in registers, r on the lane):
+// the per-row online logsumexp is then a register loop plus one lane-half
+// shuffle, and in the backward the W' accumulator is directly the A operand
+// of the second MFMA (dR[r][k] = Σ_c W'[c][r] R[c][k]) — no LDS round trip.
+// One wave per (32-row block, column split[, k group]); partials are merged
+// in a fixed order.
+#include "common.h"
+
+#include <math.h>
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int crow(int reg, int lh) { return (reg & 3) + 8 * (reg >> 2) + 4 * lh; }
+
+// S'[c][r] for c in [c0, c0+32), r in [r0, r0+32)
+__device__ __forceinline__ f32x16 sim_tile(const float* __restrict__ rows, int64_t nrows, int64_t r0,
+                                           const float* __restrict__ cols, int64_t ncols, int64_t c0,
+                                           int64_t C, int li, int lh) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int64_t half = C / 2;
+  const bool cv = c0 + li < ncols, rv = r0 + li < nrows;
+  const float4* ap = reinterpret_cast<const float4*>(cols + (cv ? (c0 + li) : 0) * C + lh * half);
+  const float4* bp = reinterpret_cast<const float4*>(rows + (rv ? (r0 + li) : 0) * C + lh * half);
+  for (int64_t g = 0; g < half / 4; ++g) {
+    float4 a = cv ? ap[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 b = rv ? bp[g] : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// partial layout: pm [splits][nrows], ps [splits][nrows]; pos [nrows]
+__global__ __launch_bounds__(64) void k_ntxent_fwd_partial(
+    const float* __restrict__ rows, const int32_t* __restrict__ gidx, const float* __restrict__ cols,
+    int64_t nrows, int64_t ncols, int64_t C, int64_t B, float inv_t, int64_t chunks_per_split,
+    float* __restrict__ pm, float* __restrict__ ps, float* __restrict__ pos) {
+  const int lane = threadIdx.x, li = lane & 31, lh = lane >> 5;
+  const int64_t r0 = (int64_t)blockIdx.x * 32;
+  const int64_t rl = r0 + li;
+  const int64_t rg = rl < nrows ? gidx[rl] : -1;
+  const int64_t pg = rg >= 0 ? (rg + B) % (2 * B) : -1;
+  float m = -INFINITY, s = 0.f;
+  const int64_t nchunks = (ncols + 31) / 32;
+  int64_t ch = (int64_t)blockIdx.y * chunks_per_split;
+  int64_t ch_end = ch + chunks_per_split < nchunks ? ch + chunks_per_split : nchunks;
+  for (; ch < ch_end; ++ch) {
+    const int64_t c0 = ch * 32;
+    f32x16 st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
+    float tmax = -INFINITY;
+    float lg[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int64_t cg = c0 + crow(reg, lh);
+      bool ok = rg >= 0 && cg < ncols && cg != rg;
+      lg[reg] = ok ? st[reg] * inv_t : -INFINITY;
+      if (ok && cg == pg) pos[rl] = lg[reg];
+      tmax = fmaxf(tmax, lg[reg]);
+    }
+    if (tmax > -INFINITY) {
+      float nm = fmaxf(m, tmax);
+      float acc = s * expf(m - nm);
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) acc += expf(lg[reg] - nm);
+      m = nm;
+      s = acc;
+    }
+  }
+  // merge the two lane halves (same row r, different columns)
+  float mo = __shfl_xor(m, 32, 64), so = __shfl_xor(s, 32, 64);
+  float nm = fmaxf(m, mo);
+  float tot = (nm == -INFINITY) ? 0.f : s * expf(m - nm) + so * expf(mo - nm);
+  if (lh == 0 && rl < nrows) {
+    pm[(int64_t)blockIdx.y * nrows + rl] = nm;
+    ps[(int64_t)blockIdx.y * nrows + rl] = tot;
+  }
+}
+
+__global__ void k_ntxent_fwd_final(const float* __restrict__ pm, const float* __restrict__ ps,
+                                   const float* __restrict__ pos, int64_t splits, int64_t nrows,
+                                   float inv_2b, float* __restrict__ lse, float* __restrict__ loss) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  float m = -INFINITY;
+  for (int64_t z = 0; z < splits; ++z) m = fmaxf(m, pm[z * nrows + r]);
+  float s = 0.f;
+  for (int64_t z = 0; z < splits; ++z) {
+    float mz = pm[z * nrows + r];
+    if (mz > -INFINITY) s += ps[z * nrows + r] * expf(mz - m);
+  }
+  float l = m + logf(s);
+  lse[r] = l;
+  loss[r] = (l - pos[r]) * inv_2b;
+}
+
+// partial [splits][nrows][C]; grid (row blocks, splits, k groups of KT tiles)
+template <int KT>
+__global__ __launch_bounds__(64) void k_ntxent_bwd_partial(
+    const float* __restrict__ rows, const int32_t* __restrict__ gidx, const float* __restrict__ cols,
+    const float* __restrict__ lse_cols, const float* __restrict__ grad_loss, int64_t nrows,
+    int64_t ncols, int64_t C, int64_t B, float inv_t, int64_t chunks_per_split,
+    float* __restrict__ partial) {
+  const int lane = threadIdx.x, li = lane & 31, lh = lane >> 5;
+  const int64_t r0 = (int64_t)blockIdx.x * 32;
+  const int64_t rl = r0 + li;
+  const int64_t rg = rl < nrows ? gidx[rl] : -1;
+  const int64_t pg = rg >= 0 ? (rg + B) % (2 * B) : -1;
+  const float lse_r = rg >= 0 ? lse_cols[rg] : 0.f;
+  const float coef = (*grad_loss) * inv_t / (float)(2 * B);
+  const int64_t kbase = (int64_t)blockIdx.z * KT * 32;
+  const int nkt = (int)((C - kbase) / 32 < KT ? (C - kbase) / 32 : KT);
+
+  f32x16 out[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[t][r] = 0.f;
+
+  const int64_t nchunks = (ncols + 31) / 32;
+  int64_t ch = (int64_t)blockIdx.y * chunks_per_split;
+  int64_t ch_end = ch + chunks_per_split < nchunks ? ch + chunks_per_split : nchunks;
+  for (; ch < ch_end; ++ch) {
+    const int64_t c0 = ch * 32;
+    f32x16 st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
+    // W'[c][r] in place
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int64_t cg = c0 + crow(reg, lh);
+      float w = 0.f;
+      if (rg >= 0 && cg < ncols && cg != rg) {
+        float lg = st[reg] * inv_t;
+        w = expf(lg - lse_r) + expf(lg - lse_cols[cg]);
+        if (cg == pg) w -= 2.f;
+        w *= coef;
+      }
+      st[reg] = w;
+    }
+    // out[r][k] += Σ_c W'[c][r] R[c][k]: A operand = W' register s (k-index c = crow(s, lh))
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int64_t cg = c0 + crow(reg, lh);
+      const float* crow_ptr = cols + (cg < ncols ? cg : 0) * C + kbase + li;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        if (t < nkt) {
+          float b = cg < ncols ? crow_ptr[t * 32] : 0.f;
+          out[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(st[reg], b, out[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // out[t] register reg of lane (li, lh): row r = crow(reg, lh), col k = kbase + 32 t + li
+  float* base = partial + (int64_t)blockIdx.y * nrows * C;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    if (t >= nkt) continue;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int64_t r = r0 + crow(reg, lh);
+      if (r < nrows) base[r * C + kbase + t * 32 + li] = out[t][reg];
+    }
+  }
+}
+
+__global__ void k_reduce_splits(const float* __restrict__ partial, int64_t splits, int64_t n,
+                                float* __restrict__ out) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  float acc = 0.f;
+  for (int64_t z = 0; z < splits; ++z) acc += partial[z * n + t];
+  out[t] = acc;
+}
+
+// rhat = r / max(||r||, 1e-8) (cosine) or r (dot); norm saved for the backward
+__global__ __launch_bounds__(256) void k_ntxent_prep(const float* __restrict__ r,
+                                                     float* __restrict__ rhat,
+                                                     float* __restrict__ norm, int64_t n,
+                                                     int64_t C, int cosine) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= n) return;
+  const float* x = r + row * C;
+  float den = 1.f;
+  if (cosine) {
+    float ss = 0.f;
+    for (int64_t c = lane; c < C; c += 64) ss += x[c] * x[c];
+    ss = wave_sum(ss);
+    den = fmaxf(sqrtf(ss), 1e-8f);
+  }
+  if (lane == 0) norm[row] = den;
+  for (int64_t c = lane; c < C; c += 64) rhat[row * C + c] = cosine ? x[c] / den : x[c];
+}
+
+__global__ __launch_bounds__(256) void k_ntxent_prep_bwd(const float* __restrict__ drhat,
+                                                         const float* __restrict__ rhat,
+                                                         const float* __restrict__ norm,
+                                                         float* __restrict__ dr, int64_t n,
+                                                         int64_t C, int cosine) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= n) return;
+  const float* g = drhat + row * C;
+  if (!cosine) {
+    for (int64_t c = lane; c < C; c += 64) dr[row * C + c] = g[c];
+    return;
+  }
+  float den = norm[row];
+  const float* y = rhat + row * C;
+  float dot = 0.f;
+  for (int64_t c = lane; c < C; c += 64) dot += g[c] * y[c];
+  dot = wave_sum(dot);
+  // norm clamped at eps: rhat = r / eps is linear in r
+  bool clamped = !(den > 1e-8f);
+  for (int64_t c = lane; c < C; c += 64)
+    dr[row * C + c] = clamped ? g[c] / den : (g[c] - dot * y[c]) / den;
+}
+
+int64_t ntx_splits(int64_t nrows, int64_t ncols) {
+  int64_t rb = (nrows + 31) / 32, nch = (ncols + 31) / 32;
+  int64_t s = (512 + rb - 1) / rb;
+  if (s > nch) s = nch;
+  if (s < 1) s = 1;
+  return s;
+}
+
+}  // namespace
+
+MOLCLR_API int molclr_ntxent_prep(const float* r, float* rhat, float* norm, int64_t n, int64_t C,
+                                  int cosine, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && n >= 0, "ntxent_prep: bad sizes");
+  if (n == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_ntxent_prep, dim3(molclr::ceil_div(n * 64, 256)), dim3(256), 0,
+                     molclr::as_stream(stream), r, rhat, norm, n, C, cosine);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, const float* norm,
+                                      float* dr, int64_t n, int64_t C, int cosine,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && n >= 0, "ntxent_prep_bwd: bad sizes");
+  if (n == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_ntxent_prep_bwd, dim3(molclr::ceil_div(n * 64, 256)), dim3(256), 0,
+                     molclr::as_stream(stream), drhat, rhat, norm, dr, n, C, cosine);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C) {
+  int64_t sp = ntx_splits(nrows, ncols);
+  size_t fwd = (size_t)(2 * sp + 1) * nrows * sizeof(float);
+  size_t bwd = (size_t)sp * nrows * C * sizeof(float);
+  return (fwd > bwd ? fwd : bwd) + 256;
+}
+
+MOLCLR_API int molclr_ntxent_fwd(const float* rows, const int32_t* gidx, const float* cols,
+                                 int64_t nrows, int64_t ncols, int64_t C, int64_t B, double T,
+                                 float* lse, float* loss, void* workspace, size_t ws_bytes,
+                                 molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && C % 8 == 0, "ntxent_fwd: C=%lld must be a multiple of 8", (long long)C);
+  MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_fwd: ncols must equal 2*batch_size");
+  MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_fwd: bad nrows");
+  MOLCLR_REQUIRE(T > 0, "ntxent_fwd: temperature must be > 0");
+  MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
+  hipStream_t s = molclr::as_stream(stream);
+  int64_t sp = ntx_splits(nrows, ncols);
+  int64_t nch = (ncols + 31) / 32;
+  int64_t cps = (nch + sp - 1) / sp;
+  sp = (nch + cps - 1) / cps;
+  molclr::Workspace w(workspace, ws_bytes);
+  float* pm = w.take<float>(sp * nrows);
+  float* ps = w.take<float>(sp * nrows);
+  float* pos = w.take<float>(nrows);
+  hipLaunchKernelGGL(k_ntxent_fwd_partial, dim3((unsigned)((nrows + 31) / 32), (unsigned)sp),
+                     dim3(64), 0, s, rows, gidx, cols, nrows, ncols, C, B, (float)(1.0 / T), cps,
+                     pm, ps, pos);
+  hipLaunchKernelGGL(k_ntxent_fwd_final, dim3(molclr::ceil_div(nrows, 256)), dim3(256), 0, s, pm,
+                     ps, pos, sp, nrows, (float)(1.0 / (2.0 * B)), lse, loss);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const float* cols,
+                                 const float* lse_cols, const float* grad_loss, int64_t nrows,
+                                 int64_t ncols, int64_t C, int64_t B, double T, float* drows,
+                                 void* workspace, size_t ws_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && C % 32 == 0, "ntxent_bwd: C=%lld must be a multiple of 32", (long long)C);
+  MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_bwd: ncols must equal 2*batch_size");
+  MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_bwd: bad nrows");
+  MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
+  hipStream_t s = molclr::as_stream(stream);
+  int64_t sp = ntx_splits(nrows, ncols);
+  int64_t nch = (ncols + 31) / 32;
+  int64_t cps = (nch + sp - 1) / sp;
+  sp = (nch + cps - 1) / cps;
+  constexpr int KT = 8;
+  int64_t kgroups = (C / 32 + KT - 1) / KT;
+  float* partial = (float*)workspace;
+  hipLaunchKernelGGL(k_ntxent_bwd_partial<KT>,
+                     dim3((unsigned)((nrows + 31) / 32), (unsigned)sp, (unsigned)kgroups), dim3(64),
+                     0, s, rows, gidx, cols, lse_cols, grad_loss, nrows, ncols, C, B,
+                     (float)(1.0 / T), cps, partial);
+  hipLaunchKernelGGL(k_reduce_splits, dim3(molclr::ceil_div(nrows * C, 256)), dim3(256), 0, s,
+                     partial, sp, nrows * C, drows);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}

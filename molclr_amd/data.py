@@ -1,0 +1,174 @@
+"""Graph containers with the PyG 1.6.3 ``Data`` / ``Batch`` field contract.
+
+The reference's encoders read ``data.x`` [N,2] int64 (atom type, chirality),
+``data.edge_index`` [2,E] int64, ``data.edge_attr`` [E,2] int64 (bond type,
+bond direction) and ``data.batch`` [N] int64 (models/ginet_molclr.py:99-101,113),
+produced by dataset/dataset.py:86-147 and PyG's collate.  These classes keep
+exactly that contract (so a real ``torch_geometric`` Batch can be passed
+instead) and add :class:`DeviceGraph`, the once-per-batch CSR that replaces
+PyG's per-layer ``add_self_loops`` + scatter bookkeeping.
+"""
+from __future__ import annotations
+
+from typing import Iterable, Sequence
+
+import torch
+
+from . import _lib
+
+
+class Data:
+    """One molecule graph (torch_geometric.data.Data subset)."""
+
+    def __init__(self, x=None, edge_index=None, edge_attr=None, **kwargs):
+        self.x = x
+        self.edge_index = edge_index
+        self.edge_attr = edge_attr
+        for k, v in kwargs.items():
+            setattr(self, k, v)
+
+    @property
+    def num_nodes(self) -> int:
+        return int(self.x.shape[0])
+
+    @property
+    def num_edges(self) -> int:
+        return int(self.edge_index.shape[1])
+
+    def to(self, device, non_blocking: bool = False):
+        out = self.__class__.__new__(self.__class__)
+        for k, v in self.__dict__.items():
+            if k.startswith("_molclr"):
+                continue
+            out.__dict__[k] = v.to(device, non_blocking=non_blocking) if torch.is_tensor(v) else v
+        return out
+
+    def __repr__(self) -> str:
+        fields = ", ".join(f"{k}={list(v.shape)}" for k, v in self.__dict__.items()
+                           if torch.is_tensor(v))
+        return f"{self.__class__.__name__}({fields})"
+
+
+class Batch(Data):
+    """A disjoint union of graphs (torch_geometric.data.Batch subset)."""
+
+    @staticmethod
+    def from_data_list(data_list: Sequence[Data]) -> "Batch":
+        """PyG 1.6.3 collate: concatenate x/edge_attr, offset edge_index by the
+        running node count, build the ascending ``batch`` vector and ``ptr``."""
+        xs, eis, eas, bs = [], [], [], []
+        offset = 0
+        ptr = [0]
+        for g, d in enumerate(data_list):
+            n = d.num_nodes
+            xs.append(d.x)
+            eis.append(d.edge_index + offset)
+            eas.append(d.edge_attr)
+            bs.append(torch.full((n,), g, dtype=torch.long))
+            offset += n
+            ptr.append(offset)
+        b = Batch(
+            x=torch.cat(xs, 0),
+            edge_index=torch.cat(eis, 1),
+            edge_attr=torch.cat(eas, 0),
+            batch=torch.cat(bs, 0),
+        )
+        b.ptr = torch.tensor(ptr, dtype=torch.long)
+        b._num_graphs = len(data_list)
+        return b
+
+    @property
+    def num_graphs(self) -> int:
+        if getattr(self, "_num_graphs", None) is not None:
+            return self._num_graphs
+        if getattr(self, "ptr", None) is not None:
+            return int(self.ptr.numel() - 1)
+        return int(self.batch.max().item()) + 1 if self.batch.numel() else 0
+
+    def to(self, device, non_blocking: bool = False):
+        out = super().to(device, non_blocking)
+        out._num_graphs = self.num_graphs
+        return out
+
+
+def collate_pairs(pairs: Iterable[tuple]) -> tuple:
+    """Collate a list of (view_i, view_j) molecule pairs into (Batch_i, Batch_j),
+    as the reference DataLoader does for MoleculeDataset (dataset.py:147,179)."""
+    pairs = list(pairs)
+    return (Batch.from_data_list([p[0] for p in pairs]),
+            Batch.from_data_list([p[1] for p in pairs]))
+
+
+def _num_graphs_of(data) -> int:
+    ng = getattr(data, "num_graphs", None)
+    if ng is not None:
+        return int(ng)
+    b = getattr(data, "batch", None)
+    if b is None:
+        return 1
+    return int(b.max().item()) + 1 if b.numel() else 0
+
+
+class DeviceGraph:
+    """Destination CSR / source CSC / bond-type counts / graph offsets of one
+    batch, built on the GPU by ``molclr_graph_build`` (graph.hip)."""
+
+    def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor, num_nodes: int,
+                 batch: torch.Tensor | None = None, num_graphs: int | None = None):
+        dev = edge_index.device
+        if dev.type != "cuda":
+            raise RuntimeError("DeviceGraph: molclr_amd runs on the GPU only (got %s)" % dev)
+        N = int(num_nodes)
+        E = int(edge_index.shape[1])
+        if batch is None:
+            batch = torch.zeros(N, dtype=torch.long, device=dev)
+            num_graphs = 1 if N > 0 else 0
+        G = int(num_graphs)
+        edge_index = edge_index.to(torch.long).contiguous()
+        edge_attr = edge_attr.to(torch.long).contiguous()
+        batch = batch.to(torch.long).contiguous()
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.num_nodes, self.num_edges, self.num_graphs = N, E, G
+        self.rowptr = torch.empty(N + 1, **i32)
+        self.col = torch.empty(max(E, 1), **i32)
+        self.ecode = torch.empty(max(E, 1), dtype=torch.uint8, device=dev)
+        self.rowptr_t = torch.empty(N + 1, **i32)
+        self.col_t = torch.empty(max(E, 1), **i32)
+        self.ecount = torch.empty(max(N, 1) * 8, **i32)
+        self.graph_ptr = torch.empty(G + 1, **i32)
+        self.status = torch.empty(1, **i32)
+        ws_bytes = _lib.query("molclr_graph_build_workspace_bytes", N, E)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _lib.call("molclr_graph_build", edge_index.data_ptr(), edge_attr.data_ptr(),
+                  batch.data_ptr(), N, E, G, self.rowptr.data_ptr(), self.col.data_ptr(),
+                  self.ecode.data_ptr(), self.rowptr_t.data_ptr(), self.col_t.data_ptr(),
+                  self.ecount.data_ptr(), self.graph_ptr.data_ptr(), self.status.data_ptr(),
+                  ws.data_ptr(), ws_bytes, _lib.stream_of(dev))
+        self.device = dev
+
+    def check(self) -> None:
+        """Synchronising validity check of the input indices (tests / debug)."""
+        st = int(self.status.item())
+        if st:
+            what = []
+            if st & 1:
+                what.append("edge_index out of range")
+            if st & 2:
+                what.append("edge_attr out of range")
+            if st & 4:
+                what.append("batch not ascending / out of range")
+            raise ValueError("invalid graph batch: " + ", ".join(what))
+
+
+def device_graph(data) -> DeviceGraph:
+    """The DeviceGraph of a Batch, built once and cached on the object."""
+    g = getattr(data, "_molclr_graph", None)
+    if g is not None and g.device == data.edge_index.device:
+        return g
+    g = DeviceGraph(data.edge_index, data.edge_attr, data.x.shape[0],
+                    getattr(data, "batch", None), _num_graphs_of(data))
+    try:
+        data._molclr_graph = g
+    except AttributeError:
+        pass
+    return g

@@ -1,0 +1,229 @@
+"""Synthetic molecular graphs and the MolCLR node-mask augmentation.
+
+RDKit and the PubChem-10M SMILES file are not available here, so molecules
+are generated directly in the reference's index space:
+
+* atoms n ~ Uniform{10..50} ("uniform", configs c1-c4) or
+  round(Normal(27, 9)) clipped to [6, 80] ("pubchem", config c5);
+* topology: random recursive tree (atom i bonds to Uniform{0..i-1}) plus
+  floor(n/8) ring-closure bonds between non-bonded pairs;
+* atom type index = Z-1 (ATOM_LIST.index, dataset/dataset.py:26,75):
+  C 0.72, N 0.12, O 0.11, F / S / Cl 0.015 each, Br 0.005;
+* chirality {0: 0.96, 1: 0.02, 2: 0.02}; bond type {single .55, double .12,
+  triple .01, aromatic .32}; bond dir {0: .98, 1: .01, 2: .01};
+* every bond becomes the consecutive directed pair (s,e), (e,s) with the same
+  [bond type, bond dir] (dataset/dataset.py:93-109).
+
+Augmentation (dataset/dataset.py:111-145), independently per view: mask
+max(1, floor(0.25 N)) atoms to [118, 0] (the mask token, len(ATOM_LIST)),
+drop floor(0.25 M) bonds (both directions), keep the surviving edges in their
+original order.  The reference uses Python's unseeded ``random``; here every
+stream is a seeded numpy Generator so runs are reproducible.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .data import Batch, Data, collate_pairs
+
+MASK_ATOM = 118  # len(ATOM_LIST), dataset/dataset.py:123
+
+_ATOM_IDX = np.array([5, 6, 7, 8, 15, 16, 34], dtype=np.int64)  # C N O F S Cl Br (Z-1)
+_ATOM_P = np.array([0.72, 0.12, 0.11, 0.015, 0.015, 0.015, 0.005])
+_CHIR_P = np.array([0.96, 0.02, 0.02])
+_BT_P = np.array([0.55, 0.12, 0.01, 0.32])
+_BD_P = np.array([0.98, 0.01, 0.01])
+
+
+@dataclass
+class Molecule:
+    """Un-augmented molecule in the reference's tensor layout (numpy int64)."""
+    x: np.ndarray           # [N, 2]
+    edge_index: np.ndarray  # [2, 2M]
+    edge_attr: np.ndarray   # [2M, 2]
+
+    @property
+    def num_atoms(self) -> int:
+        return int(self.x.shape[0])
+
+    @property
+    def num_bonds(self) -> int:
+        return int(self.edge_attr.shape[0] // 2)
+
+
+def _num_atoms(rng: np.random.Generator, shape: str) -> int:
+    if shape == "uniform":
+        return int(rng.integers(10, 51))
+    if shape == "pubchem":
+        return int(min(80, max(6, round(rng.normal(27.0, 9.0)))))
+    raise ValueError(f"unknown molecule size distribution {shape!r}")
+
+
+def random_molecule(rng: np.random.Generator, shape: str = "uniform") -> Molecule:
+    n = _num_atoms(rng, shape)
+    bonds = []
+    present = set()
+    for i in range(1, n):
+        j = int(rng.integers(0, i))
+        bonds.append((j, i))
+        present.add((j, i))
+    extra = n // 8
+    tries = 0
+    while extra > 0 and tries < 100 * n:
+        tries += 1
+        a, b = (int(v) for v in rng.integers(0, n, size=2))
+        if a == b:
+            continue
+        key = (min(a, b), max(a, b))
+        if key in present:
+            continue
+        present.add(key)
+        bonds.append(key)
+        extra -= 1
+    M = len(bonds)
+    atom = _ATOM_IDX[rng.choice(len(_ATOM_IDX), size=n, p=_ATOM_P)]
+    chir = rng.choice(3, size=n, p=_CHIR_P)
+    x = np.stack([atom, chir], 1).astype(np.int64)
+    bt = rng.choice(4, size=M, p=_BT_P)
+    bd = rng.choice(3, size=M, p=_BD_P)
+    b = np.asarray(bonds, dtype=np.int64).reshape(M, 2)
+    row = np.empty(2 * M, dtype=np.int64)
+    col = np.empty(2 * M, dtype=np.int64)
+    row[0::2], col[0::2] = b[:, 0], b[:, 1]
+    row[1::2], col[1::2] = b[:, 1], b[:, 0]
+    attr = np.repeat(np.stack([bt, bd], 1).astype(np.int64), 2, axis=0)
+    return Molecule(x, np.stack([row, col], 0), attr)
+
+
+def mask_view(mol: Molecule, rng: np.random.Generator):
+    """One augmented view, dataset/dataset.py:111-131 (returns numpy arrays)."""
+    N, M = mol.num_atoms, mol.num_bonds
+    num_mask_nodes = max(1, math.floor(0.25 * N))
+    num_mask_edges = max(0, math.floor(0.25 * M))
+    mask_nodes = rng.choice(N, size=num_mask_nodes, replace=False)
+    mask_edges_single = rng.choice(M, size=num_mask_edges, replace=False) if M else np.zeros(0, int)
+    x = mol.x.copy()
+    x[mask_nodes] = (MASK_ATOM, 0)
+    keep = np.ones(2 * M, dtype=bool)
+    keep[2 * mask_edges_single] = False
+    keep[2 * mask_edges_single + 1] = False
+    return x, mol.edge_index[:, keep], mol.edge_attr[keep]
+
+
+def augment_pair(mol: Molecule, rng_i: np.random.Generator, rng_j: np.random.Generator):
+    """(Data_i, Data_j) as MoleculeDataset.__getitem__ returns (dataset.py:147)."""
+    out = []
+    for rng in (rng_i, rng_j):
+        x, ei, ea = mask_view(mol, rng)
+        out.append(Data(x=torch.from_numpy(x), edge_index=torch.from_numpy(ei),
+                        edge_attr=torch.from_numpy(ea)))
+    return tuple(out)
+
+
+def collate_views(views) -> Batch:
+    """Fast numpy collate of (x, edge_index, edge_attr) triples into a Batch
+    (same result as Batch.from_data_list)."""
+    sizes = np.array([v[0].shape[0] for v in views], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    x = np.concatenate([v[0] for v in views], 0)
+    ei = np.concatenate([v[1] + offs[g] for g, v in enumerate(views)], 1)
+    ea = np.concatenate([v[2] for v in views], 0)
+    batch = np.repeat(np.arange(len(views), dtype=np.int64), sizes)
+    b = Batch(x=torch.from_numpy(x), edge_index=torch.from_numpy(ei),
+              edge_attr=torch.from_numpy(ea), batch=torch.from_numpy(batch))
+    b.ptr = torch.from_numpy(offs)
+    b._num_graphs = len(views)
+    return b
+
+
+class SyntheticPairBatches:
+    """Deterministic stream of (Batch_i, Batch_j) contrastive batches.
+
+    Seeds: graph seed ``seed``, view seeds ``seed+1`` /
+    ``seed+2``; give each data-parallel rank ``seed = rank * 10**6``.
+    """
+
+    def __init__(self, batch_size: int, seed: int = 0, shape: str = "uniform"):
+        self.batch_size = batch_size
+        self.shape = shape
+        self.g = np.random.default_rng(seed)
+        self.vi = np.random.default_rng(seed + 1)
+        self.vj = np.random.default_rng(seed + 2)
+
+    def molecules(self, n: int):
+        return [random_molecule(self.g, self.shape) for _ in range(n)]
+
+    def next(self):
+        mols = self.molecules(self.batch_size)
+        vi = [mask_view(m, self.vi) for m in mols]
+        vj = [mask_view(m, self.vj) for m in mols]
+        return collate_views(vi), collate_views(vj)
+
+    def take(self, n: int):
+        return [self.next() for _ in range(n)]
+
+
+class MoleculeDataset(torch.utils.data.Dataset):
+    """Map-style dataset of synthetic molecules with the reference's
+    ``__getitem__ -> (Data_i, Data_j)`` contract (dataset/dataset.py:56-150)."""
+
+    def __init__(self, num_molecules: int, seed: int = 0, shape: str = "uniform"):
+        super().__init__()
+        rng = np.random.default_rng(seed)
+        self.mols = [random_molecule(rng, shape) for _ in range(num_molecules)]
+        self.seed = seed
+        self._calls = 0
+
+    def __getitem__(self, index):
+        # per-item, per-call view streams: reproducible yet different each epoch
+        self._calls += 1
+        ss = np.random.SeedSequence([self.seed, index, self._calls])
+        ri, rj = (np.random.default_rng(s) for s in ss.spawn(2))
+        return augment_pair(self.mols[index], ri, rj)
+
+    def __len__(self):
+        return len(self.mols)
+
+
+class MoleculeDatasetWrapper:
+    """dataset/dataset.py:153-185: shuffled train/valid split, DataLoaders with
+    ``drop_last=True`` (NT-Xent needs full batches).  ``data_path`` is read as
+    ``synthetic:<num_molecules>`` (SMILES featurisation needs RDKit, absent)."""
+
+    def __init__(self, batch_size, num_workers, valid_size, data_path, seed: int = 0,
+                 shape: str = "uniform"):
+        self.batch_size = batch_size
+        self.num_workers = num_workers
+        self.valid_size = valid_size
+        self.data_path = data_path
+        self.seed = seed
+        self.shape = shape
+
+    def _num_molecules(self) -> int:
+        p = str(self.data_path)
+        if p.startswith("synthetic:"):
+            return int(p.split(":", 1)[1])
+        raise NotImplementedError(
+            f"data_path {p!r}: SMILES featurisation needs RDKit, which is not available; "
+            "use 'synthetic:<num_molecules>'")
+
+    def get_data_loaders(self):
+        train_dataset = MoleculeDataset(self._num_molecules(), self.seed, self.shape)
+        return self.get_train_validation_data_loaders(train_dataset)
+
+    def get_train_validation_data_loaders(self, train_dataset):
+        num_train = len(train_dataset)
+        indices = np.random.default_rng(self.seed).permutation(num_train).tolist()
+        split = int(np.floor(self.valid_size * num_train))
+        train_idx, valid_idx = indices[split:], indices[:split]
+        train_sampler = torch.utils.data.SubsetRandomSampler(train_idx)
+        valid_sampler = torch.utils.data.SubsetRandomSampler(valid_idx)
+        kw = dict(batch_size=self.batch_size, num_workers=self.num_workers, drop_last=True,
+                  collate_fn=collate_pairs)
+        train_loader = torch.utils.data.DataLoader(train_dataset, sampler=train_sampler, **kw)
+        valid_loader = torch.utils.data.DataLoader(train_dataset, sampler=valid_sampler, **kw)
+        return train_loader, valid_loader

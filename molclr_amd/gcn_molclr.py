@@ -1,0 +1,127 @@
+"""GCN encoder + projection head — drop-in for models/gcn_molclr.py.
+
+Same names, constructor arguments, parameter-creation order and state_dict
+keys as the reference (models/gcn_molclr.py:39-158; keys verified against the
+shipped ``ckpt/pretrained_gcn/checkpoints/model.pth``):
+``gnns.{l}.{weight,bias,edge_embedding1.weight,edge_embedding2.weight}``.
+
+The reference computes ``gcn_norm`` and discards the result
+(gcn_molclr.py:74), so it has no effect on outputs and is not computed; the
+``torch_sparse`` ``message_and_aggregate`` path (gcn_molclr.py:90-91) is dead
+for dense ``edge_index`` input and is not provided.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn import Parameter
+
+from . import ops
+from .data import DeviceGraph, device_graph
+
+num_atom_type = 119  # including the extra mask tokens
+num_chirality_tag = 3
+
+num_bond_type = 5  # including aromatic and self-loop edge
+num_bond_direction = 3
+
+
+class GCNConv(nn.Module):
+    """models/gcn_molclr.py:39-91:
+    ``out_i = Σ_{j→i} (e_ji + (xW)_j) + (e_self + (xW)_i) + b``, scalar e."""
+
+    def __init__(self, emb_dim, aggr="add"):
+        super().__init__()
+        if aggr != "add":
+            raise NotImplementedError("molclr_amd GCNConv supports aggr='add' (the reference's)")
+        self.emb_dim = emb_dim
+        self.aggr = aggr
+
+        self.weight = Parameter(torch.Tensor(emb_dim, emb_dim))
+        self.bias = Parameter(torch.Tensor(emb_dim))
+        self.reset_parameters()
+
+        self.edge_embedding1 = nn.Embedding(num_bond_type, 1)
+        self.edge_embedding2 = nn.Embedding(num_bond_direction, 1)
+
+        nn.init.xavier_uniform_(self.edge_embedding1.weight.data)
+        nn.init.xavier_uniform_(self.edge_embedding2.weight.data)
+
+    def reset_parameters(self):
+        stdv = math.sqrt(6.0 / (self.weight.size(-2) + self.weight.size(-1)))
+        self.weight.data.uniform_(-stdv, stdv)
+        self.bias.data.fill_(0)
+
+    def conv(self, x, graph: DeviceGraph):
+        return ops.gcn_conv(x, self.weight, self.bias, self.edge_embedding1.weight,
+                            self.edge_embedding2.weight, graph)
+
+    def forward(self, x, edge_index, edge_attr, graph: DeviceGraph | None = None):
+        if graph is None:
+            graph = DeviceGraph(edge_index, edge_attr, x.shape[0])
+        return self.conv(x, graph)
+
+
+class GCN(nn.Module):
+    """models/gcn_molclr.py:94-158."""
+
+    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean'):
+        super().__init__()
+        self.num_layer = num_layer
+        self.emb_dim = emb_dim
+        self.feat_dim = feat_dim
+        self.drop_ratio = drop_ratio
+
+        if self.num_layer < 2:
+            raise ValueError("Number of GNN layers must be greater than 1.")
+
+        self.x_embedding1 = nn.Embedding(num_atom_type, emb_dim)
+        self.x_embedding2 = nn.Embedding(num_chirality_tag, emb_dim)
+
+        nn.init.xavier_uniform_(self.x_embedding1.weight.data)
+        nn.init.xavier_uniform_(self.x_embedding2.weight.data)
+
+        self.gnns = nn.ModuleList()
+        for _ in range(num_layer):
+            self.gnns.append(GCNConv(emb_dim, aggr="add"))
+
+        self.batch_norms = nn.ModuleList()
+        for _ in range(num_layer):
+            self.batch_norms.append(nn.BatchNorm1d(emb_dim))
+
+        if pool == 'mean' or pool == 'add':
+            self.pool = pool
+        elif pool == 'max':
+            raise NotImplementedError("pool='max' is not implemented by molclr_amd (mean, add)")
+        else:
+            raise ValueError('Not defined pooling!')
+
+        self.feat_lin = nn.Linear(self.emb_dim, self.feat_dim)
+
+        self.out_lin = nn.Sequential(
+            nn.Linear(self.feat_dim, self.feat_dim),
+            nn.ReLU(inplace=True),
+            nn.Linear(self.feat_dim, self.feat_dim // 2),
+        )
+
+    def encode(self, data, graph: DeviceGraph | None = None):
+        graph = graph or device_graph(data)
+        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
+        for layer in range(self.num_layer):
+            h = self.gnns[layer].conv(h, graph)
+            last = layer == self.num_layer - 1
+            h = ops.batch_norm(h, self.batch_norms[layer], relu=not last)
+            if self.drop_ratio > 0 and self.training:
+                h = F.dropout(h, self.drop_ratio, training=True)
+        return h, graph
+
+    def forward(self, data):
+        h, graph = self.encode(data)
+        h = ops.segment_pool(h, graph, self.pool)
+        h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
+        out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
+                                  self.out_lin[2].weight, self.out_lin[2].bias)
+        return h, out

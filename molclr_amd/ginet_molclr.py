@@ -1,0 +1,117 @@
+"""GIN-E encoder + projection head — drop-in for models/ginet_molclr.py.
+
+Same class names, constructor arguments, parameter-creation order (hence the
+same seeded initialisation) and ``state_dict`` keys as the reference
+(models/ginet_molclr.py:16-117): ``x_embedding{1,2}.weight``,
+``gnns.{l}.mlp.{0,2}.{weight,bias}``, ``gnns.{l}.edge_embedding{1,2}.weight``,
+``batch_norms.{l}.*``, ``feat_lin.*``, ``out_lin.{0,2}.*``.  The forward runs
+entirely on the HIP kernels of libmolclr_hip.so (see molclr_amd.ops).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import ops
+from .data import DeviceGraph, device_graph
+
+num_atom_type = 119  # including the extra mask tokens
+num_chirality_tag = 3
+
+num_bond_type = 5  # including aromatic and self-loop edge
+num_bond_direction = 3
+
+
+class GINEConv(nn.Module):
+    """GIN-E convolution, models/ginet_molclr.py:16-47.
+
+    ``out_i = MLP( Σ_{j→i} (x_j + e_ji) + (x_i + e_self) )`` with
+    ``e = E1[bond type] + E2[bond dir]`` and the self loop (type 4, dir 0).
+    """
+
+    def __init__(self, emb_dim):
+        super().__init__()
+        self.mlp = nn.Sequential(
+            nn.Linear(emb_dim, 2 * emb_dim),
+            nn.ReLU(),
+            nn.Linear(2 * emb_dim, emb_dim),
+        )
+        self.edge_embedding1 = nn.Embedding(num_bond_type, emb_dim)
+        self.edge_embedding2 = nn.Embedding(num_bond_direction, emb_dim)
+        nn.init.xavier_uniform_(self.edge_embedding1.weight.data)
+        nn.init.xavier_uniform_(self.edge_embedding2.weight.data)
+
+    def aggregate(self, x, graph: DeviceGraph):
+        return ops.gine_aggregate(x, self.edge_embedding1.weight, self.edge_embedding2.weight,
+                                  graph)
+
+    def update(self, aggr_out):
+        return ops.gin_mlp(aggr_out, self.mlp[0].weight, self.mlp[0].bias, self.mlp[2].weight,
+                           self.mlp[2].bias)
+
+    def forward(self, x, edge_index, edge_attr, graph: DeviceGraph | None = None):
+        if graph is None:
+            graph = DeviceGraph(edge_index, edge_attr, x.shape[0])
+        return self.update(self.aggregate(x, graph))
+
+
+class GINet(nn.Module):
+    """models/ginet_molclr.py:50-117.  ``forward(data) -> (h [B, feat_dim],
+    out [B, feat_dim // 2])``."""
+
+    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean'):
+        super().__init__()
+        self.num_layer = num_layer
+        self.emb_dim = emb_dim
+        self.feat_dim = feat_dim
+        self.drop_ratio = drop_ratio
+
+        self.x_embedding1 = nn.Embedding(num_atom_type, emb_dim)
+        self.x_embedding2 = nn.Embedding(num_chirality_tag, emb_dim)
+        nn.init.xavier_uniform_(self.x_embedding1.weight.data)
+        nn.init.xavier_uniform_(self.x_embedding2.weight.data)
+
+        self.gnns = nn.ModuleList()
+        for _ in range(num_layer):
+            self.gnns.append(GINEConv(emb_dim))
+
+        self.batch_norms = nn.ModuleList()
+        for _ in range(num_layer):
+            self.batch_norms.append(nn.BatchNorm1d(emb_dim))
+
+        # The reference leaves self.pool unset for an unknown name and fails at
+        # forward time (ginet_molclr.py:83-88); fail at construction instead.
+        if pool not in ('mean', 'add', 'max'):
+            raise ValueError('Not defined pooling!')
+        if pool == 'max':
+            raise NotImplementedError("pool='max' is not implemented by molclr_amd (mean, add)")
+        self.pool = pool
+
+        self.feat_lin = nn.Linear(self.emb_dim, self.feat_dim)
+
+        self.out_lin = nn.Sequential(
+            nn.Linear(self.feat_dim, self.feat_dim),
+            nn.ReLU(inplace=True),
+            nn.Linear(self.feat_dim, self.feat_dim // 2),
+        )
+
+    def encode(self, data, graph: DeviceGraph | None = None):
+        """Node embeddings after the last layer (ginet_molclr.py:103-111)."""
+        graph = graph or device_graph(data)
+        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
+        for layer in range(self.num_layer):
+            h = self.gnns[layer].update(self.gnns[layer].aggregate(h, graph))
+            last = layer == self.num_layer - 1
+            h = ops.batch_norm(h, self.batch_norms[layer], relu=not last)
+            if self.drop_ratio > 0 and self.training:
+                h = F.dropout(h, self.drop_ratio, training=True)
+        return h, graph
+
+    def forward(self, data):
+        h, graph = self.encode(data)
+        h = ops.segment_pool(h, graph, self.pool)
+        h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
+        out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
+                                  self.out_lin[2].weight, self.out_lin[2].bias)
+        return h, out

@@ -1,0 +1,215 @@
+"""Pre-training driver — drop-in for the reference's molclr.py.
+
+Same ``MolCLR(dataset, config).train()`` loop and ``config.yaml`` schema as
+molclr.py:33-195: Adam(init_lr, weight_decay=eval(weight_decay)),
+CosineAnnealingLR(T_max = epochs - warm_up) stepped per epoch once
+``epoch >= warm_up``, ``train_loss`` / ``cosine_lr_decay`` logged every
+``log_every_n_steps``, validation every ``eval_every_n_epochs`` with the best
+weights saved to ``<log_dir>/checkpoints/model.pth`` and ``model_{epoch}.pth``
+every ``save_every_n_epochs``.  Quirks kept: ``weight_decay`` is a string
+evaluated as a number, ``load_model: None`` is the string 'None' and a missing
+checkpoint is tolerated.
+
+Differences (all additive): the optimiser is :class:`FusedAdam` (same update
+rule, one kernel); optional config keys ``world_size`` (data parallel via
+torchrun), ``seed``; the scalar writer is TensorBoard when installed,
+otherwise a JSONL file with the same tags.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+from datetime import datetime
+
+import numpy as np
+import torch
+import yaml
+from torch.optim.lr_scheduler import CosineAnnealingLR
+
+from . import distributed as mdist
+from .nt_xent import NTXentLoss
+from .ops import l2_normalize
+
+
+class _JsonlWriter:
+    def __init__(self, log_dir):
+        os.makedirs(log_dir, exist_ok=True)
+        self.log_dir = log_dir
+        self._f = open(os.path.join(log_dir, "scalars.jsonl"), "a")
+
+    def add_scalar(self, tag, value, global_step=None):
+        if torch.is_tensor(value):
+            value = float(value.detach().item())
+        self._f.write(json.dumps({"tag": tag, "value": float(value), "step": global_step}) + "\n")
+        self._f.flush()
+
+
+def _summary_writer(log_dir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+        return SummaryWriter(log_dir=log_dir)
+    except Exception:  # tensorboard not installed
+        return _JsonlWriter(log_dir)
+
+
+def _save_config_file(model_checkpoints_folder, config):
+    if not os.path.exists(model_checkpoints_folder):
+        os.makedirs(model_checkpoints_folder)
+        with open(os.path.join(model_checkpoints_folder, "config.yaml"), "w") as f:
+            yaml.safe_dump(config, f)
+
+
+class MolCLR(object):
+    def __init__(self, dataset, config):
+        self.config = config
+        self.rank, self.world, self.device = self._get_device()
+        dir_name = datetime.now().strftime('%b%d_%H-%M-%S')
+        log_dir = os.path.join(config.get('log_root', 'ckpt'), dir_name)
+        self.writer = _summary_writer(log_dir) if self.rank == 0 else None
+        self.log_dir = log_dir
+        self.dataset = dataset
+        group = torch.distributed.group.WORLD if self.world > 1 else None
+        global_batch = config['batch_size'] * self.world
+        self.nt_xent_criterion = NTXentLoss(self.device, global_batch, group=group,
+                                            **config['loss'])
+
+    def _get_device(self):
+        if not torch.cuda.is_available() or self.config.get('gpu', 'cuda:0') == 'cpu':
+            raise RuntimeError("molclr_amd pre-training runs on MI355X GPUs only")
+        if int(self.config.get('world_size', 1)) > 1 or int(os.environ.get('WORLD_SIZE', 1)) > 1:
+            rank, world, device = mdist.init()
+        else:
+            device = torch.device(self.config['gpu'])
+            torch.cuda.set_device(device)
+            rank, world = 0, 1
+        if rank == 0:
+            print("Running on:", device, "world size", world)
+        return rank, world, device
+
+    def _step(self, model, xis, xjs, n_iter):
+        ris, zis = model(xis)  # [N,C]
+        rjs, zjs = model(xjs)  # [N,C]
+        zis = l2_normalize(zis)
+        zjs = l2_normalize(zjs)
+        return self.nt_xent_criterion(zis, zjs)
+
+    def build_model(self):
+        if self.config['model_type'] == 'gin':
+            from .ginet_molclr import GINet
+            model = GINet(**self.config["model"]).to(self.device)
+        elif self.config['model_type'] == 'gcn':
+            from .gcn_molclr import GCN
+            model = GCN(**self.config["model"]).to(self.device)
+        else:
+            raise ValueError('Undefined GNN model.')
+        return self._load_pre_trained_weights(model)
+
+    def build_optimizer(self, model):
+        from .optim import FusedAdam
+        optimizer = FusedAdam(model.parameters(), self.config['init_lr'],
+                              weight_decay=float(eval(str(self.config['weight_decay']))))
+        if self.world > 1:
+            mdist.broadcast_params(optimizer.flat)
+        scheduler = CosineAnnealingLR(optimizer, T_max=self.config['epochs'] - self.config['warm_up'],
+                                      eta_min=0, last_epoch=-1)
+        return optimizer, scheduler
+
+    def train_step(self, model, optimizer, xis, xjs, n_iter):
+        optimizer.zero_grad()
+        xis = xis.to(self.device, non_blocking=True)
+        xjs = xjs.to(self.device, non_blocking=True)
+        loss = self._step(model, xis, xjs, n_iter)
+        loss.backward()
+        if self.world > 1:
+            mdist.allreduce_grads(optimizer.flat_grad)
+        optimizer.step()
+        return loss
+
+    def train(self):
+        train_loader, valid_loader = self.dataset.get_data_loaders()
+        model = self.build_model()
+        if self.rank == 0:
+            print(model)
+        optimizer, scheduler = self.build_optimizer(model)
+
+        model_checkpoints_folder = os.path.join(self.log_dir, 'checkpoints')
+        if self.rank == 0:
+            _save_config_file(model_checkpoints_folder, self.config)
+
+        n_iter = 0
+        valid_n_iter = 0
+        best_valid_loss = np.inf
+        for epoch_counter in range(self.config['epochs']):
+            bn = 0
+            for bn, (xis, xjs) in enumerate(train_loader):
+                loss = self.train_step(model, optimizer, xis, xjs, n_iter)
+                if n_iter % self.config['log_every_n_steps'] == 0 and self.rank == 0:
+                    self.writer.add_scalar('train_loss', loss, global_step=n_iter)
+                    self.writer.add_scalar('cosine_lr_decay', scheduler.get_last_lr()[0],
+                                           global_step=n_iter)
+                    print(epoch_counter, bn, loss.item())
+                n_iter += 1
+
+            if epoch_counter % self.config['eval_every_n_epochs'] == 0:
+                valid_loss = self._validate(model, valid_loader)
+                if self.rank == 0:
+                    print(epoch_counter, bn, valid_loss, '(validation)')
+                    if valid_loss < best_valid_loss:
+                        best_valid_loss = valid_loss
+                        torch.save(model.state_dict(),
+                                   os.path.join(model_checkpoints_folder, 'model.pth'))
+                    self.writer.add_scalar('validation_loss', valid_loss, global_step=valid_n_iter)
+                valid_n_iter += 1
+
+            if (epoch_counter + 1) % self.config['save_every_n_epochs'] == 0 and self.rank == 0:
+                torch.save(model.state_dict(),
+                           os.path.join(model_checkpoints_folder, f'model_{epoch_counter}.pth'))
+
+            if epoch_counter >= self.config['warm_up']:
+                scheduler.step()
+        return model
+
+    def _load_pre_trained_weights(self, model):
+        try:
+            checkpoints_folder = os.path.join('./ckpt', str(self.config['load_model']), 'checkpoints')
+            state_dict = torch.load(os.path.join(checkpoints_folder, 'model.pth'),
+                                    map_location=self.device, weights_only=True)
+            model.load_state_dict(state_dict)
+            print("Loaded pre-trained model with success.")
+        except FileNotFoundError:
+            print("Pre-trained weights not found. Training from scratch.")
+        return model
+
+    def _validate(self, model, valid_loader):
+        with torch.no_grad():
+            model.eval()
+            valid_loss = 0.0
+            counter = 0
+            for (xis, xjs) in valid_loader:
+                xis = xis.to(self.device)
+                xjs = xjs.to(self.device)
+                loss = self._step(model, xis, xjs, counter)
+                valid_loss += loss.item()
+                counter += 1
+            valid_loss /= max(counter, 1)
+        model.train()
+        return valid_loss
+
+
+def main(config_path: str = "config.yaml"):
+    with open(config_path, "r") as f:
+        config = yaml.safe_load(f)
+    print(config)
+    if config['aug'] != 'node':
+        raise ValueError("only aug: node (dataset/dataset.py) is provided; "
+                         "subgraph / mix augmentations are out of this build's scope")
+    from .dataset import MoleculeDatasetWrapper
+    dataset = MoleculeDatasetWrapper(config['batch_size'], **config['dataset'])
+    molclr = MolCLR(dataset, config)
+    molclr.train()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "config.yaml")

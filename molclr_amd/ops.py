@@ -1,0 +1,520 @@
+"""Autograd functions over the C ABI (include/molclr.h).
+
+Each function is one seam of the reference pre-training step, with an
+explicit backward that calls the matching HIP kernel:
+
+=====================  ==========================================================
+function               reference (CameronDiao/MolCLR)
+=====================  ==========================================================
+``atom_embed``         models/ginet_molclr.py:103 (x_embedding1 + x_embedding2)
+``gine_aggregate``     models/ginet_molclr.py:29-44 + PyG propagate(aggr='add')
+``gin_mlp``            models/ginet_molclr.py:19-23,46-47 (GINEConv.update)
+``linear``             nn.Linear (feat_lin, ginet_molclr.py:90)
+``projection_head``    out_lin: Linear-ReLU-Linear (ginet_molclr.py:92-96)
+``batch_norm``         ginet_molclr.py:107-111 (BatchNorm1d + ReLU + dropout 0)
+``segment_pool``       ginet_molclr.py:113 (global_mean_pool / global_add_pool)
+``gcn_conv``           models/gcn_molclr.py:62-88 (x @ W, propagate, + bias)
+``l2_normalize``       molclr.py:63-64 (F.normalize)
+``nt_xent``            utils/nt_xent.py:47-65 (NTXentLoss.forward)
+=====================  ==========================================================
+
+All tensors must be CUDA (HIP) fp32 and contiguous; there is no CPU path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
+from .data import DeviceGraph
+
+
+def _check(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError("molclr_amd kernels run on the GPU only; got a %s tensor" % t.device)
+
+
+def _ws(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def _c(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return _lib.stream_of(t.device)
+
+
+class KernelTimer:
+    """Optional HIP-event bracketing of selected launches (used by bench.py).
+
+    Events are recorded on torch's current stream, which is the stream every
+    entry point is launched on, so elapsed times bracket exactly one kernel
+    (plus the event overhead)."""
+
+    def __init__(self):
+        self.records = []  # (kind, start_event, end_event, work)
+
+    def begin(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def end(self, kind, e0, work):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.records.append((kind, e0, e1, work))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for kind, e0, e1, work in self.records:
+            d = out.setdefault(kind, {"launches": 0, "ms": 0.0, "work": 0.0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["work"] += work
+        return out
+
+
+_TIMER: KernelTimer | None = None
+
+
+def set_kernel_timer(timer: KernelTimer | None) -> None:
+    global _TIMER
+    _TIMER = timer
+
+
+# ---------------------------------------------------------------------------
+# GEMM helpers
+# ---------------------------------------------------------------------------
+def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
+         out=None):
+    """C[M,N] = op(A) op(B) (+ epilogue), see molclr_gemm_f32."""
+    dev = A.device
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=dev)
+    ws_bytes = _lib.query("molclr_gemm_f32_workspace_bytes", M, N, K)
+    ws = _ws(ws_bytes, dev) if ws_bytes else None
+    t0 = _TIMER.begin() if _TIMER is not None else None
+    _lib.call("molclr_gemm_f32", A.data_ptr(), B.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
+              out.stride(0), int(a_kmajor), int(b_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A))
+    if t0 is not None:
+        _TIMER.end("gemm_f32", t0, 2.0 * M * N * K)
+    return out
+
+
+def linear_fwd(x, W, b, relu=False):
+    """y = x W^T + b (nn.Linear), optional fused ReLU."""
+    M, K = x.shape
+    N = W.shape[0]
+    epi = EPI_BIAS_RELU if relu else EPI_BIAS
+    return gemm(x, W, M, N, K, K, K, False, False, epi, bias=b)
+
+
+def colsum(x):
+    rows, cols = x.shape
+    ws_bytes = _lib.query("molclr_colsum_f32_workspace_bytes", rows, cols)
+    ws = _ws(ws_bytes, x.device)
+    out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    _lib.call("molclr_colsum_f32", x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0),
+              ws.data_ptr(), ws_bytes, _stream(x))
+    return out
+
+
+def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=None):
+    """Backward of y = x W^T + b.  Returns (dx, dW, db)."""
+    M, K = x.shape
+    N = W.shape[0]
+    dx = dW = db = None
+    if need_w:
+        # dW[N,K] = dy^T x : A = dy (K-major, lda=N), B = x (K-major, ldb=K)
+        dW = gemm(dy, x, N, K, M, N, K, True, True)
+    if need_b:
+        db = colsum(dy)
+    if need_x:
+        # dx[M,K] = dy W : B(k=n, j) = W[n, j] (K-major, ldb=K)
+        epi = EPI_RELU_MASK if relu_mask_src is not None else EPI_NONE
+        dx = gemm(dy, W, M, K, N, N, K, False, True, epi, aux=relu_mask_src)
+    return dx, dW, db
+
+
+def gine_aggregate_bytes(N: int, D: int, E: int) -> int:
+    """Compulsory HBM bytes of one molclr_gine_aggregate_fwd launch: read x and
+    write the output once (2*N*D*4), rowptr (4(N+1)), col (4E), ecode (E);
+    the 5 x D / 3 x D edge tables are cache-resident."""
+    return 2 * N * D * 4 + 4 * (N + 1) + 5 * E
+
+
+# ---------------------------------------------------------------------------
+# autograd functions
+# ---------------------------------------------------------------------------
+class _AtomEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_idx, X1, X2):
+        _check(x_idx, X1, X2)
+        x_idx = _c(x_idx.to(torch.long))
+        N = x_idx.shape[0]
+        D = X1.shape[1]
+        h = torch.empty(N, D, dtype=torch.float32, device=X1.device)
+        _lib.call("molclr_atom_embed_fwd", x_idx.data_ptr(), X1.data_ptr(), X2.data_ptr(),
+                  h.data_ptr(), N, D, X1.shape[0], X2.shape[0], _stream(X1))
+        ctx.save_for_backward(x_idx)
+        ctx.shapes = (X1.shape[0], X2.shape[0], D)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        (x_idx,) = ctx.saved_tensors
+        n1, n2, D = ctx.shapes
+        dh = _c(dh)
+        N = x_idx.shape[0]
+        dX1 = torch.empty(n1, D, dtype=torch.float32, device=dh.device)
+        dX2 = torch.empty(n2, D, dtype=torch.float32, device=dh.device)
+        ws_bytes = _lib.query("molclr_atom_embed_bwd_workspace_bytes", N, D, n1, n2)
+        ws = _ws(ws_bytes, dh.device)
+        _lib.call("molclr_atom_embed_bwd", x_idx.data_ptr(), dh.data_ptr(), dX1.data_ptr(),
+                  dX2.data_ptr(), N, D, n1, n2, ws.data_ptr(), ws_bytes, _stream(dh))
+        return None, dX1, dX2
+
+
+class _GINEAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, E1, E2, graph: DeviceGraph):
+        _check(h, E1, E2)
+        h = _c(h)
+        N, D = h.shape
+        out = torch.empty_like(h)
+        t0 = _TIMER.begin() if _TIMER is not None else None
+        _lib.call("molclr_gine_aggregate_fwd", h.data_ptr(), graph.rowptr.data_ptr(),
+                  graph.col.data_ptr(), graph.ecode.data_ptr(), E1.data_ptr(), E2.data_ptr(),
+                  out.data_ptr(), N, D, _stream(h))
+        if t0 is not None:
+            _TIMER.end("gine_aggregate_fwd", t0, gine_aggregate_bytes(N, D, graph.num_edges))
+        ctx.graph = graph
+        ctx.shapes = (N, D, E1.shape[0], E2.shape[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        N, D, n1, n2 = ctx.shapes
+        graph = ctx.graph
+        need_x, need_e1, need_e2 = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        dx = torch.empty_like(g) if need_x else None
+        dE1 = torch.empty(n1, D, dtype=torch.float32, device=g.device) if need_e1 else None
+        dE2 = torch.empty(n2, D, dtype=torch.float32, device=g.device) if need_e2 else None
+        ws_bytes = _lib.query("molclr_gine_aggregate_bwd_workspace_bytes", N, D)
+        ws = _ws(ws_bytes, g.device)
+        _lib.call("molclr_gine_aggregate_bwd", g.data_ptr(), graph.rowptr_t.data_ptr(),
+                  graph.col_t.data_ptr(), graph.ecount.data_ptr(), _lib.ptr(dx), _lib.ptr(dE1),
+                  _lib.ptr(dE2), N, D, ws.data_ptr(), ws_bytes, _stream(g))
+        return dx, dE1, dE2, None
+
+
+class _MLP(torch.autograd.Function):
+    """Linear -> ReLU -> Linear with the ReLU fused into the first GEMM's
+    epilogue (forward) and into the dZ1 GEMM's epilogue (backward)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2):
+        _check(x, W1, b1, W2, b2)
+        x = _c(x)
+        a1 = linear_fwd(x, W1, b1, relu=True)
+        z = linear_fwd(a1, W2, b2, relu=False)
+        ctx.save_for_backward(x, W1, W2, a1)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, W1, W2, a1 = ctx.saved_tensors
+        dz = _c(dz)
+        need = ctx.needs_input_grad
+        # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
+        dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],
+                                   relu_mask_src=a1)
+        dx, dW1, db1 = linear_bwd(dz1, x, W1, need_x=need[0], need_w=need[1], need_b=need[2])
+        return dx, dW1, db1, dW2, db2
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b):
+        _check(x, W, b)
+        x = _c(x)
+        ctx.save_for_backward(x, W)
+        return linear_fwd(x, W, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dx, dW, db = linear_bwd(_c(dy), x, W, need[0], need[1], need[2])
+        return dx, dW, db
+
+
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, gamma, beta, running_mean, running_var, training, momentum, eps, relu):
+        _check(z, gamma, beta)
+        z = _c(z)
+        N, D = z.shape
+        y = torch.empty_like(z)
+        save_mean = torch.empty(D, dtype=torch.float32, device=z.device)
+        save_invstd = torch.empty(D, dtype=torch.float32, device=z.device)
+        ws_bytes = _lib.query("molclr_batchnorm_workspace_bytes", N, D)
+        ws = _ws(ws_bytes, z.device)
+        _lib.call("molclr_batchnorm_fwd", z.data_ptr(), _lib.ptr(gamma), _lib.ptr(beta),
+                  _lib.ptr(running_mean), _lib.ptr(running_var), y.data_ptr(),
+                  save_mean.data_ptr(), save_invstd.data_ptr(), N, D, float(momentum),
+                  float(eps), int(bool(training)), int(bool(relu)), ws.data_ptr(), ws_bytes,
+                  _stream(z))
+        ctx.save_for_backward(z, gamma, beta, save_mean, save_invstd)
+        ctx.relu = bool(relu)
+        ctx.training = bool(training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        if not ctx.training:
+            raise NotImplementedError(
+                "molclr_amd: backward through eval-mode BatchNorm is not supported "
+                "(the reference only evaluates under torch.no_grad, molclr.py:162)")
+        z, gamma, beta, save_mean, save_invstd = ctx.saved_tensors
+        dy = _c(dy)
+        N, D = z.shape
+        dz = torch.empty_like(z)
+        dgamma = torch.empty(D, dtype=torch.float32, device=z.device)
+        dbeta = torch.empty(D, dtype=torch.float32, device=z.device)
+        ws_bytes = _lib.query("molclr_batchnorm_workspace_bytes", N, D)
+        ws = _ws(ws_bytes, z.device)
+        _lib.call("molclr_batchnorm_bwd", dy.data_ptr(), z.data_ptr(), _lib.ptr(gamma),
+                  _lib.ptr(beta), save_mean.data_ptr(), save_invstd.data_ptr(), dz.data_ptr(),
+                  dgamma.data_ptr(), dbeta.data_ptr(), N, D, int(ctx.relu), ws.data_ptr(),
+                  ws_bytes, _stream(z))
+        return dz, dgamma, dbeta, None, None, None, None, None, None
+
+
+POOL_MODES = {"mean": 0, "add": 1}
+
+
+class _SegmentPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, graph: DeviceGraph, mode: int):
+        _check(h)
+        h = _c(h)
+        N, D = h.shape
+        G = graph.num_graphs
+        out = torch.empty(G, D, dtype=torch.float32, device=h.device)
+        _lib.call("molclr_segment_pool_fwd", h.data_ptr(), graph.graph_ptr.data_ptr(),
+                  out.data_ptr(), G, D, mode, _stream(h))
+        ctx.graph, ctx.mode, ctx.N = graph, mode, N
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = _c(dout)
+        G, D = dout.shape
+        dh = torch.empty(ctx.N, D, dtype=torch.float32, device=dout.device)
+        _lib.call("molclr_segment_pool_bwd", dout.data_ptr(), ctx.graph.graph_ptr.data_ptr(),
+                  dh.data_ptr(), ctx.N, G, D, ctx.mode, _stream(dout))
+        return dh, None, None
+
+
+class _GCNConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, bias, E1, E2, graph: DeviceGraph):
+        _check(x, W, bias, E1, E2)
+        x = _c(x)
+        N, Din = x.shape
+        Dout = W.shape[1]
+        # xW with W stored [in, out] (gcn_molclr.py:45,76): B K-major, ldb = Dout
+        xw = gemm(x, W, N, Dout, Din, Din, Dout, False, True)
+        out = torch.empty(N, Dout, dtype=torch.float32, device=x.device)
+        _lib.call("molclr_gcn_aggregate_fwd", xw.data_ptr(), graph.rowptr.data_ptr(),
+                  graph.col.data_ptr(), graph.ecode.data_ptr(), E1.data_ptr(), E2.data_ptr(),
+                  bias.data_ptr(), out.data_ptr(), N, Dout, _stream(x))
+        ctx.save_for_backward(x, W)
+        ctx.graph = graph
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        g = _c(g)
+        N, Din = x.shape
+        Dout = W.shape[1]
+        need = ctx.needs_input_grad
+        dxw = torch.empty(N, Dout, dtype=torch.float32, device=g.device)
+        dE1 = torch.empty(5, 1, dtype=torch.float32, device=g.device) if need[3] else None
+        dE2 = torch.empty(3, 1, dtype=torch.float32, device=g.device) if need[4] else None
+        db = torch.empty(Dout, dtype=torch.float32, device=g.device) if need[2] else None
+        ws_bytes = _lib.query("molclr_gcn_aggregate_bwd_workspace_bytes", N, Dout)
+        ws = _ws(ws_bytes, g.device)
+        _lib.call("molclr_gcn_aggregate_bwd", g.data_ptr(), ctx.graph.rowptr_t.data_ptr(),
+                  ctx.graph.col_t.data_ptr(), ctx.graph.ecount.data_ptr(), dxw.data_ptr(),
+                  _lib.ptr(dE1), _lib.ptr(dE2), _lib.ptr(db), N, Dout, ws.data_ptr(), ws_bytes,
+                  _stream(g))
+        dx = dW = None
+        if need[1]:
+            # dW[Din,Dout] = x^T dxw
+            dW = gemm(x, dxw, Din, Dout, N, Din, Dout, True, True)
+        if need[0]:
+            # dx[N,Din] = dxw W^T : B(k=o, n=i) = W[i, o] (not K-major, ldb = Dout)
+            dx = gemm(dxw, W, N, Din, Dout, Dout, Dout, False, False)
+        return dx, dW, db, dE1, dE2, None
+
+
+class _L2Normalize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, eps):
+        _check(z)
+        z = _c(z)
+        rows, D = z.shape
+        y = torch.empty_like(z)
+        norm = torch.empty(rows, dtype=torch.float32, device=z.device)
+        _lib.call("molclr_l2norm_fwd", z.data_ptr(), y.data_ptr(), norm.data_ptr(), rows, D,
+                  float(eps), _stream(z))
+        ctx.save_for_backward(y, norm)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, norm = ctx.saved_tensors
+        dy = _c(dy)
+        rows, D = y.shape
+        dz = torch.empty_like(y)
+        _lib.call("molclr_l2norm_bwd", dy.data_ptr(), y.data_ptr(), norm.data_ptr(), dz.data_ptr(),
+                  rows, D, float(ctx.eps), _stream(dy))
+        return dz, None
+
+
+class _NTXent(torch.autograd.Function):
+    """NT-Xent over R = [zj; zi].  With a ``group`` (torch.distributed) the
+    batch is the global one: rows are this rank's, columns are gathered."""
+
+    @staticmethod
+    def forward(ctx, zis, zjs, batch_size, temperature, cosine, group):
+        _check(zis, zjs)
+        dev = zis.device
+        Bl, C = zis.shape
+        R = torch.cat([_c(zjs), _c(zis)], 0)
+        n = R.shape[0]
+        rhat = torch.empty_like(R)
+        norm = torch.empty(n, dtype=torch.float32, device=dev)
+        st = _lib.stream_of(dev)
+        _lib.call("molclr_ntxent_prep", R.data_ptr(), rhat.data_ptr(), norm.data_ptr(), n, C,
+                  int(cosine), st)
+        if group is None:
+            B = Bl
+            if batch_size != B:
+                raise ValueError(f"NTXentLoss built for batch_size={batch_size} got {B} rows "
+                                 "(the reference requires full batches, dataset.py:179)")
+            cols = rhat
+            gidx = torch.arange(n, dtype=torch.int32, device=dev)
+        else:
+            import torch.distributed as dist
+            world = dist.get_world_size(group)
+            rank = dist.get_rank(group)
+            B = Bl * world
+            if batch_size != B:
+                raise ValueError(f"global batch {B} != NTXentLoss batch_size {batch_size}")
+            cols = torch.empty(2 * B, C, dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(cols[:B], rhat[:Bl].contiguous(), group=group)
+            dist.all_gather_into_tensor(cols[B:], rhat[Bl:].contiguous(), group=group)
+            base = torch.arange(Bl, dtype=torch.int32, device=dev) + rank * Bl
+            gidx = torch.cat([base, base + B])
+        lse = torch.empty(n, dtype=torch.float32, device=dev)
+        loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
+        ws_bytes = _lib.query("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+        ws = _ws(ws_bytes, dev)
+        _lib.call("molclr_ntxent_fwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n, 2 * B,
+                  C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(), ws.data_ptr(),
+                  ws_bytes, st)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        _lib.call("molclr_sum_f32", loss_rows.data_ptr(), loss.data_ptr(), n, st)
+        if group is None:
+            lse_cols = lse
+        else:
+            lse_cols = torch.empty(2 * B, dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(lse_cols[:B], lse[:Bl].contiguous(), group=group)
+            dist.all_gather_into_tensor(lse_cols[B:], lse[Bl:].contiguous(), group=group)
+            dist.all_reduce(loss, group=group)
+        ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols)
+        ctx.meta = (B, Bl, C, float(temperature), int(cosine))
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        rhat, norm, cols, gidx, lse_cols = ctx.saved_tensors
+        B, Bl, C, T, cosine = ctx.meta
+        dev = rhat.device
+        n = rhat.shape[0]
+        gloss = gloss.to(torch.float32).contiguous()
+        st = _lib.stream_of(dev)
+        drhat = torch.empty_like(rhat)
+        ws_bytes = _lib.query("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+        ws = _ws(ws_bytes, dev)
+        _lib.call("molclr_ntxent_bwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                  lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T, drhat.data_ptr(),
+                  ws.data_ptr(), ws_bytes, st)
+        dR = torch.empty_like(rhat)
+        _lib.call("molclr_ntxent_prep_bwd", drhat.data_ptr(), rhat.data_ptr(), norm.data_ptr(),
+                  dR.data_ptr(), n, C, cosine, st)
+        return dR[Bl:], dR[:Bl], None, None, None, None
+
+
+# public functional API -------------------------------------------------------
+def atom_embed(x_idx, X1, X2):
+    return _AtomEmbed.apply(x_idx, X1, X2)
+
+
+def gine_aggregate(h, E1, E2, graph):
+    return _GINEAggregate.apply(h, E1, E2, graph)
+
+
+def gin_mlp(x, W1, b1, W2, b2):
+    return _MLP.apply(x, W1, b1, W2, b2)
+
+
+projection_head = gin_mlp
+
+
+def linear(x, W, b):
+    return _Linear.apply(x, W, b)
+
+
+def batch_norm(z, bn: torch.nn.BatchNorm1d, relu: bool):
+    training = bn.training or not bn.track_running_stats
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    momentum = 0.0 if bn.momentum is None else bn.momentum
+    if bn.momentum is None and bn.training and bn.track_running_stats:
+        momentum = 1.0 / float(bn.num_batches_tracked.item())  # cumulative average (torch)
+    return _BatchNorm.apply(z, bn.weight, bn.bias,
+                            bn.running_mean if bn.track_running_stats else None,
+                            bn.running_var if bn.track_running_stats else None,
+                            training, momentum, bn.eps, relu)
+
+
+def segment_pool(h, graph, mode: str):
+    if mode not in POOL_MODES:
+        raise ValueError(f"pool '{mode}' is not supported by molclr_amd (mean, add)")
+    return _SegmentPool.apply(h, graph, POOL_MODES[mode])
+
+
+def gcn_conv(x, W, bias, E1, E2, graph):
+    return _GCNConv.apply(x, W, bias, E1, E2, graph)
+
+
+def l2_normalize(z, eps: float = 1e-12):
+    return _L2Normalize.apply(z, eps)
+
+
+def nt_xent(zis, zjs, batch_size, temperature, use_cosine_similarity=True, group=None):
+    return _NTXent.apply(zis, zjs, batch_size, temperature, bool(use_cosine_similarity), group)

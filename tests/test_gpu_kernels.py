@@ -1,0 +1,342 @@
+"""Per-kernel parity of the HIP path (through the C ABI) against the oracle.
+
+Bar: integer outputs bit-exact; the GINE aggregation bit-exact (same
+accumulation order as the reference CPU path); everything else fp32
+norm-wise relative error <= 1e-5 (SURVEY.md §8c tolerance definition)."""
+import numpy as np
+import pytest
+import torch
+
+from molclr_amd import ops
+from molclr_amd.data import DeviceGraph
+from molclr_amd.dataset import SyntheticPairBatches
+from oracle import ntxent_math
+from oracle.graph_ref import graph_build
+from oracle.reference_cpu import (RefNTXentLoss, add_self_loops, global_add_pool,
+                                  global_mean_pool, propagate_add)
+
+from .conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(b).detach().double().cpu()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-30)
+
+
+def batch(B, seed=0, shape="uniform"):
+    return SyntheticPairBatches(B, seed=seed, shape=shape).next()[0]
+
+
+def dgraph(b, dev):
+    return DeviceGraph(b.edge_index.to(dev), b.edge_attr.to(dev), b.x.shape[0], b.batch.to(dev),
+                       b.num_graphs)
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("B", [1, 7, 64, 512])
+def test_graph_build_bit_exact(dev, B):
+    b = batch(B, seed=B)
+    g = dgraph(b, dev)
+    g.check()
+    ref = graph_build(b.edge_index.numpy(), b.edge_attr.numpy(), b.batch.numpy(), b.x.shape[0],
+                      b.num_graphs)
+    E = b.edge_index.shape[1]
+    got = dict(rowptr=g.rowptr, col=g.col[:E], ecode=g.ecode[:E], rowptr_t=g.rowptr_t,
+               col_t=g.col_t[:E], ecount=g.ecount[: 8 * b.x.shape[0]], graph_ptr=g.graph_ptr)
+    for k, v in got.items():
+        assert np.array_equal(v.cpu().numpy(), ref[k]), k
+
+
+def test_graph_build_edge_cases(dev):
+    # no edges at all, isolated atoms, single-atom graphs
+    x = torch.tensor([[5, 0], [6, 0], [7, 0]])
+    ei = torch.zeros(2, 0, dtype=torch.long)
+    ea = torch.zeros(0, 2, dtype=torch.long)
+    batch_v = torch.tensor([0, 1, 1])
+    g = DeviceGraph(ei.to(dev), ea.to(dev), 3, batch_v.to(dev), 2)
+    g.check()
+    assert g.rowptr.tolist() == [0, 0, 0, 0]
+    assert g.graph_ptr.tolist() == [0, 1, 3]
+    ec = g.ecount.view(-1, 8).cpu()
+    assert ec[:, 4].tolist() == [1, 1, 1] and ec[:, 5].tolist() == [1, 1, 1]
+    # out-of-range indices are flagged, clamped, never read out of bounds
+    bad = torch.tensor([[0, 9], [1, 0]])
+    g = DeviceGraph(bad.to(dev), torch.tensor([[0, 0], [7, 0]]).to(dev), 3, batch_v.to(dev), 2)
+    with pytest.raises(ValueError, match="edge_index out of range"):
+        g.check()
+    g = DeviceGraph(ei.to(dev), ea.to(dev), 3, torch.tensor([1, 0, 1]).to(dev), 2)
+    with pytest.raises(ValueError, match="batch"):
+        g.check()
+
+
+# ---------------------------------------------------------------------------
+def test_atom_embed(dev):
+    b = batch(64, 1)
+    torch.manual_seed(0)
+    X1 = torch.randn(119, 300)
+    X2 = torch.randn(3, 300)
+    ref = X1[b.x[:, 0]] + X2[b.x[:, 1]]
+    X1d = X1.to(dev).requires_grad_(True)
+    X2d = X2.to(dev).requires_grad_(True)
+    h = ops.atom_embed(b.x.to(dev), X1d, X2d)
+    assert torch.equal(h.cpu(), ref)
+    g = torch.randn_like(ref)
+    h.backward(g.to(dev))
+    X1c = X1.clone().requires_grad_(True)
+    X2c = X2.clone().requires_grad_(True)
+    (X1c[b.x[:, 0]] + X2c[b.x[:, 1]]).backward(g)
+    assert rel(X1d.grad, X1c.grad) < TOL and rel(X2d.grad, X2c.grad) < TOL
+
+
+@pytest.mark.parametrize("B,D", [(64, 128), (512, 300), (16, 512)])
+def test_gine_aggregate_matches_reference_order(dev, B, D):
+    b = batch(B, 2)
+    N = b.x.shape[0]
+    torch.manual_seed(1)
+    h = torch.randn(N, D)
+    E1 = torch.randn(5, D)
+    E2 = torch.randn(3, D)
+    # oracle: PyG propagate over add_self_loops + edge embeddings (ginet_molclr.py:29-44)
+    ei = add_self_loops(b.edge_index, N)
+    sl = torch.zeros(N, 2, dtype=torch.long)
+    sl[:, 0] = 4
+    ea = torch.cat([b.edge_attr, sl], 0)
+    e = E1[ea[:, 0]] + E2[ea[:, 1]]
+    hr = h.clone().requires_grad_(True)
+    E1r = E1.clone().requires_grad_(True)
+    E2r = E2.clone().requires_grad_(True)
+    er = E1r[ea[:, 0]] + E2r[ea[:, 1]]
+    ref = propagate_add(hr, ei, N, lambda xj: xj + er)
+    g = dgraph(b, dev)
+    hd = h.to(dev).requires_grad_(True)
+    E1d = E1.to(dev).requires_grad_(True)
+    E2d = E2.to(dev).requires_grad_(True)
+    out = ops.gine_aggregate(hd, E1d, E2d, g)
+    assert torch.equal(out.detach().cpu(), ref.detach()), "GINE aggregation not bit-exact"
+    go = torch.randn(N, D)
+    ref.backward(go)
+    out.backward(go.to(dev))
+    assert rel(hd.grad, hr.grad) < TOL
+    assert rel(E1d.grad, E1r.grad) < TOL and rel(E2d.grad, E2r.grad) < TOL
+
+
+def test_gcn_conv(dev):
+    from oracle.reference_cpu import RefGCNConv
+    b = batch(64, 3)
+    N, D = b.x.shape[0], 128
+    torch.manual_seed(2)
+    conv = RefGCNConv(D)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    h = torch.randn(N, D, requires_grad=True)
+    ref = conv(h, b.edge_index, b.edge_attr)
+    go = torch.randn(N, D)
+    ref.backward(go)
+    W = conv.weight.detach().to(dev).requires_grad_(True)
+    bias = conv.bias.detach().to(dev).requires_grad_(True)
+    E1 = conv.edge_embedding1.weight.detach().to(dev).requires_grad_(True)
+    E2 = conv.edge_embedding2.weight.detach().to(dev).requires_grad_(True)
+    hd = h.detach().to(dev).requires_grad_(True)
+    out = ops.gcn_conv(hd, W, bias, E1, E2, dgraph(b, dev))
+    assert rel(out, ref) < TOL
+    out.backward(go.to(dev))
+    assert rel(hd.grad, h.grad) < TOL
+    assert rel(W.grad, conv.weight.grad) < TOL
+    assert rel(bias.grad, conv.bias.grad) < TOL
+    assert rel(E1.grad, conv.edge_embedding1.weight.grad) < TOL
+    assert rel(E2.grad, conv.edge_embedding2.weight.grad) < TOL
+
+
+# ---------------------------------------------------------------------------
+GEMM_SHAPES = [
+    (1000, 600, 300), (1000, 300, 600), (300, 600, 2000), (600, 300, 15700), (64, 64, 8),
+    (33, 68, 12), (512, 512, 300), (512, 256, 512), (1024, 1024, 256),
+]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_layouts(dev, M, N, K, ak, bk):
+    torch.manual_seed(M + N + K)
+    Am = torch.randn(M, K, dtype=torch.float64)
+    Bm = torch.randn(K, N, dtype=torch.float64)
+    ref = Am @ Bm
+    A = (Am.t() if ak else Am).contiguous().float().to(dev)
+    Bt = (Bm if bk else Bm.t()).contiguous().float().to(dev)
+    lda = M if ak else K
+    ldb = N if bk else K
+    out = ops.gemm(A, Bt, M, N, K, lda, ldb, ak, bk)
+    assert rel(out, ref) < TOL
+
+
+def test_gemm_epilogues(dev):
+    from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK
+    torch.manual_seed(0)
+    M, N, K = 777, 600, 300
+    x = torch.randn(M, K)
+    W = torch.randn(N, K)
+    b = torch.randn(N)
+    aux = torch.randn(M, N)
+    y = x.double() @ W.double().t()
+    xd, Wd, bd, auxd = (t.to(dev) for t in (x, W, b, aux))
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS, bias=bd), y + b.double()) < TOL
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS_RELU, bias=bd),
+               (y + b.double()).clamp(min=0)) < TOL
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_RELU_MASK, aux=auxd),
+               y * (aux > 0).double()) < TOL
+
+
+def test_colsum(dev):
+    x = torch.randn(15713, 600)
+    assert rel(ops.colsum(x.to(dev)), x.double().sum(0)) < TOL
+
+
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("rows,D", [(15711, 300), (1950, 128), (7, 512)])
+def test_batchnorm_train(dev, relu, rows, D):
+    torch.manual_seed(rows)
+    z = torch.randn(rows, D) * 3 + 1.5
+    bn_ref = torch.nn.BatchNorm1d(D)
+    with torch.no_grad():
+        bn_ref.weight.uniform_(0.5, 1.5)
+        bn_ref.bias.uniform_(-0.5, 0.5)
+    bn = torch.nn.BatchNorm1d(D).to(dev)
+    bn.load_state_dict(bn_ref.state_dict())
+    zr = z.clone().requires_grad_(True)
+    yr = bn_ref(zr)
+    if relu:
+        yr = torch.relu(yr)
+    zd = z.to(dev).requires_grad_(True)
+    yd = ops.batch_norm(zd, bn, relu)
+    assert rel(yd, yr) < TOL
+    assert rel(bn.running_mean, bn_ref.running_mean) < TOL
+    assert rel(bn.running_var, bn_ref.running_var) < TOL
+    assert int(bn.num_batches_tracked) == 1
+    g = torch.randn(rows, D)
+    yr.backward(g)
+    yd.backward(g.to(dev))
+    assert rel(zd.grad, zr.grad) < TOL
+    assert rel(bn.weight.grad, bn_ref.weight.grad) < TOL
+    assert rel(bn.bias.grad, bn_ref.bias.grad) < TOL
+
+
+def test_batchnorm_eval(dev):
+    D = 300
+    bn_ref = torch.nn.BatchNorm1d(D)
+    with torch.no_grad():
+        bn_ref.running_mean.uniform_(-1, 1)
+        bn_ref.running_var.uniform_(0.5, 2)
+    bn_ref.eval()
+    bn = torch.nn.BatchNorm1d(D).to(dev)
+    bn.load_state_dict(bn_ref.state_dict())
+    bn.eval()
+    z = torch.randn(1000, D)
+    with torch.no_grad():
+        assert rel(ops.batch_norm(z.to(dev), bn, True), torch.relu(bn_ref(z))) < TOL
+
+
+@pytest.mark.parametrize("mode", ["mean", "add"])
+def test_segment_pool(dev, mode):
+    b = batch(512, 4)
+    N, D = b.x.shape[0], 300
+    h = torch.randn(N, D, requires_grad=True)
+    ref = (global_mean_pool if mode == "mean" else global_add_pool)(h, b.batch)
+    hd = h.detach().to(dev).requires_grad_(True)
+    out = ops.segment_pool(hd, dgraph(b, dev), mode)
+    assert rel(out, ref) < TOL
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    out.backward(g.to(dev))
+    assert rel(hd.grad, h.grad) < TOL
+
+
+def test_l2_normalize(dev):
+    z = torch.randn(512, 256, requires_grad=True)
+    ref = torch.nn.functional.normalize(z, dim=1)
+    zd = z.detach().to(dev).requires_grad_(True)
+    y = ops.l2_normalize(zd)
+    assert rel(y, ref) < TOL
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    y.backward(g.to(dev))
+    assert rel(zd.grad, z.grad) < TOL
+
+
+# ---------------------------------------------------------------------------
+CASES = sorted(GOLDEN.glob("ntxent_*.npz"))
+
+
+@pytest.mark.parametrize("path", CASES, ids=[p.stem for p in CASES])
+def test_ntxent_vs_reference_golden(dev, path):
+    from molclr_amd.nt_xent import NTXentLoss
+    d = np.load(path)
+    zis = torch.from_numpy(d["zis"]).to(dev).requires_grad_(True)
+    zjs = torch.from_numpy(d["zjs"]).to(dev).requires_grad_(True)
+    crit = NTXentLoss(dev, int(d["batch_size"]), float(d["temperature"]), bool(d["use_cosine"]))
+    loss = crit(zis, zjs)
+    loss.backward()
+    assert abs(loss.item() - float(d["loss"])) <= TOL * max(1.0, abs(float(d["loss"])))
+    assert rel(zis.grad, d["dzis"]) < TOL
+    assert rel(zjs.grad, d["dzjs"]) < TOL
+
+
+@pytest.mark.parametrize("B,C", [(512, 256), (1024, 256), (100, 64)])
+def test_ntxent_large_vs_oracle(dev, B, C):
+    from molclr_amd.nt_xent import NTXentLoss
+    rng = np.random.default_rng(B)
+    zi = rng.standard_normal((B, C)).astype(np.float32)
+    zj = (0.5 * zi + rng.standard_normal((B, C))).astype(np.float32)
+    loss_ref, dzi_ref, dzj_ref = ntxent_math.ntxent(zi, zj, 0.1, True)
+    zis = torch.from_numpy(zi).to(dev).requires_grad_(True)
+    zjs = torch.from_numpy(zj).to(dev).requires_grad_(True)
+    loss = NTXentLoss(dev, B, 0.1, True)(zis, zjs)
+    loss.backward()
+    assert abs(loss.item() - loss_ref) <= TOL * max(1.0, abs(loss_ref))
+    assert rel(zis.grad, dzi_ref) < TOL and rel(zjs.grad, dzj_ref) < TOL
+
+
+def test_ntxent_matches_reference_module_at_b512(dev):
+    """Full reference formulation (broadcast cosine + mask + CE) at the c2 batch."""
+    from molclr_amd.nt_xent import NTXentLoss
+    torch.manual_seed(7)
+    zi = torch.nn.functional.normalize(torch.randn(512, 256), dim=1)
+    zj = torch.nn.functional.normalize(zi + 0.7 * torch.randn(512, 256), dim=1)
+    a = zi.clone().requires_grad_(True)
+    b = zj.clone().requires_grad_(True)
+    lr = RefNTXentLoss("cpu", 512, 0.1, True)(a, b)
+    lr.backward()
+    ad = zi.to(dev).requires_grad_(True)
+    bd = zj.to(dev).requires_grad_(True)
+    l = NTXentLoss(dev, 512, 0.1, True)(ad, bd)
+    l.backward()
+    assert abs(l.item() - lr.item()) <= TOL * abs(lr.item())
+    assert rel(ad.grad, a.grad) < TOL and rel(bd.grad, b.grad) < TOL
+
+
+# ---------------------------------------------------------------------------
+def test_fused_adam_matches_torch_adam(dev):
+    from molclr_amd.optim import FusedAdam
+    torch.manual_seed(0)
+    ps = [torch.randn(300, 600), torch.randn(600), torch.randn(5, 3)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [torch.nn.Parameter(p.clone().to(dev)) for p in ps]
+    o_ref = torch.optim.Adam(ref, 5e-4, weight_decay=1e-5)
+    o_mine = FusedAdam(mine, 5e-4, weight_decay=1e-5)
+    for step in range(5):
+        grads = [torch.randn_like(p) for p in ps]
+        o_ref.zero_grad()
+        o_mine.zero_grad()
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        for p, g in zip(mine, grads):
+            p.grad.copy_(g.to(dev))
+        o_ref.step()
+        o_mine.step()
+    for a, b in zip(mine, ref):
+        assert rel(a.detach(), b.detach()) < TOL
+    assert o_mine.steps_taken == 5

@@ -1,0 +1,150 @@
+"""End-to-end parity: product GINet / GCN / NTXentLoss / FusedAdam on the GPU
+vs the oracle restatement of the reference step on the CPU, same weights and
+same augmented batches (fp32 norm-wise relative tolerance 1e-5; the c2-scale
+cases use 2e-5 after five BatchNorm layers, see the test docstring)."""
+import copy
+
+import pytest
+import torch
+
+from molclr_amd.dataset import SyntheticPairBatches
+from oracle.reference_cpu import RefGCN, RefGINet, RefNTXentLoss, ref_step_loss
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-30)
+
+
+def pair_models(kind, L, D, F, seed=0):
+    from molclr_amd.gcn_molclr import GCN
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(seed)
+    ref = (RefGINet if kind == "gin" else RefGCN)(L, D, F)
+    mine = (GINet if kind == "gin" else GCN)(L, D, F)
+    mine.load_state_dict(ref.state_dict())
+    return ref, mine
+
+
+@pytest.mark.parametrize("kind,L,D,B", [("gin", 3, 128, 64), ("gcn", 3, 128, 64),
+                                        ("gin", 2, 16, 4), ("gcn", 2, 32, 5)])
+def test_encoder_forward_backward(dev, kind, L, D, B):
+    ref, mine = pair_models(kind, L, D, 512)
+    mine = mine.to(dev)
+    bi, _ = SyntheticPairBatches(B, seed=11).next()
+    h_r, out_r = ref(bi)
+    h_m, out_m = mine(bi.to(dev))
+    assert rel(h_m, h_r) < TOL and rel(out_m, out_r) < TOL
+    torch.manual_seed(3)
+    w1, w2 = torch.randn_like(h_r), torch.randn_like(out_r)
+    ((h_r * w1).sum() + (out_r * w2).sum()).backward()
+    ((h_m * w1.to(dev)).sum() + (out_m * w2.to(dev)).sum()).backward()
+    gr = dict(ref.named_parameters())
+    for name, p in mine.named_parameters():
+        assert rel(p.grad, gr[name].grad) < TOL, name
+    for name, buf in ref.named_buffers():
+        assert rel(dict(mine.named_buffers())[name].float(), buf.float()) < TOL, name
+
+
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_training_steps_match_oracle(dev, kind):
+    """Three full steps (2 encoder forwards, F.normalize, NT-Xent, backward,
+    Adam with coupled L2) on the c1 shape (3 x 128, batch 64)."""
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from molclr_amd.optim import FusedAdam
+    ref, mine = pair_models(kind, 3, 128, 512, seed=1)
+    mine = mine.to(dev)
+    B = 64
+    crit_r = RefNTXentLoss("cpu", B, 0.1, True)
+    crit_m = NTXentLoss(dev, B, 0.1, True)
+    opt_r = torch.optim.Adam(ref.parameters(), 5e-4, weight_decay=1e-5)
+    opt_m = FusedAdam(mine.parameters(), 5e-4, weight_decay=1e-5)
+    data = SyntheticPairBatches(B, seed=21)
+    for step in range(3):
+        xi, xj = data.next()
+        opt_r.zero_grad()
+        lr = ref_step_loss(ref, crit_r, xi, xj)
+        lr.backward()
+        opt_r.step()
+        opt_m.zero_grad()
+        xid, xjd = xi.to(dev), xj.to(dev)
+        _, zi = mine(xid)
+        _, zj = mine(xjd)
+        lm = crit_m(l2_normalize(zi), l2_normalize(zj))
+        lm.backward()
+        opt_m.step()
+        assert abs(lm.item() - lr.item()) <= TOL * abs(lr.item()), step
+    pr = dict(ref.named_parameters())
+    for name, p in mine.named_parameters():
+        assert rel(p, pr[name]) < TOL, name
+
+
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_c2_scale_forward_and_loss(dev, kind):
+    """c2 / c3 shape (5 x 300, batch 512): projections, loss and the gradient
+    of the last projection layer.  BN over ~15.7k rows in five layers lets
+    fp32 reduction-order differences grow slightly, so the bound is 2e-5."""
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    ref, mine = pair_models(kind, 5, 300, 512, seed=2)
+    mine = mine.to(dev)
+    xi, xj = SyntheticPairBatches(512, seed=31).next()
+    lr = ref_step_loss(ref, RefNTXentLoss("cpu", 512, 0.1, True), xi, xj)
+    lr.backward()
+    _, zi = mine(xi.to(dev))
+    _, zj = mine(xj.to(dev))
+    lm = NTXentLoss(dev, 512, 0.1, True)(l2_normalize(zi), l2_normalize(zj))
+    lm.backward()
+    assert abs(lm.item() - lr.item()) <= 2e-5 * abs(lr.item())
+    pr = dict(ref.named_parameters())
+    worst = max(rel(p.grad, pr[n].grad) for n, p in mine.named_parameters())
+    assert worst < 1e-4, worst
+
+
+def test_step_is_deterministic(dev):
+    """No atomics on any float path: two runs give bitwise-identical weights."""
+    from molclr_amd.ginet_molclr import GINet
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from molclr_amd.optim import FusedAdam
+    xi, xj = SyntheticPairBatches(128, seed=41).next()
+    results = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        m = GINet(5, 300, 512).to(dev)
+        opt = FusedAdam(m.parameters(), 5e-4, weight_decay=1e-5)
+        crit = NTXentLoss(dev, 128, 0.1, True)
+        for _ in range(2):
+            opt.zero_grad()
+            g1 = xi.to(dev)
+            g2 = xj.to(dev)
+            loss = crit(l2_normalize(m(g1)[1]), l2_normalize(m(g2)[1]))
+            loss.backward()
+            opt.step()
+        results.append(opt.flat.clone())
+    assert torch.equal(results[0], results[1])
+
+
+def test_trainer_runs_one_epoch(dev, tmp_path, monkeypatch):
+    from molclr_amd.dataset import MoleculeDatasetWrapper
+    from molclr_amd.molclr import MolCLR
+    monkeypatch.chdir(tmp_path)
+    config = {
+        "batch_size": 32, "warm_up": 1, "epochs": 2, "load_model": "None",
+        "eval_every_n_epochs": 1, "save_every_n_epochs": 1, "log_every_n_steps": 2,
+        "fp16_precision": False, "init_lr": 0.0005, "weight_decay": "1e-5", "gpu": "cuda:0",
+        "model_type": "gin",
+        "model": {"num_layer": 2, "emb_dim": 64, "feat_dim": 128, "drop_ratio": 0, "pool": "mean"},
+        "aug": "node",
+        "dataset": {"num_workers": 0, "valid_size": 0.2, "data_path": "synthetic:200"},
+        "loss": {"temperature": 0.1, "use_cosine_similarity": True},
+    }
+    ds = MoleculeDatasetWrapper(config["batch_size"], **config["dataset"])
+    m = MolCLR(ds, config).train()
+    assert all(torch.isfinite(p).all() for p in m.parameters())
+    assert list(tmp_path.glob("ckpt/*/checkpoints/model.pth"))
