@@ -307,9 +307,11 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
   MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU || bias,
                  "gemm_f32: bias epilogue needs bias");
   MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux, "gemm_f32: relu-mask epilogue needs aux");
-  MOLCLR_REQUIRE(K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0,
-                 "gemm_f32: K (%lld), lda, ldb must be multiples of 4", (long long)K);
-  MOLCLR_REQUIRE(!a_kmajor || M % 4 == 0 || true, "");
+  // float4 loads along K for the operands stored with K contiguous
+  MOLCLR_REQUIRE(a_kmajor || (K % 4 == 0 && lda % 4 == 0),
+                 "gemm_f32: A with K contiguous needs K (%lld) and lda multiples of 4", (long long)K);
+  MOLCLR_REQUIRE(b_kmajor || (K % 4 == 0 && ldb % 4 == 0),
+                 "gemm_f32: B with K contiguous needs K (%lld) and ldb multiples of 4", (long long)K);
   MOLCLR_REQUIRE(ldc >= N && (a_kmajor ? lda >= M : lda >= K) && (b_kmajor ? ldb >= N : ldb >= K),
                  "gemm_f32: leading dimension too small");
   if (M == 0 || N == 0) return MOLCLR_OK;

@@ -1,0 +1,26 @@
+#!/bin/bash
+# GPU-box check: per-step time limits; stop on anything worse than a test failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -5 "gpurun_out/$name.log"
+  return $rc
+}
+steps="${STEPS:-kernels models bench}"
+for s in $steps; do
+  case $s in
+    kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    models)  run models 900 python -m pytest tests/test_gpu_models.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    smoke)   run smoke 300 python __graft_entry__.py smoke; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    bench)   run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    benchfull) run benchfull 900 python bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    prof)    export TMPDIR=/tmp; rm -rf gpurun_out/prof
+             run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+  esac
+done
+exit 0
