@@ -43,11 +43,11 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
 // block = 64 threads (one column each), LDS table [n1+n2][64].
 __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
     const int64_t* __restrict__ x, const float* __restrict__ dh, int64_t N, int64_t D,
-    int64_t n1, int64_t n2, int64_t rows_per_part, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float tab[];  // [(n1+n2)][64]
+    int64_t n1, int64_t n2, int64_t rows_per_part, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double tab[];  // [(n1+n2)][64]
   const int lane = threadIdx.x;
   const int64_t nt = n1 + n2;
-  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.f;
+  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.0;
   const int64_t c = (int64_t)blockIdx.y * 64 + lane;
   const bool active = c < D;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
@@ -80,23 +80,25 @@ __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
     tab[(n1 + bb) * 64 + lane] += v;
   }
   if (!active) return;
-  float* out = partial + (int64_t)blockIdx.x * nt * D;
+  double* out = partial + (int64_t)blockIdx.x * nt * D;
   for (int64_t r = 0; r < nt; ++r) out[r * D + c] = tab[r * 64 + lane];
 }
 
 // out[r][c] = Σ_p partial[p][r][c], rows [0,n1) -> dX1, [n1,n1+n2) -> dX2.
-__global__ void k_reduce_partials_split(const float* __restrict__ partial, int64_t P,
+// The small embedding-table gradients are sums of ~10^4-10^6 nearly cancelling
+// terms (ill-conditioned): they are accumulated in fp64 and rounded once.
+__global__ void k_reduce_partials_split(const double* __restrict__ partial, int64_t P,
                                         int64_t rows, int64_t D, int64_t split,
                                         float* __restrict__ outA, float* __restrict__ outB) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= rows * D) return;
-  float acc = 0.f;
+  double acc = 0.0;
   for (int64_t p = 0; p < P; ++p) acc += partial[p * rows * D + t];
   int64_t r = t / D;
   if (r < split) {
-    if (outA) outA[t] = acc;
+    if (outA) outA[t] = (float)acc;
   } else {
-    if (outB) outB[t - split * D] = acc;
+    if (outB) outB[t - split * D] = (float)acc;
   }
 }
 
@@ -163,19 +165,21 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restric
   dx[t] = acc;
 }
 
-// Edge-table gradient partials: partial[p][s][c4] = Σ_{i in part p} ecount[i][s] * g[i][c4]
-// grid (P, ceil(d4/64)), block 64.
+// Edge-table gradient partials (fp64): partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c]
+// grid (P, ceil(d4/64)), block 64; thread = one float4 column.
 __global__ __launch_bounds__(64) void k_ecount_weighted_partial(
     const float4* __restrict__ g, const int32_t* __restrict__ ecount, int64_t N, int d4,
-    int64_t rows_per_part, float4* __restrict__ partial) {
+    int64_t rows_per_part, double* __restrict__ partial) {
   const int c = blockIdx.y * 64 + threadIdx.x;
   if (c >= d4) return;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
   int64_t end = beg + rows_per_part;
   if (end > N) end = N;
-  float4 acc[8];
+  double acc[8][4];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) acc[s] = f4zero();
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[s][q] = 0.0;
   for (int64_t i = beg; i < end; ++i) {
     const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
     int4 lo = ec[0], hi = ec[1];
@@ -183,16 +187,19 @@ __global__ __launch_bounds__(64) void k_ecount_weighted_partial(
     int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      float w = (float)cnt[s];
-      acc[s].x += w * v.x;
-      acc[s].y += w * v.y;
-      acc[s].z += w * v.z;
-      acc[s].w += w * v.w;
+      if (cnt[s] == 0) continue;
+      double w = (double)cnt[s];
+      acc[s][0] += w * v.x;
+      acc[s][1] += w * v.y;
+      acc[s][2] += w * v.z;
+      acc[s][3] += w * v.w;
     }
   }
-  float4* out = partial + (int64_t)blockIdx.x * 8 * d4;
+  double* out = partial + (int64_t)blockIdx.x * 8 * (4 * d4);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) out[s * d4 + c] = acc[s];
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[s * 4 * d4 + 4 * c + q] = acc[s][q];
 }
 
 // ---------------------------------------------------------------------------
@@ -223,27 +230,28 @@ __global__ __launch_bounds__(kT) void k_gcn_agg_fwd(
   out[t] = f4add(acc, bias[c]);
 }
 
-// One wave per row: rowsum(g_i) weighted by ecount[i][0..8); per-wave partials.
+// One wave per row: rowsum(g_i) weighted by ecount[i][0..8); per-wave fp64 partials.
 __global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __restrict__ g,
                                                                const int32_t* __restrict__ ecount,
                                                                int64_t N, int d4,
-                                                               float* __restrict__ partial) {
+                                                               double* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int64_t i = wave; i < N; i += nwaves) {
-    float s = 0.f;
+    double s = 0.0;
     for (int c = lane; c < d4; c += 64) {
       float4 v = g[i * d4 + c];
-      s += (v.x + v.y) + (v.z + v.w);
+      s += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
     }
-    s = wave_sum(s);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] += (float)ecount[i * 8 + q] * s;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += (double)ecount[i * 8 + q] * s;
   }
   if (lane < 8) {
-    float v = acc[0];
+    double v = acc[0];
 #pragma unroll
     for (int q = 1; q < 8; ++q)
       if (lane == q) v = acc[q];
@@ -251,16 +259,16 @@ __global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __r
   }
 }
 
-__global__ void k_reduce_rowsum_partial(const float* __restrict__ partial, int64_t nparts,
+__global__ void k_reduce_rowsum_partial(const double* __restrict__ partial, int64_t nparts,
                                         float* __restrict__ dE1, float* __restrict__ dE2) {
   int q = threadIdx.x;
   if (q >= 8) return;
-  float acc = 0.f;
+  double acc = 0.0;
   for (int64_t p = 0; p < nparts; ++p) acc += partial[p * 8 + q];
   if (q < 5) {
-    if (dE1) dE1[q] = acc;
+    if (dE1) dE1[q] = (float)acc;
   } else {
-    if (dE2) dE2[q - 5] = acc;
+    if (dE2) dE2[q - 5] = (float)acc;
   }
 }
 
@@ -303,7 +311,7 @@ MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const fl
 
 MOLCLR_API size_t molclr_atom_embed_bwd_workspace_bytes(int64_t N, int64_t D, int64_t n1,
                                                         int64_t n2) {
-  return (size_t)atom_parts(N) * (n1 + n2) * D * sizeof(float) + 256;
+  return (size_t)atom_parts(N) * (n1 + n2) * D * sizeof(double) + 256;
 }
 
 MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
@@ -311,13 +319,13 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
                                      void* workspace, size_t workspace_bytes,
                                      molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd: bad sizes");
-  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd: tables too large");
+  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(double) <= 65536, "atom_embed_bwd: tables too large");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
   hipStream_t s = molclr::as_stream(stream);
   int64_t P = atom_parts(N);
   int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
-  float* partial = (float*)workspace;
-  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
+  double* partial = (double*)workspace;
+  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(double);
   hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
                      x, dh, N, D, n1, n2, rpp, partial);
   hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, kT)), dim3(kT),
@@ -343,7 +351,7 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
 }
 
 MOLCLR_API size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t N, int64_t D) {
-  return (size_t)ecount_parts(N) * 8 * D * sizeof(float) + 256;
+  return (size_t)ecount_parts(N) * 8 * D * sizeof(double) + 256;
 }
 
 MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t,
@@ -362,9 +370,9 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
     MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
     int64_t P = ecount_parts(N);
     int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
-    float* partial = (float*)workspace;
+    double* partial = (double*)workspace;
     hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P, molclr::ceil_div(d4, 64)), dim3(64), 0,
-                       s, (const float4*)g, ecount, N, d4, rpp, (float4*)partial);
+                       s, (const float4*)g, ecount, N, d4, rpp, partial);
     hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, kT)), dim3(kT), 0, s,
                        partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2);
   }
@@ -389,7 +397,7 @@ MOLCLR_API int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr,
 }
 
 MOLCLR_API size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t N, int64_t D) {
-  size_t a = (size_t)kRowsumBlocks * 4 * 8 * sizeof(float) + 256;
+  size_t a = (size_t)kRowsumBlocks * 4 * 8 * sizeof(double) + 256;
   return a + molclr_colsum_ws(N, D);
 }
 
@@ -407,7 +415,7 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
                        (const float4*)g, rowptr_t, col_t, (float4*)dxw, N, d4);
   }
   molclr::Workspace w(workspace, workspace_bytes);
-  float* partial = w.take<float>(kRowsumBlocks * 4 * 8);
+  double* partial = w.take<double>(kRowsumBlocks * 4 * 8);
   if (dE1 || dE2) {
     hipLaunchKernelGGL(k_rowsum_ecount_partial, dim3(kRowsumBlocks), dim3(256), 0, s,
                        (const float4*)g, ecount, N, d4, partial);

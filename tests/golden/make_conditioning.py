@@ -30,13 +30,11 @@ from oracle.reference_cpu import RefGCN, RefGINet, RefNTXentLoss, ref_step_loss 
 OUT = Path(__file__).resolve().parent / "c2_grad_conditioning.json"
 
 
-def measure(kind):
-    torch.manual_seed(2)  # == pair_models(kind, 5, 300, 512, seed=2)
-    ref = (RefGINet if kind == "gin" else RefGCN)(5, 300, 512)
-    r64 = copy.deepcopy(ref).double()
-    xi, xj = SyntheticPairBatches(512, seed=31).next()
-    ref_step_loss(ref, RefNTXentLoss("cpu", 512, 0.1, True), xi, xj).backward()
-    ref_step_loss(r64, RefNTXentLoss("cpu", 512, 0.1, True), xi, xj).backward()
+# test_encoder_forward_backward cases (seed 0, batch seed 11, random linear loss)
+ENCODER_CASES = [("gin", 3, 128, 64), ("gcn", 3, 128, 64), ("gin", 2, 16, 4), ("gcn", 2, 32, 5)]
+
+
+def _errors(ref, r64):
     g64 = dict(r64.named_parameters())
     out = {}
     for n, p in ref.named_parameters():
@@ -45,10 +43,36 @@ def measure(kind):
     return out
 
 
+def measure_encoder(kind, L, D, B):
+    torch.manual_seed(0)  # == pair_models(kind, L, D, 512)
+    ref = (RefGINet if kind == "gin" else RefGCN)(L, D, 512)
+    r64 = copy.deepcopy(ref).double()
+    bi, _ = SyntheticPairBatches(B, seed=11).next()
+    h, o = ref(bi)
+    h6, o6 = r64(bi)
+    torch.manual_seed(3)
+    w1, w2 = torch.randn_like(h), torch.randn_like(o)
+    ((h * w1).sum() + (o * w2).sum()).backward()
+    ((h6 * w1.double()).sum() + (o6 * w2.double()).sum()).backward()
+    return _errors(ref, r64)
+
+
+def measure(kind):
+    torch.manual_seed(2)  # == pair_models(kind, 5, 300, 512, seed=2)
+    ref = (RefGINet if kind == "gin" else RefGCN)(5, 300, 512)
+    r64 = copy.deepcopy(ref).double()
+    xi, xj = SyntheticPairBatches(512, seed=31).next()
+    ref_step_loss(ref, RefNTXentLoss("cpu", 512, 0.1, True), xi, xj).backward()
+    ref_step_loss(r64, RefNTXentLoss("cpu", 512, 0.1, True), xi, xj).backward()
+    return _errors(ref, r64)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     res = {"host_note": "oracle fp32 vs fp64 on the build container host (Intel Xeon, torch "
                         + torch.__version__ + ")",
            "gin": measure("gin"), "gcn": measure("gcn")}
+    for kind, L, D, B in ENCODER_CASES:
+        res[f"enc_{kind}_{L}_{D}_{B}"] = measure_encoder(kind, L, D, B)
     OUT.write_text(json.dumps(res, indent=1))
     print("wrote", OUT)

@@ -90,7 +90,8 @@ def test_encoder_forward_backward(dev, kind, L, D, B):
     ((h_r * w1).sum() + (out_r * w2).sum()).backward()
     ((h_6 * w1.double()).sum() + (out_6 * w2.double()).sum()).backward()
     ((h_m * w1.to(dev)).sum() + (out_m * w2.to(dev)).sum()).backward()
-    check_grads(mine, ref64)
+    cond = json.loads((GOLDEN / "c2_grad_conditioning.json").read_text())[f"enc_{kind}_{L}_{D}_{B}"]
+    check_grads(mine, ref64, cond)
     for name, buf in ref.named_buffers():
         assert rel(dict(mine.named_buffers())[name].float(), buf.float()) < TOL, name
 
@@ -124,16 +125,22 @@ def test_training_steps_match_oracle(dev, kind):
         lm.backward()
         opt_m.step()
         assert abs(lm.item() - lr.item()) <= TOL * abs(lr.item()), step
+    # Adam's first steps move every element by ~lr * sign(g): an element whose
+    # gradient is within fp32 rounding of 0 may legitimately step the other way
+    # (a 2*lr difference) in ANY fp32 implementation, the reference's included.
+    # So: every element within the Adam step bound, and all but a handful of
+    # elements equal to the fp64 trajectory to 1e-5 relative.
     pr = dict(ref.named_parameters())
+    n_total = n_far = 0
     for name, p in mine.named_parameters():
-        if pre_bn_bias(name):  # rounding-noise gradient: Adam moves it by <= lr per step
-            assert (p.detach().double().cpu() - pr[name].detach()).abs().max() <= 3 * 5e-4 * 1.01
-        else:
-            # Adam's first steps move every element by ~lr * sign(g): an element
-            # whose gradient is within rounding of 0 may step the other way
-            # (2 lr) in ANY fp32 implementation, hence 1e-4 on the parameters
-            # (the losses above are held to 1e-5).
-            assert rel(p, pr[name]) < 1e-4, name
+        a = p.detach().double().cpu()
+        b = pr[name].detach()
+        d = (a - b).abs()
+        assert d.max().item() <= 3 * 2 * 5e-4 * 1.01, name
+        if not pre_bn_bias(name):
+            n_total += d.numel()
+            n_far += int((d > 1e-5 * b.abs() + 1e-7).sum())
+    assert n_far <= 1e-3 * n_total, (n_far, n_total)
 
 
 @pytest.mark.parametrize("kind", ["gin", "gcn"])
