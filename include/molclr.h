@@ -97,11 +97,14 @@ int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
 int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
                           float* h, int64_t num_nodes, int64_t dim, int64_t n1,
                           int64_t n2, molclr_stream_t stream);
-/* dX1 [n1,D], dX2 [n2,D] = Σ over nodes of each type of dh (deterministic). */
+/* dX1 [n1,D], dX2 [n2,D] = Σ over nodes of each type of dh (deterministic, fp64
+ * accumulation).  accumulate != 0 adds into dX1/dX2 (fused gradient
+ * accumulation into a parameter's .grad); the same flag on the other
+ * backward entry points below applies to their parameter-gradient outputs. */
 size_t molclr_atom_embed_bwd_workspace_bytes(int64_t num_nodes, int64_t dim, int64_t n1,
                                              int64_t n2);
 int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
-                          int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,
+                          int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2, int accumulate,
                           void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
 /* GINE aggregation (ginet_molclr.py:39-44 + PyG aggr='add'):
@@ -119,7 +122,7 @@ int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32
 size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
 int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
                               const int32_t* ecount, float* dx, float* dE1, float* dE2,
-                              int64_t num_nodes, int64_t dim, void* workspace,
+                              int64_t num_nodes, int64_t dim, int accumulate, void* workspace,
                               size_t workspace_bytes, molclr_stream_t stream);
 
 /* GCN aggregation (gcn_molclr.py:72-88; gcn_norm at :74 is computed and
@@ -135,8 +138,8 @@ int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr, const int32
 size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
 int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
                              const int32_t* ecount, float* dxw, float* dE1, float* dE2,
-                             float* dbias, int64_t num_nodes, int64_t dim, void* workspace,
-                             size_t workspace_bytes, molclr_stream_t stream);
+                             float* dbias, int64_t num_nodes, int64_t dim, int accumulate,
+                             void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * FP32 GEMM on the gfx950 f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32 FMA
@@ -147,23 +150,26 @@ int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int3
  * so nn.Linear forward (x W^T) is a_kmajor=0, b_kmajor=0; dX = dY W is
  * a_kmajor=0, b_kmajor=1; dW = dY^T X is a_kmajor=1, b_kmajor=1.
  * Epilogues: MOLCLR_EPI_NONE, _BIAS (C += bias[n]), _BIAS_RELU,
- * _RELU_MASK (C *= (aux[m*ldaux+n] > 0), the ReLU backward).
- * Requires K, lda, ldb, ldc and the contiguous dims to be multiples of 4.
+ * _RELU_MASK (C *= (aux[m*ldaux+n] > 0), the ReLU backward), optionally
+ * OR-ed with MOLCLR_EPI_ACCUMULATE (C = C_old + result).
+ * An operand stored with K contiguous needs K and its ld to be multiples of 4.
  * Split-K (for the weight-gradient shape, K = number of nodes) runs when the
  * workspace is large enough: molclr_gemm_f32_workspace_bytes(M,N,K). */
 enum { MOLCLR_EPI_NONE = 0, MOLCLR_EPI_BIAS = 1, MOLCLR_EPI_BIAS_RELU = 2,
-       MOLCLR_EPI_RELU_MASK = 3 };
+       MOLCLR_EPI_RELU_MASK = 3,
+       MOLCLR_EPI_ACCUMULATE = 16 /* OR-able flag: C += result (gradient accumulation) */ };
 size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K);
 int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
                     int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
-                    int b_kmajor, int epilogue, const float* bias, const float* aux,
+                    int b_kmajor, int epilogue_flags, const float* bias, const float* aux,
                     int64_t ldaux, void* workspace, size_t workspace_bytes,
                     molclr_stream_t stream);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
 int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
-                      void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+                      int accumulate, void* workspace, size_t workspace_bytes,
+                      molclr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * BatchNorm1d over the rows of z [N,D] (+ ReLU), ginet_molclr.py:107-111.
@@ -183,7 +189,7 @@ int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
 int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
                          const float* beta, const float* save_mean,
                          const float* save_invstd, float* dz, float* dgamma, float* dbeta,
-                         int64_t rows, int64_t dim, int relu, void* workspace,
+                         int64_t rows, int64_t dim, int relu, int accumulate, void* workspace,
                          size_t workspace_bytes, molclr_stream_t stream);
 
 /* Segment pooling over graph_ptr (PyG global_mean_pool / global_add_pool):

@@ -32,25 +32,26 @@ SIGNATURES = {
                                    _P, c_size_t, _P]),
     "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "molclr_atom_embed_bwd_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64]),
-    "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, c_size_t, _P]),
+    "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
+                                      _P]),
     "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
     "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, c_size_t,
-                                          _P]),
+    "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
+                                          c_size_t, _P]),
     "molclr_gcn_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
     "molclr_gcn_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_gcn_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, c_size_t,
-                                         _P]),
+    "molclr_gcn_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
+                                         c_size_t, _P]),
     "molclr_gemm_f32_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_gemm_f32": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, c_int, c_int, c_int,
                                 _P, _P, _I64, _P, c_size_t, _P]),
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, _P, c_size_t, _P]),
+    "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_batchnorm_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_double, c_double,
                                      c_int, c_int, _P, c_size_t, _P]),
-    "molclr_batchnorm_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
-                                     c_size_t, _P]),
+    "molclr_batchnorm_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, c_int,
+                                     _P, c_size_t, _P]),
     "molclr_segment_pool_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
     "molclr_segment_pool_bwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_l2norm_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_double, _P]),
@@ -68,6 +69,7 @@ SIGNATURES = {
 }
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
+EPI_ACCUMULATE = 16
 
 
 class MolclrError(RuntimeError):

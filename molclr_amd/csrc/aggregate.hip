@@ -87,19 +87,25 @@ __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
 // out[r][c] = Σ_p partial[p][r][c], rows [0,n1) -> dX1, [n1,n1+n2) -> dX2.
 // The small embedding-table gradients are sums of ~10^4-10^6 nearly cancelling
 // terms (ill-conditioned): they are accumulated in fp64 and rounded once.
-__global__ void k_reduce_partials_split(const double* __restrict__ partial, int64_t P,
-                                        int64_t rows, int64_t D, int64_t split,
-                                        float* __restrict__ outA, float* __restrict__ outB) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= rows * D) return;
+// A block owns 64 consecutive elements; 16 lanes fold strided partials, then a
+// fixed-order merge (deterministic).
+__global__ __launch_bounds__(1024) void k_reduce_partials_split(
+    const double* __restrict__ partial, int64_t P, int64_t rows, int64_t D, int64_t split,
+    float* __restrict__ outA, float* __restrict__ outB, int accumulate) {
+  __shared__ double red[16][64];
+  const int cl = threadIdx.x % 64, rl = threadIdx.x / 64;
+  const int64_t t = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t n = rows * D;
   double acc = 0.0;
-  for (int64_t p = 0; p < P; ++p) acc += partial[p * rows * D + t];
+  if (t < n)
+    for (int64_t p = rl; p < P; p += 16) acc += partial[p * n + t];
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl != 0 || t >= n) return;
+  for (int q = 1; q < 16; ++q) acc += red[q][cl];
   int64_t r = t / D;
-  if (r < split) {
-    if (outA) outA[t] = (float)acc;
-  } else {
-    if (outB) outB[t - split * D] = (float)acc;
-  }
+  float* o = r < split ? (outA ? outA + t : nullptr) : (outB ? outB + (t - split * D) : nullptr);
+  if (o) *o = accumulate ? *o + (float)acc : (float)acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -260,16 +266,14 @@ __global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __r
 }
 
 __global__ void k_reduce_rowsum_partial(const double* __restrict__ partial, int64_t nparts,
-                                        float* __restrict__ dE1, float* __restrict__ dE2) {
+                                        float* __restrict__ dE1, float* __restrict__ dE2,
+                                        int accumulate) {
   int q = threadIdx.x;
   if (q >= 8) return;
   double acc = 0.0;
   for (int64_t p = 0; p < nparts; ++p) acc += partial[p * 8 + q];
-  if (q < 5) {
-    if (dE1) dE1[q] = (float)acc;
-  } else {
-    if (dE2) dE2[q - 5] = (float)acc;
-  }
+  float* o = q < 5 ? (dE1 ? dE1 + q : nullptr) : (dE2 ? dE2 + (q - 5) : nullptr);
+  if (o) *o = accumulate ? *o + (float)acc : (float)acc;
 }
 
 int64_t atom_parts(int64_t N) {
@@ -290,7 +294,7 @@ constexpr int64_t kRowsumBlocks = 128;
 
 // Column sums shared with norm.hip (declared there).
 int molclr_colsum_impl(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
-                       molclr::Workspace& w, hipStream_t s);
+                       int accumulate, molclr::Workspace& w, hipStream_t s);
 size_t molclr_colsum_ws(int64_t rows, int64_t cols);
 
 MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
@@ -315,7 +319,7 @@ MOLCLR_API size_t molclr_atom_embed_bwd_workspace_bytes(int64_t N, int64_t D, in
 }
 
 MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
-                                     int64_t N, int64_t D, int64_t n1, int64_t n2,
+                                     int64_t N, int64_t D, int64_t n1, int64_t n2, int accumulate,
                                      void* workspace, size_t workspace_bytes,
                                      molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd: bad sizes");
@@ -328,8 +332,8 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
   size_t lds = (size_t)(n1 + n2) * 64 * sizeof(double);
   hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
                      x, dh, N, D, n1, n2, rpp, partial);
-  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, kT)), dim3(kT),
-                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2);
+  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 64)), dim3(1024),
+                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -357,7 +361,7 @@ MOLCLR_API size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t N, int64_t D
 MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t,
                                          const int32_t* col_t, const int32_t* ecount, float* dx,
                                          float* dE1, float* dE2, int64_t N, int64_t D,
-                                         void* workspace, size_t workspace_bytes,
+                                         int accumulate, void* workspace, size_t workspace_bytes,
                                          molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_bwd: dim must be a multiple of 4");
   hipStream_t s = molclr::as_stream(stream);
@@ -373,8 +377,8 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
     double* partial = (double*)workspace;
     hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P, molclr::ceil_div(d4, 64)), dim3(64), 0,
                        s, (const float4*)g, ecount, N, d4, rpp, partial);
-    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, kT)), dim3(kT), 0, s,
-                       partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2);
+    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 64)), dim3(1024), 0, s,
+                       partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2, accumulate);
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
@@ -404,8 +408,8 @@ MOLCLR_API size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t N, int64_t D)
 MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
                                         const int32_t* col_t, const int32_t* ecount, float* dxw,
                                         float* dE1, float* dE2, float* dbias, int64_t N,
-                                        int64_t D, void* workspace, size_t workspace_bytes,
-                                        molclr_stream_t stream) {
+                                        int64_t D, int accumulate, void* workspace,
+                                        size_t workspace_bytes, molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gcn_aggregate_bwd: dim must be a multiple of 4");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gcn_aggregate_bwd_workspace_bytes(N, D));
   hipStream_t s = molclr::as_stream(stream);
@@ -420,11 +424,11 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
     hipLaunchKernelGGL(k_rowsum_ecount_partial, dim3(kRowsumBlocks), dim3(256), 0, s,
                        (const float4*)g, ecount, N, d4, partial);
     hipLaunchKernelGGL(k_reduce_rowsum_partial, dim3(1), dim3(64), 0, s, partial,
-                       kRowsumBlocks * 4, dE1, dE2);
+                       kRowsumBlocks * 4, dE1, dE2, accumulate);
   }
   MOLCLR_LAUNCHED();
   if (dbias) {
-    int rc = molclr_colsum_impl(g, dbias, N, D, D, w, s);
+    int rc = molclr_colsum_impl(g, dbias, N, D, D, accumulate, w, s);
     if (rc) return rc;
   }
   return MOLCLR_OK;

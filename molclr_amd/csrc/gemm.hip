@@ -29,36 +29,51 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int BK = 32;
-constexpr int LDK = BK + 4;  // LDS row pitch (floats)
+constexpr int LDK = BK + 4;  // [row][k] image pitch (floats): conflict-free ds_read_b128
+constexpr int RPAD = 4;      // [k][row] image pad (floats)
+
+// One operand's K-slice in LDS.
+//  K contiguous in memory ([rows][K]): image [row][LDK]; a lane reads 4
+//    consecutive k of one row with one ds_read_b128.
+//  rows contiguous ([K][rows], e.g. dY^T of a weight gradient): image
+//    [k][ROWS+RPAD]; a lane reads one element per k with ds_read_b32
+//    (32 consecutive rows per half-wave: conflict-free).
+// Both are filled from float4 global loads (16 B per lane, coalesced).
+template <bool KMAJOR, int ROWS>
+struct Image {
+  static constexpr int FLOATS = KMAJOR ? BK * (ROWS + RPAD) : ROWS * LDK;
+};
 
 template <bool KMAJOR, int ROWS, int T>
 struct Stager {
-  // non-K-major: ROWS x BK floats as float4 along k
-  // K-major: ROWS x BK, source stored [k][row]; each item = 4 consecutive k of one row
-  static constexpr int ITEMS = ROWS * BK / 4;
+  static constexpr int ITEMS = ROWS * BK / 4;  // float4 items per slice
   static constexpr int PER_THREAD = (ITEMS + T - 1) / T;
   float4 r[PER_THREAD];
 
   __device__ __forceinline__ void load(const float* __restrict__ src, int64_t ld, int64_t row0,
-                                       int64_t rows, int64_t k0, int64_t K, int tid) {
+                                       int64_t rows, int64_t k0, int64_t K, int tid, bool vec) {
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
-      int idx = tid + j * T;
+      const int idx = tid + j * T;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (idx < ITEMS) {
         if (!KMAJOR) {
-          int row = idx / (BK / 4), k4 = idx % (BK / 4);
-          int64_t gr = row0 + row, gk = k0 + 4 * k4;
+          const int row = idx / (BK / 4), k4 = idx % (BK / 4);
+          const int64_t gr = row0 + row, gk = k0 + 4 * k4;
           if (gr < rows && gk < K) v = *reinterpret_cast<const float4*>(src + gr * ld + gk);
         } else {
-          int row = idx % ROWS, k4 = idx / ROWS;
-          int64_t gr = row0 + row, gk = k0 + 4 * k4;
-          if (gr < rows) {
+          const int k = idx / (ROWS / 4), r4 = idx % (ROWS / 4);
+          const int64_t gk = k0 + k, gr = row0 + 4 * r4;
+          if (gk < K) {
             const float* p = src + gk * ld + gr;
-            if (gk + 0 < K) v.x = p[0];
-            if (gk + 1 < K) v.y = p[ld];
-            if (gk + 2 < K) v.z = p[2 * ld];
-            if (gk + 3 < K) v.w = p[3 * ld];
+            if (vec && gr + 3 < rows) {
+              v = *reinterpret_cast<const float4*>(p);
+            } else {
+              if (gr + 0 < rows) v.x = p[0];
+              if (gr + 1 < rows) v.y = p[1];
+              if (gr + 2 < rows) v.z = p[2];
+              if (gr + 3 < rows) v.w = p[3];
+            }
           }
         }
       }
@@ -69,21 +84,27 @@ struct Stager {
   __device__ __forceinline__ void store(float* __restrict__ lds, int tid) const {
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
-      int idx = tid + j * T;
+      const int idx = tid + j * T;
       if (idx < ITEMS) {
-        int row, k4;
         if (!KMAJOR) {
-          row = idx / (BK / 4);
-          k4 = idx % (BK / 4);
+          const int row = idx / (BK / 4), k4 = idx % (BK / 4);
+          *reinterpret_cast<float4*>(lds + row * LDK + 4 * k4) = r[j];
         } else {
-          row = idx % ROWS;
-          k4 = idx / ROWS;
+          const int k = idx / (ROWS / 4), r4 = idx % (ROWS / 4);
+          *reinterpret_cast<float4*>(lds + k * (ROWS + RPAD) + 4 * r4) = r[j];
         }
-        *reinterpret_cast<float4*>(lds + row * LDK + 4 * k4) = r[j];
       }
     }
   }
 };
+
+// Fragment for MFMA k-steps 4q..4q+3 of lane half lh (k = 16 lh + 4q + j), row `row`.
+template <bool KMAJOR, int ROWS>
+__device__ __forceinline__ float4 frag(const float* __restrict__ lds, int row, int lh, int q) {
+  if (!KMAJOR) return *reinterpret_cast<const float4*>(lds + row * LDK + lh * 16 + 4 * q);
+  const float* p = lds + (lh * 16 + 4 * q) * (ROWS + RPAD) + row;
+  return make_float4(p[0], p[ROWS + RPAD], p[2 * (ROWS + RPAD)], p[3 * (ROWS + RPAD)]);
+}
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // bijective: XCD x (= bid % 8) receives a contiguous range of tile ids
@@ -97,13 +118,12 @@ template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT
 __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
     int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
-    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split) {
+    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
   constexpr int T = WM * WN * 64;
   constexpr int BM = WM * TM * 32;
   constexpr int BN = WN * TN * 32;
-  __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * LDK];
-  float* As = lds;
-  float* Bs = lds + BM * LDK;
+  constexpr int AF = Image<AK, BM>::FLOATS, BF = Image<BKM, BN>::FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[2 * (AF + BF)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -121,6 +141,8 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
   const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
   int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
   if (kt_end > nk_total) kt_end = nk_total;
+  const bool avec = (lda % 4 == 0) && (M % 4 == 0);
+  const bool bvec = (ldb % 4 == 0) && (N % 4 == 0);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -132,28 +154,29 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 
   Stager<AK, BM, T> sa;
   Stager<BKM, BN, T> sb;
+  int cur = 0;
   if (kt_beg < kt_end) {
-    sa.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid);
-    sb.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tid);
+    sa.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid, avec);
+    sb.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tid, bvec);
+    sa.store(lds, tid);
+    sb.store(lds + AF, tid);
+    __syncthreads();
   }
   for (int kt = kt_beg; kt < kt_end; ++kt) {
-    __syncthreads();  // previous slice fully consumed
-    sa.store(As, tid);
-    sb.store(Bs, tid);
-    __syncthreads();
-    if (kt + 1 < kt_end) {  // prefetch the next slice into registers
-      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * BK, K, tid);
-      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * BK, K, tid);
+    const bool more = kt + 1 < kt_end;
+    if (more) {  // next slice in flight while this one is consumed
+      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * BK, K, tid, avec);
+      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * BK, K, tid, bvec);
     }
+    const float* As = lds + cur * (AF + BF);
+    const float* Bs = As + AF;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float4 af[TM], bf[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a)
-        af[a] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + a * 32 + li) * LDK + lh * 16 + 4 * q);
+      for (int a = 0; a < TM; ++a) af[a] = frag<AK, BM>(As, wm * TM * 32 + a * 32 + li, lh, q);
 #pragma unroll
-      for (int b = 0; b < TN; ++b)
-        bf[b] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + b * 32 + li) * LDK + lh * 16 + 4 * q);
+      for (int b = 0; b < TN; ++b) bf[b] = frag<BKM, BN>(Bs, wn * TN * 32 + b * 32 + li, lh, q);
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -164,6 +187,13 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].w, bf[b].w, acc[a][b], 0, 0, 0);
         }
     }
+    if (more) {
+      float* nxt = lds + (cur ^ 1) * (AF + BF);
+      sa.store(nxt, tid);
+      sb.store(nxt + AF, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
   }
 
   // epilogue: acc register r of lane (li, lh) -> row (r&3) + 8*(r>>2) + 4*lh, col li
@@ -186,6 +216,7 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
           if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
           if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
           if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+          if (accumulate) v += Cout[m * ldo + n];
         }
         Cout[m * ldo + n] = v;
       }
@@ -197,7 +228,7 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 template <int EPI>
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
                                 float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
-                                const float* __restrict__ aux, int64_t ldaux) {
+                                const float* __restrict__ aux, int64_t ldaux, int accumulate) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= M * N) return;
   int64_t m = t / N, n = t - m * N;
@@ -206,6 +237,7 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   if (EPI == MOLCLR_EPI_BIAS) v = v + bias[n];
   if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bias[n], 0.f);
   if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+  if (accumulate) v += C[m * ldc + n];
   C[m * ldc + n] = v;
 }
 
@@ -215,42 +247,43 @@ struct Cfg {
   int bn() const { return wn * tn * 32; }
 };
 
-Cfg pick_cfg(int64_t M, int64_t N) {
-  if (M <= 1024 && N <= 1024) return {2, 2, 1, 1};  // 64 x 64: small (heads, NT-Xent-sized)
-  // prefer the wide 128 x 128 tile unless it wastes > 12% of the N extent
-  int64_t pad128 = (N + 127) / 128 * 128, pad64 = (N + 63) / 64 * 64;
-  if ((double)pad128 / N <= 1.12 * (double)pad64 / N) return {2, 2, 2, 2};
-  return {4, 1, 1, 2};  // 128 x 64
-}
+// 64 x 64 tiles (4 waves x one 32x32 MFMA tile): many small workgroups keep
+// every CU's matrix pipe fed to the end of the grid (at M ~ 15k rows a 128 x 128
+// tiling leaves 600 tiles for 512 resident slots: a 17%-full second wave).
+Cfg pick_cfg(int64_t, int64_t) { return {2, 2, 1, 1}; }
 
 int pick_splits(const Cfg& c, int64_t M, int64_t N, int64_t K) {
   int64_t tiles = ((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn());
   int64_t nk = (K + BK - 1) / BK;
-  if (tiles >= 256 || nk < 8) return 1;
-  int64_t s = (512 + tiles - 1) / tiles;
-  if (s > nk / 4) s = nk / 4;  // keep >= 4 K-slices per split
+  if (tiles >= 512 || nk < 16) return 1;
+  int64_t s = (1024 + tiles - 1) / tiles;
+  if (s > nk / 8) s = nk / 8;  // keep >= 8 K-slices per split
   if (s > 64) s = 64;
   return s < 1 ? 1 : (int)s;
 }
 
+struct Args {
+  const float *A, *B;
+  float* C;
+  int64_t M, N, K, lda, ldb, ldc;
+  const float *bias, *aux;
+  int64_t ldaux;
+  int kps, accumulate;
+};
+
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
-void launch_t(dim3 grid, hipStream_t s, const float* A, const float* B, float* C, int64_t M,
-              int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* bias,
-              const float* aux, int64_t ldaux, int kps) {
+void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   hipLaunchKernelGGL((k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
-                     0, s, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, kps);
+                     0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
+                     a.ldaux, a.kps, a.accumulate);
 }
 
 template <int WM, int WN, int TM, int TN, bool SPLIT>
-int dispatch_layout(int ak, int bk, int epi, dim3 grid, hipStream_t s, const float* A,
-                    const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
-                    int64_t ldb, int64_t ldc, const float* bias, const float* aux, int64_t ldaux,
-                    int kps) {
-#define MOLCLR_GEMM_CASE(AKV, BKV, EPV)                                                        \
-  if (ak == AKV && bk == BKV && (SPLIT || epi == EPV)) {                                       \
-    launch_t<WM, WN, TM, TN, AKV, BKV, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(                  \
-        grid, s, A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, kps);                      \
-    return 0;                                                                                  \
+int dispatch_layout(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
+#define MOLCLR_GEMM_CASE(AKV, BKV, EPV)                                                   \
+  if (ak == AKV && bk == BKV && (SPLIT || epi == EPV)) {                                  \
+    launch_t<WM, WN, TM, TN, AKV, BKV, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(grid, s, a); \
+    return 0;                                                                             \
   }
 #define MOLCLR_GEMM_EPIS(AKV, BKV)                \
   MOLCLR_GEMM_CASE(AKV, BKV, MOLCLR_EPI_NONE)      \
@@ -274,18 +307,9 @@ int dispatch_layout(int ak, int bk, int epi, dim3 grid, hipStream_t s, const flo
 }
 
 template <bool SPLIT>
-int dispatch_cfg(const Cfg& c, int ak, int bk, int epi, dim3 grid, hipStream_t s, const float* A,
-                 const float* B, float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
-                 int64_t ldb, int64_t ldc, const float* bias, const float* aux, int64_t ldaux,
-                 int kps) {
-  if (c.wm == 2 && c.wn == 2 && c.tm == 2 && c.tn == 2)
-    return dispatch_layout<2, 2, 2, 2, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb,
-                                              ldc, bias, aux, ldaux, kps);
-  if (c.wm == 4 && c.wn == 1 && c.tm == 1 && c.tn == 2)
-    return dispatch_layout<4, 1, 1, 2, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb,
-                                              ldc, bias, aux, ldaux, kps);
-  return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, A, B, C, M, N, K, lda, ldb, ldc,
-                                            bias, aux, ldaux, kps);
+int dispatch_cfg(const Cfg& c, int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
+  (void)c;
+  return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, a);
 }
 
 }  // namespace
@@ -298,13 +322,15 @@ MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t 
 
 MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
                                int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
-                               int b_kmajor, int epilogue, const float* bias, const float* aux,
+                               int b_kmajor, int epilogue_flags, const float* bias, const float* aux,
                                int64_t ldaux, void* workspace, size_t workspace_bytes,
                                molclr_stream_t stream) {
+  const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
+  const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32: negative size");
   MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
                  "gemm_f32: bad epilogue %d", epilogue);
-  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU || bias,
+  MOLCLR_REQUIRE((epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU) || bias,
                  "gemm_f32: bias epilogue needs bias");
   MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux, "gemm_f32: relu-mask epilogue needs aux");
   // float4 loads along K for the operands stored with K contiguous
@@ -317,7 +343,6 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
   if (M == 0 || N == 0) return MOLCLR_OK;
   hipStream_t s = molclr::as_stream(stream);
   if (K == 0) {
-    // empty reduction: C = epilogue(0)
     molclr::set_error("gemm_f32: K == 0 unsupported");
     return MOLCLR_ERR_UNSUPPORTED;
   }
@@ -326,36 +351,36 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
   MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
   int sp = pick_splits(c, M, N, K);
   if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
+  Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate};
   int rc;
   if (sp == 1) {
-    rc = dispatch_cfg<false>(c, a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, A,
-                             B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0);
+    rc = dispatch_cfg<false>(c, a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, a);
   } else {
     int64_t nk = (K + BK - 1) / BK;
     int kps = (int)((nk + sp - 1) / sp);
     sp = (int)((nk + kps - 1) / kps);
     float* partial = (float*)workspace;
+    Args ap{A, B, partial, M, N, K, lda, ldb, N, nullptr, nullptr, 0, kps, 0};
     rc = dispatch_cfg<true>(c, a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
-                            dim3((unsigned)tiles, sp), s, A, B, partial, M, N, K, lda, ldb, N,
-                            nullptr, nullptr, 0, kps);
+                            dim3((unsigned)tiles, sp), s, ap);
     if (rc == 0) {
       dim3 g((unsigned)molclr::ceil_div(M * N, 256));
       switch (epilogue) {
         case MOLCLR_EPI_NONE:
           hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s, partial, sp, M,
-                             N, C, ldc, bias, aux, ldaux);
+                             N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         case MOLCLR_EPI_BIAS:
           hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s, partial, sp, M,
-                             N, C, ldc, bias, aux, ldaux);
+                             N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         case MOLCLR_EPI_BIAS_RELU:
           hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0, s, partial, sp,
-                             M, N, C, ldc, bias, aux, ldaux);
+                             M, N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         default:
           hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0, s, partial, sp,
-                             M, N, C, ldc, bias, aux, ldaux);
+                             M, N, C, ldc, bias, aux, ldaux, accumulate);
       }
     }
   }

@@ -49,13 +49,27 @@ __global__ void k_colsum_partial(const float4* __restrict__ X, int64_t rows, int
   }
 }
 
-__global__ void k_colsum_final(const float* __restrict__ partial, int64_t P, int64_t cols,
-                               float* __restrict__ out) {
-  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// Final column reductions: a block owns 64 columns; its 16 row-lanes each
+// fold a strided subset of the P partials, then the 16 results are combined
+// in a fixed order through LDS (deterministic, no serial P-long chain).
+constexpr int kRedCols = 64, kRedLanes = 16;
+
+__global__ __launch_bounds__(kRedCols* kRedLanes) void k_colsum_final(
+    const float* __restrict__ partial, int64_t P, int64_t cols, float* __restrict__ out,
+    int accumulate) {
+  __shared__ float red[kRedLanes][kRedCols];
+  const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
   float acc = 0.f;
-  for (int64_t p = 0; p < P; ++p) acc += partial[p * cols + c];
-  out[c] = acc;
+  if (c < cols)
+    for (int64_t p = rl; p < P; p += kRedLanes) acc += partial[p * cols + c];
+  red[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float s = red[0][cl];
+    for (int q = 1; q < kRedLanes; ++q) s += red[q][cl];
+    out[c] = accumulate ? out[c] + s : s;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -133,34 +147,42 @@ __device__ __forceinline__ void bn_coeffs(float gamma, float beta, float mean, f
   shift = beta - mean * scale;
 }
 
-// One thread per column: merge partials in order, update running stats,
-// write save_mean/save_invstd and the apply coefficients.
-__global__ void k_bn_stats_final(const float* __restrict__ pmean, const float* __restrict__ pm2,
-                                 const float* __restrict__ pn, int64_t P, int64_t D,
-                                 const float* __restrict__ gamma, const float* __restrict__ beta,
-                                 float* __restrict__ running_mean, float* __restrict__ running_var,
-                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                 float* __restrict__ scale, float* __restrict__ shift,
-                                 float momentum, float eps) {
-  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int64_t p = 0; p < P; ++p) {
-    float nb = pn[p];
-    if (nb == 0.f) continue;
-    float mb = pmean[p * D + c], qb = pm2[p * D + c];
-    if (n == 0.f) {
-      n = nb;
-      mean = mb;
-      m2 = qb;
-      continue;
-    }
-    float nn = n + nb;
-    float d = mb - mean;
-    mean = mean + d * (nb / nn);
-    m2 = m2 + qb + d * d * (n * nb / nn);
-    n = nn;
+__device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb, float mb, float qb) {
+  if (nb == 0.f) return;
+  if (n == 0.f) {
+    n = nb;
+    mean = mb;
+    m2 = qb;
+    return;
   }
+  float nn = n + nb;
+  float d = mb - mean;
+  mean = mean + d * (nb / nn);
+  m2 = m2 + qb + d * d * (n * nb / nn);
+  n = nn;
+}
+
+// Per column: Chan-merge the P partials (16 strided lanes, then a fixed-order
+// merge of the lanes), update running stats, write save_mean/save_invstd and
+// the apply coefficients.  grid = ceil(D/64), block = 1024.
+__global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
+    const float* __restrict__ pmean, const float* __restrict__ pm2, const float* __restrict__ pn,
+    int64_t P, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* __restrict__ running_mean, float* __restrict__ running_var,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ scale,
+    float* __restrict__ shift, float momentum, float eps) {
+  __shared__ float rn[kRedLanes][kRedCols], rm[kRedLanes][kRedCols], rq[kRedLanes][kRedCols];
+  const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  if (c < D)
+    for (int64_t p = rl; p < P; p += kRedLanes) chan1(n, mean, m2, pn[p], pmean[p * D + c], pm2[p * D + c]);
+  rn[rl][cl] = n;
+  rm[rl][cl] = mean;
+  rq[rl][cl] = m2;
+  __syncthreads();
+  if (rl != 0 || c >= D) return;
+  for (int q = 1; q < kRedLanes; ++q) chan1(n, mean, m2, rn[q][cl], rm[q][cl], rq[q][cl]);
   float var = m2 / n;
   float invstd = 1.0f / sqrtf(var + eps);
   save_mean[c] = mean;
@@ -267,19 +289,29 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
   }
 }
 
-__global__ void k_bn_bwd_final(const float* __restrict__ p1, const float* __restrict__ p2,
-                               int64_t P, int64_t D, float* __restrict__ dgamma,
-                               float* __restrict__ dbeta, float* __restrict__ k1,
-                               float* __restrict__ k2, float inv_rows) {
-  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
+__global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
+    const float* __restrict__ p1, const float* __restrict__ p2, int64_t P, int64_t D,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
+    float* __restrict__ k2, float inv_rows, int accumulate) {
+  __shared__ float ra[kRedLanes][kRedCols], rb[kRedLanes][kRedCols];
+  const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
   float a = 0.f, b = 0.f;
-  for (int64_t p = 0; p < P; ++p) {
-    a += p1[p * D + c];
-    b += p2[p * D + c];
+  if (c < D)
+    for (int64_t p = rl; p < P; p += kRedLanes) {
+      a += p1[p * D + c];
+      b += p2[p * D + c];
+    }
+  ra[rl][cl] = a;
+  rb[rl][cl] = b;
+  __syncthreads();
+  if (rl != 0 || c >= D) return;
+  for (int q = 1; q < kRedLanes; ++q) {
+    a += ra[q][cl];
+    b += rb[q][cl];
   }
-  if (dbeta) dbeta[c] = a;
-  if (dgamma) dgamma[c] = b;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + a : a;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + b : b;
   k1[c] = a * inv_rows;
   k2[c] = b * inv_rows;
 }
@@ -409,7 +441,7 @@ size_t molclr_colsum_ws(int64_t rows, int64_t cols) {
 }
 
 int molclr_colsum_impl(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
-                       molclr::Workspace& w, hipStream_t s) {
+                       int accumulate, molclr::Workspace& w, hipStream_t s) {
   MOLCLR_REQUIRE(cols > 0 && cols % 4 == 0 && ld % 4 == 0, "colsum: cols/ld must be multiples of 4");
   molclr::Band b = molclr::make_band(cols);
   int64_t P = band_parts(rows, b.band);
@@ -422,8 +454,8 @@ int molclr_colsum_impl(const float* X, float* out, int64_t rows, int64_t cols, i
   size_t lds = (size_t)b.band * b.d4 * sizeof(float4);
   hipLaunchKernelGGL(k_colsum_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)X, rows,
                      b.d4, ld / 4, b.band, rpp, (float4*)partial);
-  hipLaunchKernelGGL(k_colsum_final, dim3(molclr::ceil_div(cols, kT)), dim3(kT), 0, s, partial, P,
-                     cols, out);
+  hipLaunchKernelGGL(k_colsum_final, dim3(molclr::ceil_div(cols, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, partial, P,
+                     cols, out, accumulate);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -433,11 +465,11 @@ MOLCLR_API size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols) 
 }
 
 MOLCLR_API int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols,
-                                 int64_t ld, void* workspace, size_t workspace_bytes,
-                                 molclr_stream_t stream) {
+                                 int64_t ld, int accumulate, void* workspace,
+                                 size_t workspace_bytes, molclr_stream_t stream) {
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_colsum_ws(rows, cols));
   molclr::Workspace w(workspace, workspace_bytes);
-  return molclr_colsum_impl(X, out, rows, cols, ld, w, molclr::as_stream(stream));
+  return molclr_colsum_impl(X, out, rows, cols, ld, accumulate, w, molclr::as_stream(stream));
 }
 
 MOLCLR_API size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t D) {
@@ -479,7 +511,7 @@ MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const fl
     size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
     hipLaunchKernelGGL(k_bn_stats_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)z, rows,
                        b.d4, b.band, rpp, (float4*)pmean, (float4*)pm2, pn);
-    hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, pmean, pm2,
+    hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, pmean, pm2,
                        pn, P, D, gamma, beta, running_mean, running_var, save_mean, save_invstd,
                        scale, shift, (float)momentum, (float)eps);
   } else {
@@ -500,7 +532,7 @@ MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float
                                     const float* beta, const float* save_mean,
                                     const float* save_invstd, float* dz, float* dgamma,
                                     float* dbeta, int64_t rows, int64_t D, int relu,
-                                    void* workspace, size_t workspace_bytes,
+                                    int accumulate, void* workspace, size_t workspace_bytes,
                                     molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_bwd: dim must be a multiple of 4");
   MOLCLR_REQUIRE(rows > 0 && dy && z && save_mean && save_invstd && dz, "batchnorm_bwd: bad args");
@@ -525,8 +557,8 @@ MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float
                      (const float4*)z, (const float4*)save_mean, (const float4*)save_invstd,
                      (const float4*)scale, (const float4*)shift, rows, b.d4, b.band, rpp, relu,
                      (float4*)p1, (float4*)p2);
-  hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, p1, p2, P, D,
-                     dgamma, dbeta, k1, k2, 1.0f / (float)rows);
+  hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, p1, p2, P, D,
+                     dgamma, dbeta, k1, k2, 1.0f / (float)rows, accumulate);
   int64_t total4 = rows * (D / 4);
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
                      (const float4*)dy, (const float4*)z, (const float4*)save_mean,

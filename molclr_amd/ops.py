@@ -24,9 +24,32 @@ from __future__ import annotations
 
 import torch
 
+import functools
+
 from . import _lib
-from ._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
+from ._lib import EPI_ACCUMULATE, EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
 from .data import DeviceGraph
+
+
+@functools.lru_cache(maxsize=4096)
+def _wsq(name: str, *args) -> int:
+    """Cached workspace-size query (pure function of the sizes)."""
+    return _lib.query(name, *args)
+
+
+def _grad_sink(param, shape, device):
+    """Where a parameter gradient is written.
+
+    A parameter owned by FusedAdam (flag ``_molclr_fused_grad``) already has
+    ``.grad`` as a view of the flat gradient buffer: the kernel adds into it
+    directly (accumulate = 1) and the autograd function returns None for that
+    input, so autograd launches no separate accumulation kernel.  Otherwise a
+    fresh tensor is returned to autograd as usual.
+    Returns (buffer, accumulate_flag, value_to_return)."""
+    if param is not None and getattr(param, "_molclr_fused_grad", False) and param.grad is not None:
+        return param.grad, 1, None
+    t = torch.empty(shape, dtype=torch.float32, device=device)
+    return t, 0, t
 
 
 def _check(*ts):
@@ -92,12 +115,14 @@ def set_kernel_timer(timer: KernelTimer | None) -> None:
 # GEMM helpers
 # ---------------------------------------------------------------------------
 def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
-         out=None):
-    """C[M,N] = op(A) op(B) (+ epilogue), see molclr_gemm_f32."""
+         out=None, accumulate=0):
+    """C[M,N] = op(A) op(B) (+ epilogue, + C if accumulate), see molclr_gemm_f32."""
     dev = A.device
     if out is None:
         out = torch.empty(M, N, dtype=torch.float32, device=dev)
-    ws_bytes = _lib.query("molclr_gemm_f32_workspace_bytes", M, N, K)
+    if accumulate:
+        epi |= EPI_ACCUMULATE
+    ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, N, K)
     ws = _ws(ws_bytes, dev) if ws_bytes else None
     t0 = _TIMER.begin() if _TIMER is not None else None
     _lib.call("molclr_gemm_f32", A.data_ptr(), B.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
@@ -116,26 +141,31 @@ def linear_fwd(x, W, b, relu=False):
     return gemm(x, W, M, N, K, K, K, False, False, epi, bias=b)
 
 
-def colsum(x):
+def colsum(x, out=None, accumulate=0):
     rows, cols = x.shape
-    ws_bytes = _lib.query("molclr_colsum_f32_workspace_bytes", rows, cols)
+    ws_bytes = _wsq("molclr_colsum_f32_workspace_bytes", rows, cols)
     ws = _ws(ws_bytes, x.device)
-    out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty(cols, dtype=torch.float32, device=x.device)
     _lib.call("molclr_colsum_f32", x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0),
-              ws.data_ptr(), ws_bytes, _stream(x))
+              int(accumulate), ws.data_ptr(), ws_bytes, _stream(x))
     return out
 
 
-def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=None):
-    """Backward of y = x W^T + b.  Returns (dx, dW, db)."""
+def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=None,
+               W_param=None, b_param=None):
+    """Backward of y = x W^T + b.  Returns (dx, dW, db); dW / db are None when
+    they were accumulated straight into a FusedAdam-owned .grad."""
     M, K = x.shape
     N = W.shape[0]
     dx = dW = db = None
     if need_w:
         # dW[N,K] = dy^T x : A = dy (K-major, lda=N), B = x (K-major, ldb=K)
-        dW = gemm(dy, x, N, K, M, N, K, True, True)
+        buf, acc, dW = _grad_sink(W_param, (N, K), dy.device)
+        gemm(dy, x, N, K, M, N, K, True, True, out=buf, accumulate=acc)
     if need_b:
-        db = colsum(dy)
+        buf, acc, db = _grad_sink(b_param, (N,), dy.device)
+        colsum(dy, out=buf, accumulate=acc)
     if need_x:
         # dx[M,K] = dy W : B(k=n, j) = W[n, j] (K-major, ldb=K)
         epi = EPI_RELU_MASK if relu_mask_src is not None else EPI_NONE
@@ -165,6 +195,7 @@ class _AtomEmbed(torch.autograd.Function):
                   h.data_ptr(), N, D, X1.shape[0], X2.shape[0], _stream(X1))
         ctx.save_for_backward(x_idx)
         ctx.shapes = (X1.shape[0], X2.shape[0], D)
+        ctx.params = (X1, X2)
         return h
 
     @staticmethod
@@ -173,13 +204,17 @@ class _AtomEmbed(torch.autograd.Function):
         n1, n2, D = ctx.shapes
         dh = _c(dh)
         N = x_idx.shape[0]
-        dX1 = torch.empty(n1, D, dtype=torch.float32, device=dh.device)
-        dX2 = torch.empty(n2, D, dtype=torch.float32, device=dh.device)
-        ws_bytes = _lib.query("molclr_atom_embed_bwd_workspace_bytes", N, D, n1, n2)
+        X1, X2 = ctx.params
+        b1, acc1, r1 = _grad_sink(X1, (n1, D), dh.device)
+        b2, acc2, r2 = _grad_sink(X2, (n2, D), dh.device)
+        if acc1 != acc2:  # mixed ownership: write fresh tensors for both
+            b1, acc1, r1 = _grad_sink(None, (n1, D), dh.device)
+            b2, acc2, r2 = _grad_sink(None, (n2, D), dh.device)
+        ws_bytes = _wsq("molclr_atom_embed_bwd_workspace_bytes", N, D, n1, n2)
         ws = _ws(ws_bytes, dh.device)
-        _lib.call("molclr_atom_embed_bwd", x_idx.data_ptr(), dh.data_ptr(), dX1.data_ptr(),
-                  dX2.data_ptr(), N, D, n1, n2, ws.data_ptr(), ws_bytes, _stream(dh))
-        return None, dX1, dX2
+        _lib.call("molclr_atom_embed_bwd", x_idx.data_ptr(), dh.data_ptr(), b1.data_ptr(),
+                  b2.data_ptr(), N, D, n1, n2, acc1, ws.data_ptr(), ws_bytes, _stream(dh))
+        return None, r1, r2
 
 
 class _GINEAggregate(torch.autograd.Function):
@@ -197,6 +232,7 @@ class _GINEAggregate(torch.autograd.Function):
             _TIMER.end("gine_aggregate_fwd", t0, gine_aggregate_bytes(N, D, graph.num_edges))
         ctx.graph = graph
         ctx.shapes = (N, D, E1.shape[0], E2.shape[0])
+        ctx.params = (E1, E2)
         return out
 
     @staticmethod
@@ -206,14 +242,27 @@ class _GINEAggregate(torch.autograd.Function):
         graph = ctx.graph
         need_x, need_e1, need_e2 = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         dx = torch.empty_like(g) if need_x else None
-        dE1 = torch.empty(n1, D, dtype=torch.float32, device=g.device) if need_e1 else None
-        dE2 = torch.empty(n2, D, dtype=torch.float32, device=g.device) if need_e2 else None
-        ws_bytes = _lib.query("molclr_gine_aggregate_bwd_workspace_bytes", N, D)
+        E1, E2 = ctx.params
+        b1 = b2 = r1 = r2 = None
+        acc = 0
+        if need_e1 and need_e2:
+            b1, a1, r1 = _grad_sink(E1, (n1, D), g.device)
+            b2, a2, r2 = _grad_sink(E2, (n2, D), g.device)
+            if a1 != a2:
+                b1, a1, r1 = _grad_sink(None, (n1, D), g.device)
+                b2, a2, r2 = _grad_sink(None, (n2, D), g.device)
+            acc = a1
+        elif need_e1 or need_e2:
+            if need_e1:
+                b1, _, r1 = _grad_sink(None, (n1, D), g.device)
+            else:
+                b2, _, r2 = _grad_sink(None, (n2, D), g.device)
+        ws_bytes = _wsq("molclr_gine_aggregate_bwd_workspace_bytes", N, D)
         ws = _ws(ws_bytes, g.device)
         _lib.call("molclr_gine_aggregate_bwd", g.data_ptr(), graph.rowptr_t.data_ptr(),
-                  graph.col_t.data_ptr(), graph.ecount.data_ptr(), _lib.ptr(dx), _lib.ptr(dE1),
-                  _lib.ptr(dE2), N, D, ws.data_ptr(), ws_bytes, _stream(g))
-        return dx, dE1, dE2, None
+                  graph.col_t.data_ptr(), graph.ecount.data_ptr(), _lib.ptr(dx), _lib.ptr(b1),
+                  _lib.ptr(b2), N, D, acc, ws.data_ptr(), ws_bytes, _stream(g))
+        return dx, r1, r2, None
 
 
 class _MLP(torch.autograd.Function):
@@ -227,17 +276,20 @@ class _MLP(torch.autograd.Function):
         a1 = linear_fwd(x, W1, b1, relu=True)
         z = linear_fwd(a1, W2, b2, relu=False)
         ctx.save_for_backward(x, W1, W2, a1)
+        ctx.params = (W1, b1, W2, b2)
         return z
 
     @staticmethod
     def backward(ctx, dz):
         x, W1, W2, a1 = ctx.saved_tensors
+        pW1, pb1, pW2, pb2 = ctx.params
         dz = _c(dz)
         need = ctx.needs_input_grad
         # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
         dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],
-                                   relu_mask_src=a1)
-        dx, dW1, db1 = linear_bwd(dz1, x, W1, need_x=need[0], need_w=need[1], need_b=need[2])
+                                   relu_mask_src=a1, W_param=pW2, b_param=pb2)
+        dx, dW1, db1 = linear_bwd(dz1, x, W1, need_x=need[0], need_w=need[1], need_b=need[2],
+                                  W_param=pW1, b_param=pb1)
         return dx, dW1, db1, dW2, db2
 
 
@@ -247,13 +299,15 @@ class _Linear(torch.autograd.Function):
         _check(x, W, b)
         x = _c(x)
         ctx.save_for_backward(x, W)
+        ctx.params = (W, b)
         return linear_fwd(x, W, b)
 
     @staticmethod
     def backward(ctx, dy):
         x, W = ctx.saved_tensors
         need = ctx.needs_input_grad
-        dx, dW, db = linear_bwd(_c(dy), x, W, need[0], need[1], need[2])
+        dx, dW, db = linear_bwd(_c(dy), x, W, need[0], need[1], need[2],
+                                W_param=ctx.params[0], b_param=ctx.params[1])
         return dx, dW, db
 
 
@@ -266,7 +320,7 @@ class _BatchNorm(torch.autograd.Function):
         y = torch.empty_like(z)
         save_mean = torch.empty(D, dtype=torch.float32, device=z.device)
         save_invstd = torch.empty(D, dtype=torch.float32, device=z.device)
-        ws_bytes = _lib.query("molclr_batchnorm_workspace_bytes", N, D)
+        ws_bytes = _wsq("molclr_batchnorm_workspace_bytes", N, D)
         ws = _ws(ws_bytes, z.device)
         _lib.call("molclr_batchnorm_fwd", z.data_ptr(), _lib.ptr(gamma), _lib.ptr(beta),
                   _lib.ptr(running_mean), _lib.ptr(running_var), y.data_ptr(),
@@ -274,6 +328,7 @@ class _BatchNorm(torch.autograd.Function):
                   float(eps), int(bool(training)), int(bool(relu)), ws.data_ptr(), ws_bytes,
                   _stream(z))
         ctx.save_for_backward(z, gamma, beta, save_mean, save_invstd)
+        ctx.params = (gamma, beta)
         ctx.relu = bool(relu)
         ctx.training = bool(training)
         return y
@@ -288,15 +343,19 @@ class _BatchNorm(torch.autograd.Function):
         dy = _c(dy)
         N, D = z.shape
         dz = torch.empty_like(z)
-        dgamma = torch.empty(D, dtype=torch.float32, device=z.device)
-        dbeta = torch.empty(D, dtype=torch.float32, device=z.device)
-        ws_bytes = _lib.query("molclr_batchnorm_workspace_bytes", N, D)
+        pg, pb = ctx.params
+        bg, ag, rg = _grad_sink(pg, (D,), z.device)
+        bb, ab, rb = _grad_sink(pb, (D,), z.device)
+        if ag != ab:
+            bg, ag, rg = _grad_sink(None, (D,), z.device)
+            bb, ab, rb = _grad_sink(None, (D,), z.device)
+        ws_bytes = _wsq("molclr_batchnorm_workspace_bytes", N, D)
         ws = _ws(ws_bytes, z.device)
         _lib.call("molclr_batchnorm_bwd", dy.data_ptr(), z.data_ptr(), _lib.ptr(gamma),
                   _lib.ptr(beta), save_mean.data_ptr(), save_invstd.data_ptr(), dz.data_ptr(),
-                  dgamma.data_ptr(), dbeta.data_ptr(), N, D, int(ctx.relu), ws.data_ptr(),
+                  bg.data_ptr(), bb.data_ptr(), N, D, int(ctx.relu), ag, ws.data_ptr(),
                   ws_bytes, _stream(z))
-        return dz, dgamma, dbeta, None, None, None, None, None, None
+        return dz, rg, rb, None, None, None, None, None, None
 
 
 POOL_MODES = {"mean": 0, "add": 1}
@@ -340,6 +399,7 @@ class _GCNConv(torch.autograd.Function):
                   bias.data_ptr(), out.data_ptr(), N, Dout, _stream(x))
         ctx.save_for_backward(x, W)
         ctx.graph = graph
+        ctx.params = (W, bias, E1, E2)
         return out
 
     @staticmethod
@@ -349,20 +409,27 @@ class _GCNConv(torch.autograd.Function):
         N, Din = x.shape
         Dout = W.shape[1]
         need = ctx.needs_input_grad
+        pW, pb, pE1, pE2 = ctx.params
         dxw = torch.empty(N, Dout, dtype=torch.float32, device=g.device)
-        dE1 = torch.empty(5, 1, dtype=torch.float32, device=g.device) if need[3] else None
-        dE2 = torch.empty(3, 1, dtype=torch.float32, device=g.device) if need[4] else None
-        db = torch.empty(Dout, dtype=torch.float32, device=g.device) if need[2] else None
-        ws_bytes = _lib.query("molclr_gcn_aggregate_bwd_workspace_bytes", N, Dout)
+        sinks = {}
+        owned = all(getattr(p, "_molclr_fused_grad", False) and p.grad is not None
+                    for p, n in ((pb, need[2]), (pE1, need[3]), (pE2, need[4])) if n)
+        for key, p, shape, n in (("b", pb, (Dout,), need[2]), ("e1", pE1, (5, 1), need[3]),
+                                 ("e2", pE2, (3, 1), need[4])):
+            sinks[key] = _grad_sink(p if owned else None, shape, g.device) if n else (None, 0, None)
+        acc = 1 if owned and any(need[2:5]) else 0
+        ws_bytes = _wsq("molclr_gcn_aggregate_bwd_workspace_bytes", N, Dout)
         ws = _ws(ws_bytes, g.device)
         _lib.call("molclr_gcn_aggregate_bwd", g.data_ptr(), ctx.graph.rowptr_t.data_ptr(),
                   ctx.graph.col_t.data_ptr(), ctx.graph.ecount.data_ptr(), dxw.data_ptr(),
-                  _lib.ptr(dE1), _lib.ptr(dE2), _lib.ptr(db), N, Dout, ws.data_ptr(), ws_bytes,
-                  _stream(g))
+                  _lib.ptr(sinks["e1"][0]), _lib.ptr(sinks["e2"][0]), _lib.ptr(sinks["b"][0]),
+                  N, Dout, acc, ws.data_ptr(), ws_bytes, _stream(g))
+        db, dE1, dE2 = sinks["b"][2], sinks["e1"][2], sinks["e2"][2]
         dx = dW = None
         if need[1]:
             # dW[Din,Dout] = x^T dxw
-            dW = gemm(x, dxw, Din, Dout, N, Din, Dout, True, True)
+            buf, a, dW = _grad_sink(pW, (Din, Dout), g.device)
+            gemm(x, dxw, Din, Dout, N, Din, Dout, True, True, out=buf, accumulate=a)
         if need[0]:
             # dx[N,Din] = dxw W^T : B(k=o, n=i) = W[i, o] (not K-major, ldb = Dout)
             dx = gemm(dxw, W, N, Din, Dout, Dout, Dout, False, False)
@@ -431,7 +498,7 @@ class _NTXent(torch.autograd.Function):
             gidx = torch.cat([base, base + B])
         lse = torch.empty(n, dtype=torch.float32, device=dev)
         loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
-        ws_bytes = _lib.query("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+        ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
         ws = _ws(ws_bytes, dev)
         _lib.call("molclr_ntxent_fwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n, 2 * B,
                   C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(), ws.data_ptr(),
@@ -458,7 +525,7 @@ class _NTXent(torch.autograd.Function):
         gloss = gloss.to(torch.float32).contiguous()
         st = _lib.stream_of(dev)
         drhat = torch.empty_like(rhat)
-        ws_bytes = _lib.query("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+        ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
         ws = _ws(ws_bytes, dev)
         _lib.call("molclr_ntxent_bwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
                   lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T, drhat.data_ptr(),

@@ -8,8 +8,10 @@ parameters are re-seated as views of one contiguous fp32 buffer and their
 
 * the optimizer step is a single kernel over every parameter;
 * data-parallel gradient reduction is one collective over ``flat_grad``;
-* autograd accumulates straight into the flat buffer (``zero_grad`` zeroes
-  it in place and never sets grads to ``None``).
+* the backward kernels of molclr_amd.ops accumulate straight into the flat
+  buffer (no separate autograd accumulation kernels); gradients produced by
+  other ops are accumulated there by autograd as usual.  ``zero_grad``
+  zeroes it in place and never sets grads to ``None``.
 
 Learning rate and step counter live on the device, so a captured step
 replays with the scheduler's current learning rate.  Parameters that receive
@@ -53,6 +55,9 @@ class FusedAdam(torch.optim.Optimizer):
                 self.flat[off:off + n].copy_(p.detach().reshape(-1))
                 p.data = self.flat[off:off + n].view_as(p)
                 p.grad = self.flat_grad[off:off + n].view_as(p)
+                # molclr_amd's backward kernels add straight into this .grad
+                # view (ops._grad_sink) instead of handing autograd a tensor
+                p._molclr_fused_grad = True
                 self.views.append((p, off, n))
                 off += _align4(n)
         self.numel = total

@@ -164,6 +164,30 @@ def test_c2_scale_forward_and_loss(dev, kind):
     check_grads(mine, ref64, cond)
 
 
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_fused_grad_accumulation_matches_autograd(dev, kind):
+    """FusedAdam-owned parameters get their gradients added in-kernel
+    (ops._grad_sink); the result must equal autograd's own accumulation over
+    the two views (bitwise: same kernels, same order)."""
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from molclr_amd.optim import FusedAdam
+    _, _, m1 = pair_models(kind, 3, 64, 128, seed=5)
+    m2 = copy.deepcopy(m1)
+    m1, m2 = m1.to(dev), m2.to(dev)
+    opt = FusedAdam(m2.parameters(), 5e-4, weight_decay=1e-5)
+    opt.zero_grad()
+    xi, xj = SyntheticPairBatches(32, seed=51).next()
+    xi, xj = xi.to(dev), xj.to(dev)
+    crit = NTXentLoss(dev, 32, 0.1, True)
+    for m in (m1, m2):
+        loss = crit(l2_normalize(m(xi)[1]), l2_normalize(m(xj)[1]))
+        loss.backward()
+    g2 = dict(m2.named_parameters())
+    for n, p in m1.named_parameters():
+        assert torch.allclose(p.grad, g2[n].grad, rtol=1e-6, atol=1e-7), n
+
+
 def test_step_is_deterministic(dev):
     """No atomics on any float path: two runs give bitwise-identical weights."""
     from molclr_amd.ginet_molclr import GINet
