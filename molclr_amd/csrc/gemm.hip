@@ -49,35 +49,44 @@ struct Stager {
   static constexpr int ITEMS = ROWS * BK / 4;  // float4 items per slice
   static constexpr int PER_THREAD = (ITEMS + T - 1) / T;
   float4 r[PER_THREAD];
+  uint32_t ok;  // bit j: item j in range (applied at store time, so the loads
+                // are never waited on until the LDS write that consumes them)
 
+  // Branch-free: out-of-range items load from a clamped (valid) address.
   __device__ __forceinline__ void load(const float* __restrict__ src, int64_t ld, int64_t row0,
                                        int64_t rows, int64_t k0, int64_t K, int tid, bool vec) {
+    ok = 0;
 #pragma unroll
     for (int j = 0; j < PER_THREAD; ++j) {
       const int idx = tid + j * T;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < ITEMS) {
-        if (!KMAJOR) {
-          const int row = idx / (BK / 4), k4 = idx % (BK / 4);
-          const int64_t gr = row0 + row, gk = k0 + 4 * k4;
-          if (gr < rows && gk < K) v = *reinterpret_cast<const float4*>(src + gr * ld + gk);
-        } else {
-          const int k = idx / (ROWS / 4), r4 = idx % (ROWS / 4);
-          const int64_t gk = k0 + k, gr = row0 + 4 * r4;
-          if (gk < K) {
-            const float* p = src + gk * ld + gr;
-            if (vec && gr + 3 < rows) {
-              v = *reinterpret_cast<const float4*>(p);
-            } else {
-              if (gr + 0 < rows) v.x = p[0];
-              if (gr + 1 < rows) v.y = p[1];
-              if (gr + 2 < rows) v.z = p[2];
-              if (gr + 3 < rows) v.w = p[3];
-            }
-          }
+      if (!KMAJOR) {
+        const int row = idx / (BK / 4), k4 = idx % (BK / 4);
+        const int64_t gr = row0 + row, gk = k0 + 4 * k4;
+        const bool in = idx < ITEMS && gr < rows && gk < K;
+        const int64_t cr = gr < rows ? gr : rows - 1, ck = gk < K ? gk : 0;
+        r[j] = *reinterpret_cast<const float4*>(src + cr * ld + ck);
+        ok |= (uint32_t)in << j;
+      } else {
+        const int k = idx / (ROWS / 4), r4 = idx % (ROWS / 4);
+        const int64_t gk = k0 + k, gr = row0 + 4 * r4;
+        const bool kin = idx < ITEMS && gk < K;
+        const int64_t ck = gk < K ? gk : K - 1;
+        if (vec) {
+          const bool in = kin && gr + 3 < rows;
+          const int64_t cr = gr + 3 < rows ? gr : 0;
+          r[j] = *reinterpret_cast<const float4*>(src + ck * ld + cr);
+          ok |= (uint32_t)in << j;
+        } else {  // unaligned rows: per-element guards (rare path)
+          const float* p = src + ck * ld;
+          float4 v;
+          v.x = (kin && gr + 0 < rows) ? p[gr + 0 < rows ? gr + 0 : 0] : 0.f;
+          v.y = (kin && gr + 1 < rows) ? p[gr + 1 < rows ? gr + 1 : 0] : 0.f;
+          v.z = (kin && gr + 2 < rows) ? p[gr + 2 < rows ? gr + 2 : 0] : 0.f;
+          v.w = (kin && gr + 3 < rows) ? p[gr + 3 < rows ? gr + 3 : 0] : 0.f;
+          r[j] = v;
+          ok |= 1u << j;
         }
       }
-      r[j] = v;
     }
   }
 
@@ -86,12 +95,13 @@ struct Stager {
     for (int j = 0; j < PER_THREAD; ++j) {
       const int idx = tid + j * T;
       if (idx < ITEMS) {
+        const float4 v = ((ok >> j) & 1u) ? r[j] : make_float4(0.f, 0.f, 0.f, 0.f);
         if (!KMAJOR) {
           const int row = idx / (BK / 4), k4 = idx % (BK / 4);
-          *reinterpret_cast<float4*>(lds + row * LDK + 4 * k4) = r[j];
+          *reinterpret_cast<float4*>(lds + row * LDK + 4 * k4) = v;
         } else {
           const int k = idx / (ROWS / 4), r4 = idx % (ROWS / 4);
-          *reinterpret_cast<float4*>(lds + k * (ROWS + RPAD) + 4 * r4) = r[j];
+          *reinterpret_cast<float4*>(lds + k * (ROWS + RPAD) + 4 * r4) = v;
         }
       }
     }
@@ -152,23 +162,16 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  Stager<AK, BM, T> sa;
-  Stager<BKM, BN, T> sb;
-  int cur = 0;
-  if (kt_beg < kt_end) {
-    sa.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid, avec);
-    sb.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tid, bvec);
-    sa.store(lds, tid);
-    sb.store(lds + AF, tid);
-    __syncthreads();
-  }
-  for (int kt = kt_beg; kt < kt_end; ++kt) {
-    const bool more = kt + 1 < kt_end;
-    if (more) {  // next slice in flight while this one is consumed
-      sa.load(A, lda, m0, M, (int64_t)(kt + 1) * BK, K, tid, avec);
-      sb.load(B, ldb, n0, N, (int64_t)(kt + 1) * BK, K, tid, bvec);
-    }
-    const float* As = lds + cur * (AF + BF);
+  // 3-stage pipeline: the global loads of slice k+2 are issued before slice k
+  // is computed and written to LDS after slice k+1 is computed, so every load
+  // has two compute phases to land; LDS is double-buffered (one barrier per
+  // slice).  Two named register sets (no runtime-indexed arrays).
+  Stager<AK, BM, T> sa0, sa1;
+  Stager<BKM, BN, T> sb0, sb1;
+  float* buf0 = lds;
+  float* buf1 = lds + (AF + BF);
+
+  auto compute = [&](const float* As) {
     const float* Bs = As + AF;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -187,14 +190,40 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a].w, bf[b].w, acc[a][b], 0, 0, 0);
         }
     }
-    if (more) {
-      float* nxt = lds + (cur ^ 1) * (AF + BF);
-      sa.store(nxt, tid);
-      sb.store(nxt + AF, tid);
+  };
+
+  const int nsteps = kt_end - kt_beg;
+  if (nsteps > 0) {
+    sa0.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid, avec);
+    sb0.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tid, bvec);
+    if (nsteps > 1) {
+      sa1.load(A, lda, m0, M, (int64_t)(kt_beg + 1) * BK, K, tid, avec);
+      sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + 1) * BK, K, tid, bvec);
     }
+    sa0.store(buf0, tid);
+    sb0.store(buf0 + AF, tid);
     __syncthreads();
-    cur ^= 1;
   }
+  // Straight-line body: loads past the last slice re-read a clamped (valid)
+  // slice and their LDS writes land in the buffer nobody reads any more.
+  int i = 0;
+  for (; i + 2 <= nsteps; i += 2) {
+    // slice i in buf0; slice i+1 in set 1; set 0 free
+    sa0.load(A, lda, m0, M, (int64_t)(kt_beg + i + 2) * BK, K, tid, avec);
+    sb0.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 2) * BK, K, tid, bvec);
+    compute(buf0);
+    sa1.store(buf1, tid);
+    sb1.store(buf1 + AF, tid);
+    __syncthreads();
+    // slice i+1 in buf1; slice i+2 in set 0; set 1 free
+    sa1.load(A, lda, m0, M, (int64_t)(kt_beg + i + 3) * BK, K, tid, avec);
+    sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 3) * BK, K, tid, bvec);
+    compute(buf1);
+    sa0.store(buf0, tid);
+    sb0.store(buf0 + AF, tid);
+    __syncthreads();
+  }
+  if (i < nsteps) compute(buf0);  // odd slice count: the last slice is in buf0
 
   // epilogue: acc register r of lane (li, lh) -> row (r&3) + 8*(r>>2) + 4*lh, col li
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
