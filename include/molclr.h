@@ -175,13 +175,15 @@ int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, in
  * BatchNorm1d over the rows of z [N,D] (+ ReLU), ginet_molclr.py:107-111.
  * training != 0: batch statistics (biased variance for normalising),
  *   running_mean/var updated in place with `momentum` and the unbiased
- *   variance, exactly as torch.nn.BatchNorm1d; save_mean / save_invstd [D]
- *   receive the statistics for the backward.
+ *   variance, exactly as torch.nn.BatchNorm1d, and *num_batches_tracked
+ *   (may be NULL) incremented; save_mean / save_invstd [D] receive the
+ *   statistics for the backward.
  * training == 0: running statistics are used and nothing is updated.
  * relu != 0 applies max(y, 0) to the output. */
 size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t dim);
 int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
-                         float* running_mean, float* running_var, float* y,
+                         float* running_mean, float* running_var,
+                         int64_t* num_batches_tracked, float* y,
                          float* save_mean, float* save_invstd, int64_t rows, int64_t dim,
                          double momentum, double eps, int training, int relu,
                          void* workspace, size_t workspace_bytes, molclr_stream_t stream);

@@ -48,8 +48,8 @@ SIGNATURES = {
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_batchnorm_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_double, c_double,
-                                     c_int, c_int, _P, c_size_t, _P]),
+    "molclr_batchnorm_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_double,
+                                     c_double, c_int, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, c_int,
                                      _P, c_size_t, _P]),
     "molclr_segment_pool_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),

@@ -44,10 +44,11 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
 __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
     const int64_t* __restrict__ x, const float* __restrict__ dh, int64_t N, int64_t D,
     int64_t n1, int64_t n2, int64_t rows_per_part, double* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) double tab[];  // [(n1+n2)][64]
+  // fp32 table within a partition (<= 128 rows), fp64 partials across partitions
+  extern __shared__ __attribute__((aligned(16))) float tab[];  // [(n1+n2)][64]
   const int lane = threadIdx.x;
   const int64_t nt = n1 + n2;
-  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.0;
+  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.f;
   const int64_t c = (int64_t)blockIdx.y * 64 + lane;
   const bool active = c < D;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
@@ -181,31 +182,33 @@ __global__ __launch_bounds__(64) void k_ecount_weighted_partial(
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
   int64_t end = beg + rows_per_part;
   if (end > N) end = N;
-  double acc[8][4];
+  // fp32 within a partition (<= 64 rows), fp64 across partitions
+  float4 acc[8];
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[s][q] = 0.0;
+  for (int s = 0; s < 8; ++s) acc[s] = f4zero();
   for (int64_t i = beg; i < end; ++i) {
     const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
-    int4 lo = ec[0], hi = ec[1];
-    float4 v = g[i * d4 + c];
-    int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int4 lo = ec[0], hi = ec[1];
+    const float4 v = g[i * d4 + c];
+    const int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-      if (cnt[s] == 0) continue;
-      double w = (double)cnt[s];
-      acc[s][0] += w * v.x;
-      acc[s][1] += w * v.y;
-      acc[s][2] += w * v.z;
-      acc[s][3] += w * v.w;
+      const float w = (float)cnt[s];
+      acc[s].x += w * v.x;
+      acc[s].y += w * v.y;
+      acc[s].z += w * v.z;
+      acc[s].w += w * v.w;
     }
   }
   double* out = partial + (int64_t)blockIdx.x * 8 * (4 * d4);
 #pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) out[s * 4 * d4 + 4 * c + q] = acc[s][q];
+  for (int s = 0; s < 8; ++s) {
+    double* o = out + s * 4 * d4 + 4 * c;
+    o[0] = acc[s].x;
+    o[1] = acc[s].y;
+    o[2] = acc[s].z;
+    o[3] = acc[s].w;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -323,13 +326,13 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
                                      void* workspace, size_t workspace_bytes,
                                      molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd: bad sizes");
-  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(double) <= 65536, "atom_embed_bwd: tables too large");
+  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd: tables too large");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
   hipStream_t s = molclr::as_stream(stream);
   int64_t P = atom_parts(N);
   int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
   double* partial = (double*)workspace;
-  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(double);
+  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
   hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
                      x, dh, N, D, n1, n2, rpp, partial);
   hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 64)), dim3(1024),

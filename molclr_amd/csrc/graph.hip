@@ -59,45 +59,54 @@ __global__ void k_graph_count(const int64_t* __restrict__ ei, const int64_t* __r
   atomicAdd(&ecount[d * MOLCLR_ECOUNT_STRIDE + 5 + bd], 1);
 }
 
-// Exclusive scan of deg[0..n) into ptr[0..n]; blockIdx.x selects one of two arrays.
+// Exclusive scan of deg[0..n) into ptr[0..n]; blockIdx.x selects one of two
+// arrays.  Tiles of 1024 elements (coalesced), 8 tiles' loads in flight per
+// thread, block-wide scan per tile with a running carry.
 __global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ degA,
                                                         int32_t* __restrict__ ptrA,
                                                         const int32_t* __restrict__ degB,
                                                         int32_t* __restrict__ ptrB, int64_t n) {
+  constexpr int CH = 8;
   const int32_t* deg = blockIdx.x == 0 ? degA : degB;
   int32_t* ptr = blockIdx.x == 0 ? ptrA : ptrB;
   __shared__ int32_t wsum[kScanThreads / 64];
-  int tid = threadIdx.x;
-  int64_t per = (n + kScanThreads - 1) / kScanThreads;
-  int64_t beg = tid * per, end = beg + per < n ? beg + per : n;
-  int32_t local = 0;
-  for (int64_t i = beg; i < end; ++i) local += deg[i];
-  // inclusive scan of `local` across the block
-  int lane = tid & 63, wid = tid >> 6;
-  int32_t v = local;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int32_t carry = 0;
+  for (int64_t base = 0; base < n; base += (int64_t)CH * kScanThreads) {
+    int32_t v[CH];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int32_t u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
-  if (lane == 63) wsum[wid] = v;
-  __syncthreads();
-  if (wid == 0) {
-    int32_t w = lane < kScanThreads / 64 ? wsum[lane] : 0;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      int32_t u = __shfl_up(w, o, 64);
-      if (lane >= o) w += u;
+    for (int c = 0; c < CH; ++c) {
+      int64_t idx = base + (int64_t)c * kScanThreads + tid;
+      v[c] = idx < n ? deg[idx] : 0;
     }
-    if (lane < kScanThreads / 64) wsum[lane] = w;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      int32_t x = v[c];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int32_t u = __shfl_up(x, o, 64);
+        if (lane >= o) x += u;
+      }
+      if (lane == 63) wsum[wid] = x;
+      __syncthreads();
+      if (wid == 0) {
+        int32_t w = lane < kScanThreads / 64 ? wsum[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          int32_t u = __shfl_up(w, o, 64);
+          if (lane >= o) w += u;
+        }
+        if (lane < kScanThreads / 64) wsum[lane] = w;
+      }
+      __syncthreads();
+      const int32_t before = (wid > 0 ? wsum[wid - 1] : 0) + x - v[c];
+      const int64_t idx = base + (int64_t)c * kScanThreads + tid;
+      if (idx < n) ptr[idx] = carry + before;
+      carry += wsum[kScanThreads / 64 - 1];
+      __syncthreads();
+    }
   }
-  __syncthreads();
-  int32_t run = v - local + (wid > 0 ? wsum[wid - 1] : 0);
-  for (int64_t i = beg; i < end; ++i) {
-    ptr[i] = run;
-    run += deg[i];
-  }
-  if (tid == kScanThreads - 1) ptr[n] = run;
+  if (tid == 0) ptr[n] = carry;
 }
 
 __global__ void k_graph_fill(const int32_t* __restrict__ src32, const int32_t* __restrict__ dst32,

@@ -18,8 +18,9 @@ namespace {
 constexpr int kT = 256;
 
 int64_t band_parts(int64_t rows, int band) {
-  // ~16 row-iterations per thread, at most 1024 partitions
-  int64_t P = molclr::ceil_div(rows, (int64_t)band * 16);
+  // ~48 row-iterations per thread (enough loads in flight per thread, few
+  // partials for the final merge), at most 1024 partitions
+  int64_t P = molclr::ceil_div(rows, (int64_t)band * 48);
   if (P > 1024) P = 1024;
   if (P < 1) P = 1;
   return P;
@@ -170,8 +171,9 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
     int64_t P, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ running_mean, float* __restrict__ running_var,
     float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ scale,
-    float* __restrict__ shift, float momentum, float eps) {
+    float* __restrict__ shift, float momentum, float eps, int64_t* __restrict__ nbt) {
   __shared__ float rn[kRedLanes][kRedCols], rm[kRedLanes][kRedCols], rq[kRedLanes][kRedCols];
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
   float n = 0.f, mean = 0.f, m2 = 0.f;
@@ -245,9 +247,19 @@ __global__ __launch_bounds__(kT) void k_bn_apply(const float4* __restrict__ z,
 }
 
 // BN backward pass 1: per-column Σ dyr and Σ dyr * xhat (fixed order).
+__device__ __forceinline__ void bn_coeffs4(const float* gamma, const float* beta, float4 mu,
+                                           float4 is, int c, float4& sc, float4& sh) {
+  float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c] : make_float4(1.f, 1.f, 1.f, 1.f);
+  float4 b = beta ? reinterpret_cast<const float4*>(beta)[c] : f4zero();
+  bn_coeffs(g.x, b.x, mu.x, is.x, sc.x, sh.x);
+  bn_coeffs(g.y, b.y, mu.y, is.y, sc.y, sh.y);
+  bn_coeffs(g.z, b.z, mu.z, is.z, sc.z, sh.z);
+  bn_coeffs(g.w, b.w, mu.w, is.w, sc.w, sh.w);
+}
+
 __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __restrict__ z,
                                  const float4* __restrict__ mean, const float4* __restrict__ invstd,
-                                 const float4* __restrict__ scale, const float4* __restrict__ shift,
+                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                  int64_t rows, int d4, int band, int64_t rows_per_part, int relu,
                                  float4* __restrict__ p1, float4* __restrict__ p2) {
   extern __shared__ __attribute__((aligned(16))) float4 red[];  // [2][band][d4]
@@ -259,7 +271,8 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
   if (end > rows) end = rows;
   float4 s1 = f4zero(), s2 = f4zero();
   if (live) {
-    float4 mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+    float4 mu = mean[c], is = invstd[c], sc, sh;
+    bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
     for (int64_t i = beg + r; i < end; i += band) {
       float4 g = dy[i * d4 + c], x = z[i * d4 + c];
       if (relu) {
@@ -318,13 +331,14 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
 
 __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
     const float4* __restrict__ dy, const float4* __restrict__ z, const float4* __restrict__ mean,
-    const float4* __restrict__ invstd, const float4* __restrict__ scale,
-    const float4* __restrict__ shift, const float4* __restrict__ k1,
+    const float4* __restrict__ invstd, const float* __restrict__ gamma,
+    const float* __restrict__ beta, const float4* __restrict__ k1,
     const float4* __restrict__ k2, float4* __restrict__ dz, int64_t total4, int d4, int relu) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total4) return;
   int c = (int)(t % d4);
-  float4 g = dy[t], x = z[t], mu = mean[c], is = invstd[c], sc = scale[c], sh = shift[c];
+  float4 g = dy[t], x = z[t], mu = mean[c], is = invstd[c], sc, sh;
+  bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
   float4 a = k1[c], b = k2[c];
   if (relu) {
     g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
@@ -487,7 +501,8 @@ MOLCLR_API size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t D) {
 }
 
 MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
-                                    float* running_mean, float* running_var, float* y,
+                                    float* running_mean, float* running_var,
+                                    int64_t* num_batches_tracked, float* y,
                                     float* save_mean, float* save_invstd, int64_t rows,
                                     int64_t D, double momentum, double eps, int training,
                                     int relu, void* workspace, size_t workspace_bytes,
@@ -513,7 +528,7 @@ MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const fl
                        b.d4, b.band, rpp, (float4*)pmean, (float4*)pm2, pn);
     hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, pmean, pm2,
                        pn, P, D, gamma, beta, running_mean, running_var, save_mean, save_invstd,
-                       scale, shift, (float)momentum, (float)eps);
+                       scale, shift, (float)momentum, (float)eps, num_batches_tracked);
   } else {
     hipLaunchKernelGGL(k_bn_eval_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma,
                        beta, running_mean, running_var, D, (float)eps, save_mean, save_invstd,
@@ -548,22 +563,19 @@ MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float
   float* shift = w.take<float>(D);
   float* k1 = w.take<float>(D);
   float* k2 = w.take<float>(D);
-  // the same coefficients as the forward (same expression -> same ReLU mask)
-  hipLaunchKernelGGL(k_bn_saved_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma, beta,
-                     save_mean, save_invstd, D, scale, shift);
+  // the forward's coefficient expression is recomputed in-kernel (same ReLU mask)
   int64_t rpp = molclr::ceil_div(rows, P);
   size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
   hipLaunchKernelGGL(k_bn_bwd_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)dy,
-                     (const float4*)z, (const float4*)save_mean, (const float4*)save_invstd,
-                     (const float4*)scale, (const float4*)shift, rows, b.d4, b.band, rpp, relu,
-                     (float4*)p1, (float4*)p2);
+                     (const float4*)z, (const float4*)save_mean, (const float4*)save_invstd, gamma,
+                     beta, rows, b.d4, b.band, rpp, relu, (float4*)p1, (float4*)p2);
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, p1, p2, P, D,
                      dgamma, dbeta, k1, k2, 1.0f / (float)rows, accumulate);
   int64_t total4 = rows * (D / 4);
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
                      (const float4*)dy, (const float4*)z, (const float4*)save_mean,
-                     (const float4*)save_invstd, (const float4*)scale, (const float4*)shift,
-                     (const float4*)k1, (const float4*)k2, (float4*)dz, total4, (int)(D / 4), relu);
+                     (const float4*)save_invstd, gamma, beta, (const float4*)k1, (const float4*)k2,
+                     (float4*)dz, total4, (int)(D / 4), relu);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -313,7 +313,8 @@ class _Linear(torch.autograd.Function):
 
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z, gamma, beta, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, z, gamma, beta, running_mean, running_var, training, momentum, eps, relu,
+                num_batches_tracked=None):
         _check(z, gamma, beta)
         z = _c(z)
         N, D = z.shape
@@ -323,7 +324,8 @@ class _BatchNorm(torch.autograd.Function):
         ws_bytes = _wsq("molclr_batchnorm_workspace_bytes", N, D)
         ws = _ws(ws_bytes, z.device)
         _lib.call("molclr_batchnorm_fwd", z.data_ptr(), _lib.ptr(gamma), _lib.ptr(beta),
-                  _lib.ptr(running_mean), _lib.ptr(running_var), y.data_ptr(),
+                  _lib.ptr(running_mean), _lib.ptr(running_var), _lib.ptr(num_batches_tracked),
+                  y.data_ptr(),
                   save_mean.data_ptr(), save_invstd.data_ptr(), N, D, float(momentum),
                   float(eps), int(bool(training)), int(bool(relu)), ws.data_ptr(), ws_bytes,
                   _stream(z))
@@ -355,7 +357,7 @@ class _BatchNorm(torch.autograd.Function):
                   _lib.ptr(beta), save_mean.data_ptr(), save_invstd.data_ptr(), dz.data_ptr(),
                   bg.data_ptr(), bb.data_ptr(), N, D, int(ctx.relu), ag, ws.data_ptr(),
                   ws_bytes, _stream(z))
-        return dz, rg, rb, None, None, None, None, None, None
+        return dz, rg, rb, None, None, None, None, None, None, None
 
 
 POOL_MODES = {"mean": 0, "add": 1}
@@ -558,15 +560,21 @@ def linear(x, W, b):
 
 def batch_norm(z, bn: torch.nn.BatchNorm1d, relu: bool):
     training = bn.training or not bn.track_running_stats
-    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
-    momentum = 0.0 if bn.momentum is None else bn.momentum
-    if bn.momentum is None and bn.training and bn.track_running_stats:
-        momentum = 1.0 / float(bn.num_batches_tracked.item())  # cumulative average (torch)
+    update = bn.training and bn.track_running_stats
+    nbt = bn.num_batches_tracked if update and bn.num_batches_tracked is not None else None
+    if bn.momentum is None:
+        if nbt is not None:
+            nbt.add_(1)  # cumulative average needs the count now (torch semantics)
+            momentum = 1.0 / float(nbt.item())
+            nbt = None
+        else:
+            momentum = 0.0
+    else:
+        momentum = bn.momentum  # num_batches_tracked += 1 happens in the stats kernel
     return _BatchNorm.apply(z, bn.weight, bn.bias,
                             bn.running_mean if bn.track_running_stats else None,
                             bn.running_var if bn.track_running_stats else None,
-                            training, momentum, bn.eps, relu)
+                            training, momentum, bn.eps, relu, nbt)
 
 
 def segment_pool(h, graph, mode: str):
