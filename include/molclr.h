@@ -165,6 +165,11 @@ int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t
                     int64_t ldaux, void* workspace, size_t workspace_bytes,
                     molclr_stream_t stream);
 
+/* Tuning knob (process-wide, not thread-safe; for benchmarks): 0 = LDS-staged
+ * 64x64 workgroup tiles (default), 1 = register-direct 64x64 per wave,
+ * 2 = register-direct 32x64 per wave. */
+int molclr_gemm_set_impl(int impl);
+
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
 int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,

@@ -253,6 +253,146 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Register-direct variant.  One wave owns a (32 TM) x (32 TN) tile; each
+// K-slice's A and B fragments are loaded straight from global memory into the
+// MFMA operand layout (lane (li, lh) holds row li, k = 16 lh .. 16 lh + 15:
+// four float4 loads of 64 contiguous bytes for a K-contiguous operand, 16
+// coalesced 128-byte rows for a K-major one), double-buffered by K-slice.  No
+// LDS and no barriers: fp32 MFMA needs only ~16 FLOP per byte from L2 at
+// 64 x 64 per wave, so the reuse LDS would provide across waves is not needed.
+// Out-of-range rows read a clamped row (their results are never stored); K
+// past the end is zeroed at use time (the mask select sits next to the MFMA,
+// so no load is waited on early).
+template <bool KMAJOR, int TT>
+struct DFrag {
+  float4 v[TT][4];
+  uint32_t kmask;  // bit (4*q + j): k = 16 lh + 4 q + j in range
+
+  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int64_t r0,
+                                       int64_t rows, int64_t k0, int64_t K, int li, int lh) {
+    const int64_t kb = k0 + 16 * lh;
+    kmask = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) kmask |= (uint32_t)(kb + j < K) << j;
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      int64_t r = r0 + t * 32 + li;
+      r = r < rows ? r : rows - 1;
+      if (!KMAJOR) {
+        const float* p = X + r * ld;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t k = kb + 4 * q;
+          v[t][q] = *reinterpret_cast<const float4*>(p + (k < K ? k : 0));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float e[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t k = kb + 4 * q + j;
+            e[j] = X[(k < K ? k : K - 1) * ld + r];
+          }
+          v[t][q] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ float get(int t, int q, int j) const {
+    const float4 x = v[t][q];
+    const float e = j == 0 ? x.x : (j == 1 ? x.y : (j == 2 ? x.z : x.w));
+    return ((kmask >> (4 * q + j)) & 1u) ? e : 0.f;
+  }
+};
+
+template <int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
+__global__ __launch_bounds__(256) void k_gemm_f32_direct(
+    const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
+    int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
+    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
+  constexpr int BM = TM * 32, BN = TN * 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int nt = ntm * ntn;
+  const int nwg = (nt + 3) / 4;
+  const int tile = xcd_remap(blockIdx.x, nwg) * 4 + wave;  // 4 neighbouring tiles per WG
+  if (tile >= nt) return;  // whole wave
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+  const int nk_total = (int)((K + BK - 1) / BK);
+  const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
+  int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
+  if (kt_end > nk_total) kt_end = nk_total;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  DFrag<AK, TM> fa0, fa1;
+  DFrag<BKM, TN> fb0, fb1;
+  auto compute = [&](const DFrag<AK, TM>& fa, const DFrag<BKM, TN>& fb) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.get(a, q, j), fb.get(b, q, j),
+                                                             acc[a][b], 0, 0, 0);
+  };
+  const int nsteps = kt_end - kt_beg;
+  if (nsteps > 0) {
+    fa0.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, li, lh);
+    fb0.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, li, lh);
+  }
+  int i = 0;
+  for (; i + 2 <= nsteps; i += 2) {
+    fa1.load(A, lda, m0, M, (int64_t)(kt_beg + i + 1) * BK, K, li, lh);
+    fb1.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 1) * BK, K, li, lh);
+    compute(fa0, fb0);
+    fa0.load(A, lda, m0, M, (int64_t)(kt_beg + i + 2) * BK, K, li, lh);
+    fb0.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 2) * BK, K, li, lh);
+    compute(fa1, fb1);
+  }
+  if (i < nsteps) compute(fa0, fb0);
+
+  float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
+  const int64_t ldo = SPLIT ? N : ldc;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t n = n0 + b * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= M) continue;
+        float v = acc[a][b][r];
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
+          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+          if (accumulate) v += Cout[m * ldo + n];
+        }
+        Cout[m * ldo + n] = v;
+      }
+    }
+  }
+}
+
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
 template <int EPI>
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
@@ -281,8 +421,18 @@ struct Cfg {
 // tiling leaves 600 tiles for 512 resident slots: a 17%-full second wave).
 Cfg pick_cfg(int64_t, int64_t) { return {2, 2, 1, 1}; }
 
+// 0 = LDS-staged 64x64 (default), 1 = register-direct 64x64 per wave,
+// 2 = register-direct 32x64 per wave (tuning knob, molclr_gemm_set_impl)
+int g_impl = 0;
+int tiles_for(int impl, int64_t M, int64_t N) {
+  if (impl == 1) return (int)((((M + 63) / 64) * ((N + 63) / 64) + 3) / 4);
+  if (impl == 2) return (int)((((M + 31) / 32) * ((N + 63) / 64) + 3) / 4);
+  return (int)(((M + 63) / 64) * ((N + 63) / 64));
+}
+
 int pick_splits(const Cfg& c, int64_t M, int64_t N, int64_t K) {
-  int64_t tiles = ((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn());
+  (void)c;
+  int64_t tiles = tiles_for(g_impl, M, N) * (g_impl ? 4 : 1);
   int64_t nk = (K + BK - 1) / BK;
   if (tiles >= 512 || nk < 16) return 1;
   int64_t s = (1024 + tiles - 1) / tiles;
@@ -302,6 +452,18 @@ struct Args {
 
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
+  if (g_impl == 1) {
+    hipLaunchKernelGGL((k_gemm_f32_direct<2, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
+                       a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
+                       a.accumulate);
+    return;
+  }
+  if (g_impl == 2) {
+    hipLaunchKernelGGL((k_gemm_f32_direct<1, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
+                       a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
+                       a.accumulate);
+    return;
+  }
   hipLaunchKernelGGL((k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
                      0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
                      a.ldaux, a.kps, a.accumulate);
@@ -376,7 +538,7 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     return MOLCLR_ERR_UNSUPPORTED;
   }
   Cfg c = pick_cfg(M, N);
-  int64_t tiles = ((M + c.bm() - 1) / c.bm()) * ((N + c.bn() - 1) / c.bn());
+  int64_t tiles = tiles_for(g_impl, M, N);  // workgroups along x
   MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
   int sp = pick_splits(c, M, N, K);
   if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
@@ -418,5 +580,11 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     return MOLCLR_ERR_UNSUPPORTED;
   }
   MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gemm_set_impl(int impl) {
+  MOLCLR_REQUIRE(impl >= 0 && impl <= 2, "gemm_set_impl: impl must be 0, 1 or 2");
+  g_impl = impl;
   return MOLCLR_OK;
 }

@@ -61,11 +61,34 @@ def main():
     ]
     print(f"rows={Nr}  (fp32; torch.backends.cuda.matmul.allow_tf32="
           f"{torch.backends.cuda.matmul.allow_tf32})")
+    from molclr_amd import _lib
+    lib = _lib.load()
     for name, flops, mine, ref in cases:
-        tm = timeit(mine)
+        res = []
+        for impl in (0, 1, 2):
+            lib.molclr_gemm_set_impl(impl)
+            tm = timeit(mine)
+            res.append(f"impl{impl} {tm*1e6:6.1f}us {flops/tm/1e12:5.1f}TF")
+        lib.molclr_gemm_set_impl(0)
         tr = timeit(ref)
-        print(f"{name:28s} mine {tm*1e6:7.1f} us {flops/tm/1e12:6.1f} TF/s | "
-              f"torch {tr*1e6:7.1f} us {flops/tr/1e12:6.1f} TF/s")
+        print(f"{name:26s} " + " | ".join(res) + f" | torch {tr*1e6:6.1f}us {flops/tr/1e12:5.1f}TF",
+              flush=True)
+    # correctness of every impl on one shape per layout
+    torch.manual_seed(1)
+    for impl in (1, 2):
+        lib.molclr_gemm_set_impl(impl)
+        for (ak, bk) in ((0, 0), (0, 1), (1, 1), (1, 0)):
+            M, N, K = 333, 300, 1000
+            Am = torch.randn(M, K, dtype=torch.float64)
+            Bm = torch.randn(K, N, dtype=torch.float64)
+            A = (Am.t() if ak else Am).contiguous().float().to(dev)
+            Bt = (Bm if bk else Bm.t()).contiguous().float().to(dev)
+            out = ops.gemm(A, Bt, M, N, K, M if ak else K, N if bk else K, ak, bk)
+            ref = Am @ Bm
+            err = ((out.double().cpu() - ref).norm() / ref.norm()).item()
+            print(f"impl{impl} ak={ak} bk={bk} rel err {err:.2e}", flush=True)
+            assert err < 1e-5
+    lib.molclr_gemm_set_impl(0)
 
 
 if __name__ == "__main__":
