@@ -172,42 +172,60 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restric
   dx[t] = acc;
 }
 
-// Edge-table gradient partials (fp64): partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c]
-// grid (P, ceil(d4/64)), block 64; thread = one float4 column.
-__global__ __launch_bounds__(64) void k_ecount_weighted_partial(
-    const float4* __restrict__ g, const int32_t* __restrict__ ecount, int64_t N, int d4,
-    int64_t rows_per_part, double* __restrict__ partial) {
-  const int c = blockIdx.y * 64 + threadIdx.x;
-  if (c >= d4) return;
+// Edge-table gradient partials: partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c].
+// Band layout (a block covers `band` rows x all D/4 float4 columns, 1 KiB
+// contiguous per wave); fp32 within a partition, fp64 partials across.
+__global__ void k_ecount_weighted_partial(const float4* __restrict__ g,
+                                          const int32_t* __restrict__ ecount, int64_t N, int d4,
+                                          int band, int64_t rows_per_part,
+                                          double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float4 red[];  // [band][8][d4]
+  const int tid = threadIdx.x;
+  const bool live = tid < band * d4;
+  const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
   int64_t end = beg + rows_per_part;
   if (end > N) end = N;
-  // fp32 within a partition (<= 64 rows), fp64 across partitions
   float4 acc[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = f4zero();
-  for (int64_t i = beg; i < end; ++i) {
-    const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
-    const int4 lo = ec[0], hi = ec[1];
-    const float4 v = g[i * d4 + c];
-    const int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  if (live) {
+#pragma unroll 2
+    for (int64_t i = beg + r; i < end; i += band) {
+      const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
+      const int4 lo = ec[0], hi = ec[1];
+      const float4 v = g[i * d4 + c];
+      const int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const float w = (float)cnt[s];
-      acc[s].x += w * v.x;
-      acc[s].y += w * v.y;
-      acc[s].z += w * v.z;
-      acc[s].w += w * v.w;
+      for (int s = 0; s < 8; ++s) {
+        const float w = (float)cnt[s];
+        acc[s].x += w * v.x;
+        acc[s].y += w * v.y;
+        acc[s].z += w * v.z;
+        acc[s].w += w * v.w;
+      }
     }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) red[(r * 8 + s) * d4 + c] = acc[s];
   }
+  __syncthreads();
+  if (!live || r != 0) return;
   double* out = partial + (int64_t)blockIdx.x * 8 * (4 * d4);
 #pragma unroll
   for (int s = 0; s < 8; ++s) {
+    double x = 0.0, y = 0.0, z = 0.0, w = 0.0;
+    for (int q = 0; q < band; ++q) {
+      const float4 v = red[(q * 8 + s) * d4 + c];
+      x += v.x;
+      y += v.y;
+      z += v.z;
+      w += v.w;
+    }
     double* o = out + s * 4 * d4 + 4 * c;
-    o[0] = acc[s].x;
-    o[1] = acc[s].y;
-    o[2] = acc[s].z;
-    o[3] = acc[s].w;
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+    o[3] = w;
   }
 }
 
@@ -285,9 +303,9 @@ int64_t atom_parts(int64_t N) {
   if (P < 1) P = 1;
   return P;
 }
-int64_t ecount_parts(int64_t N) {
-  int64_t P = molclr::ceil_div(N, 64);
-  if (P > 256) P = 256;
+int64_t ecount_parts(int64_t N, int band) {
+  int64_t P = molclr::ceil_div(N, (int64_t)band * 16);
+  if (P > 1024) P = 1024;
   if (P < 1) P = 1;
   return P;
 }
@@ -358,7 +376,7 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
 }
 
 MOLCLR_API size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t N, int64_t D) {
-  return (size_t)ecount_parts(N) * 8 * D * sizeof(double) + 256;
+  return (size_t)ecount_parts(N, molclr::make_band(D).band) * 8 * D * sizeof(double) + 256;
 }
 
 MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t,
@@ -375,11 +393,14 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
   }
   if (dE1 || dE2) {
     MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
-    int64_t P = ecount_parts(N);
+    molclr::Band b = molclr::make_band(D);
+    int64_t P = ecount_parts(N, b.band);
     int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
     double* partial = (double*)workspace;
-    hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P, molclr::ceil_div(d4, 64)), dim3(64), 0,
-                       s, (const float4*)g, ecount, N, d4, rpp, partial);
+    size_t lds = (size_t)b.band * 8 * b.d4 * sizeof(float4);
+    MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd: dim too large for the edge-table reduction");
+    hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P), dim3(b.threads), lds, s,
+                       (const float4*)g, ecount, N, d4, b.band, rpp, partial);
     hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 64)), dim3(1024), 0, s,
                        partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2, accumulate);
   }

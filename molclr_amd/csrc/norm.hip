@@ -18,9 +18,9 @@ namespace {
 constexpr int kT = 256;
 
 int64_t band_parts(int64_t rows, int band) {
-  // ~48 row-iterations per thread (enough loads in flight per thread, few
-  // partials for the final merge), at most 1024 partitions
-  int64_t P = molclr::ceil_div(rows, (int64_t)band * 48);
+  // ~16 row-iterations per thread: many blocks keep enough loads in flight;
+  // the final merge over the partitions is parallel (k_*_final)
+  int64_t P = molclr::ceil_div(rows, (int64_t)band * 16);
   if (P > 1024) P = 1024;
   if (P < 1) P = 1;
   return P;
@@ -39,8 +39,10 @@ __global__ void k_colsum_partial(const float4* __restrict__ X, int64_t rows, int
   int64_t end = beg + rows_per_part;
   if (end > rows) end = rows;
   float4 acc = f4zero();
-  if (live)
+  if (live) {
+#pragma unroll 4
     for (int64_t i = beg + r; i < end; i += band) acc = f4add(acc, X[i * ld4 + c]);
+  }
   if (live) red[r * d4 + c] = acc;
   __syncthreads();
   if (live && r == 0) {
@@ -113,6 +115,7 @@ __global__ void k_bn_stats_partial(const float4* __restrict__ z, int64_t rows, i
   float n = 0.f;
   float4 mean = f4zero(), m2 = f4zero();
   if (live) {
+#pragma unroll 4
     for (int64_t i = beg + r; i < end; i += band) {
       float4 x = z[i * d4 + c];
       n += 1.f;
@@ -273,6 +276,7 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
   if (live) {
     float4 mu = mean[c], is = invstd[c], sc, sh;
     bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
+#pragma unroll 4
     for (int64_t i = beg + r; i < end; i += band) {
       float4 g = dy[i * d4 + c], x = z[i * d4 + c];
       if (relu) {
