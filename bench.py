@@ -15,10 +15,12 @@ one rank per GPU over RCCL: the NT-Xent batch is global (512 N), weak scaling.
 
 The JSON line adds:
   roofline      — the GIN scatter-add (molclr_gine_aggregate_fwd), HBM-bound:
-                  algorithmic bytes per launch / HIP-event launch time in the
-                  timed region, against 8.0 TB/s.
-  roofline_mfma — all fp32 MFMA GEMM launches in the timed region, against
-                  157.3 TF/s (fp32 dense MFMA peak).
+                  algorithmic bytes per launch / mean kernel duration in the
+                  timed region, against 8.0 TB/s.  Durations are the
+                  dispatch-recorded events of hipExtLaunchKernelGGL
+                  (molclr_ktimer_*), i.e. the kernel's own execution window.
+  roofline_mfma — all molclr_gemm_f32 kernels (GEMM + split-K reduce) in the
+                  timed region, against 157.3 TF/s (fp32 dense MFMA peak).
   cpu_baseline  — the oracle (CPU restatement of the reference step, incl.
                   the broadcast-cosine NT-Xent) on this host, rank 0, N=1 only,
                   a bounded sample of the same workload.
@@ -183,7 +185,8 @@ def main():
                         "traffic": load_pmc_traffic(),
                         "bytes_per_launch": int(per_launch_bytes),
                         "us_per_launch": round(per_launch_s * 1e6, 2),
-                        "launches": agg["launches"]}
+                        "launches": agg["launches"],
+                        "timing": "hipExtLaunchKernelGGL dispatch events"}
         gm = s.get("gemm_f32")
         if gm:
             tfs = gm["work"] / (gm["ms"] / 1e3) / 1e12

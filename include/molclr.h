@@ -258,6 +258,21 @@ int molclr_adam_step(float* param, const float* grad, float* exp_avg, float* exp
                      int64_t n, const float* lr, int32_t* step, double beta1, double beta2,
                      double eps, double weight_decay, molclr_stream_t stream);
 
+/* ---- Benchmark instrumentation (no reference counterpart) -------------------
+ * Opt-in kernel timer.  While a kind is enabled, its launches go through
+ * hipExtLaunchKernelGGL with a start/stop event pair recorded by the dispatch
+ * itself, so each sample is the kernel's own execution window (the figure
+ * rocprofv3 --kernel-trace reports).  Kinds: 1 = k_gine_agg_fwd,
+ * 2 = every kernel of molclr_gemm_f32 (main GEMM + split-K reduce). */
+#define MOLCLR_KTIMER_GINE_AGG 1
+#define MOLCLR_KTIMER_GEMM 2
+int molclr_ktimer_start(int kinds_mask);
+/* Waits for the recorded launches of `kind`, returns their summed duration
+ * and count, and forgets them. */
+int molclr_ktimer_read(int kind, double* total_ms, int64_t* launches);
+/* Disables timing and discards unread samples. */
+int molclr_ktimer_stop(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,10 +67,15 @@ SIGNATURES = {
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
+    "molclr_ktimer_start": (c_int, [c_int]),
+    "molclr_ktimer_read": (c_int, [c_int, _P, _P]),
+    "molclr_ktimer_stop": (c_int, []),
 }
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
 EPI_ACCUMULATE = 16
+KTIMER_GINE_AGG = 1
+KTIMER_GEMM = 2
 
 
 class MolclrError(RuntimeError):

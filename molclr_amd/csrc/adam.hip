@@ -11,6 +11,9 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+#include <vector>
+
 namespace molclr {
 static thread_local char g_err[512] = "";
 void set_error(const char* fmt, ...) {
@@ -18,6 +21,20 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
+}
+
+struct TimerRec {
+  int kind;
+  hipEvent_t e0, e1;
+};
+static std::mutex g_tmu;
+static int g_tmask = 0;
+static std::vector<TimerRec> g_trecs;
+
+bool timer_wants(int kind) { return (g_tmask & kind) != 0; }
+void timer_record(int kind, hipEvent_t e0, hipEvent_t e1) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_trecs.push_back({kind, e0, e1});
 }
 }  // namespace molclr
 
@@ -75,5 +92,47 @@ MOLCLR_API int molclr_adam_step(float* param, const float* grad, float* exp_avg,
                        n4, lr, step, (float)beta1, (float)beta2, (float)eps, (float)weight_decay);
   hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);
   MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ktimer_start(int kinds) {
+  std::lock_guard<std::mutex> lk(molclr::g_tmu);
+  molclr::g_tmask = kinds;
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ktimer_read(int kind, double* total_ms, int64_t* launches) {
+  MOLCLR_REQUIRE(total_ms && launches, "ktimer_read: null output");
+  std::lock_guard<std::mutex> lk(molclr::g_tmu);
+  double ms = 0.0;
+  int64_t n = 0;
+  std::vector<molclr::TimerRec> keep;
+  for (auto& r : molclr::g_trecs) {
+    if (r.kind != kind) {
+      keep.push_back(r);
+      continue;
+    }
+    float t = 0.f;
+    if (hipEventSynchronize(r.e1) == hipSuccess && hipEventElapsedTime(&t, r.e0, r.e1) == hipSuccess) {
+      ms += t;
+      ++n;
+    }
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  molclr::g_trecs.swap(keep);
+  *total_ms = ms;
+  *launches = n;
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ktimer_stop(void) {
+  std::lock_guard<std::mutex> lk(molclr::g_tmu);
+  molclr::g_tmask = 0;
+  for (auto& r : molclr::g_trecs) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
+  molclr::g_trecs.clear();
   return MOLCLR_OK;
 }

@@ -368,9 +368,10 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && rowptr && E1 && E2 && out, "gine_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_gine_agg_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), (const float4*)x, rowptr, col, ecode,
-                     (const float4*)E1, (const float4*)E2, (float4*)out, N, d4);
+  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd,
+                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
+                       (const float4*)x, rowptr, col, ecode, (const float4*)E1,
+                       (const float4*)E2, (float4*)out, N, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -1,6 +1,7 @@
 // Shared helpers for the MolCLR gfx950 kernels (see include/molclr.h for the ABI).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
@@ -53,6 +54,29 @@ inline Band make_band(int64_t dim) {
   b.band = band;
   b.threads = (band * b.d4 + 63) / 64 * 64;
   return b;
+}
+
+// Opt-in per-launch kernel timer (molclr_ktimer_*; benchmarks only).  A timed
+// launch goes through hipExtLaunchKernelGGL, whose start/stop events are
+// written by the kernel dispatch itself: the elapsed time is the kernel's own
+// execution window (what rocprofv3's kernel trace reports), not a bracket of
+// separately queued event packets.
+enum { kTimeGineAgg = MOLCLR_KTIMER_GINE_AGG, kTimeGemm = MOLCLR_KTIMER_GEMM };
+bool timer_wants(int kind);
+void timer_record(int kind, hipEvent_t start, hipEvent_t stop);
+
+template <typename... Args, typename F = void (*)(Args...)>
+void launch_timed(int kind, F kernel, dim3 grid, dim3 block, uint32_t shmem,
+                  hipStream_t stream, Args... args) {
+  if (timer_wants(kind)) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, e0, e1, 0u, args...);
+      timer_record(kind, e0, e1);
+      return;
+    }
+  }
+  hipLaunchKernelGGL(kernel, grid, block, shmem, stream, args...);
 }
 
 }  // namespace molclr

@@ -453,18 +453,18 @@ struct Args {
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   if (g_impl == 1) {
-    hipLaunchKernelGGL((k_gemm_f32_direct<2, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32_direct<2, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
                        a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
                        a.accumulate);
     return;
   }
   if (g_impl == 2) {
-    hipLaunchKernelGGL((k_gemm_f32_direct<1, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32_direct<1, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
                        a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
                        a.accumulate);
     return;
   }
-  hipLaunchKernelGGL((k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
                      0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
                      a.ldaux, a.kps, a.accumulate);
 }
@@ -558,19 +558,19 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
       dim3 g((unsigned)molclr::ceil_div(M * N, 256));
       switch (epilogue) {
         case MOLCLR_EPI_NONE:
-          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s, partial, sp, M,
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s, partial, sp, M,
                              N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         case MOLCLR_EPI_BIAS:
-          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s, partial, sp, M,
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s, partial, sp, M,
                              N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         case MOLCLR_EPI_BIAS_RELU:
-          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0, s, partial, sp,
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0, s, partial, sp,
                              M, N, C, ldc, bias, aux, ldaux, accumulate);
           break;
         default:
-          hipLaunchKernelGGL(k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0, s, partial, sp,
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0, s, partial, sp,
                              M, N, C, ldc, bias, aux, ldaux, accumulate);
       }
     }

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import torch
 
+import ctypes
 import functools
 
 from . import _lib
@@ -73,33 +74,39 @@ def _stream(t: torch.Tensor) -> int:
 
 
 class KernelTimer:
-    """Optional HIP-event bracketing of selected launches (used by bench.py).
+    """Per-kernel timing of the scatter-add and GEMM launches (used by bench.py).
 
-    Events are recorded on torch's current stream, which is the stream every
-    entry point is launched on, so elapsed times bracket exactly one kernel
-    (plus the event overhead)."""
+    Durations come from the library's dispatch-recorded events
+    (molclr_ktimer_*, hipExtLaunchKernelGGL): each sample is the kernel's own
+    execution window, the same figure rocprofv3's kernel trace reports.  This
+    class only counts calls and adds up their algorithmic work (bytes for the
+    scatter-add, 2MNK flops for a GEMM)."""
+
+    KINDS = {"gine_aggregate_fwd": _lib.KTIMER_GINE_AGG, "gemm_f32": _lib.KTIMER_GEMM}
 
     def __init__(self):
-        self.records = []  # (kind, start_event, end_event, work)
+        self.work = {k: 0.0 for k in self.KINDS}
+        self.calls = {k: 0 for k in self.KINDS}
+        mask = 0
+        for v in self.KINDS.values():
+            mask |= v
+        _lib.call("molclr_ktimer_start", mask)
 
-    def begin(self):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
-
-    def end(self, kind, e0, work):
-        e1 = torch.cuda.Event(enable_timing=True)
-        e1.record()
-        self.records.append((kind, e0, e1, work))
+    def add(self, kind, work):
+        self.work[kind] += work
+        self.calls[kind] += 1
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for kind, e0, e1, work in self.records:
-            d = out.setdefault(kind, {"launches": 0, "ms": 0.0, "work": 0.0})
-            d["launches"] += 1
-            d["ms"] += e0.elapsed_time(e1)
-            d["work"] += work
+        for kind, code in self.KINDS.items():
+            ms = ctypes.c_double(0.0)
+            n = ctypes.c_int64(0)
+            _lib.call("molclr_ktimer_read", code, ctypes.addressof(ms), ctypes.addressof(n))
+            if self.calls[kind]:
+                out[kind] = {"launches": self.calls[kind], "kernel_launches": n.value,
+                             "ms": ms.value, "work": self.work[kind]}
+        _lib.call("molclr_ktimer_stop")
         return out
 
 
@@ -124,12 +131,11 @@ def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, a
         epi |= EPI_ACCUMULATE
     ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, N, K)
     ws = _ws(ws_bytes, dev) if ws_bytes else None
-    t0 = _TIMER.begin() if _TIMER is not None else None
     _lib.call("molclr_gemm_f32", A.data_ptr(), B.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
               out.stride(0), int(a_kmajor), int(b_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
               aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A))
-    if t0 is not None:
-        _TIMER.end("gemm_f32", t0, 2.0 * M * N * K)
+    if _TIMER is not None:
+        _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
 
 
@@ -224,12 +230,11 @@ class _GINEAggregate(torch.autograd.Function):
         h = _c(h)
         N, D = h.shape
         out = torch.empty_like(h)
-        t0 = _TIMER.begin() if _TIMER is not None else None
         _lib.call("molclr_gine_aggregate_fwd", h.data_ptr(), graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), graph.ecode.data_ptr(), E1.data_ptr(), E2.data_ptr(),
                   out.data_ptr(), N, D, _stream(h))
-        if t0 is not None:
-            _TIMER.end("gine_aggregate_fwd", t0, gine_aggregate_bytes(N, D, graph.num_edges))
+        if _TIMER is not None:
+            _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges))
         ctx.graph = graph
         ctx.shapes = (N, D, E1.shape[0], E2.shape[0])
         ctx.params = (E1, E2)

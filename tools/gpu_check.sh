@@ -16,6 +16,9 @@ for s in $steps; do
   case $s in
     kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
     models)  run models 900 python -m pytest tests/test_gpu_models.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    pmc)     export TMPDIR=/tmp; rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
+             run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
+             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     gemm)    run gemm 300 python tools/gemm_bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     smoke)   run smoke 300 python __graft_entry__.py smoke; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench)   run bench 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
