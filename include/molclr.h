@@ -165,10 +165,12 @@ int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t
                     int64_t ldaux, void* workspace, size_t workspace_bytes,
                     molclr_stream_t stream);
 
-/* Tuning knob (process-wide, not thread-safe; for benchmarks): 0 = LDS-staged
- * 64x64 workgroup tiles (default), 1 = register-direct 64x64 per wave,
- * 2 = register-direct 32x64 per wave. */
+/* Implementation switch (process-wide, not thread-safe): 0 = f32-input MFMA
+ * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 = split-bf16 ("x6": each fp32
+ * operand split exactly into 3 bf16 parts, six bf16 MFMA products, fp32
+ * accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64. */
 int molclr_gemm_set_impl(int impl);
+int molclr_gemm_get_impl(void);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);

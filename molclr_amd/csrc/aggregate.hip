@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
     const float4* __restrict__ E1, const float4* __restrict__ E2, float4* __restrict__ out,
     int64_t N, int d4) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restric
                                                          const int32_t* __restrict__ col_t,
                                                          float4* __restrict__ dx, int64_t N,
                                                          int d4) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t j = t / d4;
   int c = (int)(t - j * d4);
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kT) void k_gcn_agg_fwd(
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
     const float* __restrict__ E1, const float* __restrict__ E2, const float4* __restrict__ bias,
     float4* __restrict__ out, int64_t N, int d4) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);

@@ -113,6 +113,18 @@ void launch_timed(int kind, F kernel, dim3 grid, dim3 block, uint32_t shmem,
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+// Workgroups are dealt round-robin to the 8 XCDs (bid % 8), each with its own
+// L2.  Remapping so XCD x runs a contiguous range of logical blocks keeps
+// neighbouring rows -- e.g. the atoms of one molecule that gather each other's
+// features -- inside one L2 instead of fetching every row into several.
+// Bijective for any nwg.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  int q = nwg / 8, r = nwg % 8;
+  int x = bid % 8, pos = bid / 8;
+  int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + pos;
+}
+
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
 __device__ __forceinline__ float wave_sum(float v) {

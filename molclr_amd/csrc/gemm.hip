@@ -116,14 +116,6 @@ __device__ __forceinline__ float4 frag(const float* __restrict__ lds, int row, i
   return make_float4(p[0], p[ROWS + RPAD], p[2 * (ROWS + RPAD)], p[3 * (ROWS + RPAD)]);
 }
 
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  // bijective: XCD x (= bid % 8) receives a contiguous range of tile ids
-  int q = nwg / 8, r = nwg % 8;
-  int x = bid % 8, pos = bid / 8;
-  int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-  return base + pos;
-}
-
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
@@ -254,141 +246,240 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 }
 
 // ---------------------------------------------------------------------------
-// Register-direct variant.  One wave owns a (32 TM) x (32 TN) tile; each
-// K-slice's A and B fragments are loaded straight from global memory into the
-// MFMA operand layout (lane (li, lh) holds row li, k = 16 lh .. 16 lh + 15:
-// four float4 loads of 64 contiguous bytes for a K-contiguous operand, 16
-// coalesced 128-byte rows for a K-major one), double-buffered by K-slice.  No
-// LDS and no barriers: fp32 MFMA needs only ~16 FLOP per byte from L2 at
-// 64 x 64 per wave, so the reuse LDS would provide across waves is not needed.
-// Out-of-range rows read a clamped row (their results are never stored); K
-// past the end is zeroed at use time (the mask select sits next to the MFMA,
-// so no load is waited on early).
-template <bool KMAJOR, int TT>
-struct DFrag {
-  float4 v[TT][4];
-  uint32_t kmask;  // bit (4*q + j): k = 16 lh + 4 q + j in range
+// Split-bf16 variant ("x6") on v_mfma_f32_32x32x16_bf16.
+//
+// Every fp32 operand element is split EXACTLY into three bf16 parts,
+//   x = hi + mid + lo,   hi = x with the low 16 bits cleared,
+//   mid = (x - hi) likewise, lo = x - hi - mid (<= 8 significant bits),
+// and C = Σ_k a b is accumulated in fp32 from the six products whose
+// magnitude is >= 2^-16 |a b|:  hi·lo + lo·hi + mid·mid + hi·mid + mid·hi +
+// hi·hi.  The three dropped products (mid·lo, lo·mid, lo·lo) are below
+// 2^-23 |a b| in total, i.e. one fp32 rounding of the product, and every
+// bf16 x bf16 product is exact in the fp32 accumulator; the result is fp32
+// GEMM accuracy (tests/test_gpu_kernels.py compares both implementations
+// against float64).  bf16 MFMA runs at 16x the f32-input MFMA rate, so six
+// of them cost 3/8 of one f32 MFMA chain.
+//
+// The split happens once per element while staging (global -> registers ->
+// split -> LDS), into a [plane][row][k] bf16 image with an 80-byte pitch: a
+// lane's 8 consecutive k of one row are one conflict-free ds_read_b128, the
+// A/B fragment of the 32x32x16 MFMA (lane (r, h) holds k = 8h .. 8h+7).
+// Staging works on 4-row x 4-k blocks, so a K-major operand (dY^T, X^T of a
+// weight gradient) is transposed in registers for free.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-  __device__ __forceinline__ void load(const float* __restrict__ X, int64_t ld, int64_t r0,
-                                       int64_t rows, int64_t k0, int64_t K, int li, int lh) {
-    const int64_t kb = k0 + 16 * lh;
-    kmask = 0;
+constexpr int XK = 40;  // bf16 pitch of one image row (32 k + 8 pad = 80 B)
+
+__device__ __forceinline__ void split4(float4 v, uint2& hi, uint2& mid, uint2& lo) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t h[4], m[4], l[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) kmask |= (uint32_t)(kb + j < K) << j;
+  for (int e = 0; e < 4; ++e) {
+    h[e] = __float_as_uint(x[e]) & 0xffff0000u;
+    const float r1 = x[e] - __uint_as_float(h[e]);  // exact
+    m[e] = __float_as_uint(r1) & 0xffff0000u;
+    l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));  // exact, <= 8 significant bits
+  }
+  hi = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
+  mid = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
+  lo = make_uint2((l[0] >> 16) | (l[1] & 0xffff0000u), (l[2] >> 16) | (l[3] & 0xffff0000u));
+}
+
+// One operand's K-slice (ROWS x BK) as ROWS/4 x BK/4 blocks of 4 rows x 4 k.
+// Block b: k group kb = b % 8 (fastest: 8 lanes read 128 contiguous bytes of a
+// K-contiguous row, and the LDS writes of 16 lanes hit 32 distinct banks),
+// row group rb = b / 8.  `off` rotates the thread->block map so that two
+// operands with fewer blocks than threads are staged by different waves.
+template <bool KMAJOR, int ROWS, int T>
+struct XStager {
+  static constexpr int BLOCKS = (ROWS / 4) * (BK / 4);
+  static constexpr int PER = (BLOCKS + T - 1) / T;
+  float4 r[PER][4];
+  uint32_t ok;  // bit 4j+i: load i of block j in range
+
+  __device__ __forceinline__ void load(const float* __restrict__ src, int64_t ld, int64_t row0,
+                                       int64_t rows, int64_t k0, int64_t K, int t) {
+    ok = 0;
 #pragma unroll
-    for (int t = 0; t < TT; ++t) {
-      int64_t r = r0 + t * 32 + li;
-      r = r < rows ? r : rows - 1;
-      if (!KMAJOR) {
-        const float* p = X + r * ld;
+    for (int j = 0; j < PER; ++j) {
+      const int b = t + j * T;
+      const int kb = b % (BK / 4), rb = b / (BK / 4);
+      const bool bin = b < BLOCKS;
+      if (!bin) continue;  // wave-uniform: BLOCKS is a multiple of 64
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t k = kb + 4 * q;
-          v[t][q] = *reinterpret_cast<const float4*>(p + (k < K ? k : 0));
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float e[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int64_t k = kb + 4 * q + j;
-            e[j] = X[(k < K ? k : K - 1) * ld + r];
-          }
-          v[t][q] = make_float4(e[0], e[1], e[2], e[3]);
+      for (int i = 0; i < 4; ++i) {
+        if (!KMAJOR) {  // load i = row 4rb+i, k = 4kb .. 4kb+3
+          const int64_t gr = row0 + 4 * rb + i, gk = k0 + 4 * kb;
+          const bool in = bin && gr < rows && gk < K;
+          r[j][i] = *reinterpret_cast<const float4*>(src + (gr < rows ? gr : rows - 1) * ld +
+                                                     (gk < K ? gk : 0));
+          ok |= (uint32_t)in << (4 * j + i);
+        } else {  // load i = k 4kb+i, rows 4rb .. 4rb+3 (rows % 4 == 0)
+          const int64_t gk = k0 + 4 * kb + i, gr = row0 + 4 * rb;
+          const bool in = bin && gk < K && gr < rows;
+          r[j][i] = *reinterpret_cast<const float4*>(src + (gk < K ? gk : K - 1) * ld +
+                                                     (gr < rows ? gr : 0));
+          ok |= (uint32_t)in << (4 * j + i);
         }
       }
     }
   }
-  __device__ __forceinline__ float get(int t, int q, int j) const {
-    const float4 x = v[t][q];
-    const float e = j == 0 ? x.x : (j == 1 ? x.y : (j == 2 ? x.z : x.w));
-    return ((kmask >> (4 * q + j)) & 1u) ? e : 0.f;
+
+  // image: 3 planes of [ROWS][XK] bf16
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int b = t + j * T;
+      if (b >= BLOCKS) continue;
+      const int kb = b % (BK / 4), rb = b / (BK / 4);
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        v[i] = ((ok >> (4 * j + i)) & 1u) ? r[j][i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 row[4];
+      if (!KMAJOR) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) row[i] = v[i];
+      } else {  // register transpose: row i takes component i of the 4 k loads
+        row[0] = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
+        row[1] = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
+        row[2] = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
+        row[3] = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint2 hi, mid, lo;
+        split4(row[i], hi, mid, lo);
+        const int o = (4 * rb + i) * XK + 4 * kb;
+        *reinterpret_cast<uint2*>(img + o) = hi;
+        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
+        *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
+      }
+    }
   }
 };
 
-template <int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
-__global__ __launch_bounds__(256) void k_gemm_f32_direct(
+__device__ __forceinline__ bf16x8 xfrag(const uint16_t* __restrict__ img, int row, int kofs) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + row * XK + kofs));
+}
+
+// 2 x 2 waves, wave tile (32 TM) x 32, workgroup tile (64 TM) x 64.
+template <int TM, bool AK, bool BKM, int EPI, bool SPLIT>
+__global__ __launch_bounds__(256) void k_gemm_x6(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
     int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
     const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
-  constexpr int BM = TM * 32, BN = TN * 32;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int T = 256;
+  constexpr int BM = 64 * TM, BN = 64;
+  constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (AI + BI)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
+
   const int ntn = (int)((N + BN - 1) / BN);
   const int ntm = (int)((M + BM - 1) / BM);
-  const int nt = ntm * ntn;
-  const int nwg = (nt + 3) / 4;
-  const int tile = xcd_remap(blockIdx.x, nwg) * 4 + wave;  // 4 neighbouring tiles per WG
-  if (tile >= nt) return;  // whole wave
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   const int64_t m0 = (int64_t)(tile / ntn) * BM;
   const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
   const int nk_total = (int)((K + BK - 1) / BK);
   const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
   int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
   if (kt_end > nk_total) kt_end = nk_total;
 
-  f32x16 acc[TM][TN];
+  f32x16 acc[TM];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
 
-  DFrag<AK, TM> fa0, fa1;
-  DFrag<BKM, TN> fb0, fb1;
-  auto compute = [&](const DFrag<AK, TM>& fa, const DFrag<BKM, TN>& fb) {
+  XStager<AK, BM, T> sa0, sa1;
+  XStager<BKM, BN, T> sb0, sb1;
+  // B blocks go to the threads A leaves idle (A has 2 BM blocks, B 128)
+  const int tb = (tid + (2 * BM) % T) % T;
+  uint16_t* buf0 = lds;
+  uint16_t* buf1 = lds + (AI + BI);
+
+  auto compute = [&](const uint16_t* As) {
+    const uint16_t* Bs = As + AI;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kofs = ks * 16 + lh * 8;
+      const int bro = wn * 32 + li;
+      const bf16x8 bh = xfrag(Bs, bro, kofs);
+      const bf16x8 bm = xfrag(Bs + BN * XK, bro, kofs);
+      const bf16x8 bl = xfrag(Bs + 2 * BN * XK, bro, kofs);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.get(a, q, j), fb.get(b, q, j),
-                                                             acc[a][b], 0, 0, 0);
+      for (int a = 0; a < TM; ++a) {
+        const int aro = wm * TM * 32 + a * 32 + li;
+        const bf16x8 ah = xfrag(As, aro, kofs);
+        const bf16x8 am = xfrag(As + BM * XK, aro, kofs);
+        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, kofs);
+        // small terms first
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[a], 0, 0, 0);
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[a], 0, 0, 0);
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[a], 0, 0, 0);
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[a], 0, 0, 0);
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[a], 0, 0, 0);
+        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[a], 0, 0, 0);
+      }
+    }
   };
+
   const int nsteps = kt_end - kt_beg;
   if (nsteps > 0) {
-    fa0.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, li, lh);
-    fb0.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, li, lh);
+    sa0.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid);
+    sb0.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tb);
+    if (nsteps > 1) {
+      sa1.load(A, lda, m0, M, (int64_t)(kt_beg + 1) * BK, K, tid);
+      sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + 1) * BK, K, tb);
+    }
+    sa0.store(buf0, tid);
+    sb0.store(buf0 + AI, tb);
+    __syncthreads();
   }
   int i = 0;
   for (; i + 2 <= nsteps; i += 2) {
-    fa1.load(A, lda, m0, M, (int64_t)(kt_beg + i + 1) * BK, K, li, lh);
-    fb1.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 1) * BK, K, li, lh);
-    compute(fa0, fb0);
-    fa0.load(A, lda, m0, M, (int64_t)(kt_beg + i + 2) * BK, K, li, lh);
-    fb0.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 2) * BK, K, li, lh);
-    compute(fa1, fb1);
+    sa0.load(A, lda, m0, M, (int64_t)(kt_beg + i + 2) * BK, K, tid);
+    sb0.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 2) * BK, K, tb);
+    compute(buf0);
+    sa1.store(buf1, tid);
+    sb1.store(buf1 + AI, tb);
+    __syncthreads();
+    sa1.load(A, lda, m0, M, (int64_t)(kt_beg + i + 3) * BK, K, tid);
+    sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 3) * BK, K, tb);
+    compute(buf1);
+    sa0.store(buf0, tid);
+    sb0.store(buf0 + AI, tb);
+    __syncthreads();
   }
-  if (i < nsteps) compute(fa0, fb0);
+  if (i < nsteps) compute(buf0);
 
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
   const int64_t ldo = SPLIT ? N : ldc;
+  const int64_t n = n0 + wn * 32 + li;
+  if (n >= N) return;
+  float bv = 0.f;
+  if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
 #pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int64_t n = n0 + b * 32 + li;
-    if (n >= N) continue;
-    float bv = 0.f;
-    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
+  for (int a = 0; a < TM; ++a) {
 #pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= M) continue;
-        float v = acc[a][b][r];
-        if (!SPLIT) {
-          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
-          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
-          if (accumulate) v += Cout[m * ldo + n];
-        }
-        Cout[m * ldo + n] = v;
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (m >= M) continue;
+      float v = acc[a][r];
+      if (!SPLIT) {
+        if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
+        if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+        if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+        if (accumulate) v += Cout[m * ldo + n];
       }
+      Cout[m * ldo + n] = v;
     }
   }
 }
@@ -410,29 +501,24 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   C[m * ldc + n] = v;
 }
 
-struct Cfg {
-  int wm, wn, tm, tn;
-  int bm() const { return wm * tm * 32; }
-  int bn() const { return wn * tn * 32; }
-};
-
-// 64 x 64 tiles (4 waves x one 32x32 MFMA tile): many small workgroups keep
-// every CU's matrix pipe fed to the end of the grid (at M ~ 15k rows a 128 x 128
-// tiling leaves 600 tiles for 512 resident slots: a 17%-full second wave).
-Cfg pick_cfg(int64_t, int64_t) { return {2, 2, 1, 1}; }
-
-// 0 = LDS-staged 64x64 (default), 1 = register-direct 64x64 per wave,
-// 2 = register-direct 32x64 per wave (tuning knob, molclr_gemm_set_impl)
+// 0 = f32-input MFMA, 64 x 64 tiles; 1 = split-bf16 64 x 64; 2 = split-bf16
+// 128 x 64 (molclr_gemm_set_impl).  The split-bf16 kernels stage K-major
+// operands 4 rows at a time, so they need rows % 4 == 0 and ld % 4 == 0 there;
+// other shapes take impl 0.
 int g_impl = 0;
+int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
+  if (g_impl == 0) return 0;
+  if (ak && (M % 4 || lda % 4)) return 0;
+  if (bk && (N % 4 || ldb % 4)) return 0;
+  return g_impl;
+}
 int tiles_for(int impl, int64_t M, int64_t N) {
-  if (impl == 1) return (int)((((M + 63) / 64) * ((N + 63) / 64) + 3) / 4);
-  if (impl == 2) return (int)((((M + 31) / 32) * ((N + 63) / 64) + 3) / 4);
-  return (int)(((M + 63) / 64) * ((N + 63) / 64));
+  const int64_t bm = impl == 2 ? 128 : 64;
+  return (int)(((M + bm - 1) / bm) * ((N + 63) / 64));
 }
 
-int pick_splits(const Cfg& c, int64_t M, int64_t N, int64_t K) {
-  (void)c;
-  int64_t tiles = tiles_for(g_impl, M, N) * (g_impl ? 4 : 1);
+int pick_splits(int impl, int64_t M, int64_t N, int64_t K) {
+  int64_t tiles = tiles_for(impl, M, N);
   int64_t nk = (K + BK - 1) / BK;
   if (tiles >= 512 || nk < 16) return 1;
   int64_t s = (1024 + tiles - 1) / tiles;
@@ -448,25 +534,26 @@ struct Args {
   const float *bias, *aux;
   int64_t ldaux;
   int kps, accumulate;
+  int impl;
 };
 
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
-  if (g_impl == 1) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32_direct<2, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
-                       a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
-                       a.accumulate);
+  if (a.impl == 1) {
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.kps, a.accumulate);
     return;
   }
-  if (g_impl == 2) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32_direct<1, 2, AK, BKM, EPI, SPLIT>), grid, dim3(256), 0, s, a.A,
-                       a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux, a.ldaux, a.kps,
-                       a.accumulate);
+  if (a.impl == 2) {
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.kps, a.accumulate);
     return;
   }
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid, dim3(WM * WN * 64),
-                     0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
-                     a.ldaux, a.kps, a.accumulate);
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid,
+                       dim3(WM * WN * 64), 0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc,
+                       a.bias, a.aux, a.ldaux, a.kps, a.accumulate);
 }
 
 template <int WM, int WN, int TM, int TN, bool SPLIT>
@@ -498,16 +585,19 @@ int dispatch_layout(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Arg
 }
 
 template <bool SPLIT>
-int dispatch_cfg(const Cfg& c, int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
-  (void)c;
+int dispatch(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
   return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, a);
 }
 
 }  // namespace
 
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
-  Cfg c = pick_cfg(M, N);
-  int sp = pick_splits(c, M, N, K);
+  // sized for the largest split count any implementation would pick
+  int sp = pick_splits(0, M, N, K);
+  for (int impl = 1; impl <= 2; ++impl) {
+    const int s2 = pick_splits(impl, M, N, K);
+    sp = s2 > sp ? s2 : sp;
+  }
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) + 256 : 0;
 }
 
@@ -537,22 +627,22 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     molclr::set_error("gemm_f32: K == 0 unsupported");
     return MOLCLR_ERR_UNSUPPORTED;
   }
-  Cfg c = pick_cfg(M, N);
-  int64_t tiles = tiles_for(g_impl, M, N);  // workgroups along x
+  const int impl = impl_for(M, N, lda, ldb, a_kmajor, b_kmajor);
+  int64_t tiles = tiles_for(impl, M, N);  // workgroups along x
   MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
-  int sp = pick_splits(c, M, N, K);
+  int sp = pick_splits(impl, M, N, K);
   if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
-  Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate};
+  Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate, impl};
   int rc;
   if (sp == 1) {
-    rc = dispatch_cfg<false>(c, a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, a);
+    rc = dispatch<false>(a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, a);
   } else {
     int64_t nk = (K + BK - 1) / BK;
     int kps = (int)((nk + sp - 1) / sp);
     sp = (int)((nk + kps - 1) / kps);
     float* partial = (float*)workspace;
-    Args ap{A, B, partial, M, N, K, lda, ldb, N, nullptr, nullptr, 0, kps, 0};
-    rc = dispatch_cfg<true>(c, a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
+    Args ap{A, B, partial, M, N, K, lda, ldb, N, nullptr, nullptr, 0, kps, 0, impl};
+    rc = dispatch<true>(a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
                             dim3((unsigned)tiles, sp), s, ap);
     if (rc == 0) {
       dim3 g((unsigned)molclr::ceil_div(M * N, 256));
@@ -582,6 +672,8 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
+
+MOLCLR_API int molclr_gemm_get_impl(void) { return g_impl; }
 
 MOLCLR_API int molclr_gemm_set_impl(int impl) {
   MOLCLR_REQUIRE(impl >= 0 && impl <= 2, "gemm_set_impl: impl must be 0, 1 or 2");

@@ -158,9 +158,20 @@ GEMM_SHAPES = [
 ]
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["f32", "x6_64", "x6_128"])
+def gemm_impl(request, dev):
+    """Run a GEMM test under each implementation of molclr_gemm_f32."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    prev = lib.molclr_gemm_get_impl()
+    lib.molclr_gemm_set_impl(request.param)
+    yield request.param
+    lib.molclr_gemm_set_impl(prev)
+
+
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 1), (1, 0)])
-def test_gemm_layouts(dev, M, N, K, ak, bk):
+def test_gemm_layouts(dev, gemm_impl, M, N, K, ak, bk):
     torch.manual_seed(M + N + K)
     Am = torch.randn(M, K, dtype=torch.float64)
     Bm = torch.randn(K, N, dtype=torch.float64)
@@ -173,7 +184,7 @@ def test_gemm_layouts(dev, M, N, K, ak, bk):
     assert rel(out, ref) < TOL
 
 
-def test_gemm_epilogues(dev):
+def test_gemm_epilogues(dev, gemm_impl):
     from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK
     torch.manual_seed(0)
     M, N, K = 777, 600, 300
@@ -188,6 +199,36 @@ def test_gemm_epilogues(dev):
                (y + b.double()).clamp(min=0)) < TOL
     assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_RELU_MASK, aux=auxd),
                y * (aux > 0).double()) < TOL
+
+
+@pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 1), (1, 0)])
+def test_gemm_split_bf16_accuracy(dev, ak, bk):
+    """The split-bf16 GEMM is as accurate as the f32-input MFMA one: its
+    error against float64 stays within 2x of the f32 kernel's, elementwise-
+    max and norm-wise, including a long K (the weight-gradient shape)."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    prev = lib.molclr_gemm_get_impl()
+    try:
+        for M, N, K in ((1000, 600, 300), (300, 600, 15700)):
+            torch.manual_seed(K)
+            Am = torch.randn(M, K, dtype=torch.float64) * torch.logspace(-3, 3, K).double()
+            Bm = torch.randn(K, N, dtype=torch.float64)
+            A = (Am.t() if ak else Am).contiguous().float()
+            Bt = (Bm if bk else Bm.t()).contiguous().float()
+            # reference on the fp32-rounded inputs: only the GEMM's own error counts
+            ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
+            errs = {}
+            for impl in (0, 1, 2):
+                lib.molclr_gemm_set_impl(impl)
+                out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K, N if bk else K,
+                               ak, bk).double().cpu()
+                errs[impl] = (rel(out, ref), (out - ref).abs().max().item())
+            for impl in (1, 2):
+                assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
+                assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
+    finally:
+        lib.molclr_gemm_set_impl(prev)
 
 
 def test_colsum(dev):
