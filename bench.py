@@ -151,6 +151,15 @@ def main():
         loss = step(i)
     torch.cuda.synchronize()
     log(rank, f"warm-up done, loss {loss.item():.4f}")
+    # host cost of one step: enqueue time starting from an idle device (extra,
+    # untimed steps; if it approaches ms_per_step the step is launch-bound)
+    host = []
+    for i in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step(args.warmup + args.steps + i)
+        host.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
 
     timer = None if args.no_kernel_timing else ops.KernelTimer()
     ops.set_kernel_timer(timer)
@@ -214,6 +223,7 @@ def main():
                        "mean_nodes_per_view": round(n_nodes), "mean_edges_per_view": round(n_edges),
                        "parallelism": f"dp{world}"},
             "final_loss": round(final_loss, 5),
+            "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
             "roofline": roofline, "roofline_mfma": roofline_mfma, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -166,9 +166,10 @@ int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t
                     molclr_stream_t stream);
 
 /* Implementation switch (process-wide, not thread-safe): 0 = f32-input MFMA
- * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 = split-bf16 ("x6": each fp32
+ * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 (default) = split-bf16 ("x6": each fp32
  * operand split exactly into 3 bf16 parts, six bf16 MFMA products, fp32
- * accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64. */
+ * accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64;
+ * 3 = split-bf16, 128x128. */
 int molclr_gemm_set_impl(int impl);
 int molclr_gemm_get_impl(void);
 

@@ -248,43 +248,57 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 // ---------------------------------------------------------------------------
 // Split-bf16 variant ("x6") on v_mfma_f32_32x32x16_bf16.
 //
-// Every fp32 operand element is split EXACTLY into three bf16 parts,
-//   x = hi + mid + lo,   hi = x with the low 16 bits cleared,
-//   mid = (x - hi) likewise, lo = x - hi - mid (<= 8 significant bits),
-// and C = Σ_k a b is accumulated in fp32 from the six products whose
-// magnitude is >= 2^-16 |a b|:  hi·lo + lo·hi + mid·mid + hi·mid + mid·hi +
-// hi·hi.  The three dropped products (mid·lo, lo·mid, lo·lo) are below
-// 2^-23 |a b| in total, i.e. one fp32 rounding of the product, and every
-// bf16 x bf16 product is exact in the fp32 accumulator; the result is fp32
+// Every fp32 operand element is split into three bf16 parts, each the
+// round-to-nearest bf16 of what is left:
+//   x = hi + mid + lo + t,  |mid| <= 2^-8 |x|,  |lo| <= 2^-16 |x|,  |t| <= 2^-24 |x|
+// and C = Σ_k a b is accumulated in fp32 from the six products down to order
+// 2^-16: hi·lo + lo·hi + mid·mid + hi·mid + mid·hi + hi·hi.  What is left out
+// (mid·lo, lo·mid, lo·lo and the tails t) is below 4·2^-24 |a b| per product,
+// of random sign: the order of one fp32 rounding of the product.  Every
+// bf16 x bf16 product is exact in the fp32 accumulator.  The result has fp32
 // GEMM accuracy (tests/test_gpu_kernels.py compares both implementations
 // against float64).  bf16 MFMA runs at 16x the f32-input MFMA rate, so six
-// of them cost 3/8 of one f32 MFMA chain.
+// of them cost 3/8 of one f32 MFMA chain.  (Inputs beyond the bf16 range,
+// |x| > 3.39e38, are not supported.)
 //
 // The split happens once per element while staging (global -> registers ->
-// split -> LDS), into a [plane][row][k] bf16 image with an 80-byte pitch: a
-// lane's 8 consecutive k of one row are one conflict-free ds_read_b128, the
-// A/B fragment of the 32x32x16 MFMA (lane (r, h) holds k = 8h .. 8h+7).
+// split -> LDS), into a [plane][row][k] bf16 image of 64-byte rows whose four
+// 16-byte chunks are XOR-swizzled by (row >> 2) & 3: a lane's 8 consecutive k
+// of one row (the A/B fragment of the 32x32x16 MFMA: lane (r, h) holds
+// k = 8h .. 8h+7) are one ds_read_b128, conflict-free over every 16-lane
+// group, with no padding.
 // Staging works on 4-row x 4-k blocks, so a K-major operand (dY^T, X^T of a
 // weight gradient) is transposed in registers for free.
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int XK = 40;  // bf16 pitch of one image row (32 k + 8 pad = 80 B)
+constexpr int XK = 32;  // bf16 per image row (64 B, unpadded, chunk-swizzled)
+
+// bf16 offset of k = 8 * chunk (+ 4 * half) in image row `row`
+__device__ __forceinline__ int xoff(int row, int chunk) {
+  return row * XK + ((chunk ^ ((row >> 2) & 3)) << 3);
+}
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// Two floats -> packed hi / mid / lo bf16 pairs, each part the round-to-nearest
+// bf16 of the remaining residual (v_cvt_pk_bf16_f32); both subtractions are
+// exact (Sterbenz), so a = hi + mid + lo + t with |t| <= 2^-24 |a|.
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const bf16x2 hh = {(__bf16)a, (__bf16)b};
+  const float ra = a - (float)hh[0], rb = b - (float)hh[1];
+  const bf16x2 mm = {(__bf16)ra, (__bf16)rb};
+  const float sa = ra - (float)mm[0], sb = rb - (float)mm[1];
+  const bf16x2 ll = {(__bf16)sa, (__bf16)sb};
+  h = __builtin_bit_cast(uint32_t, hh);
+  m = __builtin_bit_cast(uint32_t, mm);
+  l = __builtin_bit_cast(uint32_t, ll);
+}
 
 __device__ __forceinline__ void split4(float4 v, uint2& hi, uint2& mid, uint2& lo) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-  uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    h[e] = __float_as_uint(x[e]) & 0xffff0000u;
-    const float r1 = x[e] - __uint_as_float(h[e]);  // exact
-    m[e] = __float_as_uint(r1) & 0xffff0000u;
-    l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));  // exact, <= 8 significant bits
-  }
-  hi = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
-  mid = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
-  lo = make_uint2((l[0] >> 16) | (l[1] & 0xffff0000u), (l[2] >> 16) | (l[3] & 0xffff0000u));
+  split2(v.x, v.y, hi.x, mid.x, lo.x);
+  split2(v.z, v.w, hi.y, mid.y, lo.y);
 }
 
 // One operand's K-slice (ROWS x BK) as ROWS/4 x BK/4 blocks of 4 rows x 4 k.
@@ -352,7 +366,7 @@ struct XStager {
       for (int i = 0; i < 4; ++i) {
         uint2 hi, mid, lo;
         split4(row[i], hi, mid, lo);
-        const int o = (4 * rb + i) * XK + 4 * kb;
+        const int o = xoff(4 * rb + i, kb >> 1) + 4 * (kb & 1);
         *reinterpret_cast<uint2*>(img + o) = hi;
         *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
         *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
@@ -361,18 +375,22 @@ struct XStager {
   }
 };
 
-__device__ __forceinline__ bf16x8 xfrag(const uint16_t* __restrict__ img, int row, int kofs) {
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + row * XK + kofs));
+__device__ __forceinline__ bf16x8 xfrag(const uint16_t* __restrict__ img, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + xoff(row, chunk)));
 }
 
-// 2 x 2 waves, wave tile (32 TM) x 32, workgroup tile (64 TM) x 64.
-template <int TM, bool AK, bool BKM, int EPI, bool SPLIT>
-__global__ __launch_bounds__(256) void k_gemm_x6(
+// 2 x 2 waves, wave tile (32 TM) x (32 TN), workgroup tile (64 TM) x (64 TN).
+// NP = 6 or 9 products per element pair.  hi·hi goes to its own accumulator and
+// the smaller products to a second one, added at the end: the correction terms
+// then accumulate with ~2^-8 of the rounding error they would pick up in the
+// large running sum.
+template <int TM, int TN, int NP, bool AK, bool BKM, int EPI, bool SPLIT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TM * TN == 1 ? 3 : 1))) void k_gemm_x6(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
     int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
     const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
   constexpr int T = 256;
-  constexpr int BM = 64 * TM, BN = 64;
+  constexpr int BM = 64 * TM, BN = 64 * TN;
   constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (AI + BI)];
 
@@ -392,15 +410,17 @@ __global__ __launch_bounds__(256) void k_gemm_x6(
   int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
   if (kt_end > nk_total) kt_end = nk_total;
 
-  f32x16 acc[TM];
+  f32x16 acc[TM][TN], acl[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[a][r] = 0.f;
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = acl[a][b][r] = 0.f;
 
   XStager<AK, BM, T> sa0, sa1;
   XStager<BKM, BN, T> sb0, sb1;
-  // B blocks go to the threads A leaves idle (A has 2 BM blocks, B 128)
+  // B blocks go to the threads A leaves idle (A has 2 BM blocks, B 2 BN)
   const int tb = (tid + (2 * BM) % T) % T;
   uint16_t* buf0 = lds;
   uint16_t* buf1 = lds + (AI + BI);
@@ -409,24 +429,35 @@ __global__ __launch_bounds__(256) void k_gemm_x6(
     const uint16_t* Bs = As + AI;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int kofs = ks * 16 + lh * 8;
-      const int bro = wn * 32 + li;
-      const bf16x8 bh = xfrag(Bs, bro, kofs);
-      const bf16x8 bm = xfrag(Bs + BN * XK, bro, kofs);
-      const bf16x8 bl = xfrag(Bs + 2 * BN * XK, bro, kofs);
+      const int ch = ks * 2 + lh;
+      bf16x8 bh[TN], bm[TN], bl[TN];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int bro = wn * TN * 32 + b * 32 + li;
+        bh[b] = xfrag(Bs, bro, ch);
+        bm[b] = xfrag(Bs + BN * XK, bro, ch);
+        bl[b] = xfrag(Bs + 2 * BN * XK, bro, ch);
+      }
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
         const int aro = wm * TM * 32 + a * 32 + li;
-        const bf16x8 ah = xfrag(As, aro, kofs);
-        const bf16x8 am = xfrag(As + BM * XK, aro, kofs);
-        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, kofs);
-        // small terms first
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[a], 0, 0, 0);
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[a], 0, 0, 0);
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[a], 0, 0, 0);
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[a], 0, 0, 0);
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[a], 0, 0, 0);
-        acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[a], 0, 0, 0);
+        const bf16x8 ah = xfrag(As, aro, ch);
+        const bf16x8 am = xfrag(As + BM * XK, aro, ch);
+        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, ch);
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          if (NP == 9) {
+            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bl[b], acl[a][b], 0, 0, 0);
+            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bl[b], acl[a][b], 0, 0, 0);
+            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bm[b], acl[a][b], 0, 0, 0);
+          }
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[b], acl[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[b], acc[a][b], 0, 0, 0);
+        }
       }
     }
   };
@@ -462,24 +493,27 @@ __global__ __launch_bounds__(256) void k_gemm_x6(
 
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
   const int64_t ldo = SPLIT ? N : ldc;
-  const int64_t n = n0 + wn * 32 + li;
-  if (n >= N) return;
-  float bv = 0.f;
-  if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
 #pragma unroll
-  for (int a = 0; a < TM; ++a) {
+  for (int b = 0; b < TN; ++b) {
+    const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (m >= M) continue;
-      float v = acc[a][r];
-      if (!SPLIT) {
-        if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
-        if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-        if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
-        if (accumulate) v += Cout[m * ldo + n];
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= M) continue;
+        float v = acc[a][b][r] + acl[a][b][r];
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
+          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+          if (accumulate) v += Cout[m * ldo + n];
+        }
+        Cout[m * ldo + n] = v;
       }
-      Cout[m * ldo + n] = v;
     }
   }
 }
@@ -501,11 +535,12 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   C[m * ldc + n] = v;
 }
 
-// 0 = f32-input MFMA, 64 x 64 tiles; 1 = split-bf16 64 x 64; 2 = split-bf16
-// 128 x 64 (molclr_gemm_set_impl).  The split-bf16 kernels stage K-major
+// 0 = f32-input MFMA, 64 x 64 tiles; split-bf16 with 6 products and 1 = 64 x 64,
+// 2 = 128 x 64, 3 = 128 x 128 tiles; 4 = split-bf16 with all 9 products, 64 x 64
+// (molclr_gemm_set_impl).  The split-bf16 kernels stage K-major
 // operands 4 rows at a time, so they need rows % 4 == 0 and ld % 4 == 0 there;
 // other shapes take impl 0.
-int g_impl = 0;
+int g_impl = 1;  // split-bf16 64 x 64: fastest on every shape of the step (profiles/)
 int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   if (g_impl == 0) return 0;
   if (ak && (M % 4 || lda % 4)) return 0;
@@ -513,8 +548,8 @@ int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   return g_impl;
 }
 int tiles_for(int impl, int64_t M, int64_t N) {
-  const int64_t bm = impl == 2 ? 128 : 64;
-  return (int)(((M + bm - 1) / bm) * ((N + 63) / 64));
+  const int64_t bm = (impl == 2 || impl == 3) ? 128 : 64, bn = impl == 3 ? 128 : 64;
+  return (int)(((M + bm - 1) / bm) * ((N + bn - 1) / bn));
 }
 
 int pick_splits(int impl, int64_t M, int64_t N, int64_t K) {
@@ -540,13 +575,25 @@ struct Args {
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   if (a.impl == 1) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, 1, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
                          0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
                          a.ldaux, a.kps, a.accumulate);
     return;
   }
   if (a.impl == 2) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, 1, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.kps, a.accumulate);
+    return;
+  }
+  if (a.impl == 4) {
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, 1, 9, AK, BKM, EPI, SPLIT>), grid, dim3(256),
+                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.kps, a.accumulate);
+    return;
+  }
+  if (a.impl == 3) {
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, 2, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
                          0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
                          a.ldaux, a.kps, a.accumulate);
     return;
@@ -594,7 +641,7 @@ int dispatch(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   // sized for the largest split count any implementation would pick
   int sp = pick_splits(0, M, N, K);
-  for (int impl = 1; impl <= 2; ++impl) {
+  for (int impl = 1; impl <= 4; ++impl) {
     const int s2 = pick_splits(impl, M, N, K);
     sp = s2 > sp ? s2 : sp;
   }
@@ -676,7 +723,7 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
 MOLCLR_API int molclr_gemm_get_impl(void) { return g_impl; }
 
 MOLCLR_API int molclr_gemm_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl >= 0 && impl <= 2, "gemm_set_impl: impl must be 0, 1 or 2");
+  MOLCLR_REQUIRE(impl >= 0 && impl <= 4, "gemm_set_impl: impl must be 0..4");
   g_impl = impl;
   return MOLCLR_OK;
 }

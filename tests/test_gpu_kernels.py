@@ -158,7 +158,7 @@ GEMM_SHAPES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["f32", "x6_64", "x6_128"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["f32", "x6_64x64", "x6_128x64", "x6_128x128", "x9_64x64"])
 def gemm_impl(request, dev):
     """Run a GEMM test under each implementation of molclr_gemm_f32."""
     from molclr_amd import _lib
@@ -210,23 +210,31 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
     lib = _lib.load()
     prev = lib.molclr_gemm_get_impl()
     try:
-        for M, N, K in ((1000, 600, 300), (300, 600, 15700)):
+        for M, N, K, positive in ((1000, 600, 300, False), (300, 600, 15700, False),
+                                  (1000, 600, 300, True), (300, 600, 15700, True)):
             torch.manual_seed(K)
-            Am = torch.randn(M, K, dtype=torch.float64) * torch.logspace(-3, 3, K).double()
-            Bm = torch.randn(K, N, dtype=torch.float64)
+            if positive:  # no cancellation: elementwise relative error is meaningful
+                Am = torch.rand(M, K, dtype=torch.float64)
+                Bm = torch.rand(K, N, dtype=torch.float64)
+            else:
+                Am = torch.randn(M, K, dtype=torch.float64) * torch.logspace(-3, 3, K).double()
+                Bm = torch.randn(K, N, dtype=torch.float64)
             A = (Am.t() if ak else Am).contiguous().float()
             Bt = (Bm if bk else Bm.t()).contiguous().float()
             # reference on the fp32-rounded inputs: only the GEMM's own error counts
             ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
             errs = {}
-            for impl in (0, 1, 2):
+            for impl in (0, 1, 2, 3, 4):
                 lib.molclr_gemm_set_impl(impl)
                 out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K, N if bk else K,
                                ak, bk).double().cpu()
-                errs[impl] = (rel(out, ref), (out - ref).abs().max().item())
-            for impl in (1, 2):
+                errs[impl] = (rel(out, ref), (out - ref).abs().max().item(),
+                              ((out - ref).abs() / ref.abs().clamp(min=1e-30)).max().item())
+            for impl in (1, 2, 3, 4):
                 assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
                 assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
+                if positive:
+                    assert errs[impl][2] <= 2 * errs[0][2], errs
     finally:
         lib.molclr_gemm_set_impl(prev)
 

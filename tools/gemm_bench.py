@@ -65,7 +65,7 @@ def main():
     lib = _lib.load()
     for name, flops, mine, ref in cases:
         res = []
-        for impl in (0, 1, 2):
+        for impl in (0, 1, 2, 3, 4):
             lib.molclr_gemm_set_impl(impl)
             tm = timeit(mine)
             res.append(f"impl{impl} {tm*1e6:6.1f}us {flops/tm/1e12:5.1f}TF")
@@ -75,7 +75,7 @@ def main():
               flush=True)
     # correctness of every impl on one shape per layout
     torch.manual_seed(1)
-    for impl in (1, 2):
+    for impl in (1, 2, 3, 4):
         lib.molclr_gemm_set_impl(impl)
         for (ak, bk) in ((0, 0), (0, 1), (1, 1), (1, 0)):
             M, N, K = 333, 300, 1000
