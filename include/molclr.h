@@ -58,6 +58,14 @@ enum {
 #define MOLCLR_NUM_BOND_DIR 3
 #define MOLCLR_SELF_LOOP_BOND_TYPE 4 /* ginet_molclr.py:35 */
 #define MOLCLR_ECOUNT_STRIDE 8       /* per-node counts: 5 bond types, 3 dirs */
+#define MOLCLR_NUM_ECOMB 15          /* combined edge-table rows: bt * 3 + bd */
+#define MOLCLR_SELF_LOOP_ECOMB 12    /* bond type 4, dir 0 */
+#define MOLCLR_NBR_SLOTS 4           /* in-edges held in a node's neighbour slots */
+#define MOLCLR_NBR_OVERFLOW 7        /* degree field: > MOLCLR_NBR_SLOTS, use the CSR */
+#define MOLCLR_NBR_MAX_NODES (1 << 24)
+
+/* ecode (bond_type | bond_dir << 3) -> combined edge-table row */
+#define MOLCLR_ECOMB(ecode) ((int)((ecode) & 7u) * 3 + (int)((ecode) >> 3))
 
 const char* molclr_version(void);
 const char* molclr_last_error(void);
@@ -77,6 +85,13 @@ const char* molclr_last_error(void);
  *       ecode = bond_type | bond_dir << 3.
  *   rowptr_t [N+1] i32, col_t [E] i32 : out-edges sorted stably by source
  *       (the accumulation order of index_select's backward).
+ *   nbr [N*4] u32, nbr_t [N*4] u32 : neighbour slots, one 16-byte entry per
+ *       node so the aggregation reads a row's neighbours with one load and
+ *       no rowptr -> col dependency.  Entry i holds the first 4 CSR (nbr) /
+ *       CSC (nbr_t) neighbours of i in row order; nbr packs
+ *       src | MOLCLR_ECOMB(ecode) << 24.  Bits 29..31 of word 0 hold the
+ *       degree, or MOLCLR_NBR_OVERFLOW when it exceeds 4 (the kernels then
+ *       walk the CSR/CSC row instead).  Requires N <= MOLCLR_NBR_MAX_NODES.
  *   ecount [N*8] i32 : per destination, counts of in-edge bond types 0..4
  *       and bond dirs 0..2, self loop included.
  *   graph_ptr [G+1] i32 : node range of every graph.
@@ -89,6 +104,7 @@ int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
                        const int64_t* batch, int64_t num_nodes, int64_t num_edges,
                        int64_t num_graphs, int32_t* rowptr, int32_t* col,
                        uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t,
+                       uint32_t* nbr, uint32_t* nbr_t,
                        int32_t* ecount, int32_t* graph_ptr, int32_t* status,
                        void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
@@ -107,13 +123,24 @@ int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* 
                           int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2, int accumulate,
                           void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
+/* Combined edge tables of `layers` GINE layers (ginet_molclr.py:24-27,39):
+ *   Ec[l][bt*3 + bd][:] = E1_l[bt][:] + E2_l[bd][:]
+ * (the edge embedding the reference computes per edge, one fp32 rounding —
+ * so using Ec is bit-identical).  E1s / E2s are HOST arrays of `layers`
+ * device pointers to [5,D] / [3,D] tables; Ec is [layers, 15, D].
+ * layers <= MOLCLR_MAX_LAYERS.  One launch for all layers. */
+#define MOLCLR_MAX_LAYERS 16
+int molclr_edge_tables_combine(int layers, const float* const* E1s, const float* const* E2s,
+                               float* Ec, int64_t dim, molclr_stream_t stream);
+
 /* GINE aggregation (ginet_molclr.py:39-44 + PyG aggr='add'):
- *   out[i] = Σ_{k in in(i), edge order} (x[src_k] + (E1[bt_k] + E2[bd_k]))
- *            + (x[i] + (E1[4] + E2[0]))                    (self loop last)
+ *   out[i] = Σ_{k in in(i), edge order} (x[src_k] + Ec[bt_k*3+bd_k])
+ *            + (x[i] + Ec[12])                              (self loop last)
  * Same operation order as the reference CPU path, so results are
- * bit-identical to it.  x, out [N,D] f32; E1 [5,D]; E2 [3,D]. */
+ * bit-identical to it.  x, out [N,D] f32; Ec [15,D] (molclr_edge_tables_combine);
+ * nbr from molclr_graph_build, with rowptr/col/ecode for rows of degree > 4. */
 int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32_t* col,
-                              const uint8_t* ecode, const float* E1, const float* E2,
+                              const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
                               float* out, int64_t num_nodes, int64_t dim,
                               molclr_stream_t stream);
 /* Backward: dx[j] = Σ_{k in out(j), edge order} g[dst_k] + g[j];
@@ -121,7 +148,7 @@ int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32
  * dx may be NULL (first layer input needs no grad); dE1/dE2 may be NULL. */
 size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
 int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
-                              const int32_t* ecount, float* dx, float* dE1, float* dE2,
+                              const uint32_t* nbr_t, const int32_t* ecount, float* dx, float* dE1, float* dE2,
                               int64_t num_nodes, int64_t dim, int accumulate, void* workspace,
                               size_t workspace_bytes, molclr_stream_t stream);
 
@@ -130,14 +157,15 @@ int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int
  *   out[i] = Σ_{k in in(i)} (e_k + xw[src_k]) + (e_self + xw[i]) + bias
  * with scalar e = E1[bt][0] + E2[bd][0] (tables [5,1], [3,1]). */
 int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr, const int32_t* col,
-                             const uint8_t* ecode, const float* E1, const float* E2,
+                             const uint8_t* ecode, const uint32_t* nbr, const float* E1,
+                             const float* E2,
                              const float* bias, float* out, int64_t num_nodes,
                              int64_t dim, molclr_stream_t stream);
 /* Backward: dxw[j] = Σ_{out(j)} g[dst] + g[j]; dE1[t] = Σ_i ecount[i][t]·Σ_d g[i][d];
  * dE2 likewise; dbias = Σ_i g[i].  Any output pointer may be NULL. */
 size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t num_nodes, int64_t dim);
 int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t, const int32_t* col_t,
-                             const int32_t* ecount, float* dxw, float* dE1, float* dE2,
+                             const uint32_t* nbr_t, const int32_t* ecount, float* dxw, float* dE1, float* dE2,
                              float* dbias, int64_t num_nodes, int64_t dim, int accumulate,
                              void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 

@@ -29,19 +29,20 @@ SIGNATURES = {
     "molclr_last_error": (c_char_p, []),
     "molclr_graph_build_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_graph_build": (c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
-                                   _P, c_size_t, _P]),
+                                   _P, _P, _P, c_size_t, _P]),
     "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "molclr_atom_embed_bwd_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64]),
     "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
                                       _P]),
+    "molclr_edge_tables_combine": (c_int, [c_int, _P, _P, _P, _I64, _P]),
     "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
     "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
+    "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
                                           c_size_t, _P]),
-    "molclr_gcn_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_gcn_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
     "molclr_gcn_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
-    "molclr_gcn_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
-                                         c_size_t, _P]),
+    "molclr_gcn_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int,
+                                         _P, c_size_t, _P]),
     "molclr_gemm_f32_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_gemm_f32": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, c_int, c_int, c_int,
                                 _P, _P, _I64, _P, c_size_t, _P]),
@@ -75,6 +76,8 @@ SIGNATURES = {
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
 EPI_ACCUMULATE = 16
+NUM_ECOMB = 15  # combined edge-table rows (bond type * 3 + bond dir)
+MAX_LAYERS = 16
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
 

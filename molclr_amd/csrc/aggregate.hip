@@ -112,63 +112,98 @@ __global__ __launch_bounds__(1024) void k_reduce_partials_split(
 // ---------------------------------------------------------------------------
 // GINE aggregation
 // ---------------------------------------------------------------------------
+// Ec[l][r][c] = E1_l[r / 3][c] + E2_l[r % 3][c]: the per-edge embedding of the
+// reference (one fp32 add), tabulated once per forward for all layers.
+struct TablePtrs {
+  const float* e1[MOLCLR_MAX_LAYERS];
+  const float* e2[MOLCLR_MAX_LAYERS];
+};
+__global__ void k_edge_tables_combine(TablePtrs p, float* __restrict__ Ec, int layers, int64_t D) {
+  const int64_t per = (int64_t)MOLCLR_NUM_ECOMB * D;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= layers * per) return;
+  const int l = (int)(t / per);
+  const int64_t rc = t - l * per;
+  const int r = (int)(rc / D);
+  const int64_t c = rc - (int64_t)r * D;
+  Ec[t] = p.e1[l][(r / 3) * D + c] + p.e2[l][(r % 3) * D + c];
+}
+
+__device__ __forceinline__ uint32_t nbr_degree(uint32_t w0) { return w0 >> 29; }
+__device__ __forceinline__ int32_t nbr_node(uint32_t w) { return (int32_t)(w & 0xFFFFFFu); }
+__device__ __forceinline__ int nbr_ecomb(uint32_t w) { return (int)((w >> 24) & 15u); }
+
+// message x[src] + Ec[type] of a packed slot
+__device__ __forceinline__ float4 gine_msg(const float4* __restrict__ x, const float4* __restrict__ Ec,
+                                           uint32_t w, int d4, int c) {
+  return f4add(x[(int64_t)nbr_node(w) * d4 + c], Ec[nbr_ecomb(w) * d4 + c]);
+}
+
+// Row i's neighbour entry is one 16-byte load shared by the row's D/4 lanes;
+// for degree <= 4 every gather is issued before the ordered adds, so the row
+// costs two dependent memory latencies (slots, then features).  Rows of
+// higher degree walk the CSR.  Order of the adds: in-edges in edge order,
+// self loop last — the reference's, so the sums are bit-identical.
 __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
-    const float4* __restrict__ E1, const float4* __restrict__ E2, float4* __restrict__ out,
+    const uint4* __restrict__ nbr, const float4* __restrict__ Ec, float4* __restrict__ out,
     int64_t N, int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
-  int32_t k = rowptr[i];
-  const int32_t end = rowptr[i + 1];
+  const uint4 s = nbr[i];
+  const float4 self = x[t];
+  const float4 es = Ec[MOLCLR_SELF_LOOP_ECOMB * d4 + c];
+  const uint32_t deg = nbr_degree(s.x);
   float4 acc = f4zero();
-  // two neighbours per step: both gathers are issued before the ordered adds
-  for (; k + 2 <= end; k += 2) {
-    int32_t j0 = col[k], j1 = col[k + 1];
-    uint8_t q0 = ecode[k], q1 = ecode[k + 1];
-    float4 x0 = x[(int64_t)j0 * d4 + c];
-    float4 x1 = x[(int64_t)j1 * d4 + c];
-    float4 e0 = f4add(E1[(q0 & 7) * d4 + c], E2[(q0 >> 3) * d4 + c]);
-    float4 e1 = f4add(E1[(q1 & 7) * d4 + c], E2[(q1 >> 3) * d4 + c]);
-    acc = f4add(acc, f4add(x0, e0));
-    acc = f4add(acc, f4add(x1, e1));
+  if (deg <= MOLCLR_NBR_SLOTS) {
+    const float4 m0 = deg > 0 ? gine_msg(x, Ec, s.x, d4, c) : acc;
+    const float4 m1 = deg > 1 ? gine_msg(x, Ec, s.y, d4, c) : acc;
+    const float4 m2 = deg > 2 ? gine_msg(x, Ec, s.z, d4, c) : acc;
+    const float4 m3 = deg > 3 ? gine_msg(x, Ec, s.w, d4, c) : acc;
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) acc = f4add(acc, m2);
+    if (deg > 3) acc = f4add(acc, m3);
+  } else {
+    for (int32_t k = rowptr[i], e = rowptr[i + 1]; k < e; ++k)
+      acc = f4add(acc, f4add(x[(int64_t)col[k] * d4 + c], Ec[MOLCLR_ECOMB(ecode[k]) * d4 + c]));
   }
-  if (k < end) {
-    int32_t j0 = col[k];
-    uint8_t q0 = ecode[k];
-    float4 e0 = f4add(E1[(q0 & 7) * d4 + c], E2[(q0 >> 3) * d4 + c]);
-    acc = f4add(acc, f4add(x[(int64_t)j0 * d4 + c], e0));
-  }
-  // self loop: bond type 4, bond dir 0, appended last (ginet_molclr.py:31-37)
-  float4 es = f4add(E1[MOLCLR_SELF_LOOP_BOND_TYPE * d4 + c], E2[c]);
-  acc = f4add(acc, f4add(x[t], es));
+  acc = f4add(acc, f4add(self, es));
   out[t] = acc;
 }
 
-// dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]
+// dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC)
 __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restrict__ g,
                                                          const int32_t* __restrict__ rowptr_t,
                                                          const int32_t* __restrict__ col_t,
+                                                         const uint4* __restrict__ nbr_t,
                                                          float4* __restrict__ dx, int64_t N,
                                                          int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t j = t / d4;
   int c = (int)(t - j * d4);
-  int32_t k = rowptr_t[j];
-  const int32_t end = rowptr_t[j + 1];
+  const uint4 s = nbr_t[j];
+  const float4 self = g[t];
+  const uint32_t deg = nbr_degree(s.x);
   float4 acc = f4zero();
-  for (; k + 2 <= end; k += 2) {
-    int32_t i0 = col_t[k], i1 = col_t[k + 1];
-    float4 g0 = g[(int64_t)i0 * d4 + c];
-    float4 g1 = g[(int64_t)i1 * d4 + c];
-    acc = f4add(acc, g0);
-    acc = f4add(acc, g1);
+  if (deg <= MOLCLR_NBR_SLOTS) {
+    const float4 m0 = deg > 0 ? g[(int64_t)nbr_node(s.x) * d4 + c] : acc;
+    const float4 m1 = deg > 1 ? g[(int64_t)nbr_node(s.y) * d4 + c] : acc;
+    const float4 m2 = deg > 2 ? g[(int64_t)nbr_node(s.z) * d4 + c] : acc;
+    const float4 m3 = deg > 3 ? g[(int64_t)nbr_node(s.w) * d4 + c] : acc;
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) acc = f4add(acc, m2);
+    if (deg > 3) acc = f4add(acc, m3);
+  } else {
+    for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k)
+      acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
   }
-  if (k < end) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
-  acc = f4add(acc, g[t]);
+  acc = f4add(acc, self);
   dx[t] = acc;
 }
 
@@ -232,28 +267,42 @@ __global__ void k_ecount_weighted_partial(const float4* __restrict__ g,
 // ---------------------------------------------------------------------------
 // GCN aggregation (scalar edge embedding, bias)
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 gcn_msg(const float4* __restrict__ xw, const float* __restrict__ E1,
+                                          const float* __restrict__ E2, int32_t j, int q, int d4,
+                                          int c) {
+  const float e = E1[q / 3] + E2[q % 3];
+  const float4 v = xw[(int64_t)j * d4 + c];
+  return make_float4(e + v.x, e + v.y, e + v.z, e + v.w);
+}
+
 __global__ __launch_bounds__(kT) void k_gcn_agg_fwd(
     const float4* __restrict__ xw, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
-    const float* __restrict__ E1, const float* __restrict__ E2, const float4* __restrict__ bias,
-    float4* __restrict__ out, int64_t N, int d4) {
+    const uint4* __restrict__ nbr, const float* __restrict__ E1, const float* __restrict__ E2,
+    const float4* __restrict__ bias, float4* __restrict__ out, int64_t N, int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
-  int32_t k = rowptr[i];
-  const int32_t end = rowptr[i + 1];
+  const uint4 s = nbr[i];
+  const float4 self = xw[t];
+  const uint32_t deg = nbr_degree(s.x);
   float4 acc = f4zero();
-  for (; k < end; ++k) {
-    int32_t j = col[k];
-    uint8_t q = ecode[k];
-    float e = E1[q & 7] + E2[q >> 3];
-    float4 v = xw[(int64_t)j * d4 + c];
-    acc = f4add(acc, make_float4(e + v.x, e + v.y, e + v.z, e + v.w));
+  if (deg <= MOLCLR_NBR_SLOTS) {
+    const float4 m0 = deg > 0 ? gcn_msg(xw, E1, E2, nbr_node(s.x), nbr_ecomb(s.x), d4, c) : acc;
+    const float4 m1 = deg > 1 ? gcn_msg(xw, E1, E2, nbr_node(s.y), nbr_ecomb(s.y), d4, c) : acc;
+    const float4 m2 = deg > 2 ? gcn_msg(xw, E1, E2, nbr_node(s.z), nbr_ecomb(s.z), d4, c) : acc;
+    const float4 m3 = deg > 3 ? gcn_msg(xw, E1, E2, nbr_node(s.w), nbr_ecomb(s.w), d4, c) : acc;
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) acc = f4add(acc, m2);
+    if (deg > 3) acc = f4add(acc, m3);
+  } else {
+    for (int32_t k = rowptr[i], e = rowptr[i + 1]; k < e; ++k)
+      acc = f4add(acc, gcn_msg(xw, E1, E2, col[k], MOLCLR_ECOMB(ecode[k]), d4, c));
   }
-  float es = E1[MOLCLR_SELF_LOOP_BOND_TYPE] + E2[0];
-  float4 v = xw[t];
-  acc = f4add(acc, make_float4(es + v.x, es + v.y, es + v.z, es + v.w));
+  const float es = E1[MOLCLR_SELF_LOOP_BOND_TYPE] + E2[0];
+  acc = f4add(acc, make_float4(es + self.x, es + self.y, es + self.z, es + self.w));
   out[t] = f4add(acc, bias[c]);
 }
 
@@ -359,19 +408,40 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
   return MOLCLR_OK;
 }
 
+MOLCLR_API int molclr_edge_tables_combine(int layers, const float* const* E1s,
+                                          const float* const* E2s, float* Ec, int64_t D,
+                                          molclr_stream_t stream) {
+  MOLCLR_REQUIRE(layers >= 0 && layers <= MOLCLR_MAX_LAYERS && D > 0,
+                 "edge_tables_combine: %d layers (max %d), dim %lld", layers, MOLCLR_MAX_LAYERS,
+                 (long long)D);
+  if (layers == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(E1s && E2s && Ec, "edge_tables_combine: null pointer");
+  TablePtrs p{};
+  for (int l = 0; l < layers; ++l) {
+    MOLCLR_REQUIRE(E1s[l] && E2s[l], "edge_tables_combine: null table of layer %d", l);
+    p.e1[l] = E1s[l];
+    p.e2[l] = E2s[l];
+  }
+  const int64_t n = (int64_t)layers * MOLCLR_NUM_ECOMB * D;
+  hipLaunchKernelGGL(k_edge_tables_combine, dim3(molclr::ceil_div(n, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), p, Ec, layers, D);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
 MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
                                          const int32_t* col, const uint8_t* ecode,
-                                         const float* E1, const float* E2, float* out,
+                                         const uint32_t* nbr, const float* Ec, float* out,
                                          int64_t N, int64_t D, molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_fwd: dim %lld must be a multiple of 4",
                  (long long)D);
   if (N == 0) return MOLCLR_OK;
-  MOLCLR_REQUIRE(x && rowptr && E1 && E2 && out, "gine_aggregate_fwd: null pointer");
+  MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
   molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       (const float4*)x, rowptr, col, ecode, (const float4*)E1,
-                       (const float4*)E2, (float4*)out, N, d4);
+                       (const float4*)x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec,
+                       (float4*)out, N, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -381,7 +451,8 @@ MOLCLR_API size_t molclr_gine_aggregate_bwd_workspace_bytes(int64_t N, int64_t D
 }
 
 MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t,
-                                         const int32_t* col_t, const int32_t* ecount, float* dx,
+                                         const int32_t* col_t, const uint32_t* nbr_t,
+                                         const int32_t* ecount, float* dx,
                                          float* dE1, float* dE2, int64_t N, int64_t D,
                                          int accumulate, void* workspace, size_t workspace_bytes,
                                          molclr_stream_t stream) {
@@ -389,8 +460,10 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
   hipStream_t s = molclr::as_stream(stream);
   int d4 = (int)(D / 4);
   if (dx && N > 0) {
+    MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gine_aggregate_bwd: null pointer");
     hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
-                       (const float4*)g, rowptr_t, col_t, (float4*)dx, N, d4);
+                       (const float4*)g, rowptr_t, col_t, (const uint4*)nbr_t, (float4*)dx, N,
+                       d4);
   }
   if (dE1 || dE2) {
     MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
@@ -411,15 +484,17 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
 
 MOLCLR_API int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr,
                                         const int32_t* col, const uint8_t* ecode,
-                                        const float* E1, const float* E2, const float* bias,
+                                        const uint32_t* nbr, const float* E1, const float* E2,
+                                        const float* bias,
                                         float* out, int64_t N, int64_t D,
                                         molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gcn_aggregate_fwd: dim must be a multiple of 4");
   if (N == 0) return MOLCLR_OK;
-  MOLCLR_REQUIRE(xw && rowptr && E1 && E2 && bias && out, "gcn_aggregate_fwd: null pointer");
+  MOLCLR_REQUIRE(xw && rowptr && nbr && E1 && E2 && bias && out, "gcn_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
   hipLaunchKernelGGL(k_gcn_agg_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), (const float4*)xw, rowptr, col, ecode, E1, E2,
+                     molclr::as_stream(stream), (const float4*)xw, rowptr, col, ecode,
+                     (const uint4*)nbr, E1, E2,
                      (const float4*)bias, (float4*)out, N, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
@@ -431,7 +506,8 @@ MOLCLR_API size_t molclr_gcn_aggregate_bwd_workspace_bytes(int64_t N, int64_t D)
 }
 
 MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
-                                        const int32_t* col_t, const int32_t* ecount, float* dxw,
+                                        const int32_t* col_t, const uint32_t* nbr_t,
+                                        const int32_t* ecount, float* dxw,
                                         float* dE1, float* dE2, float* dbias, int64_t N,
                                         int64_t D, int accumulate, void* workspace,
                                         size_t workspace_bytes, molclr_stream_t stream) {
@@ -440,8 +516,10 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
   hipStream_t s = molclr::as_stream(stream);
   int d4 = (int)(D / 4);
   if (dxw && N > 0) {
+    MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gcn_aggregate_bwd: null pointer");
     hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
-                       (const float4*)g, rowptr_t, col_t, (float4*)dxw, N, d4);
+                       (const float4*)g, rowptr_t, col_t, (const uint4*)nbr_t, (float4*)dxw, N,
+                       d4);
   }
   molclr::Workspace w(workspace, workspace_bytes);
   double* partial = w.take<double>(kRowsumBlocks * 4 * 8);

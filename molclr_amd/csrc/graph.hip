@@ -122,13 +122,16 @@ __global__ void k_graph_fill(const int32_t* __restrict__ src32, const int32_t* _
 }
 
 // Threads [0,N) finish CSR row i, threads [N,2N) finish CSC row i: sort the
-// row's edge ids (insertion sort; molecular degrees are tiny) and gather.
+// row's edge ids (insertion sort; molecular degrees are tiny), gather, and
+// write the row's neighbour-slot entry (uint4, see molclr.h): the first four
+// in-edges packed with their combined edge-table index, and the degree.
 __global__ void k_graph_rows(int64_t N, const int32_t* __restrict__ src32,
                              const int32_t* __restrict__ dst32, const uint8_t* __restrict__ code8,
                              const int32_t* __restrict__ rowptr, const int32_t* __restrict__ rowptr_t,
                              int32_t* __restrict__ perm, int32_t* __restrict__ perm_t,
                              int32_t* __restrict__ col, uint8_t* __restrict__ ecode,
-                             int32_t* __restrict__ col_t) {
+                             int32_t* __restrict__ col_t, uint4* __restrict__ nbr,
+                             uint4* __restrict__ nbr_t) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * N) return;
   bool csc = t >= N;
@@ -145,15 +148,24 @@ __global__ void k_graph_rows(int64_t N, const int32_t* __restrict__ src32,
     }
     p[b + 1] = key;
   }
+  uint32_t slot[MOLCLR_NBR_SLOTS] = {0u, 0u, 0u, 0u};
   if (!csc) {
     for (int32_t a = beg; a < end; ++a) {
       int32_t k = p[a];
       col[a] = src32[k];
       ecode[a] = code8[k];
+      if (a - beg < MOLCLR_NBR_SLOTS)
+        slot[a - beg] = (uint32_t)src32[k] | ((uint32_t)MOLCLR_ECOMB(code8[k]) << 24);
     }
   } else {
-    for (int32_t a = beg; a < end; ++a) col_t[a] = dst32[p[a]];
+    for (int32_t a = beg; a < end; ++a) {
+      col_t[a] = dst32[p[a]];
+      if (a - beg < MOLCLR_NBR_SLOTS) slot[a - beg] = (uint32_t)dst32[p[a]];
+    }
   }
+  const int32_t deg = end - beg;
+  slot[0] |= (uint32_t)(deg > MOLCLR_NBR_SLOTS ? MOLCLR_NBR_OVERFLOW : deg) << 29;
+  (csc ? nbr_t : nbr)[i] = make_uint4(slot[0], slot[1], slot[2], slot[3]);
 }
 
 __global__ void k_graph_ptr(const int64_t* __restrict__ batch, int64_t N, int64_t G,
@@ -191,12 +203,16 @@ MOLCLR_API size_t molclr_graph_build_workspace_bytes(int64_t N, int64_t E) {
 MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
                                   const int64_t* batch, int64_t N, int64_t E, int64_t G,
                                   int32_t* rowptr, int32_t* col, uint8_t* ecode,
-                                  int32_t* rowptr_t, int32_t* col_t, int32_t* ecount,
-                                  int32_t* graph_ptr, int32_t* status, void* workspace,
+                                  int32_t* rowptr_t, int32_t* col_t, uint32_t* nbr,
+                                  uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
+                                  int32_t* status, void* workspace,
                                   size_t workspace_bytes, molclr_stream_t stream) {
   MOLCLR_REQUIRE(N >= 0 && E >= 0 && G >= 0, "graph_build: negative size");
-  MOLCLR_REQUIRE(N < (int64_t)1 << 31 && E < (int64_t)1 << 31, "graph_build: N/E exceed int32");
-  MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status, "graph_build: null output");
+  MOLCLR_REQUIRE(N <= MOLCLR_NBR_MAX_NODES && E < (int64_t)1 << 31,
+                 "graph_build: %lld nodes exceed the neighbour-slot limit %d (or E > int32)",
+                 (long long)N, MOLCLR_NBR_MAX_NODES);
+  MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status && (N == 0 || (nbr && nbr_t)),
+                 "graph_build: null output");
   MOLCLR_REQUIRE(E == 0 || (edge_index && edge_attr && col && ecode && col_t),
                  "graph_build: null edge buffer");
   MOLCLR_REQUIRE(N == 0 || batch, "graph_build: null batch");
@@ -228,8 +244,11 @@ MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge
   if (E > 0) {
     hipLaunchKernelGGL(k_graph_fill, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, src32, dst32, E,
                        rowptr, rowptr_t, cur, cur_t, perm, perm_t);
+  }
+  if (N > 0) {
     hipLaunchKernelGGL(k_graph_rows, dim3(molclr::ceil_div(2 * N, T)), dim3(T), 0, s, N, src32,
-                       dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t);
+                       dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t,
+                       (uint4*)nbr, (uint4*)nbr_t);
   }
   int64_t n_ptr = N > G + 1 ? N : G + 1;
   hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, batch, N, G,

@@ -134,6 +134,8 @@ class DeviceGraph:
         self.ecode = torch.empty(max(E, 1), dtype=torch.uint8, device=dev)
         self.rowptr_t = torch.empty(N + 1, **i32)
         self.col_t = torch.empty(max(E, 1), **i32)
+        self.nbr = torch.empty(max(N, 1) * 4, **i32)    # neighbour slots (molclr.h)
+        self.nbr_t = torch.empty(max(N, 1) * 4, **i32)
         self.ecount = torch.empty(max(N, 1) * 8, **i32)
         self.graph_ptr = torch.empty(G + 1, **i32)
         self.status = torch.empty(1, **i32)
@@ -142,7 +144,7 @@ class DeviceGraph:
         _lib.call("molclr_graph_build", edge_index.data_ptr(), edge_attr.data_ptr(),
                   batch.data_ptr(), N, E, G, self.rowptr.data_ptr(), self.col.data_ptr(),
                   self.ecode.data_ptr(), self.rowptr_t.data_ptr(), self.col_t.data_ptr(),
-                  self.ecount.data_ptr(), self.graph_ptr.data_ptr(), self.status.data_ptr(),
+                  self.nbr.data_ptr(), self.nbr_t.data_ptr(), self.ecount.data_ptr(), self.graph_ptr.data_ptr(), self.status.data_ptr(),
                   ws.data_ptr(), ws_bytes, _lib.stream_of(dev))
         self.device = dev
 

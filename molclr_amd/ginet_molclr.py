@@ -42,9 +42,10 @@ class GINEConv(nn.Module):
         nn.init.xavier_uniform_(self.edge_embedding1.weight.data)
         nn.init.xavier_uniform_(self.edge_embedding2.weight.data)
 
-    def aggregate(self, x, graph: DeviceGraph):
+    def aggregate(self, x, graph: DeviceGraph, Ec=None):
+        """Ec: this layer's combined edge table (ops.edge_tables_combine), or None."""
         return ops.gine_aggregate(x, self.edge_embedding1.weight, self.edge_embedding2.weight,
-                                  graph)
+                                  graph, Ec)
 
     def update(self, aggr_out):
         return ops.gin_mlp(aggr_out, self.mlp[0].weight, self.mlp[0].bias, self.mlp[2].weight,
@@ -100,8 +101,11 @@ class GINet(nn.Module):
         """Node embeddings after the last layer (ginet_molclr.py:103-111)."""
         graph = graph or device_graph(data)
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
+        # per-edge embeddings E1[bt] + E2[bd] of every layer, tabulated in one launch
+        Ec = ops.edge_tables_combine([g.edge_embedding1.weight for g in self.gnns],
+                                     [g.edge_embedding2.weight for g in self.gnns])
         for layer in range(self.num_layer):
-            h = self.gnns[layer].update(self.gnns[layer].aggregate(h, graph))
+            h = self.gnns[layer].update(self.gnns[layer].aggregate(h, graph, Ec[layer]))
             last = layer == self.num_layer - 1
             h = ops.batch_norm(h, self.batch_norms[layer], relu=not last)
             if self.drop_ratio > 0 and self.training:

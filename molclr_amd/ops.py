@@ -181,9 +181,29 @@ def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=No
 
 def gine_aggregate_bytes(N: int, D: int, E: int) -> int:
     """Compulsory HBM bytes of one molclr_gine_aggregate_fwd launch: read x and
-    write the output once (2*N*D*4), rowptr (4(N+1)), col (4E), ecode (E);
-    the 5 x D / 3 x D edge tables are cache-resident."""
-    return 2 * N * D * 4 + 4 * (N + 1) + 5 * E
+    write the output once (2*N*D*4) and the 16-byte neighbour slots of every
+    node (16N); the 15 x D combined edge table is cache-resident, and the CSR
+    tail of the few rows of degree > 4 is not counted.  (E is kept for the
+    signature: the slot layout makes the compulsory bytes independent of it.)"""
+    return 2 * N * D * 4 + 16 * N
+
+
+def edge_tables_combine(E1s, E2s) -> torch.Tensor:
+    """Ec[l] = E1_l[bt] + E2_l[bd] for every (bt, bd), all layers in one launch
+    ([L, 15, D]); not differentiable (gradients flow through the aggregation's
+    count-weighted backward to E1/E2)."""
+    L = len(E1s)
+    if L == 0 or L > _lib.MAX_LAYERS:
+        raise ValueError(f"edge_tables_combine: {L} layers (1..{_lib.MAX_LAYERS})")
+    _check(*E1s, *E2s)
+    E1s = [_c(e.detach()) for e in E1s]
+    E2s = [_c(e.detach()) for e in E2s]
+    D = E1s[0].shape[1]
+    Ec = torch.empty(L, _lib.NUM_ECOMB, D, dtype=torch.float32, device=E1s[0].device)
+    arr1 = (ctypes.c_void_p * L)(*[e.data_ptr() for e in E1s])
+    arr2 = (ctypes.c_void_p * L)(*[e.data_ptr() for e in E2s])
+    _lib.call("molclr_edge_tables_combine", L, arr1, arr2, Ec.data_ptr(), D, _stream(Ec))
+    return Ec
 
 
 # ---------------------------------------------------------------------------
@@ -225,14 +245,18 @@ class _AtomEmbed(torch.autograd.Function):
 
 class _GINEAggregate(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, E1, E2, graph: DeviceGraph):
-        _check(h, E1, E2)
+    def forward(ctx, h, E1, E2, graph: DeviceGraph, Ec):
+        _check(h, E1, E2, Ec)
         h = _c(h)
         N, D = h.shape
+        if Ec is None:
+            Ec = edge_tables_combine([E1], [E2])[0]
+        if Ec.shape != (_lib.NUM_ECOMB, D) or not Ec.is_contiguous():
+            raise ValueError(f"gine_aggregate: Ec must be a contiguous [15, {D}] table")
         out = torch.empty_like(h)
         _lib.call("molclr_gine_aggregate_fwd", h.data_ptr(), graph.rowptr.data_ptr(),
-                  graph.col.data_ptr(), graph.ecode.data_ptr(), E1.data_ptr(), E2.data_ptr(),
-                  out.data_ptr(), N, D, _stream(h))
+                  graph.col.data_ptr(), graph.ecode.data_ptr(), graph.nbr.data_ptr(),
+                  Ec.data_ptr(), out.data_ptr(), N, D, _stream(h))
         if _TIMER is not None:
             _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges))
         ctx.graph = graph
@@ -265,9 +289,10 @@ class _GINEAggregate(torch.autograd.Function):
         ws_bytes = _wsq("molclr_gine_aggregate_bwd_workspace_bytes", N, D)
         ws = _ws(ws_bytes, g.device)
         _lib.call("molclr_gine_aggregate_bwd", g.data_ptr(), graph.rowptr_t.data_ptr(),
-                  graph.col_t.data_ptr(), graph.ecount.data_ptr(), _lib.ptr(dx), _lib.ptr(b1),
-                  _lib.ptr(b2), N, D, acc, ws.data_ptr(), ws_bytes, _stream(g))
-        return dx, r1, r2, None
+                  graph.col_t.data_ptr(), graph.nbr_t.data_ptr(), graph.ecount.data_ptr(),
+                  _lib.ptr(dx), _lib.ptr(b1), _lib.ptr(b2), N, D, acc, ws.data_ptr(), ws_bytes,
+                  _stream(g))
+        return dx, r1, r2, None, None
 
 
 class _MLP(torch.autograd.Function):
@@ -402,7 +427,8 @@ class _GCNConv(torch.autograd.Function):
         xw = gemm(x, W, N, Dout, Din, Din, Dout, False, True)
         out = torch.empty(N, Dout, dtype=torch.float32, device=x.device)
         _lib.call("molclr_gcn_aggregate_fwd", xw.data_ptr(), graph.rowptr.data_ptr(),
-                  graph.col.data_ptr(), graph.ecode.data_ptr(), E1.data_ptr(), E2.data_ptr(),
+                  graph.col.data_ptr(), graph.ecode.data_ptr(), graph.nbr.data_ptr(),
+                  E1.data_ptr(), E2.data_ptr(),
                   bias.data_ptr(), out.data_ptr(), N, Dout, _stream(x))
         ctx.save_for_backward(x, W)
         ctx.graph = graph
@@ -428,7 +454,8 @@ class _GCNConv(torch.autograd.Function):
         ws_bytes = _wsq("molclr_gcn_aggregate_bwd_workspace_bytes", N, Dout)
         ws = _ws(ws_bytes, g.device)
         _lib.call("molclr_gcn_aggregate_bwd", g.data_ptr(), ctx.graph.rowptr_t.data_ptr(),
-                  ctx.graph.col_t.data_ptr(), ctx.graph.ecount.data_ptr(), dxw.data_ptr(),
+                  ctx.graph.col_t.data_ptr(), ctx.graph.nbr_t.data_ptr(),
+                  ctx.graph.ecount.data_ptr(), dxw.data_ptr(),
                   _lib.ptr(sinks["e1"][0]), _lib.ptr(sinks["e2"][0]), _lib.ptr(sinks["b"][0]),
                   N, Dout, acc, ws.data_ptr(), ws_bytes, _stream(g))
         db, dE1, dE2 = sinks["b"][2], sinks["e1"][2], sinks["e2"][2]
@@ -548,8 +575,9 @@ def atom_embed(x_idx, X1, X2):
     return _AtomEmbed.apply(x_idx, X1, X2)
 
 
-def gine_aggregate(h, E1, E2, graph):
-    return _GINEAggregate.apply(h, E1, E2, graph)
+def gine_aggregate(h, E1, E2, graph, Ec=None):
+    """Ec: this layer's [15, D] slice of edge_tables_combine (computed here if None)."""
+    return _GINEAggregate.apply(h, E1, E2, graph, Ec)
 
 
 def gin_mlp(x, W1, b1, W2, b2):

@@ -14,7 +14,10 @@ numpy restatement of the integer work on the path, for bit-exact checks of
 * bond-type / bond-dir counts per destination include the self loop
   (edge attr [4, 0], ginet_molclr.py:34-37);
 * graph offsets are the ``ptr`` of PyG's collate (nodes of graph g are
-  contiguous, batch ascending).
+  contiguous, batch ascending);
+* the neighbour slots (``nbr`` / ``nbr_t``, a layout of this build, see
+  include/molclr.h) restate the first 4 entries of every CSR / CSC row packed
+  with the combined edge-table index ``bt * 3 + bd`` and the row degree.
 """
 from __future__ import annotations
 
@@ -44,5 +47,24 @@ def graph_build(edge_index: np.ndarray, edge_attr: np.ndarray, batch: np.ndarray
     b = np.asarray(batch, dtype=np.int64)
     graph_ptr = np.searchsorted(b, np.arange(num_graphs + 1), side="left").astype(np.int32)
     graph_ptr[num_graphs] = N
+    ecomb = (ecode & 7).astype(np.uint32) * 3 + (ecode >> 3).astype(np.uint32)
+    nbr = neighbour_slots(rowptr, col.astype(np.uint32) | (ecomb << 24))
+    nbr_t = neighbour_slots(rowptr_t, col_t.astype(np.uint32))
     return dict(rowptr=rowptr, col=col, ecode=ecode, rowptr_t=rowptr_t, col_t=col_t,
-                ecount=ecount.reshape(-1), graph_ptr=graph_ptr)
+                nbr=nbr, nbr_t=nbr_t, ecount=ecount.reshape(-1), graph_ptr=graph_ptr)
+
+
+SLOTS, OVERFLOW = 4, 7
+
+
+def neighbour_slots(rowptr: np.ndarray, packed: np.ndarray) -> np.ndarray:
+    """[N*4] u32 view as int32: row i's first 4 packed entries, degree (or 7
+    when > 4) in bits 29..31 of word 0."""
+    N = len(rowptr) - 1
+    out = np.zeros((N, SLOTS), dtype=np.uint32)
+    deg = np.diff(rowptr)
+    for s in range(SLOTS):
+        rows = np.nonzero(deg > s)[0]
+        out[rows, s] = packed[rowptr[rows] + s]
+    out[:, 0] |= np.where(deg > SLOTS, OVERFLOW, deg).astype(np.uint32) << 29
+    return out.reshape(-1).view(np.int32)

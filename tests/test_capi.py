@@ -49,6 +49,11 @@ def test_version_and_error_plumbing(lib):
     assert b"epilogue" in lib.molclr_last_error()
     rc = lib.molclr_gine_aggregate_fwd(None, None, None, None, None, None, None, 10, 301, None)
     assert rc == -1 and b"multiple of 4" in lib.molclr_last_error()
+    rc = lib.molclr_edge_tables_combine(17, None, None, None, 300, None)
+    assert rc == -1 and b"layers" in lib.molclr_last_error()
+    rc = lib.molclr_graph_build(None, None, None, (1 << 24) + 1, 0, 1, None, None, None, None, None,
+                                None, None, None, None, None, None, 0, None)
+    assert rc == -1 and b"neighbour-slot" in lib.molclr_last_error()
 
 
 def test_workspace_queries(lib):

@@ -102,3 +102,15 @@ def test_oracle_graph_build_properties():
     deg = np.diff(g["rowptr"])
     assert np.array_equal(ec[:, :5].sum(1), deg + 1) and np.array_equal(ec[:, 5:].sum(1), deg + 1)
     assert np.array_equal(g["graph_ptr"], bi.ptr.numpy())
+    # neighbour slots: first 4 row entries (+ combined edge type), degree in bits 29..31
+    for key, ptr, colk in (("nbr", "rowptr", "col"), ("nbr_t", "rowptr_t", "col_t")):
+        slots = g[key].view(np.uint32).reshape(N, 4)
+        for i in range(N):
+            b, e = g[ptr][i], g[ptr][i + 1]
+            assert slots[i, 0] >> 29 == (e - b if e - b <= 4 else 7)
+            for s in range(min(4, e - b)):
+                w = int(slots[i, s]) & 0x1FFFFFFF
+                assert w & 0xFFFFFF == g[colk][b + s]
+                if key == "nbr":
+                    q = int(g["ecode"][b + s])
+                    assert w >> 24 == (q & 7) * 3 + (q >> 3)

@@ -46,7 +46,8 @@ def test_graph_build_bit_exact(dev, B):
                       b.num_graphs)
     E = b.edge_index.shape[1]
     got = dict(rowptr=g.rowptr, col=g.col[:E], ecode=g.ecode[:E], rowptr_t=g.rowptr_t,
-               col_t=g.col_t[:E], ecount=g.ecount[: 8 * b.x.shape[0]], graph_ptr=g.graph_ptr)
+               col_t=g.col_t[:E], nbr=g.nbr, nbr_t=g.nbr_t, ecount=g.ecount[: 8 * b.x.shape[0]],
+               graph_ptr=g.graph_ptr)
     for k, v in got.items():
         assert np.array_equal(v.cpu().numpy(), ref[k]), k
 
@@ -122,6 +123,50 @@ def test_gine_aggregate_matches_reference_order(dev, B, D):
     out.backward(go.to(dev))
     assert rel(hd.grad, hr.grad) < TOL
     assert rel(E1d.grad, E1r.grad) < TOL and rel(E2d.grad, E2r.grad) < TOL
+
+
+def hub_batch():
+    """Two molecules: a 10-atom star (hub in/out degree 9 > the 4 neighbour
+    slots, the CSR/CSC fallback) with a ring bond, and an isolated atom."""
+    pairs = [(0, k) for k in range(1, 10)] + [(1, 2)]
+    ei = []
+    for a, b_ in pairs:
+        ei += [(a, b_), (b_, a)]
+    ei = torch.tensor(ei, dtype=torch.long).t().contiguous()
+    E = ei.shape[1]
+    g = torch.Generator().manual_seed(0)
+    ea = torch.stack([torch.randint(0, 4, (E,), generator=g), torch.randint(0, 3, (E,), generator=g)], 1)
+    x = torch.stack([torch.randint(0, 119, (11,), generator=g), torch.randint(0, 3, (11,), generator=g)], 1)
+    from molclr_amd.data import Batch, Data
+    return Batch.from_data_list([Data(x=x[:10], edge_index=ei, edge_attr=ea),
+                                 Data(x=x[10:], edge_index=torch.zeros(2, 0, dtype=torch.long),
+                                      edge_attr=torch.zeros(0, 2, dtype=torch.long))])
+
+
+@pytest.mark.parametrize("D", [4, 300])
+def test_gine_aggregate_high_degree(dev, D):
+    b = hub_batch()
+    N = b.x.shape[0]
+    g = dgraph(b, dev)
+    ref_g = graph_build(b.edge_index.numpy(), b.edge_attr.numpy(), b.batch.numpy(), N, b.num_graphs)
+    assert np.array_equal(g.nbr.cpu().numpy(), ref_g["nbr"])
+    assert np.array_equal(g.nbr_t.cpu().numpy(), ref_g["nbr_t"])
+    assert (ref_g["nbr"].view(np.uint32)[0] >> 29) == 7  # hub row overflows the slots
+    torch.manual_seed(3)
+    h, E1, E2 = torch.randn(N, D), torch.randn(5, D), torch.randn(3, D)
+    ei = add_self_loops(b.edge_index, N)
+    sl = torch.zeros(N, 2, dtype=torch.long)
+    sl[:, 0] = 4
+    ea = torch.cat([b.edge_attr, sl], 0)
+    hr = h.clone().requires_grad_(True)
+    ref = propagate_add(hr, ei, N, lambda xj: xj + (E1[ea[:, 0]] + E2[ea[:, 1]]))
+    hd = h.to(dev).requires_grad_(True)
+    out = ops.gine_aggregate(hd, E1.to(dev), E2.to(dev), g)
+    assert torch.equal(out.detach().cpu(), ref.detach())
+    go = torch.randn(N, D)
+    ref.backward(go)
+    out.backward(go.to(dev))
+    assert torch.equal(hd.grad.cpu(), hr.grad)
 
 
 def test_gcn_conv(dev):
