@@ -194,12 +194,37 @@ int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t
                     molclr_stream_t stream);
 
 /* Implementation switch (process-wide, not thread-safe): 0 = f32-input MFMA
- * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 (default) = split-bf16 ("x6": each fp32
- * operand split exactly into 3 bf16 parts, six bf16 MFMA products, fp32
- * accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64;
- * 3 = split-bf16, 128x128. */
+ * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 = split-bf16 ("x6": each fp32
+ * operand split into 3 round-to-nearest bf16 parts, six bf16 MFMA products,
+ * fp32 accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64;
+ * 3 = split-bf16, 128x128; 4 = split-bf16 with all nine products, 64x64;
+ * 5 (default) / 6 = split-bf16 with the second-generation staging ("p6"),
+ * 64x64 / 128x64. */
 int molclr_gemm_set_impl(int impl);
 int molclr_gemm_get_impl(void);
+
+/* Pre-split weight operand.  A Linear layer's weight is the B operand of the
+ * forward (y = x W^T) and data-gradient (dx = dy W) GEMMs of every row tile;
+ * splitting it once per optimizer step instead of once per row tile takes
+ * half of the split work out of those GEMMs.
+ *   molclr_bplanes_make: planes [3][Npad][Kp] bf16 (hi, mid, lo parts, the
+ *     same split as the GEMM) of B(k, n) — stored like molclr_gemm_f32's B
+ *     (b_kmajor: B[k*ldb + n], else B[n*ldb + k]) — zero-padded to
+ *     Npad = N rounded up to 128, Kp = K rounded up to 32.
+ *     molclr_bplanes_bytes(N, K) is their size.
+ *   molclr_gemm_f32_bplanes: molclr_gemm_f32 with B given as such planes
+ *     (same epilogues, split-K workspace from molclr_gemm_f32_workspace_bytes);
+ *     a_kmajor needs M and lda multiples of 4, else K and lda. */
+size_t molclr_bplanes_bytes(int64_t N, int64_t K);
+int molclr_bplanes_make(const float* B, int64_t N, int64_t K, int64_t ldb, int b_kmajor,
+                        uint16_t* planes, molclr_stream_t stream);
+int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
+                            int64_t N, int64_t K, int64_t lda, int64_t ldc, int a_kmajor,
+                            int epilogue_flags, const float* bias, const float* aux,
+                            int64_t ldaux, void* workspace, size_t workspace_bytes,
+                            molclr_stream_t stream);
+/* tile of molclr_gemm_f32_bplanes: 5 (default) = 64x64, 6 = 128x64 */
+int molclr_gemm_bplanes_set_impl(int impl);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);

@@ -518,6 +518,356 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TM * TN == 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 GEMM, second generation ("p6"): the same six-product scheme and
+// LDS image as k_gemm_x6, with the staging cost cut down — that, not the
+// MFMA, bounds k_gemm_x6 (rocprofv3: ~20 VALU instructions per MFMA, MFMA
+// busy 22 %).
+//  * Operand sources (template AMODE / BMODE):
+//      0 fp32, K contiguous ([rows][K]): a thread stages 8 consecutive k of
+//        one row (two float4 loads) and writes one 16-byte chunk per plane;
+//      1 fp32, K-major ([K][rows], the dY^T / X^T of a weight gradient): a
+//        thread stages a 4-row x 4-k block and transposes it in registers;
+//      2 pre-split bf16 planes ([3][Npad][Kp], molclr_bplanes_make): the
+//        weights of a Linear layer, split once per optimizer step instead of
+//        once per row tile — staging is a plain 16-byte copy.
+//  * Row pointers are fixed per thread (rows clamped once; rows beyond M / N
+//    only feed output rows the epilogue never stores); K advances by pointer
+//    offsets, and only the last, partial K tile takes the masked path.
+// ---------------------------------------------------------------------------
+constexpr int kPlanesRowPad = 128;  // Npad multiple (covers every BN)
+
+__device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4& hi, u32x4& mid,
+                                       u32x4& lo) {
+  uint32_t h[4], m[4], l[4];
+  split2(a.x, a.y, h[0], m[0], l[0]);
+  split2(a.z, a.w, h[1], m[1], l[1]);
+  split2(b.x, b.y, h[2], m[2], l[2]);
+  split2(b.z, b.w, h[3], m[3], l[3]);
+  hi = u32x4{h[0], h[1], h[2], h[3]};
+  mid = u32x4{m[0], m[1], m[2], m[3]};
+  lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+// fp32, K contiguous: unit = (row, 8-k chunk); ROWS*4 units over T threads.
+template <int ROWS, int T>
+struct PStageK {
+  static constexpr int UNITS = ROWS * 4;
+  static constexpr int PER = (UNITS + T - 1) / T;
+  const float* p[PER];
+  float4 r[PER][2];
+  __device__ __forceinline__ void init(const float* __restrict__ src, int64_t ld, int64_t row0,
+                                       int64_t rows, int t) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      const int64_t gr = row0 + (u >> 2);
+      p[j] = src + (gr < rows ? gr : rows - 1) * ld + 8 * (u & 3);
+    }
+  }
+  __device__ __forceinline__ void load(int64_t k0, int64_t K, int t) {
+    const bool full = k0 + BK <= K;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (UNITS % T && t + j * T >= UNITS) continue;
+      const float* q = p[j] + k0;
+      if (full) {
+        r[j][0] = *reinterpret_cast<const float4*>(q);
+        r[j][1] = *reinterpret_cast<const float4*>(q + 4);
+      } else {  // last K tile: K % 4 == 0, so each float4 is all in or all out
+        const int64_t k = k0 + 8 * ((t + j * T) & 3);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        r[j][0] = k < K ? *reinterpret_cast<const float4*>(q) : z;
+        r[j][1] = k + 4 < K ? *reinterpret_cast<const float4*>(q + 4) : z;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      if (UNITS % T && u >= UNITS) continue;
+      u32x4 hi, mid, lo;
+      split8(r[j][0], r[j][1], hi, mid, lo);
+      const int o = xoff(u >> 2, u & 3);
+      *reinterpret_cast<u32x4*>(img + o) = hi;
+      *reinterpret_cast<u32x4*>(img + ROWS * XK + o) = mid;
+      *reinterpret_cast<u32x4*>(img + 2 * ROWS * XK + o) = lo;
+    }
+  }
+};
+
+// fp32, K-major: unit = 4 rows x 4 k (rb fastest: a wave reads 64 consecutive
+// rows of one k); (ROWS/4)*8 units.  Needs rows % 4 == 0 and ld % 4 == 0.
+template <int ROWS, int T>
+struct PStageM {
+  static constexpr int UNITS = (ROWS / 4) * (BK / 4);
+  static constexpr int PER = (UNITS + T - 1) / T;
+  const float* p[PER];
+  int64_t ld;
+  float4 r[PER][4];
+  __device__ __forceinline__ void init(const float* __restrict__ src, int64_t ld_, int64_t row0,
+                                       int64_t rows, int t) {
+    ld = ld_;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      const int rb = u % (ROWS / 4), kb = u / (ROWS / 4);
+      const int64_t gr = row0 + 4 * rb;
+      p[j] = src + (int64_t)(4 * kb) * ld + (gr < rows ? gr : rows - 4);
+    }
+  }
+  __device__ __forceinline__ void load(int64_t k0, int64_t K, int t) {
+    const bool full = k0 + BK <= K;
+    const int64_t base = k0 * ld;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      if (UNITS % T && u >= UNITS) continue;
+      const int kb = u / (ROWS / 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float* q = p[j] + base + i * ld;
+        if (full) {
+          r[j][i] = *reinterpret_cast<const float4*>(q);
+        } else {
+          r[j][i] = k0 + 4 * kb + i < K ? *reinterpret_cast<const float4*>(q)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      if (UNITS % T && u >= UNITS) continue;
+      const int rb = u % (ROWS / 4), kb = u / (ROWS / 4);
+      const float4* v = r[j];
+      const float4 row[4] = {make_float4(v[0].x, v[1].x, v[2].x, v[3].x),
+                             make_float4(v[0].y, v[1].y, v[2].y, v[3].y),
+                             make_float4(v[0].z, v[1].z, v[2].z, v[3].z),
+                             make_float4(v[0].w, v[1].w, v[2].w, v[3].w)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint2 hi, mid, lo;
+        split4(row[i], hi, mid, lo);
+        const int o = xoff(4 * rb + i, kb >> 1) + 4 * (kb & 1);
+        *reinterpret_cast<uint2*>(img + o) = hi;
+        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
+        *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
+      }
+    }
+  }
+};
+
+// pre-split planes [3][Npad][Kp] bf16: unit = (plane, row, 16-byte chunk)
+template <int ROWS, int T>
+struct PStageP {
+  static constexpr int UNITS = 3 * ROWS * 4;
+  static constexpr int PER = (UNITS + T - 1) / T;
+  const uint16_t* p[PER];
+  int off[PER];
+  u32x4 r[PER];
+  __device__ __forceinline__ void init(const uint16_t* __restrict__ planes, int64_t kp,
+                                       int64_t plane_stride, int64_t row0, int t) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      const int pl = u / (ROWS * 4), rem = u % (ROWS * 4);
+      p[j] = planes + pl * plane_stride + (row0 + (rem >> 2)) * kp + 8 * (rem & 3);
+      off[j] = pl * ROWS * XK + xoff(rem >> 2, rem & 3);
+    }
+  }
+  __device__ __forceinline__ void load(int64_t k0, int64_t, int t) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (UNITS % T && t + j * T >= UNITS) continue;
+      r[j] = *reinterpret_cast<const u32x4*>(p[j] + k0);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (UNITS % T && t + j * T >= UNITS) continue;
+      *reinterpret_cast<u32x4*>(img + off[j]) = r[j];
+    }
+  }
+};
+
+template <int MODE, int ROWS, int T>
+struct PStageSel;
+template <int ROWS, int T>
+struct PStageSel<0, ROWS, T> { using type = PStageK<ROWS, T>; };
+template <int ROWS, int T>
+struct PStageSel<1, ROWS, T> { using type = PStageM<ROWS, T>; };
+template <int ROWS, int T>
+struct PStageSel<2, ROWS, T> { using type = PStageP<ROWS, T>; };
+
+template <int TM, int TN, int AMODE, int BMODE, int EPI, bool SPLIT>
+__global__ __launch_bounds__(256) void k_gemm_p6(
+    const float* __restrict__ A, const float* __restrict__ Bf, const uint16_t* __restrict__ Bp,
+    float* __restrict__ C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+    int64_t bplane_stride, int64_t ldc, const float* __restrict__ bias,
+    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
+  constexpr int T = 256;
+  constexpr int BM = 64 * TM, BN = 64 * TN;
+  constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (AI + BI)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
+  const int nk_total = (int)((K + BK - 1) / BK);
+  const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
+  int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
+  if (kt_end > nk_total) kt_end = nk_total;
+
+  f32x16 acc[TM][TN], acl[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = acl[a][b][r] = 0.f;
+
+  using SA = typename PStageSel<AMODE, BM, T>::type;
+  using SB = typename PStageSel<BMODE, BN, T>::type;
+  // a K-major operand with fewer units than threads leaves threads idle: give
+  // the other operand's units to those threads (as k_gemm_x6 does)
+  const int ta = tid;
+  const int tb = (AMODE == 1 && SA::UNITS < T) ? (tid + SA::UNITS) % T : tid;
+  SA sa0, sa1;
+  SB sb0, sb1;
+  sa0.init(A, lda, m0, M, ta);
+  if constexpr (BMODE == 2) sb0.init(Bp, ldb, bplane_stride, n0, tb);
+  else sb0.init(Bf, ldb, n0, N, tb);
+  sa1 = sa0;
+  sb1 = sb0;
+  uint16_t* buf0 = lds;
+  uint16_t* buf1 = lds + (AI + BI);
+
+  auto compute = [&](const uint16_t* As) {
+    const uint16_t* Bs = As + AI;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 2 + lh;
+      bf16x8 bh[TN], bm[TN], bl[TN];
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int bro = wn * TN * 32 + b * 32 + li;
+        bh[b] = xfrag(Bs, bro, ch);
+        bm[b] = xfrag(Bs + BN * XK, bro, ch);
+        bl[b] = xfrag(Bs + 2 * BN * XK, bro, ch);
+      }
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int aro = wm * TM * 32 + a * 32 + li;
+        const bf16x8 ah = xfrag(As, aro, ch);
+        const bf16x8 am = xfrag(As + BM * XK, aro, ch);
+        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, ch);
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[b], acl[a][b], 0, 0, 0);
+          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[b], acl[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[b], acc[a][b], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int nsteps = kt_end - kt_beg;
+  auto kof = [&](int step) { return (int64_t)(kt_beg + step) * BK; };
+  if (nsteps > 0) {
+    sa0.load(kof(0), K, ta);
+    sb0.load(kof(0), K, tb);
+    if (nsteps > 1) {
+      sa1.load(kof(1), K, ta);
+      sb1.load(kof(1), K, tb);
+    }
+    sa0.store(buf0, ta);
+    sb0.store(buf0 + AI, tb);
+    __syncthreads();
+  }
+  int i = 0;
+  for (; i + 2 <= nsteps; i += 2) {
+    if (i + 2 < nsteps) {
+      sa0.load(kof(i + 2), K, ta);
+      sb0.load(kof(i + 2), K, tb);
+    }
+    compute(buf0);
+    sa1.store(buf1, ta);
+    sb1.store(buf1 + AI, tb);
+    __syncthreads();
+    if (i + 3 < nsteps) {
+      sa1.load(kof(i + 3), K, ta);
+      sb1.load(kof(i + 3), K, tb);
+    }
+    compute(buf1);
+    if (i + 2 < nsteps) {
+      sa0.store(buf0, ta);
+      sb0.store(buf0 + AI, tb);
+    }
+    __syncthreads();
+  }
+  if (i < nsteps) compute(buf0);
+
+  float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
+  const int64_t ldo = SPLIT ? N : ldc;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= M) continue;
+        float v = acc[a][b][r] + acl[a][b][r];
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
+          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
+          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
+          if (accumulate) v += Cout[m * ldo + n];
+        }
+        Cout[m * ldo + n] = v;
+      }
+    }
+  }
+}
+
+// planes[p][n][k] (p = hi, mid, lo) of B(k, n), zero beyond (N, K); one
+// thread per (n, k) of the padded [Npad][Kp] grid.
+__global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K, int64_t ldb,
+                               int kmajor, uint16_t* __restrict__ planes, int64_t npad,
+                               int64_t kp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= npad * kp) return;
+  const int64_t n = t / kp, k = t - n * kp;
+  float v = 0.f;
+  if (n < N && k < K) v = kmajor ? B[k * ldb + n] : B[n * ldb + k];
+  uint32_t h, m, l;
+  split2(v, 0.f, h, m, l);
+  const int64_t ps = npad * kp;
+  planes[t] = (uint16_t)(h & 0xFFFFu);
+  planes[ps + t] = (uint16_t)(m & 0xFFFFu);
+  planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
+}
+
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
 template <int EPI>
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
@@ -536,11 +886,12 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
 }
 
 // 0 = f32-input MFMA, 64 x 64 tiles; split-bf16 with 6 products and 1 = 64 x 64,
-// 2 = 128 x 64, 3 = 128 x 128 tiles; 4 = split-bf16 with all 9 products, 64 x 64
-// (molclr_gemm_set_impl).  The split-bf16 kernels stage K-major
-// operands 4 rows at a time, so they need rows % 4 == 0 and ld % 4 == 0 there;
-// other shapes take impl 0.
-int g_impl = 1;  // split-bf16 64 x 64: fastest on every shape of the step (profiles/)
+// 2 = 128 x 64, 3 = 128 x 128 tiles; 4 = split-bf16 with all 9 products, 64 x 64;
+// 5 / 6 = split-bf16 "p6" staging, 64 x 64 / 128 x 64 (molclr_gemm_set_impl).
+// The split-bf16 kernels stage K-major operands 4 rows at a time, so they need
+// rows % 4 == 0 and ld % 4 == 0 there; other shapes take impl 0.
+int g_impl = 5;
+int g_bplanes_impl = 5;  // tile of molclr_gemm_f32_bplanes: 5 = 64 x 64, 6 = 128 x 64
 int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   if (g_impl == 0) return 0;
   if (ak && (M % 4 || lda % 4)) return 0;
@@ -548,7 +899,7 @@ int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   return g_impl;
 }
 int tiles_for(int impl, int64_t M, int64_t N) {
-  const int64_t bm = (impl == 2 || impl == 3) ? 128 : 64, bn = impl == 3 ? 128 : 64;
+  const int64_t bm = (impl == 2 || impl == 3 || impl == 6) ? 128 : 64, bn = impl == 3 ? 128 : 64;
   return (int)(((M + bm - 1) / bm) * ((N + bn - 1) / bn));
 }
 
@@ -570,10 +921,27 @@ struct Args {
   int64_t ldaux;
   int kps, accumulate;
   int impl;
+  const uint16_t* Bp = nullptr;  // pre-split planes (molclr_gemm_f32_bplanes)
+  int64_t bps = 0;               // their plane stride
 };
+
+template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT>
+void launch_p6(dim3 grid, hipStream_t s, const Args& a) {
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_p6<TM, 1, AMODE, BMODE, EPI, SPLIT>), grid,
+                       dim3(256), 0, s, a.A, a.B, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.bps,
+                       a.ldc, a.bias, a.aux, a.ldaux, a.kps, a.accumulate);
+}
 
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
+  if (a.impl == 5) {
+    launch_p6<1, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
+    return;
+  }
+  if (a.impl == 6) {
+    launch_p6<2, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
+    return;
+  }
   if (a.impl == 1) {
     molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, 1, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
                          0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
@@ -636,12 +1004,109 @@ int dispatch(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
   return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, a);
 }
 
+template <int TM, bool SPLIT>
+int dispatch_bplanes_t(int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
+#define MOLCLR_BP_CASE(AKV, EPV)                                             \
+  if (ak == AKV && (SPLIT || epi == EPV)) {                                  \
+    launch_p6<TM, AKV, 2, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(grid, s, a); \
+    return 0;                                                                \
+  }
+  if (SPLIT) {
+    MOLCLR_BP_CASE(0, MOLCLR_EPI_NONE)
+    MOLCLR_BP_CASE(1, MOLCLR_EPI_NONE)
+  } else {
+    MOLCLR_BP_CASE(0, MOLCLR_EPI_NONE)
+    MOLCLR_BP_CASE(0, MOLCLR_EPI_BIAS)
+    MOLCLR_BP_CASE(0, MOLCLR_EPI_BIAS_RELU)
+    MOLCLR_BP_CASE(0, MOLCLR_EPI_RELU_MASK)
+    MOLCLR_BP_CASE(1, MOLCLR_EPI_NONE)
+    MOLCLR_BP_CASE(1, MOLCLR_EPI_BIAS)
+    MOLCLR_BP_CASE(1, MOLCLR_EPI_BIAS_RELU)
+    MOLCLR_BP_CASE(1, MOLCLR_EPI_RELU_MASK)
+  }
+#undef MOLCLR_BP_CASE
+  return -1;
+}
+
+template <bool SPLIT>
+int dispatch_bplanes(int impl, int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
+  return impl == 6 ? dispatch_bplanes_t<2, SPLIT>(ak, epi, grid, s, a)
+                   : dispatch_bplanes_t<1, SPLIT>(ak, epi, grid, s, a);
+}
+
+int64_t planes_npad(int64_t N) { return (N + kPlanesRowPad - 1) / kPlanesRowPad * kPlanesRowPad; }
+int64_t planes_kp(int64_t K) { return (K + BK - 1) / BK * BK; }
+
+// Launches the main GEMM (split-K when it pays) and the split-K reduction.
+// `bp` selects the pre-split-B kernels.
+int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int epilogue,
+             void* workspace, size_t workspace_bytes, hipStream_t s) {
+  const int64_t M = a0.M, N = a0.N, K = a0.K;
+  int64_t tiles = tiles_for(impl, M, N);  // workgroups along x
+  MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
+  int sp = pick_splits(impl, M, N, K);
+  if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
+  Args a = a0;
+  a.impl = impl;
+  int rc;
+  if (sp == 1) {
+    rc = bp ? dispatch_bplanes<false>(impl, a_kmajor, epilogue, dim3((unsigned)tiles), s, a)
+            : dispatch<false>(a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, a);
+  } else {
+    int64_t nk = (K + BK - 1) / BK;
+    int kps = (int)((nk + sp - 1) / sp);
+    sp = (int)((nk + kps - 1) / kps);
+    float* partial = (float*)workspace;
+    Args ap = a;
+    ap.C = partial;
+    ap.ldc = N;
+    ap.bias = nullptr;
+    ap.aux = nullptr;
+    ap.ldaux = 0;
+    ap.kps = kps;
+    ap.accumulate = 0;
+    rc = bp ? dispatch_bplanes<true>(impl, a_kmajor, MOLCLR_EPI_NONE, dim3((unsigned)tiles, sp), s, ap)
+            : dispatch<true>(a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
+                             dim3((unsigned)tiles, sp), s, ap);
+    if (rc == 0) {
+      dim3 g((unsigned)molclr::ceil_div(M * N, 256));
+      float* C = a.C;
+      const int64_t ldc = a.ldc, ldaux = a.ldaux;
+      const float *bias = a.bias, *aux = a.aux;
+      const int accumulate = a.accumulate;
+      switch (epilogue) {
+        case MOLCLR_EPI_NONE:
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s,
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+          break;
+        case MOLCLR_EPI_BIAS:
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s,
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+          break;
+        case MOLCLR_EPI_BIAS_RELU:
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0,
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+          break;
+        default:
+          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0,
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+      }
+    }
+  }
+  if (rc != 0) {
+    molclr::set_error("gemm_f32: no kernel for this layout");
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
 }  // namespace
 
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   // sized for the largest split count any implementation would pick
   int sp = pick_splits(0, M, N, K);
-  for (int impl = 1; impl <= 4; ++impl) {
+  for (int impl = 1; impl <= 6; ++impl) {
     const int s2 = pick_splits(impl, M, N, K);
     sp = s2 > sp ? s2 : sp;
   }
@@ -675,55 +1140,63 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     return MOLCLR_ERR_UNSUPPORTED;
   }
   const int impl = impl_for(M, N, lda, ldb, a_kmajor, b_kmajor);
-  int64_t tiles = tiles_for(impl, M, N);  // workgroups along x
-  MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
-  int sp = pick_splits(impl, M, N, K);
-  if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
   Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate, impl};
-  int rc;
-  if (sp == 1) {
-    rc = dispatch<false>(a_kmajor != 0, b_kmajor != 0, epilogue, dim3((unsigned)tiles), s, a);
-  } else {
-    int64_t nk = (K + BK - 1) / BK;
-    int kps = (int)((nk + sp - 1) / sp);
-    sp = (int)((nk + kps - 1) / kps);
-    float* partial = (float*)workspace;
-    Args ap{A, B, partial, M, N, K, lda, ldb, N, nullptr, nullptr, 0, kps, 0, impl};
-    rc = dispatch<true>(a_kmajor != 0, b_kmajor != 0, MOLCLR_EPI_NONE,
-                            dim3((unsigned)tiles, sp), s, ap);
-    if (rc == 0) {
-      dim3 g((unsigned)molclr::ceil_div(M * N, 256));
-      switch (epilogue) {
-        case MOLCLR_EPI_NONE:
-          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s, partial, sp, M,
-                             N, C, ldc, bias, aux, ldaux, accumulate);
-          break;
-        case MOLCLR_EPI_BIAS:
-          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s, partial, sp, M,
-                             N, C, ldc, bias, aux, ldaux, accumulate);
-          break;
-        case MOLCLR_EPI_BIAS_RELU:
-          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0, s, partial, sp,
-                             M, N, C, ldc, bias, aux, ldaux, accumulate);
-          break;
-        default:
-          molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0, s, partial, sp,
-                             M, N, C, ldc, bias, aux, ldaux, accumulate);
-      }
-    }
-  }
-  if (rc != 0) {
-    molclr::set_error("gemm_f32: no kernel for this layout");
-    return MOLCLR_ERR_UNSUPPORTED;
-  }
+  return run_gemm(a, impl, false, a_kmajor, b_kmajor, epilogue, workspace, workspace_bytes, s);
+}
+
+MOLCLR_API size_t molclr_bplanes_bytes(int64_t N, int64_t K) {
+  return (size_t)3 * planes_npad(N) * planes_kp(K) * sizeof(uint16_t);
+}
+
+MOLCLR_API int molclr_bplanes_make(const float* B, int64_t N, int64_t K, int64_t ldb, int b_kmajor,
+                                   uint16_t* planes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(N > 0 && K > 0 && B && planes, "bplanes_make: empty or null operand");
+  MOLCLR_REQUIRE(b_kmajor ? ldb >= N : ldb >= K, "bplanes_make: leading dimension too small");
+  const int64_t npad = planes_npad(N), kp = planes_kp(K);
+  hipLaunchKernelGGL(k_bplanes_make, dim3((unsigned)molclr::ceil_div(npad * kp, 256)), dim3(256), 0,
+                     molclr::as_stream(stream), B, N, K, ldb, b_kmajor, planes, npad, kp);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
+                                       int64_t N, int64_t K, int64_t lda, int64_t ldc,
+                                       int a_kmajor, int epilogue_flags, const float* bias,
+                                       const float* aux, int64_t ldaux, void* workspace,
+                                       size_t workspace_bytes, molclr_stream_t stream) {
+  const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
+  const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
+  MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_bplanes: negative size");
+  MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
+                 "gemm_f32_bplanes: bad epilogue %d", epilogue);
+  MOLCLR_REQUIRE((epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU) || bias,
+                 "gemm_f32_bplanes: bias epilogue needs bias");
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux,
+                 "gemm_f32_bplanes: relu-mask epilogue needs aux");
+  MOLCLR_REQUIRE(a_kmajor ? (M % 4 == 0 && lda % 4 == 0 && lda >= M)
+                          : (K % 4 == 0 && lda % 4 == 0 && lda >= K),
+                 "gemm_f32_bplanes: A needs 4-aligned rows (K-major) or K (K contiguous)");
+  MOLCLR_REQUIRE(ldc >= N, "gemm_f32_bplanes: ldc < N");
+  if (M == 0 || N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(K > 0 && A && planes && C, "gemm_f32_bplanes: null operand or K == 0");
+  const int64_t npad = planes_npad(N), kp = planes_kp(K);
+  Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, g_bplanes_impl};
+  a.Bp = planes;
+  a.bps = npad * kp;
+  return run_gemm(a, g_bplanes_impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
+                  molclr::as_stream(stream));
 }
 
 MOLCLR_API int molclr_gemm_get_impl(void) { return g_impl; }
 
 MOLCLR_API int molclr_gemm_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl >= 0 && impl <= 4, "gemm_set_impl: impl must be 0..4");
+  MOLCLR_REQUIRE(impl >= 0 && impl <= 6, "gemm_set_impl: impl must be 0..6");
   g_impl = impl;
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gemm_bplanes_set_impl(int impl) {
+  MOLCLR_REQUIRE(impl == 5 || impl == 6, "gemm_bplanes_set_impl: impl must be 5 or 6");
+  g_bplanes_impl = impl;
   return MOLCLR_OK;
 }

@@ -26,6 +26,7 @@ import torch
 
 import ctypes
 import functools
+import weakref
 
 from . import _lib
 from ._lib import EPI_ACCUMULATE, EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
@@ -139,12 +140,66 @@ def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, a
     return out
 
 
+# Pre-split weight planes (molclr_bplanes_make), cached per weight tensor and
+# invalidated when the tensor changes: torch's version counter covers in-place
+# torch ops (load_state_dict, torch.optim), PARAM_GENERATION covers FusedAdam,
+# whose kernel writes the parameters through raw pointers.
+USE_BPLANES = True
+PARAM_GENERATION = [0]
+_PLANES: dict = {}
+
+
+def bump_param_generation() -> None:
+    PARAM_GENERATION[0] += 1
+
+
+def weight_planes(W, N, K, ldb, b_kmajor) -> torch.Tensor:
+    """Split-bf16 planes of B(k, n) stored in W (molclr_gemm_f32's B layout)."""
+    key = (W.data_ptr(), N, K, ldb, int(b_kmajor))
+    tok = (W._version, PARAM_GENERATION[0])
+    ent = _PLANES.get(key)
+    if ent is not None and ent[0] == tok and ent[1]() is W:
+        return ent[2]
+    if len(_PLANES) > 512:  # drop entries of dead tensors
+        for k in [k for k, e in _PLANES.items() if e[1]() is None]:
+            del _PLANES[k]
+    nbytes = _wsq("molclr_bplanes_bytes", N, K)
+    planes = torch.empty(nbytes // 2, dtype=torch.int16, device=W.device)
+    _lib.call("molclr_bplanes_make", W.data_ptr(), N, K, ldb, int(b_kmajor), planes.data_ptr(),
+              _stream(W))
+    _PLANES[key] = (tok, weakref.ref(W), planes)
+    return planes
+
+
+def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
+           out=None, accumulate=0):
+    """gemm() whose B operand is a weight: through its cached pre-split planes
+    (molclr_gemm_f32_bplanes) when enabled."""
+    if not USE_BPLANES:
+        return gemm(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi, bias, aux, out, accumulate)
+    _check(A, W)
+    planes = weight_planes(W, N, K, ldb, b_kmajor)
+    dev = A.device
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=dev)
+    if accumulate:
+        epi |= EPI_ACCUMULATE
+    ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, N, K)
+    ws = _ws(ws_bytes, dev) if ws_bytes else None
+    _lib.call("molclr_gemm_f32_bplanes", A.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
+              lda, out.stride(0), int(a_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A))
+    if _TIMER is not None:
+        _TIMER.add("gemm_f32", 2.0 * M * N * K)
+    return out
+
+
 def linear_fwd(x, W, b, relu=False):
     """y = x W^T + b (nn.Linear), optional fused ReLU."""
     M, K = x.shape
     N = W.shape[0]
     epi = EPI_BIAS_RELU if relu else EPI_BIAS
-    return gemm(x, W, M, N, K, K, K, False, False, epi, bias=b)
+    return gemm_w(x, W, M, N, K, K, K, False, False, epi, bias=b)
 
 
 def colsum(x, out=None, accumulate=0):
@@ -175,7 +230,7 @@ def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=No
     if need_x:
         # dx[M,K] = dy W : B(k=n, j) = W[n, j] (K-major, ldb=K)
         epi = EPI_RELU_MASK if relu_mask_src is not None else EPI_NONE
-        dx = gemm(dy, W, M, K, N, N, K, False, True, epi, aux=relu_mask_src)
+        dx = gemm_w(dy, W, M, K, N, N, K, False, True, epi, aux=relu_mask_src)
     return dx, dW, db
 
 
@@ -424,7 +479,7 @@ class _GCNConv(torch.autograd.Function):
         N, Din = x.shape
         Dout = W.shape[1]
         # xW with W stored [in, out] (gcn_molclr.py:45,76): B K-major, ldb = Dout
-        xw = gemm(x, W, N, Dout, Din, Din, Dout, False, True)
+        xw = gemm_w(x, W, N, Dout, Din, Din, Dout, False, True)
         out = torch.empty(N, Dout, dtype=torch.float32, device=x.device)
         _lib.call("molclr_gcn_aggregate_fwd", xw.data_ptr(), graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), graph.ecode.data_ptr(), graph.nbr.data_ptr(),
@@ -466,7 +521,7 @@ class _GCNConv(torch.autograd.Function):
             gemm(x, dxw, Din, Dout, N, Din, Dout, True, True, out=buf, accumulate=a)
         if need[0]:
             # dx[N,Din] = dxw W^T : B(k=o, n=i) = W[i, o] (not K-major, ldb = Dout)
-            dx = gemm(dxw, W, N, Din, Dout, Dout, Dout, False, False)
+            dx = gemm_w(dxw, W, N, Din, Dout, Dout, Dout, False, False)
         return dx, dW, db, dE1, dE2, None
 
 

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, ops
 
 
 def _align4(n: int) -> int:
@@ -85,6 +85,7 @@ class FusedAdam(torch.optim.Optimizer):
                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,
                   self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(b1), float(b2),
                   float(g["eps"]), float(g["weight_decay"]), _lib.stream_of(self.flat.device))
+        ops.bump_param_generation()  # cached weight planes are stale now
         return loss
 
     @property

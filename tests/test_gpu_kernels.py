@@ -203,7 +203,8 @@ GEMM_SHAPES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["f32", "x6_64x64", "x6_128x64", "x6_128x128", "x9_64x64"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6],
+                ids=["f32", "x6_64x64", "x6_128x64", "x6_128x128", "x9_64x64", "p6_64x64", "p6_128x64"])
 def gemm_impl(request, dev):
     """Run a GEMM test under each implementation of molclr_gemm_f32."""
     from molclr_amd import _lib
@@ -269,19 +270,75 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
             # reference on the fp32-rounded inputs: only the GEMM's own error counts
             ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
             errs = {}
-            for impl in (0, 1, 2, 3, 4):
-                lib.molclr_gemm_set_impl(impl)
-                out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K, N if bk else K,
-                               ak, bk).double().cpu()
+            for impl in (0, 1, 2, 3, 4, 5, 6, "bplanes"):
+                if impl == "bplanes":
+                    planes = ops.weight_planes(Bt.to(dev), N, K, N if bk else K, bk)
+                    out = torch.empty(M, N, device=dev)
+                    ws_bytes = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
+                    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+                    Ad = A.to(dev)
+                    assert lib.molclr_gemm_f32_bplanes(
+                        Ad.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
+                        M if ak else K, N, ak, 0, None, None, 0, ws.data_ptr(), ws_bytes,
+                        None) == 0
+                    out = out.double().cpu()
+                else:
+                    lib.molclr_gemm_set_impl(impl)
+                    out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K,
+                                   N if bk else K, ak, bk).double().cpu()
                 errs[impl] = (rel(out, ref), (out - ref).abs().max().item(),
                               ((out - ref).abs() / ref.abs().clamp(min=1e-30)).max().item())
-            for impl in (1, 2, 3, 4):
+            for impl in (1, 2, 3, 4, 5, 6, "bplanes"):
                 assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
                 assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
                 if positive:
                     assert errs[impl][2] <= 2 * errs[0][2], errs
     finally:
         lib.molclr_gemm_set_impl(prev)
+
+
+@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("M,N,K", [(1000, 600, 300), (777, 300, 600), (64, 64, 8), (33, 68, 12),
+                                   (512, 256, 512), (300, 600, 2000)])
+@pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_bplanes(dev, tile, M, N, K, ak, bk):
+    """molclr_gemm_f32_bplanes (pre-split weight planes) against float64, all
+    epilogues, both B storage orders, both A layouts and both tiles."""
+    from molclr_amd import _lib
+    from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK
+    if ak and M % 4:
+        pytest.skip("K-major A needs M % 4 == 0")
+    lib = _lib.load()
+    lib.molclr_gemm_bplanes_set_impl(tile)
+    try:
+        torch.manual_seed(M * 7 + N + K)
+        Am = torch.randn(M, K, dtype=torch.float64)
+        Bm = torch.randn(K, N, dtype=torch.float64)
+        b = torch.randn(N, dtype=torch.float64)
+        aux = torch.randn(M, N)
+        A = (Am.t() if ak else Am).contiguous().float().to(dev)
+        W = (Bm if bk else Bm.t()).contiguous().float().to(dev)
+        y = (Am.float().double()) @ (Bm.float().double())
+        lda, ldb = (M if ak else K), (N if bk else K)
+        bd, auxd = b.float().to(dev), aux.to(dev)
+        got = ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk)
+        assert rel(got, y) < TOL
+        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS, bias=bd),
+                   y + b.float().double()) < TOL
+        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS_RELU, bias=bd),
+                   (y + b.float().double()).clamp(min=0)) < TOL
+        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_RELU_MASK, aux=auxd),
+                   y * (aux > 0).double()) < TOL
+        acc = torch.randn(M, N)
+        out = acc.to(dev)
+        ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, out=out, accumulate=1)
+        assert rel(out, y + acc.double()) < TOL
+        # the cached planes follow in-place changes of the weight
+        with torch.no_grad():
+            W.mul_(2.0)
+        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk), 2 * y) < TOL
+    finally:
+        lib.molclr_gemm_bplanes_set_impl(5)
 
 
 def test_colsum(dev):

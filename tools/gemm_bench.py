@@ -1,7 +1,7 @@
 """GEMM shapes of the c2 step: molclr_gemm_f32 vs torch.matmul (hipBLASLt /
 rocBLAS fp32) on the same operands.  Prints TFLOP/s per shape.
 
-    python tools/gemm_bench.py [N_rows]
+    python tools/gemm_bench.py [N_rows] [impl,impl,...]
 """
 import sys
 from pathlib import Path
@@ -39,43 +39,42 @@ def main():
     W2 = torch.randn(D, H, device=dev)
     b1 = torch.randn(H, device=dev)
     b2 = torch.randn(D, device=dev)
+    # (name, A, B, M, N, K, lda, ldb, ak, bk, epi, kwargs, B is a weight, torch reference)
     cases = [
-        ("lin1 fwd  x W1^T +b relu", 2 * Nr * H * D,
-         lambda: ops.gemm(x, W1, Nr, H, D, D, D, 0, 0, EPI_BIAS_RELU, bias=b1),
+        ("lin1 fwd  x W1^T +b relu", x, W1, Nr, H, D, D, D, 0, 0, EPI_BIAS_RELU, dict(bias=b1), True,
          lambda: torch.addmm(b1, x, W1.t()).relu_()),
-        ("lin2 fwd  a1 W2^T +b", 2 * Nr * H * D,
-         lambda: ops.gemm(a1, W2, Nr, D, H, H, H, 0, 0, EPI_BIAS, bias=b2),
+        ("lin2 fwd  a1 W2^T +b", a1, W2, Nr, D, H, H, H, 0, 0, EPI_BIAS, dict(bias=b2), True,
          lambda: torch.addmm(b2, a1, W2.t())),
-        ("dz1 = dz W2 * (a1>0)", 2 * Nr * H * D,
-         lambda: ops.gemm(dz, W2, Nr, H, D, D, H, 0, 1, EPI_RELU_MASK, aux=a1),
+        ("dz1 = dz W2 * (a1>0)", dz, W2, Nr, H, D, D, H, 0, 1, EPI_RELU_MASK, dict(aux=a1), True,
          lambda: (dz @ W2).mul_(a1 > 0)),
-        ("dagg = dz1 W1", 2 * Nr * H * D,
-         lambda: ops.gemm(dz1, W1, Nr, D, H, H, D, 0, 1),
-         lambda: dz1 @ W1),
-        ("dW2 = dz^T a1 (split-K)", 2 * Nr * H * D,
-         lambda: ops.gemm(dz, a1, D, H, Nr, D, H, 1, 1),
-         lambda: dz.t() @ a1),
-        ("dW1 = dz1^T x (split-K)", 2 * Nr * H * D,
-         lambda: ops.gemm(dz1, x, H, D, Nr, H, D, 1, 1),
-         lambda: dz1.t() @ x),
+        ("dagg = dz1 W1", dz1, W1, Nr, D, H, H, D, 0, 1, 0, {}, True, lambda: dz1 @ W1),
+        ("dW2 = dz^T a1 (split-K)", dz, a1, D, H, Nr, D, H, 1, 1, 0, {}, False, lambda: dz.t() @ a1),
+        ("dW1 = dz1^T x (split-K)", dz1, x, H, D, Nr, H, D, 1, 1, 0, {}, False, lambda: dz1.t() @ x),
     ]
     print(f"rows={Nr}  (fp32; torch.backends.cuda.matmul.allow_tf32="
           f"{torch.backends.cuda.matmul.allow_tf32})")
     from molclr_amd import _lib
     lib = _lib.load()
-    for name, flops, mine, ref in cases:
+    impls = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,1,5,6".split(","))]
+    for name, A, B, M, N, K, lda, ldb, ak, bk, epi, kw, weight, ref in cases:
+        flops = 2 * M * N * K
         res = []
-        for impl in (0, 1, 2, 3, 4):
+        for impl in impls:
             lib.molclr_gemm_set_impl(impl)
-            tm = timeit(mine)
-            res.append(f"impl{impl} {tm*1e6:6.1f}us {flops/tm/1e12:5.1f}TF")
-        lib.molclr_gemm_set_impl(0)
+            tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+            res.append(f"i{impl} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
+        if weight:
+            for t in (5, 6):
+                lib.molclr_gemm_bplanes_set_impl(t)
+                tm = timeit(lambda: ops.gemm_w(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+                res.append(f"bp{t} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
+        lib.molclr_gemm_set_impl(5)
         tr = timeit(ref)
-        print(f"{name:26s} " + " | ".join(res) + f" | torch {tr*1e6:6.1f}us {flops/tr/1e12:5.1f}TF",
+        print(f"{name:24s} " + " | ".join(res) + f" | torch {tr*1e6:5.1f}us {flops/tr/1e12:5.1f}TF",
               flush=True)
     # correctness of every impl on one shape per layout
     torch.manual_seed(1)
-    for impl in (1, 2, 3, 4):
+    for impl in (1, 2, 3, 4, 5, 6):
         lib.molclr_gemm_set_impl(impl)
         for (ak, bk) in ((0, 0), (0, 1), (1, 1), (1, 0)):
             M, N, K = 333, 300, 1000
@@ -88,7 +87,7 @@ def main():
             err = ((out.double().cpu() - ref).norm() / ref.norm()).item()
             print(f"impl{impl} ak={ak} bk={bk} rel err {err:.2e}", flush=True)
             assert err < 1e-5
-    lib.molclr_gemm_set_impl(0)
+    lib.molclr_gemm_set_impl(5)
 
 
 if __name__ == "__main__":

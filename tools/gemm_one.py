@@ -11,7 +11,9 @@ from molclr_amd._lib import EPI_BIAS_RELU  # noqa: E402
 
 
 def main():
-    impl = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    impl = sys.argv[1] if len(sys.argv) > 1 else "1"
+    bp = impl.startswith("bp")
+    impl = int(impl[2:] if bp else impl)
     case = sys.argv[2] if len(sys.argv) > 2 else "lin1"
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     dev = torch.device("cuda", 0)
@@ -21,10 +23,13 @@ def main():
     W1 = torch.randn(H, D, device=dev)
     b1 = torch.randn(H, device=dev)
     dz1 = torch.randn(Nr, H, device=dev)
-    _lib.load().molclr_gemm_set_impl(impl)
+    if bp:
+        _lib.load().molclr_gemm_bplanes_set_impl(impl)
+    else:
+        _lib.load().molclr_gemm_set_impl(impl)
     for _ in range(reps):
         if case == "lin1":
-            ops.gemm(x, W1, Nr, H, D, D, D, 0, 0, EPI_BIAS_RELU, bias=b1)
+            (ops.gemm_w if bp else ops.gemm)(x, W1, Nr, H, D, D, D, 0, 0, EPI_BIAS_RELU, bias=b1)
         else:  # dW1 = dz1^T x
             ops.gemm(dz1, x, H, D, Nr, H, D, 1, 1)
     torch.cuda.synchronize()
