@@ -314,6 +314,88 @@ int molclr_adam_step(float* param, const float* grad, float* exp_avg, float* exp
                      int64_t n, const float* lr, int32_t* step, double beta1, double beta2,
                      double eps, double weight_decay, molclr_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * GIN encoder executor (models/ginet_molclr.py:98-111 as ONE call).
+ * Runs the whole node-embedding stack of GINet on the stream — atom
+ * embedding, then per layer GINE aggregation -> Linear(D,2D)+ReLU ->
+ * Linear(2D,D) -> BatchNorm1d (+ReLU, not on the last layer) — by calling
+ * the entry points above in the order molclr_amd's per-op autograd path
+ * calls them (identical kernels, identical results), without a host round
+ * trip per operation.  The backward call replays the layers in reverse and
+ * ADDS every parameter gradient into the given buffers.
+ * Parameters are the reference's (state_dict names in the fields); the four
+ * *_planes are molclr_bplanes_make images of the MLP weights as GEMM B
+ * operands:
+ *   mlp0_planes   : B(k,n) = W0[n][k], N = 2D, K = D   (ldb = D,  b_kmajor 0)
+ *   mlp0_planes_t : B(k,n) = W0[k][n], N = D,  K = 2D  (ldb = D,  b_kmajor 1)
+ *   mlp2_planes   : B(k,n) = W2[n][k], N = D,  K = 2D  (ldb = 2D, b_kmajor 0)
+ *   mlp2_planes_t : B(k,n) = W2[k][n], N = 2D, K = D   (ldb = 2D, b_kmajor 1)
+ * BatchNorm: training = batch statistics + running-stat update (momentum,
+ * num_batches_tracked may be NULL); eval = running statistics (no backward).
+ * ------------------------------------------------------------------------ */
+typedef struct molclr_gin_encoder {
+  int32_t num_layer;  /* 1 .. MOLCLR_MAX_LAYERS */
+  int32_t training;
+  int64_t dim;        /* emb_dim, multiple of 4 */
+  int64_t n_atom;     /* x_embedding1 rows (119) */
+  int64_t n_chiral;   /* x_embedding2 rows (3) */
+  double momentum, eps;
+  const float* x_embedding1;
+  const float* x_embedding2;
+  const float* mlp0_weight[MOLCLR_MAX_LAYERS];
+  const float* mlp0_bias[MOLCLR_MAX_LAYERS];
+  const float* mlp2_weight[MOLCLR_MAX_LAYERS];
+  const float* mlp2_bias[MOLCLR_MAX_LAYERS];
+  const float* edge_embedding1[MOLCLR_MAX_LAYERS];
+  const float* edge_embedding2[MOLCLR_MAX_LAYERS];
+  const float* bn_weight[MOLCLR_MAX_LAYERS];
+  const float* bn_bias[MOLCLR_MAX_LAYERS];
+  float* bn_running_mean[MOLCLR_MAX_LAYERS];
+  float* bn_running_var[MOLCLR_MAX_LAYERS];
+  int64_t* bn_num_batches_tracked[MOLCLR_MAX_LAYERS];
+  const uint16_t* mlp0_planes[MOLCLR_MAX_LAYERS];
+  const uint16_t* mlp0_planes_t[MOLCLR_MAX_LAYERS];
+  const uint16_t* mlp2_planes[MOLCLR_MAX_LAYERS];
+  const uint16_t* mlp2_planes_t[MOLCLR_MAX_LAYERS];
+} molclr_gin_encoder;
+
+/* Gradient buffers, same shapes as the parameters; NULL = not needed. */
+typedef struct molclr_gin_encoder_grads {
+  float* x_embedding1;
+  float* x_embedding2;
+  float* mlp0_weight[MOLCLR_MAX_LAYERS];
+  float* mlp0_bias[MOLCLR_MAX_LAYERS];
+  float* mlp2_weight[MOLCLR_MAX_LAYERS];
+  float* mlp2_bias[MOLCLR_MAX_LAYERS];
+  float* edge_embedding1[MOLCLR_MAX_LAYERS];
+  float* edge_embedding2[MOLCLR_MAX_LAYERS];
+  float* bn_weight[MOLCLR_MAX_LAYERS];
+  float* bn_bias[MOLCLR_MAX_LAYERS];
+} molclr_gin_encoder_grads;
+
+/* The graph of one batch as molclr_graph_build produced it. */
+typedef struct molclr_device_graph {
+  int64_t num_nodes, num_edges, num_graphs;
+  const int32_t *rowptr, *col, *rowptr_t, *col_t, *ecount, *graph_ptr;
+  const uint8_t* ecode;
+  const uint32_t *nbr, *nbr_t;
+} molclr_device_graph;
+
+/* Saved activations of one forward (kept for the backward): arena of
+ * molclr_gin_encoder_arena_bytes; scratch: molclr_gin_encoder_workspace_bytes. */
+size_t molclr_gin_encoder_arena_bytes(int num_layer, int64_t num_nodes, int64_t dim);
+size_t molclr_gin_encoder_workspace_bytes(int num_layer, int64_t num_nodes, int64_t dim);
+/* x int64 [N,2] (atom type, chirality); h_out [N,D]: the last BatchNorm's output. */
+int molclr_gin_encoder_fwd(const molclr_gin_encoder* enc, const int64_t* x,
+                           const molclr_device_graph* graph, float* h_out, void* arena,
+                           size_t arena_bytes, void* workspace, size_t workspace_bytes,
+                           molclr_stream_t stream);
+/* dh_out [N,D]: gradient w.r.t. h_out; grads are accumulated (+=). */
+int molclr_gin_encoder_bwd(const molclr_gin_encoder* enc, const molclr_gin_encoder_grads* grads,
+                           const int64_t* x, const molclr_device_graph* graph,
+                           const float* dh_out, const void* arena, size_t arena_bytes,
+                           void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
 /* ---- Benchmark instrumentation (no reference counterpart) -------------------
  * Opt-in kernel timer.  While a kind is enabled, its launches go through
  * hipExtLaunchKernelGGL with a start/stop event pair recorded by the dispatch

@@ -74,6 +74,10 @@ SIGNATURES = {
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
+    "molclr_gin_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_gin_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_gin_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
+    "molclr_gin_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_ktimer_start": (c_int, [c_int]),
     "molclr_ktimer_read": (c_int, [c_int, _P, _P]),
     "molclr_ktimer_stop": (c_int, []),
@@ -85,6 +89,34 @@ NUM_ECOMB = 15  # combined edge-table rows (bond type * 3 + bond dir)
 MAX_LAYERS = 16
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
+
+
+_L16 = c_void_p * 16
+
+
+class GinEncoder(ctypes.Structure):
+    """struct molclr_gin_encoder (include/molclr.h)."""
+    _fields_ = [("num_layer", ctypes.c_int32), ("training", ctypes.c_int32), ("dim", c_int64),
+                ("n_atom", c_int64), ("n_chiral", c_int64), ("momentum", c_double),
+                ("eps", c_double), ("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
+        (f, _L16) for f in ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias",
+                            "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias",
+                            "bn_running_mean", "bn_running_var", "bn_num_batches_tracked",
+                            "mlp0_planes", "mlp0_planes_t", "mlp2_planes", "mlp2_planes_t")]
+
+
+class GinEncoderGrads(ctypes.Structure):
+    """struct molclr_gin_encoder_grads."""
+    _fields_ = [("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
+        (f, _L16) for f in ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias",
+                            "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias")]
+
+
+class DeviceGraphC(ctypes.Structure):
+    """struct molclr_device_graph."""
+    _fields_ = [("num_nodes", c_int64), ("num_edges", c_int64), ("num_graphs", c_int64)] + [
+        (f, c_void_p) for f in ("rowptr", "col", "rowptr_t", "col_t", "ecount", "graph_ptr",
+                                "ecode", "nbr", "nbr_t")]
 
 
 class MolclrError(RuntimeError):

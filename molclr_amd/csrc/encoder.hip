@@ -1,0 +1,206 @@
+// GIN encoder executor: GINet's node-embedding stack (models/ginet_molclr.py:98-111)
+// forward and backward as single calls over the library's own entry points.
+//
+// The per-op autograd path (molclr_amd/ops.py) pays ~30 us of Python per
+// operation — ~4 ms of host time per training step, against ~6 ms of GPU
+// time.  This file issues the same entry points, with the same arguments and
+// in the same order, from C++: the kernels and their results are identical,
+// only the host cost goes.
+//
+// Arena (saved for the backward), per layer l: agg_l [N,D], a1_l [N,2D],
+// z_l [N,D], h_l [N,D] (BatchNorm output, the next layer's input; the last
+// layer writes h_out instead), mean_l / invstd_l [D]; then h0 [N,D] (atom
+// embedding) and the combined edge tables Ec [L,15,D].
+// Workspace: backward scratch dh, dz, dagg [N,D] + dz1 [N,2D], then the
+// largest workspace any called entry point asks for.
+#include "common.h"
+
+namespace {
+
+struct ArenaLayout {
+  size_t agg[MOLCLR_MAX_LAYERS], a1[MOLCLR_MAX_LAYERS], z[MOLCLR_MAX_LAYERS],
+      h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS], invstd[MOLCLR_MAX_LAYERS];
+  size_t h0, ec, total;
+  ArenaLayout(int L, int64_t N, int64_t D) {
+    size_t used = 0;  // floats; every buffer 256-byte aligned
+    auto off = [&](size_t count) {
+      const size_t o = used;
+      used += (count + 63) / 64 * 64;
+      return o;
+    };
+    for (int l = 0; l < L; ++l) {
+      agg[l] = off(N * D);
+      a1[l] = off(N * 2 * D);
+      z[l] = off(N * D);
+      h[l] = off(N * D);
+      mean[l] = off(D);
+      invstd[l] = off(D);
+    }
+    h0 = off(N * D);
+    ec = off((size_t)L * MOLCLR_NUM_ECOMB * D);
+    total = used * sizeof(float);
+  }
+};
+
+size_t kernels_ws(int64_t N, int64_t D) {
+  size_t m = 0;
+  auto mx = [&](size_t v) { m = v > m ? v : m; };
+  mx(molclr_gemm_f32_workspace_bytes(2 * D, D, N));  // dW0 = dz1^T agg
+  mx(molclr_gemm_f32_workspace_bytes(D, 2 * D, N));  // dW2 = dz^T a1
+  mx(molclr_gemm_f32_workspace_bytes(N, 2 * D, D));
+  mx(molclr_gemm_f32_workspace_bytes(N, D, 2 * D));
+  mx(molclr_colsum_f32_workspace_bytes(N, 2 * D));
+  mx(molclr_batchnorm_workspace_bytes(N, D));
+  mx(molclr_gine_aggregate_bwd_workspace_bytes(N, D));
+  mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
+  return m;
+}
+
+size_t scratch_floats(int64_t N, int64_t D) { return (size_t)N * D * 3 + (size_t)N * 2 * D; }
+
+int check_encoder(const molclr_gin_encoder* e, const molclr_device_graph* g) {
+  MOLCLR_REQUIRE(e && g, "gin_encoder: null encoder / graph");
+  MOLCLR_REQUIRE(e->num_layer >= 1 && e->num_layer <= MOLCLR_MAX_LAYERS,
+                 "gin_encoder: num_layer %d", e->num_layer);
+  MOLCLR_REQUIRE(e->dim > 0 && e->dim % 4 == 0, "gin_encoder: dim %lld", (long long)e->dim);
+  MOLCLR_REQUIRE(e->n_atom == MOLCLR_NUM_ATOM_TYPE && e->n_chiral == MOLCLR_NUM_CHIRALITY,
+                 "gin_encoder: embedding tables must be [%d,D] and [%d,D]",
+                 MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY);
+  for (int l = 0; l < e->num_layer; ++l)
+    MOLCLR_REQUIRE(e->mlp0_planes[l] && e->mlp0_planes_t[l] && e->mlp2_planes[l] &&
+                       e->mlp2_planes_t[l] && e->bn_weight[l] && e->bn_bias[l],
+                   "gin_encoder: layer %d: missing planes or BatchNorm affine", l);
+  return MOLCLR_OK;
+}
+
+#define MOLCLR_TRY(expr)      \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_) return rc_;      \
+  } while (0)
+
+}  // namespace
+
+MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D) {
+  if (L < 1 || L > MOLCLR_MAX_LAYERS) return 0;
+  return ArenaLayout(L, N, D).total;
+}
+
+MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D) {
+  (void)L;
+  return scratch_floats(N, D) * sizeof(float) + 256 + kernels_ws(N, D) + 256;
+}
+
+MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t* x,
+                                      const molclr_device_graph* g, float* h_out, void* arena,
+                                      size_t arena_bytes, void* workspace, size_t workspace_bytes,
+                                      molclr_stream_t stream) {
+  MOLCLR_TRY(check_encoder(e, g));
+  const int L = e->num_layer;
+  const int64_t N = g->num_nodes, D = e->dim;
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && h_out && arena, "gin_encoder_fwd: null pointer");
+  const ArenaLayout lay(L, N, D);
+  MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D));
+  float* A = (float*)arena;
+  void* kws = (char*)workspace + molclr::align_up(scratch_floats(N, D) * sizeof(float), 256);
+  const size_t kws_bytes = kernels_ws(N, D);
+
+  float* h = A + lay.h0;
+  MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, h, N, D, e->n_atom,
+                                   e->n_chiral, stream));
+  float* Ec = A + lay.ec;
+  MOLCLR_TRY(molclr_edge_tables_combine(L, e->edge_embedding1, e->edge_embedding2, Ec, D, stream));
+  for (int l = 0; l < L; ++l) {
+    float* agg = A + lay.agg[l];
+    float* a1 = A + lay.a1[l];
+    float* z = A + lay.z[l];
+    const bool last = l == L - 1;
+    float* y = last ? h_out : A + lay.h[l];
+    MOLCLR_TRY(molclr_gine_aggregate_fwd(h, g->rowptr, g->col, g->ecode, g->nbr,
+                                         Ec + (size_t)l * MOLCLR_NUM_ECOMB * D, agg, N, D, stream));
+    // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
+                                       MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
+                                       kws_bytes, stream));
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
+                                       MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
+                                       kws_bytes, stream));
+    MOLCLR_TRY(molclr_batchnorm_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                    e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                    A + lay.mean[l], A + lay.invstd[l], N, D, e->momentum, e->eps,
+                                    e->training, last ? 0 : 1, kws, kws_bytes, stream));
+    h = y;
+  }
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
+                                      const molclr_gin_encoder_grads* gr, const int64_t* x,
+                                      const molclr_device_graph* g, const float* dh_out,
+                                      const void* arena, size_t arena_bytes, void* workspace,
+                                      size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_TRY(check_encoder(e, g));
+  MOLCLR_REQUIRE(gr, "gin_encoder_bwd: null grads");
+  MOLCLR_REQUIRE(e->training, "gin_encoder_bwd: backward through eval-mode BatchNorm");
+  const int L = e->num_layer;
+  const int64_t N = g->num_nodes, D = e->dim;
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && dh_out && arena, "gin_encoder_bwd: null pointer");
+  const ArenaLayout lay(L, N, D);
+  MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D));
+  const float* A = (const float*)arena;
+  float* S = (float*)workspace;
+  float* dh = S;                 // gradient w.r.t. the current layer's output
+  float* dz = S + N * D;         // w.r.t. the BatchNorm input z
+  float* dagg = S + 2 * N * D;   // w.r.t. the aggregation output
+  float* dz1 = S + 3 * N * D;    // w.r.t. the first Linear's pre-activation [N,2D]
+  void* kws = (char*)workspace + molclr::align_up(scratch_floats(N, D) * sizeof(float), 256);
+  const size_t kws_bytes = kernels_ws(N, D);
+  constexpr int ACC = MOLCLR_EPI_ACCUMULATE;
+
+  const float* dy = dh_out;
+  for (int l = L - 1; l >= 0; --l) {
+    const float* agg = A + lay.agg[l];
+    const float* a1 = A + lay.a1[l];
+    const float* z = A + lay.z[l];
+    const bool last = l == L - 1;
+    MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
+    MOLCLR_TRY(molclr_batchnorm_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
+                                    A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], N, D,
+                                    last ? 0 : 1, 1, kws, kws_bytes, stream));
+    // second Linear (ops.linear_bwd order: dW, db, dx with the ReLU mask of a1)
+    if (gr->mlp2_weight[l])
+      MOLCLR_TRY(molclr_gemm_f32(dz, a1, gr->mlp2_weight[l], D, 2 * D, N, D, 2 * D, 2 * D, 1, 1,
+                                 ACC, nullptr, nullptr, 0, kws, kws_bytes, stream));
+    if (gr->mlp2_bias[l])
+      MOLCLR_TRY(molclr_colsum_f32(dz, gr->mlp2_bias[l], N, D, D, 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(dz, e->mlp2_planes_t[l], dz1, N, 2 * D, D, D, 2 * D, 0,
+                                       MOLCLR_EPI_RELU_MASK, nullptr, a1, 2 * D, kws, kws_bytes,
+                                       stream));
+    // first Linear
+    if (gr->mlp0_weight[l])
+      MOLCLR_TRY(molclr_gemm_f32(dz1, agg, gr->mlp0_weight[l], 2 * D, D, N, 2 * D, D, D, 1, 1,
+                                 ACC, nullptr, nullptr, 0, kws, kws_bytes, stream));
+    if (gr->mlp0_bias[l])
+      MOLCLR_TRY(molclr_colsum_f32(dz1, gr->mlp0_bias[l], N, 2 * D, 2 * D, 1, kws, kws_bytes,
+                                   stream));
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(dz1, e->mlp0_planes_t[l], dagg, N, D, 2 * D, 2 * D, D, 0,
+                                       MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
+                                       stream));
+    // aggregation: dh of the layer input, edge-table gradients
+    MOLCLR_TRY(molclr_gine_aggregate_bwd(dagg, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dh,
+                                         gr->edge_embedding1[l], gr->edge_embedding2[l], N, D, 1,
+                                         kws, kws_bytes, stream));
+    dy = dh;
+  }
+  if (gr->x_embedding1 || gr->x_embedding2) {
+    MOLCLR_REQUIRE(gr->x_embedding1 && gr->x_embedding2,
+                   "gin_encoder_bwd: both atom-embedding grads or neither");
+    MOLCLR_TRY(molclr_atom_embed_bwd(x, dh, gr->x_embedding1, gr->x_embedding2, N, D, e->n_atom,
+                                     e->n_chiral, 1, kws, kws_bytes, stream));
+  }
+  return MOLCLR_OK;
+}

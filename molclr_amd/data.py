@@ -148,6 +148,17 @@ class DeviceGraph:
                   ws.data_ptr(), ws_bytes, _lib.stream_of(dev))
         self.device = dev
 
+    def cstruct(self):
+        """struct molclr_device_graph of this graph (for the encoder executor)."""
+        c = getattr(self, "_cstruct", None)
+        if c is None:
+            c = _lib.DeviceGraphC(self.num_nodes, self.num_edges, self.num_graphs, *[
+                t.data_ptr() for t in (self.rowptr, self.col, self.rowptr_t, self.col_t,
+                                       self.ecount, self.graph_ptr, self.ecode, self.nbr,
+                                       self.nbr_t)])
+            self._cstruct = c
+        return c
+
     def check(self) -> None:
         """Synchronising validity check of the input indices (tests / debug)."""
         st = int(self.status.item())

@@ -625,6 +625,105 @@ class _NTXent(torch.autograd.Function):
         return dR[Bl:], dR[:Bl], None, None, None, None
 
 
+GIN_PARAMS_PER_LAYER = 8  # mlp0.W, mlp0.b, mlp2.W, mlp2.b, edge_emb1, edge_emb2, bn.W, bn.b
+
+
+class _GINEncoder(torch.autograd.Function):
+    """The whole GINet node-embedding stack (ginet_molclr.py:98-111) through
+    molclr_gin_encoder_fwd / _bwd (encoder.hip): the same kernels as the
+    per-op path in the same order, one host call each way.
+    params: x_embedding1, x_embedding2, then per layer GIN_PARAMS_PER_LAYER."""
+
+    @staticmethod
+    def forward(ctx, x_idx, graph: DeviceGraph, bns, *params):
+        _check(x_idx, *params)
+        L = len(bns)
+        D = params[0].shape[1]
+        x_idx = _c(x_idx.to(torch.long))
+        N = graph.num_nodes
+        training = bool(bns[0].training)
+        enc = _lib.GinEncoder()
+        enc.num_layer, enc.training, enc.dim = L, int(training), D
+        enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
+        enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
+        enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
+        for l in range(L):
+            W0, b0, W2, b2, E1, E2, g, b = params[2 + GIN_PARAMS_PER_LAYER * l:
+                                                  2 + GIN_PARAMS_PER_LAYER * (l + 1)]
+            bn = bns[l]
+            enc.mlp0_weight[l], enc.mlp0_bias[l] = W0.data_ptr(), b0.data_ptr()
+            enc.mlp2_weight[l], enc.mlp2_bias[l] = W2.data_ptr(), b2.data_ptr()
+            enc.edge_embedding1[l], enc.edge_embedding2[l] = E1.data_ptr(), E2.data_ptr()
+            enc.bn_weight[l], enc.bn_bias[l] = g.data_ptr(), b.data_ptr()
+            enc.bn_running_mean[l] = bn.running_mean.data_ptr()
+            enc.bn_running_var[l] = bn.running_var.data_ptr()
+            nbt = bn.num_batches_tracked
+            enc.bn_num_batches_tracked[l] = nbt.data_ptr() if training and nbt is not None else None
+            twoD = W0.shape[0]
+            # the same planes (and cache entries) ops.linear_fwd / linear_bwd use
+            enc.mlp0_planes[l] = weight_planes(W0, twoD, D, D, 0).data_ptr()
+            enc.mlp0_planes_t[l] = weight_planes(W0, D, twoD, D, 1).data_ptr()
+            enc.mlp2_planes[l] = weight_planes(W2, D, twoD, twoD, 0).data_ptr()
+            enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1).data_ptr()
+        dev = x_idx.device
+        arena_bytes = _wsq("molclr_gin_encoder_arena_bytes", L, N, D)
+        arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)
+        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D)
+        ws = _ws(ws_bytes, dev)
+        h = torch.empty(N, D, dtype=torch.float32, device=dev)
+        gc = graph.cstruct()
+        _lib.call("molclr_gin_encoder_fwd", ctypes.addressof(enc), x_idx.data_ptr(),
+                  ctypes.addressof(gc), h.data_ptr(), arena.data_ptr(), arena_bytes,
+                  ws.data_ptr(), ws_bytes, _stream(x_idx))
+        if _TIMER is not None:
+            for _ in range(L):
+                _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges))
+                _TIMER.add("gemm_f32", 2 * 2.0 * N * D * (2 * D))
+        ctx.enc, ctx.graph, ctx.arena, ctx.arena_bytes = enc, graph, arena, arena_bytes
+        ctx.x_idx, ctx.params, ctx.training = x_idx, params, training
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        if not ctx.training:
+            raise NotImplementedError("molclr_amd: backward through eval-mode BatchNorm")
+        dh = _c(dh)
+        params = ctx.params
+        L = ctx.enc.num_layer
+        N, D = dh.shape
+        owned = all(getattr(p, "_molclr_fused_grad", False) and p.grad is not None
+                    for p in params)
+        if owned:  # FusedAdam: add straight into the flat gradient buffer
+            bufs = [p.grad for p in params]
+            ret = [None] * len(params)
+        else:
+            bufs = [torch.zeros_like(p) for p in params]
+            ret = bufs
+        gr = _lib.GinEncoderGrads()
+        gr.x_embedding1, gr.x_embedding2 = bufs[0].data_ptr(), bufs[1].data_ptr()
+        names = ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias", "edge_embedding1",
+                 "edge_embedding2", "bn_weight", "bn_bias")
+        for l in range(L):
+            for j, nm in enumerate(names):
+                getattr(gr, nm)[l] = bufs[2 + GIN_PARAMS_PER_LAYER * l + j].data_ptr()
+        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D)
+        ws = _ws(ws_bytes, dh.device)
+        gc = ctx.graph.cstruct()
+        _lib.call("molclr_gin_encoder_bwd", ctypes.addressof(ctx.enc), ctypes.addressof(gr),
+                  ctx.x_idx.data_ptr(), ctypes.addressof(gc), dh.data_ptr(), ctx.arena.data_ptr(),
+                  ctx.arena_bytes, ws.data_ptr(), ws_bytes, _stream(dh))
+        if _TIMER is not None:
+            for _ in range(L):
+                _TIMER.add("gemm_f32", 4 * 2.0 * N * D * (2 * D))
+        ctx.arena = None
+        return (None, None, None, *ret)
+
+
+def gin_encoder(x_idx, graph, bns, params):
+    """GINet.encode through the encoder executor (see _GINEncoder)."""
+    return _GINEncoder.apply(x_idx, graph, bns, *params)
+
+
 # public functional API -------------------------------------------------------
 def atom_embed(x_idx, X1, X2):
     return _AtomEmbed.apply(x_idx, X1, X2)

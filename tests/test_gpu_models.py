@@ -226,3 +226,36 @@ def test_trainer_runs_one_epoch(dev, tmp_path, monkeypatch):
     m = MolCLR(ds, config).train()
     assert all(torch.isfinite(p).all() for p in m.parameters())
     assert list(tmp_path.glob("ckpt/*/checkpoints/model.pth"))
+
+
+@pytest.mark.parametrize("L,D,B", [(5, 300, 64), (2, 16, 4), (3, 128, 33)])
+def test_encoder_executor_matches_per_op_path(dev, L, D, B):
+    """molclr_gin_encoder_fwd/_bwd (one host call each) runs the per-op path's
+    kernels in the same order: node embeddings, every parameter gradient and
+    the BatchNorm running statistics are bit-identical; eval mode too."""
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(1)
+    a = GINet(L, D, 256).to(dev)
+    b = copy.deepcopy(a)
+    b.use_executor = False
+    assert a._executor_ok() and not b._executor_ok()
+    xi, _ = SyntheticPairBatches(B, seed=L + D).next()
+    xi = xi.to(dev)
+    g = torch.randn(xi.x.shape[0], D, device=dev)
+    outs = []
+    for m in (a, b):
+        h, _ = m.encode(xi)
+        (h * g).sum().backward()
+        outs.append(h.detach())
+    assert torch.equal(outs[0], outs[1])
+    pa, pb = dict(a.named_parameters()), dict(b.named_parameters())
+    for n in pa:  # the heads are not part of encode(): no grad on either side
+        assert (pa[n].grad is None) == (pb[n].grad is None), n
+        assert pa[n].grad is None or torch.equal(pa[n].grad, pb[n].grad), n
+    assert sum(p.grad is not None for p in pa.values()) == 2 + 8 * L
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(ba, bb), n
+    a.eval()
+    b.eval()
+    with torch.no_grad():
+        assert torch.equal(a.encode(xi)[0], b.encode(xi)[0])
