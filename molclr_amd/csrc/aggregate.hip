@@ -88,22 +88,36 @@ __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
 // out[r][c] = Σ_p partial[p][r][c], rows [0,n1) -> dX1, [n1,n1+n2) -> dX2.
 // The small embedding-table gradients are sums of ~10^4-10^6 nearly cancelling
 // terms (ill-conditioned): they are accumulated in fp64 and rounded once.
-// A block owns 64 consecutive elements; 16 lanes fold strided partials, then a
-// fixed-order merge (deterministic).
+// A block owns 16 consecutive elements; 64 lanes fold strided partials (four
+// loads in flight), then a fixed-order tree through LDS (deterministic).
 __global__ __launch_bounds__(1024) void k_reduce_partials_split(
     const double* __restrict__ partial, int64_t P, int64_t rows, int64_t D, int64_t split,
     float* __restrict__ outA, float* __restrict__ outB, int accumulate) {
-  __shared__ double red[16][64];
-  const int cl = threadIdx.x % 64, rl = threadIdx.x / 64;
-  const int64_t t = (int64_t)blockIdx.x * 64 + cl;
+  constexpr int EL = 16, LANES = 64;
+  __shared__ double red[LANES][EL];
+  const int cl = threadIdx.x % EL, rl = threadIdx.x / EL;
+  const int64_t t = (int64_t)blockIdx.x * EL + cl;
   const int64_t n = rows * D;
-  double acc = 0.0;
-  if (t < n)
-    for (int64_t p = rl; p < P; p += 16) acc += partial[p * n + t];
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (t < n) {
+    int64_t p = rl;
+    for (; p + 3 * LANES < P; p += 4 * LANES) {
+      a0 += partial[p * n + t];
+      a1 += partial[(p + LANES) * n + t];
+      a2 += partial[(p + 2 * LANES) * n + t];
+      a3 += partial[(p + 3 * LANES) * n + t];
+    }
+    for (; p < P; p += LANES) a0 += partial[p * n + t];
+  }
+  double acc = (a0 + a1) + (a2 + a3);
   red[rl][cl] = acc;
   __syncthreads();
+#pragma unroll
+  for (int stride = LANES / 2; stride > 0; stride >>= 1) {
+    if (rl < stride) red[rl][cl] = acc = acc + red[rl + stride][cl];
+    __syncthreads();
+  }
   if (rl != 0 || t >= n) return;
-  for (int q = 1; q < 16; ++q) acc += red[q][cl];
   int64_t r = t / D;
   float* o = r < split ? (outA ? outA + t : nullptr) : (outB ? outB + (t - split * D) : nullptr);
   if (o) *o = accumulate ? *o + (float)acc : (float)acc;
@@ -175,7 +189,10 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
   out[t] = acc;
 }
 
-// dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC)
+// dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC).
+// Unlike the forward, the self row is read last and the gathers stay in
+// branches: measured 14.0 us against 17.3 us for the forward's structure here
+// (tools/agg_bench.py transpose).
 __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restrict__ g,
                                                          const int32_t* __restrict__ rowptr_t,
                                                          const int32_t* __restrict__ col_t,
@@ -187,24 +204,18 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restric
   int64_t j = t / d4;
   int c = (int)(t - j * d4);
   const uint4 s = nbr_t[j];
-  const float4 self = g[t];
   const uint32_t deg = nbr_degree(s.x);
   float4 acc = f4zero();
   if (deg <= MOLCLR_NBR_SLOTS) {
-    const float4 m0 = deg > 0 ? g[(int64_t)nbr_node(s.x) * d4 + c] : acc;
-    const float4 m1 = deg > 1 ? g[(int64_t)nbr_node(s.y) * d4 + c] : acc;
-    const float4 m2 = deg > 2 ? g[(int64_t)nbr_node(s.z) * d4 + c] : acc;
-    const float4 m3 = deg > 3 ? g[(int64_t)nbr_node(s.w) * d4 + c] : acc;
-    if (deg > 0) acc = f4add(acc, m0);
-    if (deg > 1) acc = f4add(acc, m1);
-    if (deg > 2) acc = f4add(acc, m2);
-    if (deg > 3) acc = f4add(acc, m3);
+    if (deg > 0) acc = f4add(acc, g[(int64_t)nbr_node(s.x) * d4 + c]);
+    if (deg > 1) acc = f4add(acc, g[(int64_t)nbr_node(s.y) * d4 + c]);
+    if (deg > 2) acc = f4add(acc, g[(int64_t)nbr_node(s.z) * d4 + c]);
+    if (deg > 3) acc = f4add(acc, g[(int64_t)nbr_node(s.w) * d4 + c]);
   } else {
     for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k)
       acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
   }
-  acc = f4add(acc, self);
-  dx[t] = acc;
+  dx[t] = f4add(acc, g[t]);
 }
 
 // Edge-table gradient partials: partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c].
@@ -402,7 +413,7 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
   size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
   hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
                      x, dh, N, D, n1, n2, rpp, partial);
-  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 64)), dim3(1024),
+  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 16)), dim3(1024),
                      0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
@@ -475,7 +486,7 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
     MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd: dim too large for the edge-table reduction");
     hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P), dim3(b.threads), lds, s,
                        (const float4*)g, ecount, N, d4, b.band, rpp, partial);
-    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 64)), dim3(1024), 0, s,
+    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 16)), dim3(1024), 0, s,
                        partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2, accumulate);
   }
   MOLCLR_LAUNCHED();

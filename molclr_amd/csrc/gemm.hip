@@ -815,10 +815,9 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
       sb1.load(kof(i + 3), K, tb);
     }
     compute(buf1);
-    if (i + 2 < nsteps) {
-      sa0.store(buf0, ta);
-      sb0.store(buf0 + AI, tb);
-    }
+    // unconditional: when i + 2 >= nsteps the image is never read again
+    sa0.store(buf0, ta);
+    sb0.store(buf0 + AI, tb);
     __syncthreads();
   }
   if (i < nsteps) compute(buf0);
@@ -877,6 +876,7 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   if (t >= M * N) return;
   int64_t m = t / N, n = t - m * N;
   float v = 0.f;
+#pragma unroll 4
   for (int z = 0; z < splits; ++z) v += partial[(int64_t)z * M * N + t];
   if (EPI == MOLCLR_EPI_BIAS) v = v + bias[n];
   if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bias[n], 0.f);

@@ -52,10 +52,40 @@ __global__ void k_colsum_partial(const float4* __restrict__ X, int64_t rows, int
   }
 }
 
-// Final column reductions: a block owns 64 columns; its 16 row-lanes each
-// fold a strided subset of the P partials, then the 16 results are combined
-// in a fixed order through LDS (deterministic, no serial P-long chain).
-constexpr int kRedCols = 64, kRedLanes = 16;
+// Final column reductions over P partial rows: a block owns kRedCols columns
+// with kRedLanes lanes each; a lane folds the partials p = lane (mod
+// kRedLanes), four loads in flight per step, then the lanes are combined by
+// a fixed-order tree through LDS (deterministic, no long serial chain: the
+// previous 16-lane form spent 8-19 us waiting on one dependent load at a time).
+constexpr int kRedCols = 16, kRedLanes = 64;
+
+// sum-tree over the lanes of red[kRedLanes][kRedCols]; lane 0 ends with the total
+template <typename T>
+__device__ __forceinline__ T lane_tree_sum(T (*red)[kRedCols], int rl, int cl, T v) {
+  red[rl][cl] = v;
+  __syncthreads();
+#pragma unroll
+  for (int stride = kRedLanes / 2; stride > 0; stride >>= 1) {
+    if (rl < stride) red[rl][cl] = v = v + red[rl + stride][cl];
+    __syncthreads();
+  }
+  return v;
+}
+
+// Σ_p partial[p][c] for the block's columns, per lane (strided, 4 loads in flight)
+__device__ __forceinline__ float lane_fold(const float* __restrict__ partial, int64_t P,
+                                           int64_t cols, int64_t c, int rl) {
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t p = rl;
+  for (; p + 3 * kRedLanes < P; p += 4 * kRedLanes) {
+    a0 += partial[p * cols + c];
+    a1 += partial[(p + kRedLanes) * cols + c];
+    a2 += partial[(p + 2 * kRedLanes) * cols + c];
+    a3 += partial[(p + 3 * kRedLanes) * cols + c];
+  }
+  for (; p < P; p += kRedLanes) a0 += partial[p * cols + c];
+  return (a0 + a1) + (a2 + a3);
+}
 
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_colsum_final(
     const float* __restrict__ partial, int64_t P, int64_t cols, float* __restrict__ out,
@@ -63,16 +93,9 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_colsum_final(
   __shared__ float red[kRedLanes][kRedCols];
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
-  float acc = 0.f;
-  if (c < cols)
-    for (int64_t p = rl; p < P; p += kRedLanes) acc += partial[p * cols + c];
-  red[rl][cl] = acc;
-  __syncthreads();
-  if (rl == 0 && c < cols) {
-    float s = red[0][cl];
-    for (int q = 1; q < kRedLanes; ++q) s += red[q][cl];
-    out[c] = accumulate ? out[c] + s : s;
-  }
+  const float acc = c < cols ? lane_fold(partial, P, cols, c, rl) : 0.f;
+  const float s = lane_tree_sum(red, rl, cl, acc);
+  if (rl == 0 && c < cols) out[c] = accumulate ? out[c] + s : s;
 }
 
 // ---------------------------------------------------------------------------
@@ -166,9 +189,10 @@ __device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb
   n = nn;
 }
 
-// Per column: Chan-merge the P partials (16 strided lanes, then a fixed-order
-// merge of the lanes), update running stats, write save_mean/save_invstd and
-// the apply coefficients.  grid = ceil(D/64), block = 1024.
+// Per column: Chan-merge the P partials (kRedLanes strided lanes, four
+// partials in flight, then a fixed-order tree over the lanes), update running
+// stats, write save_mean/save_invstd and the apply coefficients.
+// grid = ceil(D/kRedCols), block = kRedCols * kRedLanes.
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
     const float* __restrict__ pmean, const float* __restrict__ pm2, const float* __restrict__ pn,
     int64_t P, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -180,14 +204,37 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < D)
-    for (int64_t p = rl; p < P; p += kRedLanes) chan1(n, mean, m2, pn[p], pmean[p * D + c], pm2[p * D + c]);
+  if (c < D) {
+    int64_t p = rl;
+    for (; p + 3 * kRedLanes < P; p += 4 * kRedLanes) {
+      float bn[4], bm[4], bq[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t q = p + u * kRedLanes;
+        bn[u] = pn[q];
+        bm[u] = pmean[q * D + c];
+        bq[u] = pm2[q * D + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) chan1(n, mean, m2, bn[u], bm[u], bq[u]);
+    }
+    for (; p < P; p += kRedLanes) chan1(n, mean, m2, pn[p], pmean[p * D + c], pm2[p * D + c]);
+  }
   rn[rl][cl] = n;
   rm[rl][cl] = mean;
   rq[rl][cl] = m2;
   __syncthreads();
+#pragma unroll
+  for (int stride = kRedLanes / 2; stride > 0; stride >>= 1) {
+    if (rl < stride) {
+      chan1(n, mean, m2, rn[rl + stride][cl], rm[rl + stride][cl], rq[rl + stride][cl]);
+      rn[rl][cl] = n;
+      rm[rl][cl] = mean;
+      rq[rl][cl] = m2;
+    }
+    __syncthreads();
+  }
   if (rl != 0 || c >= D) return;
-  for (int q = 1; q < kRedLanes; ++q) chan1(n, mean, m2, rn[q][cl], rm[q][cl], rq[q][cl]);
   float var = m2 / n;
   float invstd = 1.0f / sqrtf(var + eps);
   save_mean[c] = mean;
@@ -314,19 +361,13 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
   float a = 0.f, b = 0.f;
-  if (c < D)
-    for (int64_t p = rl; p < P; p += kRedLanes) {
-      a += p1[p * D + c];
-      b += p2[p * D + c];
-    }
-  ra[rl][cl] = a;
-  rb[rl][cl] = b;
-  __syncthreads();
-  if (rl != 0 || c >= D) return;
-  for (int q = 1; q < kRedLanes; ++q) {
-    a += ra[q][cl];
-    b += rb[q][cl];
+  if (c < D) {
+    a = lane_fold(p1, P, D, c, rl);
+    b = lane_fold(p2, P, D, c, rl);
   }
+  a = lane_tree_sum(ra, rl, cl, a);
+  b = lane_tree_sum(rb, rl, cl, b);
+  if (rl != 0 || c >= D) return;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + a : a;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + b : b;
   k1[c] = a * inv_rows;

@@ -22,7 +22,8 @@ from molclr_amd.dataset import SyntheticPairBatches  # noqa: E402
 NAMES = {0: "v0 library (CSR)", 1: "ELL int4, remap", 2: "ELL int4, no remap",
          3: "ELL int4, nt store", 4: "ELL int4, 2/thread", 5: "copy floor (no gather)",
          6: "ELL + combined table, nt", 7: "LDS tile R32 cap56", 8: "LDS tile R16 cap40",
-         9: "LDS tile R64 cap96", 10: "LDS tile2 R32 cap48 512thr", 11: "LDS tile2 R16 cap32 512thr"}
+         9: "LDS tile R64 cap96", 10: "LDS tile2 R32 cap48 512thr", 11: "LDS tile2 R16 cap32 512thr",
+         12: "ELL + comb table, self last"}
 
 
 def main():
@@ -91,7 +92,7 @@ def main():
           lib.aggvar_run(0, 256, nb, 1, *args())
           torch.cuda.synchronize()
           ref = [o.clone() for o in outs]
-      for v in (0, 6, 10, 11, 5):
+      for v in (0, 6, 12, 5):
         lib.aggvar_set_graphs(tile_arrs[16 if v == 11 else 32], Gs)
         for block in ((256,) if v == 0 else (256,)):
           for o in outs:
@@ -104,5 +105,36 @@ def main():
                 f"bit-exact={same}", flush=True)
 
 
+def transpose_main():
+    dev = torch.device("cuda", 0)
+    lib = ctypes.CDLL(str(ROOT / "tools" / "libaggvar.so"))
+    lib.aggvar_transpose.restype = ctypes.c_double
+    D, nb = 300, 16
+    views = [v for a, b in SyntheticPairBatches(512, seed=0).take(nb // 2) for v in (a, b)]
+    gs = [device_graph(v.to(dev)) for v in views]
+    xs = [torch.randn(g.num_nodes, D, device=dev) for g in gs]
+    outs = [torch.empty_like(x) for x in xs]
+    src = torch.randn(max(g.num_nodes for g in gs), D, device=dev)
+    P = lambda ts: (ctypes.c_void_p * nb)(*[t.data_ptr() for t in ts])  # noqa: E731
+    Ns = (ctypes.c_int64 * nb)(*[g.num_nodes for g in gs])
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    arrs = [P(xs), P([g.rowptr_t for g in gs]), P([g.col_t for g in gs]), P([g.nbr_t for g in gs])]
+    outp = P(outs)
+    ref = None
+    for warm in (0, 1):
+        for v in (0, 1, 3, 4):
+            us = lib.aggvar_transpose(v, nb, 20, *arrs, Ns, outp, D // 4,
+                                      ctypes.c_void_p(src.data_ptr() if warm else 0), stream)
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = [o.clone() for o in outs]
+            same = all(torch.equal(a, b) for a, b in zip(outs, ref))
+            print(f"transpose {['csr', 'slot remap', 'slot', 'slot selflast', 'slot pairs'][v]:10s} warm={warm}: {us:6.2f} us same={same}",
+                  flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "transpose":
+        transpose_main()
+        sys.exit(0)
     main()

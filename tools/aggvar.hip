@@ -151,6 +151,34 @@ __global__ void v_ellc(const float4* __restrict__ x, const int32_t* __restrict__
   __builtin_nontemporal_store(a, reinterpret_cast<v4f*>(out) + t);
 }
 
+// v_ellc with the self row loaded last and a plain store
+__global__ void v_ellc2(const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+                        const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+                        const uint32_t* __restrict__ ell, const float4* __restrict__ Ec,
+                        const float4* __restrict__ E2, float4* __restrict__ out, int64_t N, int d4) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t i = t / d4;
+  int c = (int)(t - i * d4);
+  const uint4 s = reinterpret_cast<const uint4*>(ell)[i];
+  const uint32_t deg = s.x >> 29;
+  float4 acc = make_float4(0, 0, 0, 0);
+#define MSGC(p) f4add(x[(int64_t)((p) & 0xFFFFFF) * d4 + c], Ec[((((p) >> 24) & 7) * 3 + (((p) >> 27) & 3)) * d4 + c])
+  if (deg <= 4) {
+    if (deg > 0) acc = f4add(acc, MSGC(s.x));
+    if (deg > 1) acc = f4add(acc, MSGC(s.y));
+    if (deg > 2) acc = f4add(acc, MSGC(s.z));
+    if (deg > 3) acc = f4add(acc, MSGC(s.w));
+  } else {
+    for (int32_t k = rowptr[i], e = rowptr[i + 1]; k < e; ++k) {
+      const uint32_t p = (uint32_t)col[k] | ((uint32_t)ecode[k] << 24);
+      acc = f4add(acc, MSGC(p));
+    }
+  }
+#undef MSGC
+  out[t] = f4add(acc, f4add(x[t], Ec[12 * d4 + c]));
+}
+
 __global__ void k_make_ec(const float* E1, const float* E2, float* Ec, int D) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 15 * D) return;
@@ -331,10 +359,142 @@ __global__ void k_make_ell(const int32_t* __restrict__ rowptr, const int32_t* __
   reinterpret_cast<uint4*>(ell)[i] = make_uint4(s[0], s[1], s[2], s[3]);
 }
 
+// transpose gather, CSR (pre-slot library version) and slot versions
+__global__ __launch_bounds__(256) void t_csr(const float4* __restrict__ g, const int32_t* __restrict__ rowptr_t,
+                                             const int32_t* __restrict__ col_t, const uint4* __restrict__,
+                                             float4* __restrict__ dx, int64_t N, int d4) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t j = t / d4;
+  int c = (int)(t - j * d4);
+  int32_t k = rowptr_t[j];
+  const int32_t end = rowptr_t[j + 1];
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (; k + 2 <= end; k += 2) {
+    int32_t i0 = col_t[k], i1 = col_t[k + 1];
+    float4 g0 = g[(int64_t)i0 * d4 + c];
+    float4 g1 = g[(int64_t)i1 * d4 + c];
+    acc = f4add(acc, g0);
+    acc = f4add(acc, g1);
+  }
+  if (k < end) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+  acc = f4add(acc, g[t]);
+  dx[t] = acc;
+}
+template <bool REMAP>
+__global__ __launch_bounds__(256) void t_slot(const float4* __restrict__ g, const int32_t* __restrict__ rowptr_t,
+                                              const int32_t* __restrict__ col_t, const uint4* __restrict__ nbr_t,
+                                              float4* __restrict__ dx, int64_t N, int d4) {
+  int64_t t = (int64_t)(REMAP ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t j = t / d4;
+  int c = (int)(t - j * d4);
+  const uint4 s = nbr_t[j];
+  const float4 self = g[t];
+  const uint32_t deg = s.x >> 29;
+  float4 acc = make_float4(0, 0, 0, 0);
+  if (deg <= 4) {
+    const float4 m0 = deg > 0 ? g[(int64_t)(s.x & 0xFFFFFF) * d4 + c] : acc;
+    const float4 m1 = deg > 1 ? g[(int64_t)(s.y & 0xFFFFFF) * d4 + c] : acc;
+    const float4 m2 = deg > 2 ? g[(int64_t)(s.z & 0xFFFFFF) * d4 + c] : acc;
+    const float4 m3 = deg > 3 ? g[(int64_t)(s.w & 0xFFFFFF) * d4 + c] : acc;
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) acc = f4add(acc, m2);
+    if (deg > 3) acc = f4add(acc, m3);
+  } else {
+    for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+  }
+  dx[t] = f4add(acc, self);
+}
+__global__ void k_rewrite_t(const float4* __restrict__ src, float4* __restrict__ dst, int64_t n) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) dst[t] = src[t];
+}
+// slot variants: (3) self loaded last, (4) pairs like the CSR loop
+__global__ __launch_bounds__(256) void t_slot3(const float4* __restrict__ g, const int32_t* __restrict__ rowptr_t,
+                                               const int32_t* __restrict__ col_t, const uint4* __restrict__ nbr_t,
+                                               float4* __restrict__ dx, int64_t N, int d4) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t j = t / d4;
+  int c = (int)(t - j * d4);
+  const uint4 s = nbr_t[j];
+  const uint32_t deg = s.x >> 29;
+  float4 acc = make_float4(0, 0, 0, 0);
+  if (deg <= 4) {
+    if (deg > 0) acc = f4add(acc, g[(int64_t)(s.x & 0xFFFFFF) * d4 + c]);
+    if (deg > 1) acc = f4add(acc, g[(int64_t)(s.y & 0xFFFFFF) * d4 + c]);
+    if (deg > 2) acc = f4add(acc, g[(int64_t)(s.z & 0xFFFFFF) * d4 + c]);
+    if (deg > 3) acc = f4add(acc, g[(int64_t)(s.w & 0xFFFFFF) * d4 + c]);
+  } else {
+    for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+  }
+  dx[t] = f4add(acc, g[t]);
+}
+__global__ __launch_bounds__(256) void t_slot4(const float4* __restrict__ g, const int32_t* __restrict__ rowptr_t,
+                                               const int32_t* __restrict__ col_t, const uint4* __restrict__ nbr_t,
+                                               float4* __restrict__ dx, int64_t N, int d4) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t j = t / d4;
+  int c = (int)(t - j * d4);
+  const uint4 s = nbr_t[j];
+  const uint32_t deg = s.x >> 29;
+  float4 acc = make_float4(0, 0, 0, 0);
+  if (deg <= 4) {
+    // unconditional loads of valid rows (empty slots hold node 0, bits masked): no exec masking
+    const float4 m0 = g[(int64_t)(s.x & 0xFFFFFF) * d4 + c];
+    const float4 m1 = g[(int64_t)(s.y & 0xFFFFFF) * d4 + c];
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) {
+      const float4 m2 = g[(int64_t)(s.z & 0xFFFFFF) * d4 + c];
+      const float4 m3 = g[(int64_t)(s.w & 0xFFFFFF) * d4 + c];
+      acc = f4add(acc, m2);
+      if (deg > 3) acc = f4add(acc, m3);
+    }
+  } else {
+    for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k) acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+  }
+  dx[t] = f4add(acc, g[t]);
+}
+typedef void (*tgfn)(const float4*, const int32_t*, const int32_t*, const uint4*, float4*, int64_t, int);
+
 typedef void (*kfn)(const float4*, const int32_t*, const int32_t*, const uint8_t*, const uint32_t*,
                     const float4*, const float4*, float4*, int64_t, int);
 
 }  // namespace
+
+extern "C" double aggvar_transpose(int variant, int nb, int reps, const float** gs, const int32_t** rowptrs,
+                                   const int32_t** cols, const uint32_t** nbrs, const int64_t* Ns, float** outs,
+                                   int d4, const float* warm_src, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  tgfn f = variant == 0 ? t_csr : variant == 1 ? t_slot<true> : variant == 2 ? t_slot<false>
+          : variant == 3 ? t_slot3 : t_slot4;
+  std::vector<hipEvent_t> ev(2 * nb * reps);
+  for (auto& e : ev) (void)hipEventCreate(&e);
+  int n = 0;
+  for (int r = 0; r < reps; ++r)
+    for (int g = 0; g < nb; ++g) {
+      int64_t total = Ns[g] * d4;
+      if (warm_src)
+        hipLaunchKernelGGL(k_rewrite_t, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                           (const float4*)warm_src, (float4*)gs[g], total);
+      hipExtLaunchKernelGGL(f, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, ev[2 * n], ev[2 * n + 1], 0u,
+                            (const float4*)gs[g], rowptrs[g], cols[g], (const uint4*)nbrs[g], (float4*)outs[g], Ns[g], d4);
+      ++n;
+    }
+  (void)hipStreamSynchronize(s);
+  double tot = 0;
+  for (int k = 0; k < n; ++k) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+    tot += ms;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return tot / n * 1e3;
+}
 
 extern "C" int aggvar_make_ell(const int32_t* rowptr, const int32_t* col, const uint8_t* ecode,
                                uint32_t* ell, int64_t N, void* stream) {
@@ -376,11 +536,12 @@ extern "C" double aggvar_run(int variant, int block, int nb, int reps, const flo
     case 4: f = v_ell2; per_thread = 2; break;
     case 5: f = v_copy; break;
     case 6: f = v_ellc; break;
+    case 12: f = v_ellc2; break;
     case 7: case 8: case 9: case 10: case 11: break;
     default: return -1;
   }
   float* Ec = nullptr;
-  if (variant >= 6) {
+  if (variant >= 6 && variant != 7 && variant != 8 && variant != 9 && variant != 10 && variant != 11) {
     (void)hipMalloc(&Ec, 15 * d4 * 16);
     hipLaunchKernelGGL(k_make_ec, dim3((15 * d4 * 4 + 255) / 256), dim3(256), 0, s, E1, E2, Ec, d4 * 4);
     E1 = Ec;
@@ -396,7 +557,7 @@ extern "C" double aggvar_run(int variant, int block, int nb, int reps, const flo
       if (g_warm_src)
         hipLaunchKernelGGL(k_rewrite, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
                            (const float4*)g_warm_src, (float4*)xs[g], total, g_warm_remap);
-      if (variant >= 10) {
+      if (variant == 10 || variant == 11) {
         tfn tf = variant == 10 ? v_tile2<32, 48, 8> : v_tile2<16, 32, 5>;
         int R = variant == 10 ? 32 : 16;
         int cap = variant == 10 ? 48 : 32;
@@ -404,7 +565,7 @@ extern "C" double aggvar_run(int variant, int block, int nb, int reps, const flo
         hipExtLaunchKernelGGL(tf, tg, dim3(512), (uint32_t)((cap + 15) * d4 * 16), s, ev[2 * n], ev[2 * n + 1], 0u,
                               (const float4*)xs[g], rowptrs[g], cols[g], ecodes[g], ells[g],
                               (const float4*)E1, g_gptrs[g], g_Gs[g], (float4*)outs[g], Ns[g], d4);
-      } else if (variant >= 7) {
+      } else if (variant >= 7 && variant <= 9) {
         tfn tf = variant == 7 ? v_tile<32, 56> : variant == 8 ? v_tile<16, 40> : v_tile<64, 96>;
         int R = variant == 7 ? 32 : variant == 8 ? 16 : 64;
         int cap = variant == 7 ? 56 : variant == 8 ? 40 : 96;
