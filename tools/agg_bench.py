@@ -23,7 +23,7 @@ NAMES = {0: "v0 library (CSR)", 1: "ELL int4, remap", 2: "ELL int4, no remap",
          3: "ELL int4, nt store", 4: "ELL int4, 2/thread", 5: "copy floor (no gather)",
          6: "ELL + combined table, nt", 7: "LDS tile R32 cap56", 8: "LDS tile R16 cap40",
          9: "LDS tile R64 cap96", 10: "LDS tile2 R32 cap48 512thr", 11: "LDS tile2 R16 cap32 512thr",
-         12: "ELL + comb table, self last"}
+         12: "ELL + comb table, self last", 13: "ELL8 + comb table"}
 
 
 def main():
@@ -38,7 +38,7 @@ def main():
     torch.manual_seed(0)
     E1 = torch.randn(5, D, device=dev)
     E2 = torch.randn(3, D, device=dev)
-    gs, xs, outs, ells = [], [], [], []
+    gs, xs, outs, ells, ells8 = [], [], [], [], []
     stream = torch.cuda.current_stream().cuda_stream
     for v in views:
         v = v.to(dev)
@@ -52,14 +52,19 @@ def main():
                             ctypes.c_void_p(g.ecode.data_ptr()), ctypes.c_void_p(e.data_ptr()),
                             ctypes.c_int64(N), ctypes.c_void_p(stream))
         ells.append(e)
+        e8 = torch.empty(N * 8, dtype=torch.int32, device=dev)
+        lib.aggvar_make_ell8(ctypes.c_void_p(g.rowptr.data_ptr()), ctypes.c_void_p(g.col.data_ptr()),
+                             ctypes.c_void_p(g.ecode.data_ptr()), ctypes.c_void_p(e8.data_ptr()),
+                             ctypes.c_int64(N), ctypes.c_void_p(stream))
+        ells8.append(e8)
     deg = torch.cat([g.rowptr[1:] - g.rowptr[:-1] for g in gs])
     print(f"views {nb}, mean N {sum(g.num_nodes for g in gs)/nb:.0f}, in-degree max {int(deg.max())}, "
           f"frac deg>4 {(deg > 4).float().mean().item():.2e}")
 
     P = lambda ts: (ctypes.c_void_p * nb)(*[t.data_ptr() for t in ts])  # noqa: E731
     Ns = (ctypes.c_int64 * nb)(*[g.num_nodes for g in gs])
-    args = lambda: (P(xs), P([g.rowptr for g in gs]), P([g.col for g in gs]),  # noqa: E731
-                    P([g.ecode for g in gs]), P(ells), Ns, ctypes.c_void_p(E1.data_ptr()),
+    args = lambda v=0: (P(xs), P([g.rowptr for g in gs]), P([g.col for g in gs]),  # noqa: E731
+                    P([g.ecode for g in gs]), P(ells8 if v == 13 else ells), Ns, ctypes.c_void_p(E1.data_ptr()),
                     ctypes.c_void_p(E2.data_ptr()), P(outs), ctypes.c_int(d4),
                     ctypes.c_void_p(stream))
     def tile_ptr(g, R):
@@ -92,15 +97,15 @@ def main():
           lib.aggvar_run(0, 256, nb, 1, *args())
           torch.cuda.synchronize()
           ref = [o.clone() for o in outs]
-      for v in (0, 6, 12, 5):
+      for v in (0, 6, 13, 5):
         lib.aggvar_set_graphs(tile_arrs[16 if v == 11 else 32], Gs)
         for block in ((256,) if v == 0 else (256,)):
           for o in outs:
               o.zero_()
-          lib.aggvar_run(v, block, nb, 2, *args())  # warm + check
+          lib.aggvar_run(v, block, nb, 2, *args(v))  # warm + check
           torch.cuda.synchronize()
           same = all(torch.equal(a, b) for a, b in zip(outs, ref))
-          us = lib.aggvar_run(v, block, nb, 20, *args())
+          us = lib.aggvar_run(v, block, nb, 20, *args(v))
           print(f"{NAMES[v]:28s} block {block:4d}: {us:7.2f} us  {nbytes / us / 1e3:7.1f} GB/s  "
                 f"bit-exact={same}", flush=True)
 

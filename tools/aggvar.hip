@@ -179,6 +179,60 @@ __global__ void v_ellc2(const float4* __restrict__ x, const int32_t* __restrict_
   out[t] = f4add(acc, f4add(x[t], Ec[12 * d4 + c]));
 }
 
+// 8 neighbour slots (two uint4 per row; degree in bits 29..31 of word 0 of the
+// first uint4 as 0..7, with 7 meaning >= 7 -> CSR walk)
+__global__ void v_ellc8(const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+                        const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+                        const uint32_t* __restrict__ ell, const float4* __restrict__ Ec,
+                        const float4* __restrict__ E2, float4* __restrict__ out, int64_t N, int d4) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d4) return;
+  int64_t i = t / d4;
+  int c = (int)(t - i * d4);
+  const uint4 s = reinterpret_cast<const uint4*>(ell)[2 * i];
+  const uint4 s2 = reinterpret_cast<const uint4*>(ell)[2 * i + 1];
+  const float4 self = x[t];
+  const float4 es = Ec[12 * d4 + c];
+  const uint32_t deg = s.x >> 29;
+  float4 acc = make_float4(0, 0, 0, 0);
+#define MSGC(p) f4add(x[(int64_t)((p) & 0xFFFFFF) * d4 + c], Ec[((((p) >> 24) & 7) * 3 + (((p) >> 27) & 3)) * d4 + c])
+  if (deg < 7) {
+    float4 m0 = deg > 0 ? MSGC(s.x) : acc;
+    float4 m1 = deg > 1 ? MSGC(s.y) : acc;
+    float4 m2 = deg > 2 ? MSGC(s.z) : acc;
+    float4 m3 = deg > 3 ? MSGC(s.w) : acc;
+    if (deg > 0) acc = f4add(acc, m0);
+    if (deg > 1) acc = f4add(acc, m1);
+    if (deg > 2) acc = f4add(acc, m2);
+    if (deg > 3) acc = f4add(acc, m3);
+    if (deg > 4) {
+      float4 m4 = MSGC(s2.x);
+      float4 m5 = deg > 5 ? MSGC(s2.y) : acc;
+      acc = f4add(acc, m4);
+      if (deg > 5) acc = f4add(acc, m5);
+    }
+  } else {
+    for (int32_t k = rowptr[i], e = rowptr[i + 1]; k < e; ++k) {
+      const uint32_t p = (uint32_t)col[k] | ((uint32_t)ecode[k] << 24);
+      acc = f4add(acc, MSGC(p));
+    }
+  }
+#undef MSGC
+  out[t] = f4add(acc, f4add(self, es));
+}
+
+__global__ void k_make_ell8(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                            const uint8_t* __restrict__ ecode, uint32_t* __restrict__ ell, int64_t N) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  const int32_t b = rowptr[i], e = rowptr[i + 1], deg = e - b;
+  uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < 8 && k < deg; ++k) s[k] = (uint32_t)col[b + k] | ((uint32_t)ecode[b + k] << 24);
+  s[0] = (s[0] & 0x1FFFFFFF) | ((uint32_t)(deg >= 7 ? 7 : deg) << 29);
+  reinterpret_cast<uint4*>(ell)[2 * i] = make_uint4(s[0], s[1], s[2], s[3]);
+  reinterpret_cast<uint4*>(ell)[2 * i + 1] = make_uint4(s[4], s[5], s[6], s[7]);
+}
+
 __global__ void k_make_ec(const float* E1, const float* E2, float* Ec, int D) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 15 * D) return;
@@ -496,6 +550,13 @@ extern "C" double aggvar_transpose(int variant, int nb, int reps, const float** 
   return tot / n * 1e3;
 }
 
+extern "C" int aggvar_make_ell8(const int32_t* rowptr, const int32_t* col, const uint8_t* ecode,
+                                uint32_t* ell, int64_t N, void* stream) {
+  hipLaunchKernelGGL(k_make_ell8, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rowptr, col, ecode,
+                     ell, N);
+  return (int)hipGetLastError();
+}
+
 extern "C" int aggvar_make_ell(const int32_t* rowptr, const int32_t* col, const uint8_t* ecode,
                                uint32_t* ell, int64_t N, void* stream) {
   hipLaunchKernelGGL(k_make_ell, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, rowptr, col, ecode,
@@ -537,6 +598,7 @@ extern "C" double aggvar_run(int variant, int block, int nb, int reps, const flo
     case 5: f = v_copy; break;
     case 6: f = v_ellc; break;
     case 12: f = v_ellc2; break;
+    case 13: f = v_ellc8; break;
     case 7: case 8: case 9: case 10: case 11: break;
     default: return -1;
   }
