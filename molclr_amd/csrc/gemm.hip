@@ -597,24 +597,35 @@ struct PStageK {
   }
 };
 
-// fp32, K-major: unit = 4 rows x 4 k (rb fastest: a wave reads 64 consecutive
-// rows of one k); (ROWS/4)*8 units.  Needs rows % 4 == 0 and ld % 4 == 0.
+// fp32, K-major ([K][rows]: the dY^T / X^T of a weight gradient): the image
+// is kept K-major too, [k][ROWS] bf16 per plane, and the MFMA fragments are
+// read with the gfx950 transposed LDS read (ds_read_b64_tr_b16, kmfrag).  A
+// thread stages single float4s (4 consecutive rows at one k): split, one
+// 8-byte write per plane, no register transpose.  16 lanes write 128
+// contiguous bytes of one k-row (conflict-free); the transposed reads are
+// conflict-free through the 32-element XOR of kswz.  (The previous form,
+// 4 x 4 blocks transposed in registers into the [row][k] image, spent 60 % of
+// its LDS cycles in bank conflicts: rows 4 apart share banks.)
+// Needs ROWS == 64, rows % 4 == 0 and ld % 4 == 0.
+__device__ __forceinline__ int kswz(int k) { return ((k >> 1) & 1) << 5; }
+
 template <int ROWS, int T>
 struct PStageM {
-  static constexpr int UNITS = (ROWS / 4) * (BK / 4);
+  static_assert(ROWS == 64, "K-major staging is laid out for 64-row tiles");
+  static constexpr int UNITS = BK * (ROWS / 4);
   static constexpr int PER = (UNITS + T - 1) / T;
   const float* p[PER];
   int64_t ld;
-  float4 r[PER][4];
+  float4 r[PER];
   __device__ __forceinline__ void init(const float* __restrict__ src, int64_t ld_, int64_t row0,
                                        int64_t rows, int t) {
     ld = ld_;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
-      const int rb = u % (ROWS / 4), kb = u / (ROWS / 4);
+      const int rb = u % (ROWS / 4), k = u / (ROWS / 4);
       const int64_t gr = row0 + 4 * rb;
-      p[j] = src + (int64_t)(4 * kb) * ld + (gr < rows ? gr : rows - 4);
+      p[j] = src + (int64_t)k * ld + (gr < rows ? gr : rows - 4);
     }
   }
   __device__ __forceinline__ void load(int64_t k0, int64_t K, int t) {
@@ -624,16 +635,12 @@ struct PStageM {
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
       if (UNITS % T && u >= UNITS) continue;
-      const int kb = u / (ROWS / 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float* q = p[j] + base + i * ld;
-        if (full) {
-          r[j][i] = *reinterpret_cast<const float4*>(q);
-        } else {
-          r[j][i] = k0 + 4 * kb + i < K ? *reinterpret_cast<const float4*>(q)
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+      const float* q = p[j] + base;
+      if (full) {
+        r[j] = *reinterpret_cast<const float4*>(q);
+      } else {
+        r[j] = k0 + u / (ROWS / 4) < K ? *reinterpret_cast<const float4*>(q)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
   }
@@ -642,24 +649,37 @@ struct PStageM {
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
       if (UNITS % T && u >= UNITS) continue;
-      const int rb = u % (ROWS / 4), kb = u / (ROWS / 4);
-      const float4* v = r[j];
-      const float4 row[4] = {make_float4(v[0].x, v[1].x, v[2].x, v[3].x),
-                             make_float4(v[0].y, v[1].y, v[2].y, v[3].y),
-                             make_float4(v[0].z, v[1].z, v[2].z, v[3].z),
-                             make_float4(v[0].w, v[1].w, v[2].w, v[3].w)};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint2 hi, mid, lo;
-        split4(row[i], hi, mid, lo);
-        const int o = xoff(4 * rb + i, kb >> 1) + 4 * (kb & 1);
-        *reinterpret_cast<uint2*>(img + o) = hi;
-        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
-        *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
-      }
+      const int rb = u % (ROWS / 4), k = u / (ROWS / 4);
+      uint2 hi, mid, lo;
+      split4(r[j], hi, mid, lo);
+      const int o = k * ROWS + ((4 * rb) ^ kswz(k));
+      *reinterpret_cast<uint2*>(img + o) = hi;
+      *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
+      *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
     }
   }
 };
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// MFMA 32x32x16 operand fragment of rows row0 .. row0+31 (lane: row row0 + li,
+// k = 16 ks + 8 lh .. +7) from a [k][64] K-major image plane: two transposed
+// reads, each giving 4 consecutive k of one row.  Lane 4q+p of a 16-lane group
+// addresses k-row q, rows 4p .. 4p+3 of the group's 16 (ISA ds_read_b64_tr_b16).
+__device__ __forceinline__ bf16x8 kmfrag(const uint16_t* __restrict__ plane, int row0, int ks,
+                                         int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int m = row0 + (g & 1) * 16 + 4 * pp;
+  const int k = 16 * ks + 8 * (g >> 1) + q;
+  const uint16_t* a0 = plane + k * 64 + (m ^ kswz(k));
+  const uint16_t* a1 = plane + (k + 4) * 64 + (m ^ kswz(k + 4));
+  const v4i16 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+  const v4i16 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 // pre-split planes [3][Npad][Kp] bf16: unit = (plane, row, 16-byte chunk)
 template <int ROWS, int T>
@@ -755,25 +775,34 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
   uint16_t* buf0 = lds;
   uint16_t* buf1 = lds + (AI + BI);
 
+  // fragment of rows r0 .. r0+31 of an image plane: [row][k] images are read
+  // by row (xfrag), K-major [k][row] images by the transposed read (kmfrag)
+  auto afrag = [&](const uint16_t* plane, int r0, int ks) {
+    if constexpr (AMODE == 1) return kmfrag(plane, r0, ks, lane);
+    else return xfrag(plane, r0 + li, ks * 2 + lh);
+  };
+  auto bfrag = [&](const uint16_t* plane, int r0, int ks) {
+    if constexpr (BMODE == 1) return kmfrag(plane, r0, ks, lane);
+    else return xfrag(plane, r0 + li, ks * 2 + lh);
+  };
   auto compute = [&](const uint16_t* As) {
     const uint16_t* Bs = As + AI;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 2 + lh;
       bf16x8 bh[TN], bm[TN], bl[TN];
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        const int bro = wn * TN * 32 + b * 32 + li;
-        bh[b] = xfrag(Bs, bro, ch);
-        bm[b] = xfrag(Bs + BN * XK, bro, ch);
-        bl[b] = xfrag(Bs + 2 * BN * XK, bro, ch);
+        const int bro = wn * TN * 32 + b * 32;
+        bh[b] = bfrag(Bs, bro, ks);
+        bm[b] = bfrag(Bs + BN * XK, bro, ks);
+        bl[b] = bfrag(Bs + 2 * BN * XK, bro, ks);
       }
 #pragma unroll
       for (int a = 0; a < TM; ++a) {
-        const int aro = wm * TM * 32 + a * 32 + li;
-        const bf16x8 ah = xfrag(As, aro, ch);
-        const bf16x8 am = xfrag(As + BM * XK, aro, ch);
-        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, ch);
+        const int aro = wm * TM * 32 + a * 32;
+        const bf16x8 ah = afrag(As, aro, ks);
+        const bf16x8 am = afrag(As + BM * XK, aro, ks);
+        const bf16x8 al = afrag(As + 2 * BM * XK, aro, ks);
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
           acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[b], acl[a][b], 0, 0, 0);
@@ -896,6 +925,7 @@ int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   if (g_impl == 0) return 0;
   if (ak && (M % 4 || lda % 4)) return 0;
   if (bk && (N % 4 || ldb % 4)) return 0;
+  if (g_impl == 6 && ak) return 5;  // the K-major image is laid out for 64-row tiles
   return g_impl;
 }
 int tiles_for(int impl, int64_t M, int64_t N) {
@@ -939,7 +969,7 @@ void launch_t(dim3 grid, hipStream_t s, const Args& a) {
     return;
   }
   if (a.impl == 6) {
-    launch_p6<2, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
+    launch_p6<(AK ? 1 : 2), AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
     return;
   }
   if (a.impl == 1) {
@@ -1006,10 +1036,10 @@ int dispatch(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
 
 template <int TM, bool SPLIT>
 int dispatch_bplanes_t(int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
-#define MOLCLR_BP_CASE(AKV, EPV)                                             \
-  if (ak == AKV && (SPLIT || epi == EPV)) {                                  \
-    launch_p6<TM, AKV, 2, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(grid, s, a); \
-    return 0;                                                                \
+#define MOLCLR_BP_CASE(AKV, EPV)                                                      \
+  if (ak == AKV && (SPLIT || epi == EPV)) {                                           \
+    launch_p6<(AKV ? 1 : TM), AKV, 2, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(grid, s, a); \
+    return 0;                                                                         \
   }
   if (SPLIT) {
     MOLCLR_BP_CASE(0, MOLCLR_EPI_NONE)
@@ -1180,10 +1210,11 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   if (M == 0 || N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(K > 0 && A && planes && C, "gemm_f32_bplanes: null operand or K == 0");
   const int64_t npad = planes_npad(N), kp = planes_kp(K);
-  Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, g_bplanes_impl};
+  const int impl = (g_bplanes_impl == 6 && a_kmajor) ? 5 : g_bplanes_impl;
+  Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, impl};
   a.Bp = planes;
   a.bps = npad * kp;
-  return run_gemm(a, g_bplanes_impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
+  return run_gemm(a, impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
                   molclr::as_stream(stream));
 }
 
