@@ -607,11 +607,17 @@ struct PStageK {
 // 4 x 4 blocks transposed in registers into the [row][k] image, spent 60 % of
 // its LDS cycles in bank conflicts: rows 4 apart share banks.)
 // Needs ROWS == 64, rows % 4 == 0 and ld % 4 == 0.
-__device__ __forceinline__ int kswz(int k) { return ((k >> 1) & 1) << 5; }
+// 32-element XOR of k-row k: separates the 4 k-rows one transposed read
+// touches (64-row rows are 32 dwords: rows k and k+2 share banks; 128-row
+// rows are 64 dwords: all four do).
+template <int ROWS>
+__device__ __forceinline__ int kswz(int k) {
+  return ROWS == 64 ? ((k >> 1) & 1) << 5 : (k & 3) << 5;
+}
 
 template <int ROWS, int T>
 struct PStageM {
-  static_assert(ROWS == 64, "K-major staging is laid out for 64-row tiles");
+  static_assert(ROWS == 64 || ROWS == 128, "K-major staging is laid out for 64/128-row tiles");
   static constexpr int UNITS = BK * (ROWS / 4);
   static constexpr int PER = (UNITS + T - 1) / T;
   const float* p[PER];
@@ -652,7 +658,7 @@ struct PStageM {
       const int rb = u % (ROWS / 4), k = u / (ROWS / 4);
       uint2 hi, mid, lo;
       split4(r[j], hi, mid, lo);
-      const int o = k * ROWS + ((4 * rb) ^ kswz(k));
+      const int o = k * ROWS + ((4 * rb) ^ kswz<ROWS>(k));
       *reinterpret_cast<uint2*>(img + o) = hi;
       *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
       *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
@@ -664,16 +670,17 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 // MFMA 32x32x16 operand fragment of rows row0 .. row0+31 (lane: row row0 + li,
-// k = 16 ks + 8 lh .. +7) from a [k][64] K-major image plane: two transposed
+// k = 16 ks + 8 lh .. +7) from a [k][ROWS] K-major image plane: two transposed
 // reads, each giving 4 consecutive k of one row.  Lane 4q+p of a 16-lane group
 // addresses k-row q, rows 4p .. 4p+3 of the group's 16 (ISA ds_read_b64_tr_b16).
+template <int ROWS>
 __device__ __forceinline__ bf16x8 kmfrag(const uint16_t* __restrict__ plane, int row0, int ks,
                                          int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
   const int m = row0 + (g & 1) * 16 + 4 * pp;
   const int k = 16 * ks + 8 * (g >> 1) + q;
-  const uint16_t* a0 = plane + k * 64 + (m ^ kswz(k));
-  const uint16_t* a1 = plane + (k + 4) * 64 + (m ^ kswz(k + 4));
+  const uint16_t* a0 = plane + k * ROWS + (m ^ kswz<ROWS>(k));
+  const uint16_t* a1 = plane + (k + 4) * ROWS + (m ^ kswz<ROWS>(k + 4));
   const v4i16 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
   const v4i16 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
   typedef short v8i16 __attribute__((ext_vector_type(8)));
@@ -778,11 +785,11 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
   // fragment of rows r0 .. r0+31 of an image plane: [row][k] images are read
   // by row (xfrag), K-major [k][row] images by the transposed read (kmfrag)
   auto afrag = [&](const uint16_t* plane, int r0, int ks) {
-    if constexpr (AMODE == 1) return kmfrag(plane, r0, ks, lane);
+    if constexpr (AMODE == 1) return kmfrag<BM>(plane, r0, ks, lane);
     else return xfrag(plane, r0 + li, ks * 2 + lh);
   };
   auto bfrag = [&](const uint16_t* plane, int r0, int ks) {
-    if constexpr (BMODE == 1) return kmfrag(plane, r0, ks, lane);
+    if constexpr (BMODE == 1) return kmfrag<BN>(plane, r0, ks, lane);
     else return xfrag(plane, r0 + li, ks * 2 + lh);
   };
   auto compute = [&](const uint16_t* As) {
@@ -928,13 +935,21 @@ int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   if (g_impl == 6 && ak) return 5;  // the K-major image is laid out for 64-row tiles
   return g_impl;
 }
-int tiles_for(int impl, int64_t M, int64_t N) {
-  const int64_t bm = (impl == 2 || impl == 3 || impl == 6) ? 128 : 64, bn = impl == 3 ? 128 : 64;
+// p6 tiles of a weight-gradient product (both operands K-major): 128 along the
+// longer of M / N (8.9 -> ~6 VALU per MFMA: half the B or A split work)
+bool p6_wide(int impl, int ak, int bk) { return impl == 5 && ak && bk; }
+int tiles_for(int impl, int64_t M, int64_t N, int ak = 0, int bk = 0) {
+  int64_t bm = (impl == 2 || impl == 3 || impl == 6) ? 128 : 64,
+          bn = (impl == 3 || impl == 7) ? 128 : 64;
+  if (p6_wide(impl, ak, bk)) {
+    bm = M >= N ? 128 : 64;
+    bn = M >= N ? 64 : 128;
+  }
   return (int)(((M + bm - 1) / bm) * ((N + bn - 1) / bn));
 }
 
-int pick_splits(int impl, int64_t M, int64_t N, int64_t K) {
-  int64_t tiles = tiles_for(impl, M, N);
+int pick_splits(int impl, int64_t M, int64_t N, int64_t K, int ak = 0, int bk = 0) {
+  int64_t tiles = tiles_for(impl, M, N, ak, bk);
   int64_t nk = (K + BK - 1) / BK;
   if (tiles >= 512 || nk < 16) return 1;
   int64_t s = (1024 + tiles - 1) / tiles;
@@ -955,9 +970,9 @@ struct Args {
   int64_t bps = 0;               // their plane stride
 };
 
-template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT>
+template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1>
 void launch_p6(dim3 grid, hipStream_t s, const Args& a) {
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_p6<TM, 1, AMODE, BMODE, EPI, SPLIT>), grid,
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_p6<TM, TN, AMODE, BMODE, EPI, SPLIT>), grid,
                        dim3(256), 0, s, a.A, a.B, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.bps,
                        a.ldc, a.bias, a.aux, a.ldaux, a.kps, a.accumulate);
 }
@@ -965,7 +980,12 @@ void launch_p6(dim3 grid, hipStream_t s, const Args& a) {
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   if (a.impl == 5) {
-    launch_p6<1, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
+    if constexpr (AK && BKM) {
+      if (a.M >= a.N) launch_p6<2, 1, 1, EPI, SPLIT>(grid, s, a);
+      else launch_p6<1, 1, 1, EPI, SPLIT, 2>(grid, s, a);
+    } else {
+      launch_p6<1, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
+    }
     return;
   }
   if (a.impl == 6) {
@@ -1034,12 +1054,12 @@ int dispatch(int ak, int bk, int epi, dim3 grid, hipStream_t s, const Args& a) {
   return dispatch_layout<2, 2, 1, 1, SPLIT>(ak, bk, epi, grid, s, a);
 }
 
-template <int TM, bool SPLIT>
+template <int TM, bool SPLIT, int TN = 1>
 int dispatch_bplanes_t(int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
-#define MOLCLR_BP_CASE(AKV, EPV)                                                      \
-  if (ak == AKV && (SPLIT || epi == EPV)) {                                           \
-    launch_p6<(AKV ? 1 : TM), AKV, 2, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT>(grid, s, a); \
-    return 0;                                                                         \
+#define MOLCLR_BP_CASE(AKV, EPV)                                                               \
+  if (ak == AKV && (SPLIT || epi == EPV)) {                                                    \
+    launch_p6<(AKV ? 1 : TM), AKV, 2, SPLIT ? MOLCLR_EPI_NONE : EPV, SPLIT, TN>(grid, s, a); \
+    return 0;                                                                                  \
   }
   if (SPLIT) {
     MOLCLR_BP_CASE(0, MOLCLR_EPI_NONE)
@@ -1060,6 +1080,7 @@ int dispatch_bplanes_t(int ak, int epi, dim3 grid, hipStream_t s, const Args& a)
 
 template <bool SPLIT>
 int dispatch_bplanes(int impl, int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
+  if (impl == 7) return dispatch_bplanes_t<1, SPLIT, 2>(ak, epi, grid, s, a);
   return impl == 6 ? dispatch_bplanes_t<2, SPLIT>(ak, epi, grid, s, a)
                    : dispatch_bplanes_t<1, SPLIT>(ak, epi, grid, s, a);
 }
@@ -1072,9 +1093,9 @@ int64_t planes_kp(int64_t K) { return (K + BK - 1) / BK * BK; }
 int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int epilogue,
              void* workspace, size_t workspace_bytes, hipStream_t s) {
   const int64_t M = a0.M, N = a0.N, K = a0.K;
-  int64_t tiles = tiles_for(impl, M, N);  // workgroups along x
+  int64_t tiles = tiles_for(impl, M, N, a_kmajor, b_kmajor);  // workgroups along x
   MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
-  int sp = pick_splits(impl, M, N, K);
+  int sp = pick_splits(impl, M, N, K, a_kmajor, b_kmajor);
   if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
   Args a = a0;
   a.impl = impl;
@@ -1136,10 +1157,12 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   // sized for the largest split count any implementation would pick
   int sp = pick_splits(0, M, N, K);
-  for (int impl = 1; impl <= 6; ++impl) {
+  for (int impl = 1; impl <= 7; ++impl) {
     const int s2 = pick_splits(impl, M, N, K);
     sp = s2 > sp ? s2 : sp;
   }
+  const int s3 = pick_splits(5, M, N, K, 1, 1);  // the 128-wide weight-gradient tiles
+  sp = s3 > sp ? s3 : sp;
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) + 256 : 0;
 }
 
@@ -1227,7 +1250,7 @@ MOLCLR_API int molclr_gemm_set_impl(int impl) {
 }
 
 MOLCLR_API int molclr_gemm_bplanes_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl == 5 || impl == 6, "gemm_bplanes_set_impl: impl must be 5 or 6");
+  MOLCLR_REQUIRE(impl >= 5 && impl <= 7, "gemm_bplanes_set_impl: impl must be 5, 6 or 7");
   g_bplanes_impl = impl;
   return MOLCLR_OK;
 }

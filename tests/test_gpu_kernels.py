@@ -297,7 +297,7 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
         lib.molclr_gemm_set_impl(prev)
 
 
-@pytest.mark.parametrize("tile", [5, 6])
+@pytest.mark.parametrize("tile", [5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(1000, 600, 300), (777, 300, 600), (64, 64, 8), (33, 68, 12),
                                    (512, 256, 512), (300, 600, 2000)])
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
