@@ -37,15 +37,34 @@ __device__ __forceinline__ f32x16 sim_tile(const float* __restrict__ rows, int64
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int64_t half = C / 2;
   const bool cv = c0 + li < ncols, rv = r0 + li < nrows;
+  // out-of-range rows / columns read row 0 and are zeroed: loads stay unconditional
   const float4* ap = reinterpret_cast<const float4*>(cols + (cv ? (c0 + li) : 0) * C + lh * half);
   const float4* bp = reinterpret_cast<const float4*>(rows + (rv ? (r0 + li) : 0) * C + lh * half);
-  for (int64_t g = 0; g < half / 4; ++g) {
-    float4 a = cv ? ap[g] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 b = rv ? bp[g] : make_float4(0.f, 0.f, 0.f, 0.f);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+  const float am = cv ? 1.f : 0.f, bm = rv ? 1.f : 0.f;
+  const int64_t n4 = half / 4;
+  int64_t g = 0;
+  // four float4 pairs in flight per step (C % 32 == 0 in practice; tail below)
+  for (; g + 4 <= n4; g += 4) {
+    float4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = ap[g + u];
+      b[u] = bp[g + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x * am, b[u].x * bm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y * am, b[u].y * bm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z * am, b[u].z * bm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w * am, b[u].w * bm, acc, 0, 0, 0);
+    }
+  }
+  for (; g < n4; ++g) {
+    const float4 a = ap[g], b = bp[g];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x * am, b.x * bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y * am, b.y * bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z * am, b.z * bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w * am, b.w * bm, acc, 0, 0, 0);
   }
   return acc;
 }
@@ -187,6 +206,7 @@ __global__ void k_reduce_splits(const float* __restrict__ partial, int64_t split
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   float acc = 0.f;
+#pragma unroll 4
   for (int64_t z = 0; z < splits; ++z) acc += partial[z * n + t];
   out[t] = acc;
 }
@@ -235,9 +255,12 @@ __global__ __launch_bounds__(256) void k_ntxent_prep_bwd(const float* __restrict
     dr[row * C + c] = clamped ? g[c] / den : (g[c] - dot * y[c]) / den;
 }
 
-int64_t ntx_splits(int64_t nrows, int64_t ncols) {
+// column splits: single-wave workgroups per (32-row block, split); measured
+// best at ~512 waves for the forward and ~1024 for the backward
+// (tools/ntxent_scale.py; the backward's partials are [nrows][C] each)
+int64_t ntx_splits(int64_t nrows, int64_t ncols, int64_t target = 512) {
   int64_t rb = (nrows + 31) / 32, nch = (ncols + 31) / 32;
-  int64_t s = (512 + rb - 1) / rb;
+  int64_t s = (target + rb - 1) / rb;
   if (s > nch) s = nch;
   if (s < 1) s = 1;
   return s;
@@ -266,10 +289,12 @@ MOLCLR_API int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, con
   return MOLCLR_OK;
 }
 
+constexpr int64_t kBwdWaves = 1024;
+
 MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C) {
   int64_t sp = ntx_splits(nrows, ncols);
   size_t fwd = (size_t)(2 * sp + 1) * nrows * sizeof(float);
-  size_t bwd = (size_t)sp * nrows * C * sizeof(float);
+  size_t bwd = (size_t)ntx_splits(nrows, ncols, kBwdWaves) * nrows * C * sizeof(float);
   return (fwd > bwd ? fwd : bwd) + 256;
 }
 
@@ -309,7 +334,7 @@ MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const f
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_bwd: bad nrows");
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
-  int64_t sp = ntx_splits(nrows, ncols);
+  int64_t sp = ntx_splits(nrows, ncols, kBwdWaves);
   int64_t nch = (ncols + 31) / 32;
   int64_t cps = (nch + sp - 1) / sp;
   sp = (nch + cps - 1) / cps;
