@@ -69,7 +69,54 @@ __device__ __forceinline__ f32x16 sim_tile(const float* __restrict__ rows, int64
   return acc;
 }
 
+// The wave's 32 rows stay in registers for all its column chunks (NQ float4
+// per lane: C = 8 NQ): only the column operand is re-read per chunk.
+template <int NQ>
+struct RowRegs {
+  float4 v[NQ];
+  __device__ __forceinline__ void load(const float* __restrict__ rows, int64_t nrows, int64_t r0,
+                                       int li, int lh) {
+    const bool rv = r0 + li < nrows;
+    const float4* bp =
+        reinterpret_cast<const float4*>(rows + (rv ? (r0 + li) : 0) * (8 * NQ) + lh * 4 * NQ);
+    const float bm = rv ? 1.f : 0.f;
+#pragma unroll
+    for (int g = 0; g < NQ; ++g) {
+      const float4 b = bp[g];
+      v[g] = make_float4(b.x * bm, b.y * bm, b.z * bm, b.w * bm);
+    }
+  }
+};
+
+template <int NQ>
+__device__ __forceinline__ f32x16 sim_tile_r(const RowRegs<NQ>& rr, const float* __restrict__ cols,
+                                             int64_t ncols, int64_t c0, int li, int lh) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const bool cv = c0 + li < ncols;
+  const float4* ap =
+      reinterpret_cast<const float4*>(cols + (cv ? (c0 + li) : 0) * (8 * NQ) + lh * 4 * NQ);
+  const float am = cv ? 1.f : 0.f;
+#pragma unroll
+  for (int g = 0; g < NQ; g += 4) {
+    float4 a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = ap[g + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 b = rr.v[g + u];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].x * am, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].y * am, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].z * am, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u].w * am, b.w, acc, 0, 0, 0);
+    }
+  }
+  return acc;
+}
+
 // partial layout: pm [splits][nrows], ps [splits][nrows]; pos [nrows]
+template <int NQ>  // NQ > 0: rows in registers (C == 8 NQ); 0: any C
 __global__ __launch_bounds__(64) void k_ntxent_fwd_partial(
     const float* __restrict__ rows, const int32_t* __restrict__ gidx, const float* __restrict__ cols,
     int64_t nrows, int64_t ncols, int64_t C, int64_t B, float inv_t, int64_t chunks_per_split,
@@ -83,9 +130,13 @@ __global__ __launch_bounds__(64) void k_ntxent_fwd_partial(
   const int64_t nchunks = (ncols + 31) / 32;
   int64_t ch = (int64_t)blockIdx.y * chunks_per_split;
   int64_t ch_end = ch + chunks_per_split < nchunks ? ch + chunks_per_split : nchunks;
+  RowRegs<(NQ > 0 ? NQ : 4)> rr;
+  if constexpr (NQ > 0) rr.load(rows, nrows, r0, li, lh);
   for (; ch < ch_end; ++ch) {
     const int64_t c0 = ch * 32;
-    f32x16 st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
+    f32x16 st;
+    if constexpr (NQ > 0) st = sim_tile_r<NQ>(rr, cols, ncols, c0, li, lh);
+    else st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
     float tmax = -INFINITY;
     float lg[16];
 #pragma unroll
@@ -133,7 +184,7 @@ __global__ void k_ntxent_fwd_final(const float* __restrict__ pm, const float* __
 }
 
 // partial [splits][nrows][C]; grid (row blocks, splits, k groups of KT tiles)
-template <int KT>
+template <int KT, int NQ>
 __global__ __launch_bounds__(64) void k_ntxent_bwd_partial(
     const float* __restrict__ rows, const int32_t* __restrict__ gidx, const float* __restrict__ cols,
     const float* __restrict__ lse_cols, const float* __restrict__ grad_loss, int64_t nrows,
@@ -158,9 +209,13 @@ __global__ __launch_bounds__(64) void k_ntxent_bwd_partial(
   const int64_t nchunks = (ncols + 31) / 32;
   int64_t ch = (int64_t)blockIdx.y * chunks_per_split;
   int64_t ch_end = ch + chunks_per_split < nchunks ? ch + chunks_per_split : nchunks;
+  RowRegs<(NQ > 0 ? NQ : 4)> rr;
+  if constexpr (NQ > 0) rr.load(rows, nrows, r0, li, lh);
   for (; ch < ch_end; ++ch) {
     const int64_t c0 = ch * 32;
-    f32x16 st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
+    f32x16 st;
+    if constexpr (NQ > 0) st = sim_tile_r<NQ>(rr, cols, ncols, c0, li, lh);
+    else st = sim_tile(rows, nrows, r0, cols, ncols, c0, C, li, lh);
     // W'[c][r] in place
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -316,9 +371,17 @@ MOLCLR_API int molclr_ntxent_fwd(const float* rows, const int32_t* gidx, const f
   float* pm = w.take<float>(sp * nrows);
   float* ps = w.take<float>(sp * nrows);
   float* pos = w.take<float>(nrows);
-  hipLaunchKernelGGL(k_ntxent_fwd_partial, dim3((unsigned)((nrows + 31) / 32), (unsigned)sp),
-                     dim3(64), 0, s, rows, gidx, cols, nrows, ncols, C, B, (float)(1.0 / T), cps,
-                     pm, ps, pos);
+  const dim3 grid((unsigned)((nrows + 31) / 32), (unsigned)sp);
+  const float inv_t = (float)(1.0 / T);
+  if (C == 256)
+    hipLaunchKernelGGL(k_ntxent_fwd_partial<32>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
+                       C, B, inv_t, cps, pm, ps, pos);
+  else if (C == 128)
+    hipLaunchKernelGGL(k_ntxent_fwd_partial<16>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
+                       C, B, inv_t, cps, pm, ps, pos);
+  else
+    hipLaunchKernelGGL(k_ntxent_fwd_partial<0>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
+                       C, B, inv_t, cps, pm, ps, pos);
   hipLaunchKernelGGL(k_ntxent_fwd_final, dim3(molclr::ceil_div(nrows, 256)), dim3(256), 0, s, pm,
                      ps, pos, sp, nrows, (float)(1.0 / (2.0 * B)), lse, loss);
   MOLCLR_LAUNCHED();
@@ -341,10 +404,17 @@ MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const f
   constexpr int KT = 8;
   int64_t kgroups = (C / 32 + KT - 1) / KT;
   float* partial = (float*)workspace;
-  hipLaunchKernelGGL(k_ntxent_bwd_partial<KT>,
-                     dim3((unsigned)((nrows + 31) / 32), (unsigned)sp, (unsigned)kgroups), dim3(64),
-                     0, s, rows, gidx, cols, lse_cols, grad_loss, nrows, ncols, C, B,
-                     (float)(1.0 / T), cps, partial);
+  const dim3 grid((unsigned)((nrows + 31) / 32), (unsigned)sp, (unsigned)kgroups);
+  const float inv_t = (float)(1.0 / T);
+  if (C == 256)
+    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 32>), grid, dim3(64), 0, s, rows, gidx, cols,
+                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
+  else if (C == 128)
+    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 16>), grid, dim3(64), 0, s, rows, gidx, cols,
+                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
+  else
+    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 0>), grid, dim3(64), 0, s, rows, gidx, cols,
+                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
   hipLaunchKernelGGL(k_reduce_splits, dim3(molclr::ceil_div(nrows * C, 256)), dim3(256), 0, s,
                      partial, sp, nrows * C, drows);
   MOLCLR_LAUNCHED();
