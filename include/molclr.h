@@ -223,7 +223,8 @@ int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, in
                             int epilogue_flags, const float* bias, const float* aux,
                             int64_t ldaux, void* workspace, size_t workspace_bytes,
                             molclr_stream_t stream);
-/* tile of molclr_gemm_f32_bplanes: 5 (default) = 64x64, 6 = 128x64 */
+/* tile of molclr_gemm_f32_bplanes: 0 (default) = automatic (64x128 for N >= 512,
+ * else 64x64), 5 = 64x64, 6 = 128x64, 7 = 64x128, 8 = 128x128 */
 int molclr_gemm_bplanes_set_impl(int impl);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */

@@ -493,6 +493,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TM * TN == 
 
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
   const int64_t ldo = SPLIT ? N : ldc;
+  // Epilogue through LDS: each wave writes its accumulators as a row-major
+  // [32 TM][32 TN] fp32 tile, then stores 16-byte row pieces (4 store
+  // instructions per 32 x 32 instead of 16 dword stores: the store tail is
+  // issue-bound).  Needs 16-byte aligned rows; otherwise the dword path.
+  constexpr int WR = 32 * TM, WC = 32 * TN;
+  static_assert(4 * WR * WC * (int)sizeof(float) <= (int)sizeof(lds), "epilogue tile > LDS");
+  const bool vec = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0) &&
+                   (SPLIT || EPI != MOLCLR_EPI_RELU_MASK ||
+                    (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
+                   (SPLIT || (EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
+                    (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  if (vec) {
+    __syncthreads();  // every wave is done reading the K images
+    float* tw = reinterpret_cast<float*>(lds) + wave * WR * WC;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          tw[(a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * WC + b * 32 + li] =
+              acc[a][b][r] + acl[a][b][r];
+    __syncthreads();
+    constexpr int C4 = WC / 4;
+    const int64_t mw = m0 + wm * WR, nw = n0 + wn * WC;
+#pragma unroll
+    for (int it = 0; it < WR * C4 / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx / C4, c4 = idx - row * C4;
+      const int64_t m = mw + row, n = nw + 4 * c4;
+      if (m >= M || n >= N) continue;
+      float4 v = *reinterpret_cast<const float4*>(tw + row * WC + 4 * c4);
+      float* o = Cout + m * ldo + n;
+      if (n + 4 <= N) {
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v = f4add(v, bv);
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                            x.w > 0.f ? v.w : 0.f);
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+        }
+        *reinterpret_cast<float4*>(o) = v;
+      } else {  // the last, partial piece of a row (N % 4 != 0)
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4 && n + j < N; ++j) {
+          float x = e[j];
+          if (!SPLIT) {
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
+            if (accumulate) x += o[j];
+          }
+          o[j] = x;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
@@ -860,6 +925,71 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
 
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
   const int64_t ldo = SPLIT ? N : ldc;
+  // Epilogue through LDS: each wave writes its accumulators as a row-major
+  // [32 TM][32 TN] fp32 tile, then stores 16-byte row pieces (4 store
+  // instructions per 32 x 32 instead of 16 dword stores: the store tail is
+  // issue-bound).  Needs 16-byte aligned rows; otherwise the dword path.
+  constexpr int WR = 32 * TM, WC = 32 * TN;
+  static_assert(4 * WR * WC * (int)sizeof(float) <= (int)sizeof(lds), "epilogue tile > LDS");
+  const bool vec = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0) &&
+                   (SPLIT || EPI != MOLCLR_EPI_RELU_MASK ||
+                    (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
+                   (SPLIT || (EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
+                    (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  if (vec) {
+    __syncthreads();  // every wave is done reading the K images
+    float* tw = reinterpret_cast<float*>(lds) + wave * WR * WC;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          tw[(a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * WC + b * 32 + li] =
+              acc[a][b][r] + acl[a][b][r];
+    __syncthreads();
+    constexpr int C4 = WC / 4;
+    const int64_t mw = m0 + wm * WR, nw = n0 + wn * WC;
+#pragma unroll
+    for (int it = 0; it < WR * C4 / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx / C4, c4 = idx - row * C4;
+      const int64_t m = mw + row, n = nw + 4 * c4;
+      if (m >= M || n >= N) continue;
+      float4 v = *reinterpret_cast<const float4*>(tw + row * WC + 4 * c4);
+      float* o = Cout + m * ldo + n;
+      if (n + 4 <= N) {
+        if (!SPLIT) {
+          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v = f4add(v, bv);
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                            x.w > 0.f ? v.w : 0.f);
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+        }
+        *reinterpret_cast<float4*>(o) = v;
+      } else {  // the last, partial piece of a row (N % 4 != 0)
+        const float e[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4 && n + j < N; ++j) {
+          float x = e[j];
+          if (!SPLIT) {
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
+            if (accumulate) x += o[j];
+          }
+          o[j] = x;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
@@ -927,7 +1057,10 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
 // The split-bf16 kernels stage K-major operands 4 rows at a time, so they need
 // rows % 4 == 0 and ld % 4 == 0 there; other shapes take impl 0.
 int g_impl = 5;
-int g_bplanes_impl = 5;  // tile of molclr_gemm_f32_bplanes: 5 = 64 x 64, 6 = 128 x 64
+// tile of molclr_gemm_f32_bplanes: 0 = automatic (64 x 128 for N >= 512, else
+// 64 x 64: measured best on the step's shapes, tools/gemm_bench.py), 5 = 64 x 64,
+// 6 = 128 x 64, 7 = 64 x 128, 8 = 128 x 128
+int g_bplanes_impl = 0;
 int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
   if (g_impl == 0) return 0;
   if (ak && (M % 4 || lda % 4)) return 0;
@@ -939,8 +1072,8 @@ int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
 // longer of M / N (8.9 -> ~6 VALU per MFMA: half the B or A split work)
 bool p6_wide(int impl, int ak, int bk) { return impl == 5 && ak && bk; }
 int tiles_for(int impl, int64_t M, int64_t N, int ak = 0, int bk = 0) {
-  int64_t bm = (impl == 2 || impl == 3 || impl == 6) ? 128 : 64,
-          bn = (impl == 3 || impl == 7) ? 128 : 64;
+  int64_t bm = (impl == 2 || impl == 3 || impl == 6 || impl == 8) ? 128 : 64,
+          bn = (impl == 3 || impl == 7 || impl == 8) ? 128 : 64;
   if (p6_wide(impl, ak, bk)) {
     bm = M >= N ? 128 : 64;
     bn = M >= N ? 64 : 128;
@@ -1081,6 +1214,7 @@ int dispatch_bplanes_t(int ak, int epi, dim3 grid, hipStream_t s, const Args& a)
 template <bool SPLIT>
 int dispatch_bplanes(int impl, int ak, int epi, dim3 grid, hipStream_t s, const Args& a) {
   if (impl == 7) return dispatch_bplanes_t<1, SPLIT, 2>(ak, epi, grid, s, a);
+  if (impl == 8) return dispatch_bplanes_t<2, SPLIT, 2>(ak, epi, grid, s, a);
   return impl == 6 ? dispatch_bplanes_t<2, SPLIT>(ak, epi, grid, s, a)
                    : dispatch_bplanes_t<1, SPLIT>(ak, epi, grid, s, a);
 }
@@ -1157,7 +1291,7 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   // sized for the largest split count any implementation would pick
   int sp = pick_splits(0, M, N, K);
-  for (int impl = 1; impl <= 7; ++impl) {
+  for (int impl = 1; impl <= 8; ++impl) {
     const int s2 = pick_splits(impl, M, N, K);
     sp = s2 > sp ? s2 : sp;
   }
@@ -1233,7 +1367,8 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   if (M == 0 || N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(K > 0 && A && planes && C, "gemm_f32_bplanes: null operand or K == 0");
   const int64_t npad = planes_npad(N), kp = planes_kp(K);
-  const int impl = (g_bplanes_impl == 6 && a_kmajor) ? 5 : g_bplanes_impl;
+  int impl = g_bplanes_impl ? g_bplanes_impl : (N >= 512 ? 7 : 5);
+  if ((impl == 6 || impl == 8) && a_kmajor) impl = 5;
   Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, impl};
   a.Bp = planes;
   a.bps = npad * kp;
@@ -1250,7 +1385,8 @@ MOLCLR_API int molclr_gemm_set_impl(int impl) {
 }
 
 MOLCLR_API int molclr_gemm_bplanes_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl >= 5 && impl <= 7, "gemm_bplanes_set_impl: impl must be 5, 6 or 7");
+  MOLCLR_REQUIRE(impl == 0 || (impl >= 5 && impl <= 8),
+                 "gemm_bplanes_set_impl: impl must be 0 (automatic) or 5..8");
   g_bplanes_impl = impl;
   return MOLCLR_OK;
 }

@@ -297,7 +297,7 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
         lib.molclr_gemm_set_impl(prev)
 
 
-@pytest.mark.parametrize("tile", [5, 6, 7])
+@pytest.mark.parametrize("tile", [0, 5, 6, 7, 8])
 @pytest.mark.parametrize("M,N,K", [(1000, 600, 300), (777, 300, 600), (64, 64, 8), (33, 68, 12),
                                    (512, 256, 512), (300, 600, 2000)])
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
@@ -338,7 +338,7 @@ def test_gemm_bplanes(dev, tile, M, N, K, ak, bk):
             W.mul_(2.0)
         assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk), 2 * y) < TOL
     finally:
-        lib.molclr_gemm_bplanes_set_impl(5)
+        lib.molclr_gemm_bplanes_set_impl(0)
 
 
 def test_colsum(dev):
