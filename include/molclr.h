@@ -227,6 +227,18 @@ int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, in
  * else 64x64), 5 = 64x64, 6 = 128x64, 7 = 64x128, 8 = 128x128 */
 int molclr_gemm_bplanes_set_impl(int impl);
 
+/* Weight and bias gradients of y = x W^T + b (nn.Linear backward):
+ *   dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i],   db[n_out] (+)= Σ_r dy[r][o]
+ * dy [rows, n_out] (row stride ld_dy), x [rows, n_in] (ld_x).  One split-bf16
+ * GEMM that also takes the bias column sums from the dy tiles it stages (no
+ * separate pass over dy).  db may be NULL; accumulate != 0 adds into dW / db.
+ * db needs n_out and ld_dy multiples of 4.  Falls back to molclr_gemm_f32 +
+ * molclr_colsum_f32 for shapes the fused kernel does not take. */
+size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_out, int64_t n_in);
+int molclr_linear_wgrad(const float* dy, const float* x, float* dW, float* db, int64_t rows,
+                        int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
+                        void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
 int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,

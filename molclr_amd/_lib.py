@@ -53,6 +53,9 @@ SIGNATURES = {
     "molclr_gemm_f32_bplanes": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, c_int, _P,
                                         _P, _I64, _P, c_size_t, _P]),
     "molclr_gemm_get_impl": (c_int, []),
+    "molclr_linear_wgrad_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_linear_wgrad": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
+                                    _P]),
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),

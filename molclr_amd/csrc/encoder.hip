@@ -50,6 +50,8 @@ size_t kernels_ws(int64_t N, int64_t D) {
   mx(molclr_gemm_f32_workspace_bytes(N, 2 * D, D));
   mx(molclr_gemm_f32_workspace_bytes(N, D, 2 * D));
   mx(molclr_colsum_f32_workspace_bytes(N, 2 * D));
+  mx(molclr_linear_wgrad_workspace_bytes(N, D, 2 * D));
+  mx(molclr_linear_wgrad_workspace_bytes(N, 2 * D, D));
   mx(molclr_batchnorm_workspace_bytes(N, D));
   mx(molclr_gine_aggregate_bwd_workspace_bytes(N, D));
   mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
@@ -159,7 +161,6 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   float* dz1 = S + 3 * N * D;    // w.r.t. the first Linear's pre-activation [N,2D]
   void* kws = (char*)workspace + molclr::align_up(scratch_floats(N, D) * sizeof(float), 256);
   const size_t kws_bytes = kernels_ws(N, D);
-  constexpr int ACC = MOLCLR_EPI_ACCUMULATE;
 
   const float* dy = dh_out;
   for (int l = L - 1; l >= 0; --l) {
@@ -171,20 +172,20 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     MOLCLR_TRY(molclr_batchnorm_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
                                     A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], N, D,
                                     last ? 0 : 1, 1, kws, kws_bytes, stream));
-    // second Linear (ops.linear_bwd order: dW, db, dx with the ReLU mask of a1)
+    // second Linear (ops.linear_bwd order: dW with db, dx with the ReLU mask of a1)
     if (gr->mlp2_weight[l])
-      MOLCLR_TRY(molclr_gemm_f32(dz, a1, gr->mlp2_weight[l], D, 2 * D, N, D, 2 * D, 2 * D, 1, 1,
-                                 ACC, nullptr, nullptr, 0, kws, kws_bytes, stream));
-    if (gr->mlp2_bias[l])
+      MOLCLR_TRY(molclr_linear_wgrad(dz, a1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D, 2 * D, D,
+                                     2 * D, 1, kws, kws_bytes, stream));
+    else if (gr->mlp2_bias[l])
       MOLCLR_TRY(molclr_colsum_f32(dz, gr->mlp2_bias[l], N, D, D, 1, kws, kws_bytes, stream));
     MOLCLR_TRY(molclr_gemm_f32_bplanes(dz, e->mlp2_planes_t[l], dz1, N, 2 * D, D, D, 2 * D, 0,
                                        MOLCLR_EPI_RELU_MASK, nullptr, a1, 2 * D, kws, kws_bytes,
                                        stream));
     // first Linear
     if (gr->mlp0_weight[l])
-      MOLCLR_TRY(molclr_gemm_f32(dz1, agg, gr->mlp0_weight[l], 2 * D, D, N, 2 * D, D, D, 1, 1,
-                                 ACC, nullptr, nullptr, 0, kws, kws_bytes, stream));
-    if (gr->mlp0_bias[l])
+      MOLCLR_TRY(molclr_linear_wgrad(dz1, agg, gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D,
+                                     2 * D, D, 1, kws, kws_bytes, stream));
+    else if (gr->mlp0_bias[l])
       MOLCLR_TRY(molclr_colsum_f32(dz1, gr->mlp0_bias[l], N, 2 * D, 2 * D, 1, kws, kws_bytes,
                                    stream));
     MOLCLR_TRY(molclr_gemm_f32_bplanes(dz1, e->mlp0_planes_t[l], dagg, N, D, 2 * D, 2 * D, D, 0,

@@ -715,6 +715,14 @@ struct PStageM {
       }
     }
   }
+  // column sums over K of this thread's rows (the bias gradient of a Linear)
+  __device__ __forceinline__ void colsum_add(float4* cs, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (UNITS % T && t + j * T >= UNITS) continue;
+      cs[j] = f4add(cs[j], r[j]);
+    }
+  }
   __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -796,12 +804,17 @@ struct PStageSel<1, ROWS, T> { using type = PStageM<ROWS, T>; };
 template <int ROWS, int T>
 struct PStageSel<2, ROWS, T> { using type = PStageP<ROWS, T>; };
 
-template <int TM, int TN, int AMODE, int BMODE, int EPI, bool SPLIT>
+// CS: also the column sums of A over K (A K-major: the bias gradient Σ_rows dY
+// of a Linear's weight-gradient product), written by the n-tile-0 blocks to
+// colsum[m] (or, split-K, to colsum[split * M + m] for k_splitk_reduce).
+template <int TM, int TN, int AMODE, int BMODE, int EPI, bool SPLIT, bool CS = false>
 __global__ __launch_bounds__(256) void k_gemm_p6(
     const float* __restrict__ A, const float* __restrict__ Bf, const uint16_t* __restrict__ Bp,
     float* __restrict__ C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
     int64_t bplane_stride, int64_t ldc, const float* __restrict__ bias,
-    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
+    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate,
+    float* __restrict__ colsum) {
+  static_assert(!CS || AMODE == 1, "column sums are taken over a K-major A");
   constexpr int T = 256;
   constexpr int BM = 64 * TM, BN = 64 * TN;
   constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
@@ -890,6 +903,10 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
 
   const int nsteps = kt_end - kt_beg;
   auto kof = [&](int step) { return (int64_t)(kt_beg + step) * BK; };
+  constexpr int CSN = CS ? SA::PER : 1;
+  float4 cs[CSN];
+#pragma unroll
+  for (int j = 0; j < CSN; ++j) cs[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (nsteps > 0) {
     sa0.load(kof(0), K, ta);
     sb0.load(kof(0), K, tb);
@@ -897,6 +914,7 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
       sa1.load(kof(1), K, ta);
       sb1.load(kof(1), K, tb);
     }
+    if constexpr (CS) sa0.colsum_add(cs, ta);
     sa0.store(buf0, ta);
     sb0.store(buf0 + AI, tb);
     __syncthreads();
@@ -908,6 +926,7 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
       sb0.load(kof(i + 2), K, tb);
     }
     compute(buf0);
+    if constexpr (CS) sa1.colsum_add(cs, ta);  // K step i + 1
     sa1.store(buf1, ta);
     sb1.store(buf1 + AI, tb);
     __syncthreads();
@@ -916,12 +935,40 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
       sb1.load(kof(i + 3), K, tb);
     }
     compute(buf1);
+    if constexpr (CS) {
+      if (i + 2 < nsteps) sa0.colsum_add(cs, ta);  // K step i + 2
+    }
     // unconditional: when i + 2 >= nsteps the image is never read again
     sa0.store(buf0, ta);
     sb0.store(buf0 + AI, tb);
     __syncthreads();
   }
   if (i < nsteps) compute(buf0);
+
+  if constexpr (CS) {
+    if (n0 == 0 && colsum != nullptr) {  // block-uniform
+      // a thread's units all share one 4-row group rb = tid % (BM/4); fold them,
+      // then the T/(BM/4) threads of each group in a fixed order
+      constexpr int RB = BM / 4;
+      float4 v = cs[0];
+#pragma unroll
+      for (int j = 1; j < CSN; ++j) v = f4add(v, cs[j]);
+      __syncthreads();  // K images no longer read
+      float4* red = reinterpret_cast<float4*>(lds);
+      red[tid] = v;
+      __syncthreads();
+      if (tid < RB) {
+        float4 t4 = red[tid];
+        for (int q = 1; q < T / RB; ++q) t4 = f4add(t4, red[tid + q * RB]);
+        const float e[4] = {t4.x, t4.y, t4.z, t4.w};
+        float* o = SPLIT ? colsum + (int64_t)blockIdx.y * M : colsum;
+        for (int j = 0; j < 4; ++j) {
+          const int64_t m = m0 + 4 * tid + j;
+          if (m < M) o[m] = (!SPLIT && accumulate) ? o[m] + e[j] : e[j];
+        }
+      }
+    }
+  }
 
   float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
   const int64_t ldo = SPLIT ? N : ldc;
@@ -1034,11 +1081,18 @@ __global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K
 }
 
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
+// (and colsum[m] = Σ_z cs_partial[z][m] for t < M when cs_partial is given)
 template <int EPI>
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
                                 float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
-                                const float* __restrict__ aux, int64_t ldaux, int accumulate) {
+                                const float* __restrict__ aux, int64_t ldaux, int accumulate,
+                                const float* __restrict__ cs_partial, float* __restrict__ colsum) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (cs_partial && t < M) {
+    float c = 0.f;
+    for (int z = 0; z < splits; ++z) c += cs_partial[(int64_t)z * M + t];
+    colsum[t] = accumulate ? colsum[t] + c : c;
+  }
   if (t >= M * N) return;
   int64_t m = t / N, n = t - m * N;
   float v = 0.f;
@@ -1101,21 +1155,30 @@ struct Args {
   int impl;
   const uint16_t* Bp = nullptr;  // pre-split planes (molclr_gemm_f32_bplanes)
   int64_t bps = 0;               // their plane stride
+  float* colsum = nullptr;       // Σ_k A(m, k) out (molclr_linear_wgrad; K-major A, p6)
 };
 
-template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1>
+template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1, bool CS = false>
 void launch_p6(dim3 grid, hipStream_t s, const Args& a) {
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_p6<TM, TN, AMODE, BMODE, EPI, SPLIT>), grid,
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_p6<TM, TN, AMODE, BMODE, EPI, SPLIT, CS>), grid,
                        dim3(256), 0, s, a.A, a.B, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.bps,
-                       a.ldc, a.bias, a.aux, a.ldaux, a.kps, a.accumulate);
+                       a.ldc, a.bias, a.aux, a.ldaux, a.kps, a.accumulate, a.colsum);
 }
 
 template <int WM, int WN, int TM, int TN, bool AK, bool BKM, int EPI, bool SPLIT>
 void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   if (a.impl == 5) {
     if constexpr (AK && BKM) {
-      if (a.M >= a.N) launch_p6<2, 1, 1, EPI, SPLIT>(grid, s, a);
-      else launch_p6<1, 1, 1, EPI, SPLIT, 2>(grid, s, a);
+      if (a.colsum) {
+        if constexpr (EPI == MOLCLR_EPI_NONE) {
+          if (a.M >= a.N) launch_p6<2, 1, 1, EPI, SPLIT, 1, true>(grid, s, a);
+          else launch_p6<1, 1, 1, EPI, SPLIT, 2, true>(grid, s, a);
+        }
+      } else if (a.M >= a.N) {
+        launch_p6<2, 1, 1, EPI, SPLIT>(grid, s, a);
+      } else {
+        launch_p6<1, 1, 1, EPI, SPLIT, 2>(grid, s, a);
+      }
     } else {
       launch_p6<1, AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
     }
@@ -1230,7 +1293,8 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
   int64_t tiles = tiles_for(impl, M, N, a_kmajor, b_kmajor);  // workgroups along x
   MOLCLR_REQUIRE(tiles < (1ll << 31), "gemm_f32: too many tiles");
   int sp = pick_splits(impl, M, N, K, a_kmajor, b_kmajor);
-  if (sp > 1 && workspace_bytes < (size_t)sp * M * N * sizeof(float)) sp = 1;
+  const size_t cs_floats = a0.colsum ? (size_t)M : 0;  // per split
+  if (sp > 1 && workspace_bytes < (size_t)sp * (M * N + cs_floats) * sizeof(float)) sp = 1;
   Args a = a0;
   a.impl = impl;
   int rc;
@@ -1242,8 +1306,10 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
     int kps = (int)((nk + sp - 1) / sp);
     sp = (int)((nk + kps - 1) / kps);
     float* partial = (float*)workspace;
+    float* cs_partial = a.colsum ? partial + (size_t)sp * M * N : nullptr;
     Args ap = a;
     ap.C = partial;
+    ap.colsum = cs_partial;
     ap.ldc = N;
     ap.bias = nullptr;
     ap.aux = nullptr;
@@ -1262,19 +1328,19 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
       switch (epilogue) {
         case MOLCLR_EPI_NONE:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s,
-                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
           break;
         case MOLCLR_EPI_BIAS:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s,
-                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
           break;
         case MOLCLR_EPI_BIAS_RELU:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0,
-                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
           break;
         default:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0,
-                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate);
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
       }
     }
   }
@@ -1373,6 +1439,51 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   a.Bp = planes;
   a.bps = npad * kp;
   return run_gemm(a, impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
+                  molclr::as_stream(stream));
+}
+
+size_t molclr_colsum_ws(int64_t rows, int64_t cols);  // norm.hip
+
+MOLCLR_API size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_out, int64_t n_in) {
+  const int64_t M = n_out, N = n_in, K = rows;
+  size_t need = molclr_gemm_f32_workspace_bytes(M, N, K);
+  const int sp = pick_splits(5, M, N, K, 1, 1);
+  const size_t fused = sp > 1 ? (size_t)sp * (M * N + M) * sizeof(float) + 256 : 0;
+  const size_t cs = molclr_colsum_ws(rows, n_out);
+  need = fused > need ? fused : need;
+  return cs > need ? cs : need;
+}
+
+MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, float* db,
+                                   int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                                   int64_t ld_x, int accumulate, void* workspace,
+                                   size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rows >= 0 && n_out > 0 && n_in > 0, "linear_wgrad: bad sizes");
+  MOLCLR_REQUIRE(dy && x && dW, "linear_wgrad: null pointer");
+  MOLCLR_REQUIRE(ld_dy >= n_out && ld_x >= n_in, "linear_wgrad: leading dimension too small");
+  MOLCLR_REQUIRE(!db || (n_out % 4 == 0 && ld_dy % 4 == 0),
+                 "linear_wgrad: db needs n_out and ld_dy multiples of 4");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_linear_wgrad_workspace_bytes(rows, n_out, n_in));
+  const int flags = accumulate ? MOLCLR_EPI_ACCUMULATE : 0;
+  if (rows == 0) {  // an empty batch contributes nothing: dW = 0 (or unchanged)
+    if (!accumulate) {
+      (void)hipMemsetAsync(dW, 0, (size_t)n_out * n_in * sizeof(float), molclr::as_stream(stream));
+      if (db) (void)hipMemsetAsync(db, 0, (size_t)n_out * sizeof(float), molclr::as_stream(stream));
+    }
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  // dW = dy^T x: A = dy (K-major, lda = ld_dy), B = x (K-major, ldb = ld_x)
+  if (!db || impl_for(n_out, n_in, ld_dy, ld_x, 1, 1) != 5) {
+    int rc = molclr_gemm_f32(dy, x, dW, n_out, n_in, rows, ld_dy, ld_x, n_in, 1, 1, flags,
+                             nullptr, nullptr, 0, workspace, workspace_bytes, stream);
+    if (rc || !db) return rc;
+    return molclr_colsum_f32(dy, db, rows, n_out, ld_dy, accumulate, workspace, workspace_bytes,
+                             stream);
+  }
+  Args a{dy, x, dW, n_out, n_in, rows, ld_dy, ld_x, n_in, nullptr, nullptr, 0, 0, accumulate, 5};
+  a.colsum = db;
+  return run_gemm(a, 5, false, 1, 1, MOLCLR_EPI_NONE, workspace, workspace_bytes,
                   molclr::as_stream(stream));
 }
 

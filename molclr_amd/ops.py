@@ -220,11 +220,25 @@ def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=No
     M, K = x.shape
     N = W.shape[0]
     dx = dW = db = None
-    if need_w:
+    if need_w and need_b:
+        # dW[N,K] = dy^T x and db = Σ_rows dy in one pass (molclr_linear_wgrad)
+        wbuf, wacc, dW = _grad_sink(W_param, (N, K), dy.device)
+        bbuf, bacc, db = _grad_sink(b_param, (N,), dy.device)
+        if wacc != bacc:  # mixed ownership: fresh buffers for both
+            wbuf, wacc, dW = _grad_sink(None, (N, K), dy.device)
+            bbuf, bacc, db = _grad_sink(None, (N,), dy.device)
+        ws_bytes = _wsq("molclr_linear_wgrad_workspace_bytes", M, N, K)
+        ws = _ws(ws_bytes, dy.device)
+        _lib.call("molclr_linear_wgrad", dy.data_ptr(), x.data_ptr(), wbuf.data_ptr(),
+                  bbuf.data_ptr(), M, N, K, dy.stride(0), x.stride(0), wacc, ws.data_ptr(),
+                  ws_bytes, _stream(dy))
+        if _TIMER is not None:
+            _TIMER.add("gemm_f32", 2.0 * M * N * K)
+    elif need_w:
         # dW[N,K] = dy^T x : A = dy (K-major, lda=N), B = x (K-major, ldb=K)
         buf, acc, dW = _grad_sink(W_param, (N, K), dy.device)
         gemm(dy, x, N, K, M, N, K, True, True, out=buf, accumulate=acc)
-    if need_b:
+    elif need_b:
         buf, acc, db = _grad_sink(b_param, (N,), dy.device)
         colsum(dy, out=buf, accumulate=acc)
     if need_x:

@@ -341,6 +341,41 @@ def test_gemm_bplanes(dev, tile, M, N, K, ak, bk):
         lib.molclr_gemm_bplanes_set_impl(0)
 
 
+@pytest.mark.parametrize("rows,n_out,n_in", [(15278, 300, 600), (15278, 600, 300), (512, 512, 300),
+                                             (100, 256, 512), (37, 12, 20), (1000, 30, 64)])
+@pytest.mark.parametrize("acc", [0, 1])
+def test_linear_wgrad(dev, rows, n_out, n_in, acc):
+    """dW = dy^T x and db = column sums of dy in one split-bf16 GEMM (fused for
+    4-aligned shapes, gemm + colsum otherwise), against float64."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(rows + n_out)
+    dy = torch.randn(rows, n_out)
+    x = torch.randn(rows, n_in)
+    W0 = torch.randn(n_out, n_in)
+    b0 = torch.randn(n_out)
+    dW = W0.clone().to(dev)
+    db = b0.clone().to(dev)
+    ws_bytes = lib.molclr_linear_wgrad_workspace_bytes(rows, n_out, n_in)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    dyd, xd = dy.to(dev), x.to(dev)
+    rc = lib.molclr_linear_wgrad(dyd.data_ptr(), xd.data_ptr(), dW.data_ptr(), db.data_ptr(),
+                                 rows, n_out, n_in, n_out, n_in, acc, ws.data_ptr(), ws_bytes, None)
+    if n_out % 4:
+        assert rc == -1 and b"multiples of 4" in lib.molclr_last_error()
+    else:
+        assert rc == 0
+        refW = dy.double().t() @ x.double() + (W0.double() if acc else 0)
+        refb = dy.double().sum(0) + (b0.double() if acc else 0)
+        assert rel(dW, refW) < TOL
+        assert rel(db, refb) < TOL
+    # without db: the weight gradient alone
+    dW2 = torch.empty(n_out, n_in, device=dev)
+    assert lib.molclr_linear_wgrad(dyd.data_ptr(), xd.data_ptr(), dW2.data_ptr(), None, rows,
+                                   n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_bytes, None) == 0
+    assert rel(dW2, dy.double().t() @ x.double()) < TOL
+
+
 def test_colsum(dev):
     x = torch.randn(15713, 600)
     assert rel(ops.colsum(x.to(dev)), x.double().sum(0)) < TOL
