@@ -218,6 +218,11 @@ int molclr_gemm_get_impl(void);
 size_t molclr_bplanes_bytes(int64_t N, int64_t K);
 int molclr_bplanes_make(const float* B, int64_t N, int64_t K, int64_t ldb, int b_kmajor,
                         uint16_t* planes, molclr_stream_t stream);
+/* molclr_bplanes_make for `count` weights in one launch per 32 (host arrays of
+ * per-weight arguments); the planes of a whole model after an optimizer step. */
+int molclr_bplanes_make_batch(int count, const float* const* B, const int64_t* N,
+                              const int64_t* K, const int64_t* ldb, const int* b_kmajor,
+                              uint16_t* const* planes, molclr_stream_t stream);
 int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
                             int64_t N, int64_t K, int64_t lda, int64_t ldc, int a_kmajor,
                             int epilogue_flags, const float* bias, const float* aux,

@@ -50,6 +50,7 @@ SIGNATURES = {
     "molclr_gemm_bplanes_set_impl": (c_int, [c_int]),
     "molclr_bplanes_bytes": (c_size_t, [_I64, _I64]),
     "molclr_bplanes_make": (c_int, [_P, _I64, _I64, _I64, c_int, _P, _P]),
+    "molclr_bplanes_make_batch": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P]),
     "molclr_gemm_f32_bplanes": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, c_int, _P,
                                         _P, _I64, _P, c_size_t, _P]),
     "molclr_gemm_get_impl": (c_int, []),

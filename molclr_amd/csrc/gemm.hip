@@ -1080,6 +1080,32 @@ __global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K
   planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
 }
 
+// Batched form: blockIdx.y = job (one weight image per job).
+struct PlanesJob {
+  const float* B;
+  uint16_t* planes;
+  int64_t N, K, ldb, npad, kp;
+  int kmajor;
+};
+constexpr int kPlanesBatch = 32;
+struct PlanesJobs {
+  PlanesJob j[kPlanesBatch];
+};
+__global__ void k_bplanes_make_batch(PlanesJobs jobs) {
+  const PlanesJob& jb = jobs.j[blockIdx.y];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= jb.npad * jb.kp) return;
+  const int64_t n = t / jb.kp, k = t - n * jb.kp;
+  float v = 0.f;
+  if (n < jb.N && k < jb.K) v = jb.kmajor ? jb.B[k * jb.ldb + n] : jb.B[n * jb.ldb + k];
+  uint32_t h, m, l;
+  split2(v, 0.f, h, m, l);
+  const int64_t ps = jb.npad * jb.kp;
+  jb.planes[t] = (uint16_t)(h & 0xFFFFu);
+  jb.planes[ps + t] = (uint16_t)(m & 0xFFFFu);
+  jb.planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
+}
+
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
 // (and colsum[m] = Σ_z cs_partial[z][m] for t < M when cs_partial is given)
 template <int EPI>
@@ -1408,6 +1434,34 @@ MOLCLR_API int molclr_bplanes_make(const float* B, int64_t N, int64_t K, int64_t
   const int64_t npad = planes_npad(N), kp = planes_kp(K);
   hipLaunchKernelGGL(k_bplanes_make, dim3((unsigned)molclr::ceil_div(npad * kp, 256)), dim3(256), 0,
                      molclr::as_stream(stream), B, N, K, ldb, b_kmajor, planes, npad, kp);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_bplanes_make_batch(int count, const float* const* B, const int64_t* N,
+                                         const int64_t* K, const int64_t* ldb,
+                                         const int* b_kmajor, uint16_t* const* planes,
+                                         molclr_stream_t stream) {
+  MOLCLR_REQUIRE(count >= 0 && (count == 0 || (B && N && K && ldb && b_kmajor && planes)),
+                 "bplanes_make_batch: null arrays");
+  for (int base = 0; base < count; base += kPlanesBatch) {
+    PlanesJobs jobs{};
+    const int n = count - base < kPlanesBatch ? count - base : kPlanesBatch;
+    int64_t most = 0;
+    for (int i = 0; i < n; ++i) {
+      const int q = base + i;
+      MOLCLR_REQUIRE(N[q] > 0 && K[q] > 0 && B[q] && planes[q],
+                     "bplanes_make_batch: job %d empty or null", q);
+      MOLCLR_REQUIRE(b_kmajor[q] ? ldb[q] >= N[q] : ldb[q] >= K[q],
+                     "bplanes_make_batch: job %d leading dimension too small", q);
+      jobs.j[i] = PlanesJob{B[q], planes[q], N[q], K[q], ldb[q], planes_npad(N[q]), planes_kp(K[q]),
+                            b_kmajor[q]};
+      const int64_t e = jobs.j[i].npad * jobs.j[i].kp;
+      most = e > most ? e : most;
+    }
+    hipLaunchKernelGGL(k_bplanes_make_batch, dim3((unsigned)molclr::ceil_div(most, 256), (unsigned)n),
+                       dim3(256), 0, molclr::as_stream(stream), jobs);
+  }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -154,12 +154,21 @@ def bump_param_generation() -> None:
 
 
 def weight_planes(W, N, K, ldb, b_kmajor) -> torch.Tensor:
-    """Split-bf16 planes of B(k, n) stored in W (molclr_gemm_f32's B layout)."""
+    """Split-bf16 planes of B(k, n) stored in W (molclr_gemm_f32's B layout).
+
+    After an optimizer step every cached image is stale: the first lookup
+    regenerates all live ones in one batched launch (molclr_bplanes_make_batch),
+    not one launch per weight and orientation."""
     key = (W.data_ptr(), N, K, ldb, int(b_kmajor))
-    tok = (W._version, PARAM_GENERATION[0])
+    gen = PARAM_GENERATION[0]
     ent = _PLANES.get(key)
-    if ent is not None and ent[0] == tok and ent[1]() is W:
-        return ent[2]
+    if ent is not None and ent[1]() is W and ent[0] == (W._version, gen):
+        return ent[3]
+    if ent is not None and ent[0][1] != gen and ent[1]() is W:
+        _refresh_planes(gen)
+        ent = _PLANES.get(key)
+        if ent is not None and ent[0] == (W._version, gen):
+            return ent[3]
     if len(_PLANES) > 512:  # drop entries of dead tensors
         for k in [k for k, e in _PLANES.items() if e[1]() is None]:
             del _PLANES[k]
@@ -167,8 +176,33 @@ def weight_planes(W, N, K, ldb, b_kmajor) -> torch.Tensor:
     planes = torch.empty(nbytes // 2, dtype=torch.int16, device=W.device)
     _lib.call("molclr_bplanes_make", W.data_ptr(), N, K, ldb, int(b_kmajor), planes.data_ptr(),
               _stream(W))
-    _PLANES[key] = (tok, weakref.ref(W), planes)
+    _PLANES[key] = ((W._version, gen), weakref.ref(W), (N, K, ldb, int(b_kmajor)), planes)
     return planes
+
+
+def _refresh_planes(gen: int) -> None:
+    """Regenerate every live cached image of an older generation, batched."""
+    jobs = []
+    for k, (tok, ref, shape, planes) in list(_PLANES.items()):
+        W = ref()
+        if W is None:
+            del _PLANES[k]
+            continue
+        if tok[1] != gen and W.data_ptr() == k[0]:
+            jobs.append((k, W, shape, planes))
+    if not jobs:
+        return
+    n = len(jobs)
+    arr = lambda vals, ct: (ct * n)(*vals)  # noqa: E731
+    _lib.call("molclr_bplanes_make_batch", n,
+              arr([j[1].data_ptr() for j in jobs], ctypes.c_void_p),
+              arr([j[2][0] for j in jobs], ctypes.c_int64),
+              arr([j[2][1] for j in jobs], ctypes.c_int64),
+              arr([j[2][2] for j in jobs], ctypes.c_int64),
+              arr([j[2][3] for j in jobs], ctypes.c_int),
+              arr([j[3].data_ptr() for j in jobs], ctypes.c_void_p), _stream(jobs[0][3]))
+    for k, W, shape, planes in jobs:
+        _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, planes)
 
 
 def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
