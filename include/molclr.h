@@ -228,8 +228,11 @@ int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, in
                             int epilogue_flags, const float* bias, const float* aux,
                             int64_t ldaux, void* workspace, size_t workspace_bytes,
                             molclr_stream_t stream);
-/* tile of molclr_gemm_f32_bplanes: 0 (default) = automatic (64x128 for N >= 512,
- * else 64x64), 5 = 64x64, 6 = 128x64, 7 = 64x128, 8 = 128x128 */
+/* tile of molclr_gemm_f32_bplanes: 0 (default) = automatic (9 for a row-major A
+ * whose 128-row tiles number >= 128, else 64x128 for N >= 512, else 64x64),
+ * 5 = 64x64, 6 = 128x64, 7 = 64x128, 8 = 128x128, 9 = "q6": 128 x 160 (or
+ * 128 / 64 wide) tiles with A streamed through registers, one wave per 32
+ * rows, for K <= 1024 (a K-major A or a longer K falls back to 5 / 7) */
 int molclr_gemm_bplanes_set_impl(int impl);
 
 /* Weight and bias gradients of y = x W^T + b (nn.Linear backward):

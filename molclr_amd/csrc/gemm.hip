@@ -675,14 +675,17 @@ struct PStageK {
 // 32-element XOR of k-row k: separates the 4 k-rows one transposed read
 // touches (64-row rows are 32 dwords: rows k and k+2 share banks; 128-row
 // rows are 64 dwords: all four do).
+// 160-row rows are 80 dwords (16 mod 64 banks apart): the four k-rows of a
+// transposed read already fall on distinct banks, no XOR.
 template <int ROWS>
 __device__ __forceinline__ int kswz(int k) {
-  return ROWS == 64 ? ((k >> 1) & 1) << 5 : (k & 3) << 5;
+  return ROWS == 64 ? ((k >> 1) & 1) << 5 : ROWS == 128 ? (k & 3) << 5 : 0;
 }
 
 template <int ROWS, int T>
 struct PStageM {
-  static_assert(ROWS == 64 || ROWS == 128, "K-major staging is laid out for 64/128-row tiles");
+  static_assert(ROWS == 64 || ROWS == 128 || ROWS == 160,
+                "K-major staging is laid out for 64/128/160-row tiles");
   static constexpr int UNITS = BK * (ROWS / 4);
   static constexpr int PER = (UNITS + T - 1) / T;
   const float* p[PER];
@@ -1062,6 +1065,389 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
   }
 }
 
+// ---------------------------------------------------------------------------
+// "q6": split-bf16 GEMM of a row-major fp32 A with pre-split weight planes
+// (molclr_gemm_f32_bplanes with a_kmajor = 0): the forward and data-gradient
+// products of every Linear.  On these shapes k_gemm_p6 is bound by staging,
+// not by the MFMA: each K step of a 64 x 64 tile writes 24 KB of images to
+// LDS (a ds_write_b128 moves ~80 B/clk/CU) and splits 8 A elements per
+// thread, all for 12 MFMAs per wave and a barrier.  q6 decomposes differently:
+//  * the block's 4 waves are stacked along M: wave w owns rows m0 + 32w .. +31
+//    and all BN = 32 TN columns of the block, so no A element is needed by two
+//    waves.  A goes global -> registers -> split -> MFMA operand: no A image,
+//    no A ds_write, no redundant split;
+//  * only B (the pre-split planes: a 16-byte copy per unit) is staged,
+//    double-buffered and shared by the 4 waves: 30 KB per K step for
+//    4 x 60 MFMAs at TN = 5 (against 24 KB for 4 x 12 in p6).  The stage is
+//    written right after the barrier and the next one issued before the
+//    MFMAs, so LDS writes and load latency overlap the compute;
+//  * one accumulator: the six products of an element pair go into the same
+//    fp32 sum, which keeps the registers at two waves per SIMD (p6's separate
+//    correction sum would cost 80 more).  Over the K of a Linear's forward /
+//    data gradient (K <= 1024: 64 MFMA accumulations per sum) the error stays
+//    at p6's (tests/test_gpu_kernels.py); a 1000-step chain (K = 15700, all
+//    products positive) measured 5x p6's, so longer K go to p6 / split-K.
+// K order: for K step k0 and MFMA step s, lane half h of both operands holds
+// the actual k = k0 + 16h + 8s .. +7, so an A lane loads its row's 64
+// contiguous bytes k0 + 16h .. +15 once per K step, and the B fragment is
+// image chunk 2h + s.
+// ---------------------------------------------------------------------------
+constexpr int kQ6Waves = 4;
+constexpr int kQ6BM = 32 * kQ6Waves;
+constexpr int64_t kQ6MaxK = 1024;  // longer chains of one fp32 sum: see above
+
+// pre-split planes [3][npad][kp] -> LDS image [3][BN][XK]; unit = (plane, row,
+// 16-byte chunk), rows clamped into the planes (columns >= N are never stored)
+template <int BN, int T>
+struct QStageB {
+  static constexpr int UNITS = 3 * BN * 4;
+  static constexpr int PER = (UNITS + T - 1) / T;
+  u32x4 r[PER];
+  int goff[PER];
+  __device__ __forceinline__ void init(int64_t n0, int64_t npad, int64_t kp, int t) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      const int pl = u / (BN * 4), rem = u % (BN * 4);
+      int64_t row = n0 + (rem >> 2);
+      row = row < npad ? row : npad - 1;
+      goff[j] = (UNITS % T && u >= UNITS) ? 0 : (int)((pl * npad + row) * kp + 8 * (rem & 3));
+    }
+  }
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ Bp, int64_t k0, int t) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (UNITS % T && t + j * T >= UNITS) continue;
+      r[j] = *reinterpret_cast<const u32x4*>(Bp + goff[j] + k0);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = t + j * T;
+      if (UNITS % T && u >= UNITS) continue;
+      const int pl = u / (BN * 4), rem = u % (BN * 4);
+      *reinterpret_cast<u32x4*>(img + pl * BN * XK + xoff(rem >> 2, rem & 3)) = r[j];
+    }
+  }
+};
+
+template <int TN, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
+    const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
+    int accumulate) {
+  constexpr int T = 64 * kQ6Waves;
+  constexpr int BN = 32 * TN;
+  constexpr int BI = 3 * BN * XK;  // bf16 elements per B image
+  static_assert(kQ6Waves * 32 * 32 * (int)sizeof(float) <= 2 * BI * (int)sizeof(uint16_t),
+                "epilogue tiles exceed the LDS images");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BI];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + kQ6BM - 1) / kQ6BM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);  // a row slab's column tiles share an XCD
+  const int64_t m0 = (int64_t)(tile / ntn) * kQ6BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
+  int64_t arow_i = m0 + 32 * wave + li;
+  arow_i = arow_i < M ? arow_i : M - 1;
+  const float* __restrict__ arow = A + arow_i * lda + 16 * lh;
+  // this lane's 16 k of K step k0 (K % 4 == 0: a float4 is all in or all out)
+  auto load_a = [&](int64_t k0, float4(&r)[4]) {
+    const float* q = arow + k0;
+    if (k0 + BK <= K) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const float4*>(q + 4 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        r[j] = k0 + 16 * lh + 4 * j < K ? *reinterpret_cast<const float4*>(q + 4 * j) : f4zero();
+    }
+  };
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  auto compute = [&](const uint16_t* Bs, const float4(&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 h, m, l;
+      split8(a[2 * s], a[2 * s + 1], h, m, l);
+      const bf16x8 ah = __builtin_bit_cast(bf16x8, h);
+      const bf16x8 am = __builtin_bit_cast(bf16x8, m);
+      const bf16x8 al = __builtin_bit_cast(bf16x8, l);
+      const int ch = 2 * lh + s;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int row = 32 * b + li;
+        const bf16x8 bh = xfrag(Bs, row, ch);
+        const bf16x8 bm = xfrag(Bs + BN * XK, row, ch);
+        const bf16x8 bl = xfrag(Bs + 2 * BN * XK, row, ch);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[b], 0, 0, 0);
+      }
+    }
+  };
+
+  QStageB<BN, T> sb;
+  sb.init(n0, npad, kp, tid);
+  uint16_t* buf0 = lds;
+  uint16_t* buf1 = lds + BI;
+  const int nsteps = (int)((K + BK - 1) / BK);
+  float4 a0[4], a1[4];
+  sb.load(Bp, 0, tid);
+  load_a(0, a0);
+  sb.store(buf0, tid);
+  if (nsteps > 1) {
+    sb.load(Bp, BK, tid);
+    load_a(BK, a1);
+  }
+  __syncthreads();
+  // At the top of an iteration (i even): buf0 holds B(i) (visible), sb holds
+  // B(i+1) in flight, a0 = A(i), a1 = A(i+1) in flight.  B(i+1) is written
+  // right after the barrier into the buffer the previous step read; one
+  // barrier per K step.
+  int i = 0;
+  for (; i + 2 <= nsteps; i += 2) {
+    sb.store(buf1, tid);
+    if (i + 2 < nsteps) sb.load(Bp, (int64_t)(i + 2) * BK, tid);
+    compute(buf0, a0);
+    if (i + 2 < nsteps) load_a((int64_t)(i + 2) * BK, a0);
+    __syncthreads();
+    if (i + 2 < nsteps) {
+      sb.store(buf0, tid);
+      if (i + 3 < nsteps) sb.load(Bp, (int64_t)(i + 3) * BK, tid);
+    }
+    compute(buf1, a1);
+    if (i + 3 < nsteps) load_a((int64_t)(i + 3) * BK, a1);
+    __syncthreads();
+  }
+  if (i < nsteps) {
+    compute(buf0, a0);
+    __syncthreads();  // the images are reused by the epilogue
+  }
+
+  // Epilogue: per 32 x 32 block, the wave's accumulator goes through its own
+  // 4 KB of LDS so that rows leave as 16-byte pieces (8 rows x 128 B per
+  // store instruction).
+  const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                   (EPI != MOLCLR_EPI_RELU_MASK ||
+                    (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
+                   ((EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
+                    (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
+  const int64_t mw = m0 + 32 * wave;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t nb = n0 + 32 * b;
+    if (nb >= N) break;  // block-uniform
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, c4 = idx & 7;
+      const int64_t m = mw + row, n = nb + 4 * c4;
+      if (m >= M || n >= N) continue;
+      const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+      float* o = C + m * ldc + n;
+      if (vec && n + 4 <= N) {
+        float4 v = v4;
+        if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+          v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+          if (EPI == MOLCLR_EPI_BIAS_RELU)
+            v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+        }
+        if (EPI == MOLCLR_EPI_RELU_MASK) {
+          const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+          v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                          x.w > 0.f ? v.w : 0.f);
+        }
+        if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+        *reinterpret_cast<float4*>(o) = v;
+      } else {
+        const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+        for (int j = 0; j < 4 && n + j < N; ++j) {
+          float x = e[j];
+          if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+          if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+          if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
+          if (accumulate) x += o[j];
+          o[j] = x;
+        }
+      }
+    }
+    __syncthreads();  // the wave's tile is rewritten by the next block
+  }
+}
+
+// ---------------------------------------------------------------------------
+// "w6": the weight gradient of a Linear, C[m][n] = Σ_k A[k][m] B[k][n] with
+// both operands K-major (K = rows: dW = dY^T X), optionally with the column
+// sums Σ_k A[k][m] (the bias gradient, A = dY) taken from the staged tiles.
+// The q6 decomposition with both operands staged: the 4 waves are stacked
+// along M (32 rows each) over BN = 32 TN columns, so a wave issues TN x 6
+// MFMAs per 16 k from one A fragment (p6's 128 x 64 tile: 2 x 6).  Both
+// operands are split while staging into K-major [3][BK][rows] images read with
+// the transposed LDS read (kmfrag).  One image (54 KB at TN = 5) and one
+// accumulator per output block keep two blocks on a CU, so one block's
+// split-and-stage phase runs beside the other's MFMAs.  Split-K over the rows
+// keeps every fp32 sum short (<= ~40 MFMA accumulations); the partial tiles
+// are summed in a fixed order by k_splitk_reduce (deterministic, no atomics).
+// ---------------------------------------------------------------------------
+constexpr int kW6BM = 128;
+
+template <int TN, bool CS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_w6(
+    const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ part,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int ktiles_per_split, int splits,
+    float* __restrict__ cs_part) {
+  constexpr int T = 256;
+  constexpr int BM = kW6BM, BN = 32 * TN;
+  constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
+  static_assert(4 * 32 * 32 * (int)sizeof(float) <= (AI + BI) * (int)sizeof(uint16_t),
+                "epilogue tiles exceed the LDS image");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[AI + BI];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int ntiles = ntm * ntn;
+  // the blocks of one K slice are consecutive ids, so xcd_remap keeps them --
+  // and the rows they all read -- on one XCD
+  const int id = xcd_remap(blockIdx.x, ntiles * splits);
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+  const int nk_total = (int)((K + BK - 1) / BK);
+  const int kt_beg = split * ktiles_per_split;
+  int kt_end = kt_beg + ktiles_per_split;
+  if (kt_end > nk_total) kt_end = nk_total;
+  const int nsteps = kt_end > kt_beg ? kt_end - kt_beg : 0;
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  using SA = PStageM<BM, T>;
+  using SB = PStageM<BN, T>;
+  SA sa;
+  SB sb;
+  sa.init(A, lda, m0, M, tid);
+  sb.init(B, ldb, n0, N, tid);
+  constexpr int CSN = CS ? SA::PER : 1;
+  float4 cs[CSN];
+#pragma unroll
+  for (int j = 0; j < CSN; ++j) cs[j] = f4zero();
+  auto kof = [&](int step) { return (int64_t)(kt_beg + step) * BK; };
+  const uint16_t* As = lds;
+  const uint16_t* Bs = lds + AI;
+  auto compute = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 ah = kmfrag<BM>(As, 32 * wave, ks, lane);
+      const bf16x8 am = kmfrag<BM>(As + BM * XK, 32 * wave, ks, lane);
+      const bf16x8 al = kmfrag<BM>(As + 2 * BM * XK, 32 * wave, ks, lane);
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const bf16x8 bh = kmfrag<BN>(Bs, 32 * b, ks, lane);
+        const bf16x8 bm = kmfrag<BN>(Bs + BN * XK, 32 * b, ks, lane);
+        const bf16x8 bl = kmfrag<BN>(Bs + 2 * BN * XK, 32 * b, ks, lane);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[b], 0, 0, 0);
+      }
+    }
+  };
+
+  // per K step: split + stage the registers loaded one step earlier, barrier,
+  // issue the next step's loads, MFMAs, barrier (the image is rewritten next)
+  if (nsteps > 0) {
+    sa.load(kof(0), K, tid);
+    sb.load(kof(0), K, tid);
+  }
+  for (int i = 0; i < nsteps; ++i) {
+    if constexpr (CS) sa.colsum_add(cs, tid);
+    sa.store(lds, tid);
+    sb.store(lds + AI, tid);
+    __syncthreads();
+    if (i + 1 < nsteps) {
+      sa.load(kof(i + 1), K, tid);
+      sb.load(kof(i + 1), K, tid);
+    }
+    compute();
+    __syncthreads();
+  }
+
+  if constexpr (CS) {
+    if (n0 == 0 && cs_part != nullptr) {  // block-uniform
+      // a thread's units all share one 4-row group rb = tid % (BM/4): fold
+      // them, then the T/(BM/4) threads of each group in a fixed order
+      constexpr int RB = BM / 4;
+      float4 v = cs[0];
+#pragma unroll
+      for (int j = 1; j < CSN; ++j) v = f4add(v, cs[j]);
+      float4* red = reinterpret_cast<float4*>(lds);
+      red[tid] = v;
+      __syncthreads();
+      if (tid < RB) {
+        float4 t4 = red[tid];
+        for (int q = 1; q < T / RB; ++q) t4 = f4add(t4, red[tid + q * RB]);
+        const float e[4] = {t4.x, t4.y, t4.z, t4.w};
+        for (int j = 0; j < 4; ++j) {
+          const int64_t m = m0 + 4 * tid + j;
+          if (m < M) cs_part[(int64_t)split * M + m] = e[j];
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // partial tile, per 32 x 32 block through the wave's 4 KB of LDS, 16-byte stores
+  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
+  float* P = part + (int64_t)split * M * N;
+  const int64_t mw = m0 + 32 * wave;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t nb = n0 + 32 * b;
+    if (nb >= N) break;  // block-uniform
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, c4 = idx & 7;
+      const int64_t m = mw + row, n = nb + 4 * c4;
+      if (m < M && n < N)
+        *reinterpret_cast<float4*>(P + m * N + n) =
+            *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+    }
+    __syncthreads();
+  }
+}
+
 // planes[p][n][k] (p = hi, mid, lo) of B(k, n), zero beyond (N, K); one
 // thread per (n, k) of the padded [Npad][Kp] grid.
 __global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K, int64_t ldb,
@@ -1308,6 +1694,111 @@ int dispatch_bplanes(int impl, int ak, int epi, dim3 grid, hipStream_t s, const 
                    : dispatch_bplanes_t<1, SPLIT>(ak, epi, grid, s, a);
 }
 
+// Column-tile width 32 TN of the q6 / w6 kernels: the least padding of N
+// (ties: the wider tile), 64 for narrow outputs.
+int wide_tn(int64_t N) {
+  if (N <= 64) return 2;
+  const int64_t p4 = (N + 127) / 128 * 128, p5 = (N + 159) / 160 * 160;
+  return p5 <= p4 ? 5 : 4;
+}
+int64_t q6_blocks(int64_t M, int64_t N) {
+  const int64_t bn = 32 * wide_tn(N);
+  return ((M + kQ6BM - 1) / kQ6BM) * ((N + bn - 1) / bn);
+}
+
+template <int TN, int EPI>
+void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI>), dim3((unsigned)q6_blocks(a.M, a.N)),
+                       dim3(64 * kQ6Waves), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad,
+                       a.ldc, a.bias, a.aux, a.ldaux, a.accumulate);
+}
+
+template <int TN>
+int dispatch_q6(int epi, const Args& a, int64_t npad, hipStream_t s) {
+  switch (epi) {
+    case MOLCLR_EPI_NONE: launch_q6<TN, MOLCLR_EPI_NONE>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS: launch_q6<TN, MOLCLR_EPI_BIAS>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS_RELU: launch_q6<TN, MOLCLR_EPI_BIAS_RELU>(a, npad, s); return 0;
+    case MOLCLR_EPI_RELU_MASK: launch_q6<TN, MOLCLR_EPI_RELU_MASK>(a, npad, s); return 0;
+    default: return -1;
+  }
+}
+
+// a.ldb = kp (the planes' row pitch), a.Bp = the planes
+int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s) {
+  const int tn = wide_tn(a.N);
+  const int rc = tn == 5 ? dispatch_q6<5>(epi, a, npad, s)
+                 : tn == 4 ? dispatch_q6<4>(epi, a, npad, s)
+                           : dispatch_q6<2>(epi, a, npad, s);
+  if (rc) {
+    molclr::set_error("gemm_f32_bplanes: no q6 kernel for epilogue %d", epi);
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+// w6: tile width as q6, K split so that about two blocks per CU run, each
+// split at least 4 K tiles deep.
+struct W6Plan {
+  int tn, splits, kps;
+  int64_t ntiles;
+};
+W6Plan w6_plan(int64_t M, int64_t N, int64_t K) {
+  W6Plan p;
+  p.tn = wide_tn(N);
+  p.ntiles = ((M + kW6BM - 1) / kW6BM) * ((N + 32 * p.tn - 1) / (32 * p.tn));
+  const int64_t nk = (K + BK - 1) / BK;
+  int64_t s = (512 + p.ntiles - 1) / p.ntiles;  // two blocks per CU
+  if (s > nk / 4) s = nk / 4;
+  if (s < 1) s = 1;
+  p.kps = (int)((nk + s - 1) / s);
+  p.splits = (int)((nk + p.kps - 1) / p.kps);
+  return p;
+}
+// shapes w6 takes: 4-aligned rows (float4 staging of K-major operands, float4
+// partial stores) and a long K (the weight-gradient shape)
+bool w6_shape_ok(int64_t M, int64_t N, int64_t K) {
+  return M % 4 == 0 && N % 4 == 0 && K >= 1024 && M * N < (1ll << 28);
+}
+size_t w6_ws_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
+  const W6Plan p = w6_plan(M, N, K);
+  return (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
+}
+
+template <int TN>
+void launch_w6(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
+               int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part) {
+  const dim3 grid((unsigned)(p.ntiles * p.splits));
+  if (cs_part)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true>), grid, dim3(256), 0, s, A, B, part,
+                         M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+  else
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false>), grid, dim3(256), 0, s, A, B,
+                         part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+}
+
+// C (+)= A^T B over K-major A [K][M] (lda) and B [K][N] (ldb); colsum (+)= Σ_k A
+// when non-null.  Partial tiles in the workspace, then the fixed-order reduce.
+int run_w6(const float* A, const float* B, float* C, float* colsum, int64_t M, int64_t N,
+           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int accumulate, void* ws,
+           size_t ws_bytes, hipStream_t s) {
+  const W6Plan p = w6_plan(M, N, K);
+  MOLCLR_REQUIRE_WS(ws_bytes, w6_ws_bytes(M, N, K, colsum != nullptr));
+  float* part = static_cast<float*>(ws);
+  float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
+  if (p.tn == 5) launch_w6<5>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+  else if (p.tn == 4) launch_w6<4>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+  else launch_w6<2>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+  const float* no_f = nullptr;
+  molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>,
+                       dim3((unsigned)molclr::ceil_div(M * N, 256)), dim3(256), 0, s,
+                       static_cast<const float*>(part), p.splits, M, N, C, ldc, no_f, no_f,
+                       (int64_t)0, accumulate, static_cast<const float*>(cs_part), colsum);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
 int64_t planes_npad(int64_t N) { return (N + kPlanesRowPad - 1) / kPlanesRowPad * kPlanesRowPad; }
 int64_t planes_kp(int64_t K) { return (K + BK - 1) / BK * BK; }
 
@@ -1389,7 +1880,12 @@ MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t 
   }
   const int s3 = pick_splits(5, M, N, K, 1, 1);  // the 128-wide weight-gradient tiles
   sp = s3 > sp ? s3 : sp;
-  return sp > 1 ? (size_t)sp * M * N * sizeof(float) + 256 : 0;
+  size_t need = sp > 1 ? (size_t)sp * M * N * sizeof(float) + 256 : 0;
+  if (w6_shape_ok(M, N, K)) {  // both operands K-major: k_gemm_w6 partials
+    const size_t w6 = w6_ws_bytes(M, N, K, false);
+    need = w6 > need ? w6 : need;
+  }
+  return need;
 }
 
 MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
@@ -1419,6 +1915,11 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     return MOLCLR_ERR_UNSUPPORTED;
   }
   const int impl = impl_for(M, N, lda, ldb, a_kmajor, b_kmajor);
+  // a weight-gradient product (both operands K-major, long K): k_gemm_w6
+  if (impl == 5 && a_kmajor && b_kmajor && epilogue == MOLCLR_EPI_NONE && w6_shape_ok(M, N, K) &&
+      lda % 4 == 0 && ldb % 4 == 0 && workspace_bytes >= w6_ws_bytes(M, N, K, false))
+    return run_w6(A, B, C, nullptr, M, N, K, lda, ldb, ldc, accumulate, workspace,
+                  workspace_bytes, s);
   Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate, impl};
   return run_gemm(a, impl, false, a_kmajor, b_kmajor, epilogue, workspace, workspace_bytes, s);
 }
@@ -1487,11 +1988,18 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   if (M == 0 || N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(K > 0 && A && planes && C, "gemm_f32_bplanes: null operand or K == 0");
   const int64_t npad = planes_npad(N), kp = planes_kp(K);
-  int impl = g_bplanes_impl ? g_bplanes_impl : (N >= 512 ? 7 : 5);
+  // automatic: q6 for a row-major A whose row tiles fill the chip, else p6
+  // (64 x 128 for N >= 512, else 64 x 64; split-K when it pays)
+  int impl = g_bplanes_impl;
+  if (impl == 0) impl = (!a_kmajor && q6_blocks(M, N) >= 128) ? 9 : (N >= 512 ? 7 : 5);
+  if (impl == 9 && (a_kmajor || K > kQ6MaxK || 3 * npad * kp >= (1ll << 31) ||
+                    q6_blocks(M, N) >= (1ll << 31)))
+    impl = N >= 512 ? 7 : 5;
   if ((impl == 6 || impl == 8) && a_kmajor) impl = 5;
   Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, impl};
   a.Bp = planes;
   a.bps = npad * kp;
+  if (impl == 9) return run_q6(a, npad, epilogue, molclr::as_stream(stream));
   return run_gemm(a, impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
                   molclr::as_stream(stream));
 }
@@ -1505,6 +2013,10 @@ MOLCLR_API size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_ou
   const size_t fused = sp > 1 ? (size_t)sp * (M * N + M) * sizeof(float) + 256 : 0;
   const size_t cs = molclr_colsum_ws(rows, n_out);
   need = fused > need ? fused : need;
+  if (w6_shape_ok(M, N, K)) {
+    const size_t w6 = w6_ws_bytes(M, N, K, true);
+    need = w6 > need ? w6 : need;
+  }
   return cs > need ? cs : need;
 }
 
@@ -1528,6 +2040,9 @@ MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, f
     return MOLCLR_OK;
   }
   // dW = dy^T x: A = dy (K-major, lda = ld_dy), B = x (K-major, ldb = ld_x)
+  if (g_impl == 5 && w6_shape_ok(n_out, n_in, rows) && ld_dy % 4 == 0 && ld_x % 4 == 0)
+    return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
+                  workspace_bytes, molclr::as_stream(stream));
   if (!db || impl_for(n_out, n_in, ld_dy, ld_x, 1, 1) != 5) {
     int rc = molclr_gemm_f32(dy, x, dW, n_out, n_in, rows, ld_dy, ld_x, n_in, 1, 1, flags,
                              nullptr, nullptr, 0, workspace, workspace_bytes, stream);
@@ -1550,8 +2065,8 @@ MOLCLR_API int molclr_gemm_set_impl(int impl) {
 }
 
 MOLCLR_API int molclr_gemm_bplanes_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl == 0 || (impl >= 5 && impl <= 8),
-                 "gemm_bplanes_set_impl: impl must be 0 (automatic) or 5..8");
+  MOLCLR_REQUIRE(impl == 0 || (impl >= 5 && impl <= 9),
+                 "gemm_bplanes_set_impl: impl must be 0 (automatic) or 5..9");
   g_bplanes_impl = impl;
   return MOLCLR_OK;
 }

@@ -270,17 +270,20 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
             # reference on the fp32-rounded inputs: only the GEMM's own error counts
             ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
             errs = {}
-            for impl in (0, 1, 2, 3, 4, 5, 6, "bplanes"):
-                if impl == "bplanes":
+            for impl in (0, 1, 2, 3, 4, 5, 6, "bplanes", "q6"):
+                if impl in ("bplanes", "q6"):
+                    lib.molclr_gemm_bplanes_set_impl(9 if impl == "q6" else 0)
                     planes = ops.weight_planes(Bt.to(dev), N, K, N if bk else K, bk)
                     out = torch.empty(M, N, device=dev)
                     ws_bytes = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
                     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
                     Ad = A.to(dev)
-                    assert lib.molclr_gemm_f32_bplanes(
+                    rc = lib.molclr_gemm_f32_bplanes(
                         Ad.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
                         M if ak else K, N, ak, 0, None, None, 0, ws.data_ptr(), ws_bytes,
-                        None) == 0
+                        None)
+                    lib.molclr_gemm_bplanes_set_impl(0)
+                    assert rc == 0
                     out = out.double().cpu()
                 else:
                     lib.molclr_gemm_set_impl(impl)
@@ -288,7 +291,7 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
                                    N if bk else K, ak, bk).double().cpu()
                 errs[impl] = (rel(out, ref), (out - ref).abs().max().item(),
                               ((out - ref).abs() / ref.abs().clamp(min=1e-30)).max().item())
-            for impl in (1, 2, 3, 4, 5, 6, "bplanes"):
+            for impl in (1, 2, 3, 4, 5, 6, "bplanes", "q6"):
                 assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
                 assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
                 if positive:
@@ -297,7 +300,7 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
         lib.molclr_gemm_set_impl(prev)
 
 
-@pytest.mark.parametrize("tile", [0, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [0, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("M,N,K", [(1000, 600, 300), (777, 300, 600), (64, 64, 8), (33, 68, 12),
                                    (512, 256, 512), (300, 600, 2000)])
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 0), (1, 1)])
