@@ -1132,21 +1132,30 @@ struct QStageB {
   }
 };
 
-template <int TN, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
+// KG > 1 splits K inside the block: KG groups of 4 waves take the K steps
+// g, g + KG, ... of the same tile, each with its own B ring, and group 0 adds
+// the other groups' sums (in group order, through LDS) before the epilogue.
+// For the narrow products (N = 300: ~960 waves of 32 x 160 for 1024 SIMDs)
+// this puts two waves on every SIMD instead of one.
+template <int TN, int EPI, int KG>
+__global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
     int accumulate) {
-  constexpr int T = 64 * kQ6Waves;
+  constexpr int T = 64 * kQ6Waves;  // threads of one K group
   constexpr int BN = 32 * TN;
   constexpr int BI = 3 * BN * XK;  // bf16 elements per B image
   static_assert(kQ6Waves * 32 * 32 * (int)sizeof(float) <= 2 * BI * (int)sizeof(uint16_t),
                 "epilogue tiles exceed the LDS images");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BI];
+  static_assert(KG == 1 || (kQ6Waves * 32 * BN * (int)sizeof(float) <=
+                            KG * 2 * BI * (int)sizeof(uint16_t)),
+                "group sums exceed the LDS images");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[KG * 2 * BI];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  const int grp = wave / kQ6Waves, wm = wave % kQ6Waves, gt = tid - grp * T;
   const int li = lane & 31, lh = lane >> 5;
 
   const int ntn = (int)((N + BN - 1) / BN);
@@ -1155,7 +1164,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int64_t m0 = (int64_t)(tile / ntn) * kQ6BM;
   const int64_t n0 = (int64_t)(tile % ntn) * BN;
 
-  int64_t arow_i = m0 + 32 * wave + li;
+  int64_t arow_i = m0 + 32 * wm + li;
   arow_i = arow_i < M ? arow_i : M - 1;
   const float* __restrict__ arow = A + arow_i * lda + 16 * lh;
   // this lane's 16 k of K step k0 (K % 4 == 0: a float4 is all in or all out)
@@ -1203,91 +1212,122 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   };
 
   QStageB<BN, T> sb;
-  sb.init(n0, npad, kp, tid);
-  uint16_t* buf0 = lds;
-  uint16_t* buf1 = lds + BI;
+  sb.init(n0, npad, kp, gt);
+  uint16_t* buf0 = lds + grp * 2 * BI;
+  uint16_t* buf1 = buf0 + BI;
   const int nsteps = (int)((K + BK - 1) / BK);
+  const int rounds = (nsteps + KG - 1) / KG;   // group 0's step count; every group runs them
+  const int ns = (nsteps - grp + KG - 1) / KG;  // this group's steps: grp, grp + KG, ...
+  auto kof = [&](int r) { return (int64_t)(grp + KG * r) * BK; };
   float4 a0[4], a1[4];
-  sb.load(Bp, 0, tid);
-  load_a(0, a0);
-  sb.store(buf0, tid);
-  if (nsteps > 1) {
-    sb.load(Bp, BK, tid);
-    load_a(BK, a1);
+  if (ns > 0) {
+    sb.load(Bp, kof(0), gt);
+    load_a(kof(0), a0);
+    sb.store(buf0, gt);
+  }
+  if (ns > 1) {
+    sb.load(Bp, kof(1), gt);
+    load_a(kof(1), a1);
   }
   __syncthreads();
   // At the top of an iteration (i even): buf0 holds B(i) (visible), sb holds
   // B(i+1) in flight, a0 = A(i), a1 = A(i+1) in flight.  B(i+1) is written
   // right after the barrier into the buffer the previous step read; one
-  // barrier per K step.
+  // barrier per K step (per round of the groups).
   int i = 0;
-  for (; i + 2 <= nsteps; i += 2) {
-    sb.store(buf1, tid);
-    if (i + 2 < nsteps) sb.load(Bp, (int64_t)(i + 2) * BK, tid);
-    compute(buf0, a0);
-    if (i + 2 < nsteps) load_a((int64_t)(i + 2) * BK, a0);
+  for (; i + 2 <= rounds; i += 2) {
+    if (i + 1 < ns) sb.store(buf1, gt);
+    if (i + 2 < ns) sb.load(Bp, kof(i + 2), gt);
+    if (i < ns) compute(buf0, a0);
+    if (i + 2 < ns) load_a(kof(i + 2), a0);
     __syncthreads();
-    if (i + 2 < nsteps) {
-      sb.store(buf0, tid);
-      if (i + 3 < nsteps) sb.load(Bp, (int64_t)(i + 3) * BK, tid);
+    if (i + 2 < ns) {
+      sb.store(buf0, gt);
+      if (i + 3 < ns) sb.load(Bp, kof(i + 3), gt);
     }
-    compute(buf1, a1);
-    if (i + 3 < nsteps) load_a((int64_t)(i + 3) * BK, a1);
+    if (i + 1 < ns) compute(buf1, a1);
+    if (i + 3 < ns) load_a(kof(i + 3), a1);
     __syncthreads();
   }
-  if (i < nsteps) {
-    compute(buf0, a0);
-    __syncthreads();  // the images are reused by the epilogue
+  if (i < rounds) {
+    if (i < ns) compute(buf0, a0);
+    __syncthreads();  // the images are reused below
   }
 
-  // Epilogue: per 32 x 32 block, the wave's accumulator goes through its own
-  // 4 KB of LDS so that rows leave as 16-byte pieces (8 rows x 128 B per
-  // store instruction).
+  if constexpr (KG > 1) {
+    // the other groups' sums, added to group 0's in group order
+    float* gw = reinterpret_cast<float*>(lds) + wm * 32 * BN;
+#pragma unroll 1
+    for (int g = 1; g < KG; ++g) {
+      if (grp == g) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gw[(b * 16 + r) * 64 + lane] = acc[b][r];
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[b][r] += gw[(b * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+  }
+
+  // Epilogue (group 0): per 32 x 32 block, the wave's accumulator goes through
+  // its own 4 KB of LDS so that rows leave as 16-byte pieces (8 rows x 128 B
+  // per store instruction).
   const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
                    (EPI != MOLCLR_EPI_RELU_MASK ||
                     (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
                    ((EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
-  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
-  const int64_t mw = m0 + 32 * wave;
+  float* tw = reinterpret_cast<float*>(lds) + wm * 32 * 32;
+  const int64_t mw = m0 + 32 * wm;
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int64_t nb = n0 + 32 * b;
     if (nb >= N) break;  // block-uniform
+    if (grp == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+      for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+    }
     __syncthreads();
+    if (grp == 0) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx >> 3, c4 = idx & 7;
-      const int64_t m = mw + row, n = nb + 4 * c4;
-      if (m >= M || n >= N) continue;
-      const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
-      float* o = C + m * ldc + n;
-      if (vec && n + 4 <= N) {
-        float4 v = v4;
-        if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
-          v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
-          if (EPI == MOLCLR_EPI_BIAS_RELU)
-            v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-        }
-        if (EPI == MOLCLR_EPI_RELU_MASK) {
-          const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
-          v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
-                          x.w > 0.f ? v.w : 0.f);
-        }
-        if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
-        *reinterpret_cast<float4*>(o) = v;
-      } else {
-        const float e[4] = {v4.x, v4.y, v4.z, v4.w};
-        for (int j = 0; j < 4 && n + j < N; ++j) {
-          float x = e[j];
-          if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
-          if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
-          if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
-          if (accumulate) x += o[j];
-          o[j] = x;
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx >> 3, c4 = idx & 7;
+        const int64_t m = mw + row, n = nb + 4 * c4;
+        if (m >= M || n >= N) continue;
+        const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+        float* o = C + m * ldc + n;
+        if (vec && n + 4 <= N) {
+          float4 v = v4;
+          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+            v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                            x.w > 0.f ? v.w : 0.f);
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+          *reinterpret_cast<float4*>(o) = v;
+        } else {
+          const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+          for (int j = 0; j < 4 && n + j < N; ++j) {
+            float x = e[j];
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
+            if (accumulate) x += o[j];
+            o[j] = x;
+          }
         }
       }
     }
@@ -1715,11 +1755,23 @@ int64_t q6_blocks(int64_t M, int64_t N) {
   return ((M + kQ6BM - 1) / kQ6BM) * ((N + bn - 1) / bn);
 }
 
+// in-block K groups: two for narrow products (fewer than 1.5 blocks per CU)
+// with at least 8 K steps, else one
+int q6_groups(int64_t M, int64_t N, int64_t K) {
+  return (q6_blocks(M, N) < 384 && (K + BK - 1) / BK >= 8) ? 2 : 1;
+}
+
 template <int TN, int EPI>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI>), dim3((unsigned)q6_blocks(a.M, a.N)),
-                       dim3(64 * kQ6Waves), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad,
-                       a.ldc, a.bias, a.aux, a.ldaux, a.accumulate);
+  const dim3 grid((unsigned)q6_blocks(a.M, a.N));
+  if (q6_groups(a.M, a.N, a.K) == 2)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, 2>), grid, dim3(2 * 64 * kQ6Waves), 0,
+                         s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.accumulate);
+  else
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, 1>), grid, dim3(64 * kQ6Waves), 0, s,
+                         a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux,
+                         a.ldaux, a.accumulate);
 }
 
 template <int TN>
