@@ -234,6 +234,10 @@ int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, in
  * 128 / 64 wide) tiles with A streamed through registers, one wave per 32
  * rows, for K <= 1024 (a K-major A or a longer K falls back to 5 / 7) */
 int molclr_gemm_bplanes_set_impl(int impl);
+/* K groups per block of the weight-gradient kernel (both operands K-major,
+ * long K): 2 (default) = two 4-wave groups per block, half as many split-K
+ * partial tiles; 1 = one group per block, two blocks per CU. */
+int molclr_gemm_w6_set_groups(int kg);
 
 /* Weight and bias gradients of y = x W^T + b (nn.Linear backward):
  *   dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i],   db[n_out] (+)= Σ_r dy[r][o]

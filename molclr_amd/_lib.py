@@ -48,6 +48,7 @@ SIGNATURES = {
                                 _P, _P, _I64, _P, c_size_t, _P]),
     "molclr_gemm_set_impl": (c_int, [c_int]),
     "molclr_gemm_bplanes_set_impl": (c_int, [c_int]),
+    "molclr_gemm_w6_set_groups": (c_int, [c_int]),
     "molclr_bplanes_bytes": (c_size_t, [_I64, _I64]),
     "molclr_bplanes_make": (c_int, [_P, _I64, _I64, _I64, c_int, _P, _P]),
     "molclr_bplanes_make_batch": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P]),

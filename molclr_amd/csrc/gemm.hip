@@ -1348,23 +1348,35 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 // split-and-stage phase runs beside the other's MFMAs.  Split-K over the rows
 // keeps every fp32 sum short (<= ~40 MFMA accumulations); the partial tiles
 // are summed in a fixed order by k_splitk_reduce (deterministic, no atomics).
+//
+// KG = 2 puts two such 4-wave groups in one block, each with its own image,
+// taking the K steps g, g + 2, ... of the split; group 1 runs one phase behind
+// group 0, so at every barrier one group splits and stages while the other
+// issues MFMAs (the overlap two co-resident blocks gave), and group 0 adds
+// group 1's sums through LDS before the store.  Each split then covers twice
+// the K, so the partial tiles -- written here and read back by
+// k_splitk_reduce -- are half as many.
 // ---------------------------------------------------------------------------
 constexpr int kW6BM = 128;
 
-template <int TN, bool CS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_w6(
+template <int TN, bool CS, int KG>
+__global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_w6(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ part,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int ktiles_per_split, int splits,
     float* __restrict__ cs_part) {
-  constexpr int T = 256;
+  constexpr int T = 256;  // threads of one K group
   constexpr int BM = kW6BM, BN = 32 * TN;
   constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
   static_assert(4 * 32 * 32 * (int)sizeof(float) <= (AI + BI) * (int)sizeof(uint16_t),
                 "epilogue tiles exceed the LDS image");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[AI + BI];
+  static_assert(KG == 1 || (4 * 32 * BN * (int)sizeof(float) <=
+                            KG * (AI + BI) * (int)sizeof(uint16_t)),
+                "group sums exceed the LDS images");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[KG * (AI + BI)];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int grp = tid / T, gt = tid - grp * T;
+  const int lane = tid & 63, wave = gt >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int ntn = (int)((N + BN - 1) / BN);
   const int ntm = (int)((M + BM - 1) / BM);
@@ -1391,15 +1403,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   using SB = PStageM<BN, T>;
   SA sa;
   SB sb;
-  sa.init(A, lda, m0, M, tid);
-  sb.init(B, ldb, n0, N, tid);
+  sa.init(A, lda, m0, M, gt);
+  sb.init(B, ldb, n0, N, gt);
   constexpr int CSN = CS ? SA::PER : 1;
   float4 cs[CSN];
 #pragma unroll
   for (int j = 0; j < CSN; ++j) cs[j] = f4zero();
-  auto kof = [&](int step) { return (int64_t)(kt_beg + step) * BK; };
-  const uint16_t* As = lds;
-  const uint16_t* Bs = lds + AI;
+  // this group's K steps: grp, grp + KG, ... of the split
+  auto kof = [&](int step) { return (int64_t)(kt_beg + grp + KG * step) * BK; };
+  uint16_t* img = lds + grp * (AI + BI);
+  const uint16_t* As = img;
+  const uint16_t* Bs = img + AI;
   auto compute = [&]() {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -1421,29 +1435,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
   };
 
-  // per K step: split + stage the registers loaded one step earlier, barrier,
-  // issue the next step's loads, MFMAs, barrier (the image is rewritten next)
-  if (nsteps > 0) {
-    sa.load(kof(0), K, tid);
-    sb.load(kof(0), K, tid);
+  // per K step, two phases: (even) split + stage the registers loaded one
+  // step earlier; (odd) issue the next step's loads, MFMAs.  A barrier after
+  // every phase; group g runs g phases behind group 0.
+  const int ns = (nsteps - grp + KG - 1) / KG;  // this group's steps
+  const int ns0 = (nsteps + KG - 1) / KG;       // group 0's
+  if (ns > 0) {
+    sa.load(kof(0), K, gt);
+    sb.load(kof(0), K, gt);
   }
-  for (int i = 0; i < nsteps; ++i) {
-    if constexpr (CS) sa.colsum_add(cs, tid);
-    sa.store(lds, tid);
-    sb.store(lds + AI, tid);
-    __syncthreads();
-    if (i + 1 < nsteps) {
-      sa.load(kof(i + 1), K, tid);
-      sb.load(kof(i + 1), K, tid);
+  for (int p = 0; p < 2 * ns0 + KG - 1; ++p) {
+    const int q = p - grp;
+    if (q >= 0 && q < 2 * ns) {
+      const int i = q >> 1;
+      if ((q & 1) == 0) {
+        if constexpr (CS) sa.colsum_add(cs, gt);
+        sa.store(img, gt);
+        sb.store(img + AI, gt);
+      } else {
+        if (i + 1 < ns) {
+          sa.load(kof(i + 1), K, gt);
+          sb.load(kof(i + 1), K, gt);
+        }
+        compute();
+      }
     }
-    compute();
     __syncthreads();
   }
 
   if constexpr (CS) {
     if (n0 == 0 && cs_part != nullptr) {  // block-uniform
       // a thread's units all share one 4-row group rb = tid % (BM/4): fold
-      // them, then the T/(BM/4) threads of each group in a fixed order
+      // them, then the KG*T/(BM/4) threads of each group in a fixed order
       constexpr int RB = BM / 4;
       float4 v = cs[0];
 #pragma unroll
@@ -1453,7 +1476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
       __syncthreads();
       if (tid < RB) {
         float4 t4 = red[tid];
-        for (int q = 1; q < T / RB; ++q) t4 = f4add(t4, red[tid + q * RB]);
+        for (int q = 1; q < KG * T / RB; ++q) t4 = f4add(t4, red[tid + q * RB]);
         const float e[4] = {t4.x, t4.y, t4.z, t4.w};
         for (int j = 0; j < 4; ++j) {
           const int64_t m = m0 + 4 * tid + j;
@@ -1464,7 +1487,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
   }
 
-  // partial tile, per 32 x 32 block through the wave's 4 KB of LDS, 16-byte stores
+  if constexpr (KG > 1) {
+    // the other groups' sums, added to group 0's in group order
+    float* gw = reinterpret_cast<float*>(lds) + wave * 32 * BN;
+#pragma unroll 1
+    for (int g = 1; g < KG; ++g) {
+      if (grp == g) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) gw[(b * 16 + r) * 64 + lane] = acc[b][r];
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[b][r] += gw[(b * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+  }
+
+  // partial tile (group 0), per 32 x 32 block through the wave's 4 KB of LDS,
+  // 16-byte stores
   float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
   float* P = part + (int64_t)split * M * N;
   const int64_t mw = m0 + 32 * wave;
@@ -1472,17 +1518,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   for (int b = 0; b < TN; ++b) {
     const int64_t nb = n0 + 32 * b;
     if (nb >= N) break;  // block-uniform
+    if (grp == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+      for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+    }
     __syncthreads();
+    if (grp == 0) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx >> 3, c4 = idx & 7;
-      const int64_t m = mw + row, n = nb + 4 * c4;
-      if (m < M && n < N)
-        *reinterpret_cast<float4*>(P + m * N + n) =
-            *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx >> 3, c4 = idx & 7;
+        const int64_t m = mw + row, n = nb + 4 * c4;
+        if (m < M && n < N)
+          *reinterpret_cast<float4*>(P + m * N + n) =
+              *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+      }
     }
     __syncthreads();
   }
@@ -1799,20 +1849,25 @@ int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s) {
   return MOLCLR_OK;
 }
 
-// w6: tile width as q6, K split into ~512 blocks (two per CU; 384 / 256
-// measured 8 % / 40 % slower with the partial reduction included), each split
-// at least 4 K tiles deep.
+// w6: tile width as q6, K split over <= 512 4-wave groups (two per CU; 384 / 256
+// single-group blocks measured 8 % / 40 % slower with the partial reduction
+// included), each group at least 4 K tiles deep.  kg = 2 (default): two
+// groups per block, ~256 blocks; kg = 1: ~512 one-group blocks.
+int g_w6_groups = 2;
 struct W6Plan {
-  int tn, splits, kps;
+  int tn, splits, kps, kg;
   int64_t ntiles;
 };
 W6Plan w6_plan(int64_t M, int64_t N, int64_t K) {
   W6Plan p;
   p.tn = wide_tn(N);
+  p.kg = g_w6_groups;
   p.ntiles = ((M + kW6BM - 1) / kW6BM) * ((N + 32 * p.tn - 1) / (32 * p.tn));
   const int64_t nk = (K + BK - 1) / BK;
-  int64_t s = (512 + p.ntiles - 1) / p.ntiles;  // two blocks per CU
-  if (s > nk / 4) s = nk / 4;
+  // whole waves of blocks only: a block past 512 / kg (one per CU at kg = 2)
+  // would run alone after the rest
+  int64_t s = (512 / p.kg) / p.ntiles;
+  if (s > nk / (4 * p.kg)) s = nk / (4 * p.kg);
   if (s < 1) s = 1;
   p.kps = (int)((nk + s - 1) / s);
   p.splits = (int)((nk + p.kps - 1) / p.kps);
@@ -1823,21 +1878,37 @@ W6Plan w6_plan(int64_t M, int64_t N, int64_t K) {
 bool w6_shape_ok(int64_t M, int64_t N, int64_t K) {
   return M % 4 == 0 && N % 4 == 0 && K >= 1024 && M * N < (1ll << 28);
 }
+// sized for the larger of the two group settings (the setting may change
+// between a workspace query and the launch)
 size_t w6_ws_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
-  const W6Plan p = w6_plan(M, N, K);
-  return (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
+  const int keep = g_w6_groups;
+  size_t need = 0;
+  for (int kg = 1; kg <= 2; ++kg) {
+    g_w6_groups = kg;
+    const W6Plan p = w6_plan(M, N, K);
+    const size_t b = (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
+    need = b > need ? b : need;
+  }
+  g_w6_groups = keep;
+  return need;
 }
 
+template <int TN, int KG>
+void launch_w6_kg(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
+                  int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part) {
+  const dim3 grid((unsigned)(p.ntiles * p.splits));
+  if (cs_part)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true, KG>), grid, dim3(256 * KG), 0, s,
+                         A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+  else
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false, KG>), grid, dim3(256 * KG), 0,
+                         s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+}
 template <int TN>
 void launch_w6(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
                int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part) {
-  const dim3 grid((unsigned)(p.ntiles * p.splits));
-  if (cs_part)
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true>), grid, dim3(256), 0, s, A, B, part,
-                         M, N, K, lda, ldb, p.kps, p.splits, cs_part);
-  else
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false>), grid, dim3(256), 0, s, A, B,
-                         part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+  if (p.kg == 2) launch_w6_kg<TN, 2>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+  else launch_w6_kg<TN, 1>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
 }
 
 // C (+)= A^T B over K-major A [K][M] (lda) and B [K][N] (ldb); colsum (+)= Σ_k A
@@ -2123,6 +2194,12 @@ MOLCLR_API int molclr_gemm_get_impl(void) { return g_impl; }
 MOLCLR_API int molclr_gemm_set_impl(int impl) {
   MOLCLR_REQUIRE(impl >= 0 && impl <= 6, "gemm_set_impl: impl must be 0..6");
   g_impl = impl;
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gemm_w6_set_groups(int kg) {
+  MOLCLR_REQUIRE(kg == 1 || kg == 2, "gemm_w6_set_groups: groups must be 1 or 2");
+  g_w6_groups = kg;
   return MOLCLR_OK;
 }
 

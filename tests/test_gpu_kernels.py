@@ -347,11 +347,21 @@ def test_gemm_bplanes(dev, tile, M, N, K, ak, bk):
 @pytest.mark.parametrize("rows,n_out,n_in", [(15278, 300, 600), (15278, 600, 300), (512, 512, 300),
                                              (100, 256, 512), (37, 12, 20), (1000, 30, 64)])
 @pytest.mark.parametrize("acc", [0, 1])
-def test_linear_wgrad(dev, rows, n_out, n_in, acc):
+@pytest.mark.parametrize("groups", [2, 1])
+def test_linear_wgrad(dev, rows, n_out, n_in, acc, groups):
     """dW = dy^T x and db = column sums of dy in one split-bf16 GEMM (fused for
-    4-aligned shapes, gemm + colsum otherwise), against float64."""
+    4-aligned shapes, gemm + colsum otherwise), against float64; both K-group
+    settings of the long-K weight-gradient kernel."""
     from molclr_amd import _lib
     lib = _lib.load()
+    assert lib.molclr_gemm_w6_set_groups(groups) == 0
+    try:
+        _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc)
+    finally:
+        lib.molclr_gemm_w6_set_groups(2)
+
+
+def _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc):
     torch.manual_seed(rows + n_out)
     dy = torch.randn(rows, n_out)
     x = torch.randn(rows, n_in)

@@ -63,6 +63,13 @@ def main():
             lib.molclr_gemm_set_impl(impl)
             tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
             res.append(f"i{impl} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
+        if ak and bk:  # weight gradient: the long-K kernel with one / two K groups
+            lib.molclr_gemm_set_impl(5)
+            for kg in (1, 2):
+                lib.molclr_gemm_w6_set_groups(kg)
+                tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+                res.append(f"w6/kg{kg} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
+            lib.molclr_gemm_w6_set_groups(2)
         if weight:
             for t in (5, 7, 9):
                 lib.molclr_gemm_bplanes_set_impl(t)
