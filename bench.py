@@ -61,6 +61,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--augment", default="host", choices=("host", "device"),
+                   help="host: pre-built resident batch pairs (default); device: both views "
+                        "built inside every step by molclr_mask_views from a resident "
+                        "molecule store")
     return p.parse_args()
 
 
@@ -133,8 +137,25 @@ def main():
     group = torch.distributed.group.WORLD if world > 1 else None
     crit = NTXentLoss(dev, B * world, 0.1, True, group=group)
 
+    store = None
+    if args.augment == "device":
+        # the un-augmented molecules of NB batches resident in HBM; every step
+        # draws B of them and builds both views on the device
+        from molclr_amd.augment import DeviceMoleculeStore
+        import numpy as np
+        nmol = args.batches * B
+        store = DeviceMoleculeStore.from_molecules(
+            SyntheticPairBatches(B, seed=rank * 10**6, shape=cfg["shape"]).molecules(nmol), dev)
+        perm_rng = np.random.default_rng(rank * 10**6 + 3)
+        id_sets = [perm_rng.permutation(nmol)[:B].astype(np.int64) for _ in range(args.batches)]
+        id_sets_dev = [torch.from_numpy(v).to(dev) for v in id_sets]
+
     def step(i):
-        xi, xj = batches[i % len(batches)]
+        if store is not None:
+            k = i % len(id_sets)
+            xi, xj = store.mask_views(id_sets_dev[k], seed=i, host_ids=id_sets[k])
+        else:
+            xi, xj = batches[i % len(batches)]
         for g in (xi, xj):  # rebuild the graph every step: it is part of the work
             g.__dict__.pop("_molclr_graph", None)
         opt.zero_grad()
@@ -221,7 +242,9 @@ def main():
                        f"{cfg['num_layer']}x{cfg['emb_dim']} feat {cfg['feat_dim']}",
                        "global_batch": B * world, "per_gpu_batch": B,
                        "mean_nodes_per_view": round(n_nodes), "mean_edges_per_view": round(n_edges),
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "augment": ("host: pre-built resident batch pairs" if store is None else
+                                   "device: molclr_mask_views inside the step")},
             "final_loss": round(final_loss, 5),
             "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
             "roofline": roofline, "roofline_mfma": roofline_mfma, "cpu_baseline": cpu,

@@ -15,6 +15,8 @@
  *   - PyG 1.6.3 `add_self_loops` + self-loop edge attr, done per layer in
  *       models/ginet_molclr.py:31-37 and models/gcn_molclr.py:64-70
  *       -> molclr_graph_build (once per batch, self loops implicit)
+ *   - MoleculeDataset.__getitem__ node-mask views (dataset/dataset.py:111-145)
+ *       + the DataLoader's PyG collate    -> molclr_mask_views (on device)
  *   - atom embedding   models/ginet_molclr.py:103, models/gcn_molclr.py:144
  *       -> molclr_atom_embed_fwd / _bwd
  *   - GINEConv edge embedding + message + PyG aggr='add'
@@ -107,6 +109,32 @@ int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
                        uint32_t* nbr, uint32_t* nbr_t,
                        int32_t* ecount, int32_t* graph_ptr, int32_t* status,
                        void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
+/* On-device node-mask augmentation + collate: one contrastive view of a batch
+ * of molecules, replacing MoleculeDataset.__getitem__'s masking
+ * (dataset/dataset.py:111-145) and the DataLoader's PyG collate
+ * (Batch.from_data_list).  Per molecule: max(1, floor(N/4)) atoms become
+ * [118, 0]; floor(M/4) bonds are dropped with both directed edges; the kept
+ * edges stay in store order.  The subsets are uniform, drawn from splitmix64
+ * keys of (seed, view, molecule id, item) (restated in oracle/augment_ref.py).
+ * Store (device, int64): x [Ntot,2]; atom_ptr [G+1]; edge_index [2,store_edges]
+ * with molecule-local atom indices, molecule g's bonds as the directed pairs
+ * 2b, 2b+1 for b in [bond_ptr[g], bond_ptr[g+1]); edge_attr [store_edges,2].
+ * mol_ids [batch_size] picks the batch.  Outputs (caller-sized: num_nodes =
+ * Σ N_g, num_edges = Σ 2 (M_g - floor(M_g/4))): x_out [num_nodes,2],
+ * edge_index_out [2,num_edges], edge_attr_out [num_edges,2], batch_out
+ * [num_nodes], ptr_out [batch_size+1] -- the Batch fields.  status [1] i32:
+ * bit 0 molecule id out of range, bit 1 output sizes do not match the batch,
+ * bit 2 store edge index out of its molecule's range (clamped).  view: 0 / 1. */
+size_t molclr_mask_views_workspace_bytes(int64_t batch_size);
+int molclr_mask_views(const int64_t* store_x, const int64_t* store_atom_ptr,
+                      const int64_t* store_edge_index, const int64_t* store_edge_attr,
+                      const int64_t* store_bond_ptr, int64_t store_mols, int64_t store_edges,
+                      const int64_t* mol_ids, int64_t batch_size, uint64_t seed, int view,
+                      int64_t* x_out, int64_t* edge_index_out, int64_t* edge_attr_out,
+                      int64_t* batch_out, int64_t* ptr_out, int64_t num_nodes, int64_t num_edges,
+                      int32_t* status, void* workspace, size_t workspace_bytes,
+                      molclr_stream_t stream);
 
 /* Atom embedding: h[i] = X1[x[i,0]] + X2[x[i,1]]  (ginet_molclr.py:103).
  * x int64 [N,2]; X1 [n1,D], X2 [n2,D]; h [N,D] f32.  Indices are clamped. */

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_size_t, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int64, c_size_t, c_uint64, c_void_p
 from pathlib import Path
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
@@ -30,6 +30,9 @@ SIGNATURES = {
     "molclr_graph_build_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_graph_build": (c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P, _P, c_size_t, _P]),
+    "molclr_mask_views_workspace_bytes": (c_size_t, [_I64]),
+    "molclr_mask_views": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, c_uint64, c_int, _P, _P,
+                                  _P, _P, _P, _I64, _I64, _P, _P, c_size_t, _P]),
     "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "molclr_atom_embed_bwd_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64]),
     "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
