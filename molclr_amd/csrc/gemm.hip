@@ -1590,25 +1590,32 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
                                 const float* __restrict__ aux, int64_t ldaux, int accumulate,
                                 const float* __restrict__ cs_partial, float* __restrict__ colsum) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // Σ_z p[z * stride] in split order, sixteen partials in flight per round trip
+  auto ordered_sum = [splits](const float* __restrict__ p, int64_t stride) {
+    float v = 0.f;
+    int z = 0;
+    for (; z + 16 <= splits; z += 16) {
+      float buf[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) buf[j] = p[(int64_t)(z + j) * stride];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v += buf[j];
+    }
+    float buf[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf[j] = z + j < splits ? p[(int64_t)(z + j) * stride] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (z + j < splits) v += buf[j];
+    return v;
+  };
   if (cs_partial && t < M) {
-    float c = 0.f;
-    for (int z = 0; z < splits; ++z) c += cs_partial[(int64_t)z * M + t];
+    const float c = ordered_sum(cs_partial + t, M);
     colsum[t] = accumulate ? colsum[t] + c : c;
   }
   if (t >= M * N) return;
   int64_t m = t / N, n = t - m * N;
-  // sixteen partials in flight per round trip, summed in split order
-  const int64_t MN = M * N;
-  float v = 0.f;
-  int z = 0;
-  for (; z + 16 <= splits; z += 16) {
-    float buf[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) buf[j] = partial[(int64_t)(z + j) * MN + t];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) v += buf[j];
-  }
-  for (; z < splits; ++z) v += partial[(int64_t)z * MN + t];
+  float v = ordered_sum(partial + t, M * N);
   if (EPI == MOLCLR_EPI_BIAS) v = v + bias[n];
   if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bias[n], 0.f);
   if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;

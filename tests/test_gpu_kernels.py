@@ -75,11 +75,22 @@ def test_graph_build_edge_cases(dev):
 
 
 # ---------------------------------------------------------------------------
-def test_atom_embed(dev):
-    b = batch(64, 1)
+@pytest.mark.parametrize("B,D,types", [(64, 300, "batch"), (512, 300, "batch"),
+                                       (200, 100, "uniform"), (7, 64, "uniform"),
+                                       (1100, 300, "carbon")])
+def test_atom_embed(dev, B, D, types):
+    """Embedding lookup (bit-exact) and its table gradients: partitions with
+    every table row touched (uniform types), one hot row (all carbon), ragged
+    row and column counts."""
+    b = batch(B, 1)
     torch.manual_seed(0)
-    X1 = torch.randn(119, 300)
-    X2 = torch.randn(3, 300)
+    if types == "uniform":
+        b.x = torch.stack([torch.randint(0, 119, (b.x.shape[0],)),
+                           torch.randint(0, 3, (b.x.shape[0],))], 1)
+    elif types == "carbon":
+        b.x = torch.stack([torch.full((b.x.shape[0],), 5), torch.zeros(b.x.shape[0], dtype=torch.long)], 1)
+    X1 = torch.randn(119, D)
+    X2 = torch.randn(3, D)
     ref = X1[b.x[:, 0]] + X2[b.x[:, 1]]
     X1d = X1.to(dev).requires_grad_(True)
     X2d = X2.to(dev).requires_grad_(True)
@@ -87,10 +98,14 @@ def test_atom_embed(dev):
     assert torch.equal(h.cpu(), ref)
     g = torch.randn_like(ref)
     h.backward(g.to(dev))
-    X1c = X1.clone().requires_grad_(True)
-    X2c = X2.clone().requires_grad_(True)
-    (X1c[b.x[:, 0]] + X2c[b.x[:, 1]]).backward(g)
+    X1c = X1.double().requires_grad_(True)
+    X2c = X2.double().requires_grad_(True)
+    (X1c[b.x[:, 0]] + X2c[b.x[:, 1]]).backward(g.double())
     assert rel(X1d.grad, X1c.grad) < TOL and rel(X2d.grad, X2c.grad) < TOL
+    # untouched table rows get exactly zero
+    unused = torch.ones(119, dtype=torch.bool)
+    unused[b.x[:, 0].unique()] = False
+    assert torch.all(X1d.grad.cpu()[unused] == 0)
 
 
 @pytest.mark.parametrize("B,D", [(64, 128), (512, 300), (16, 512)])
