@@ -236,19 +236,34 @@ __global__ void k_ecount_weighted_partial(const float4* __restrict__ g,
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = f4zero();
   if (live) {
-#pragma unroll 2
-    for (int64_t i = beg + r; i < end; i += band) {
-      const int4* ec = reinterpret_cast<const int4*>(ecount + i * 8);
-      const int4 lo = ec[0], hi = ec[1];
-      const float4 v = g[i * d4 + c];
-      const int cnt[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    // eight rows' loads in flight per round trip (a block holds ~5 waves per
+    // CU at c2, so the latency is hidden by ILP, not occupancy); the adds stay
+    // in row order
+    constexpr int U = 8;
+    for (int64_t i0 = beg + r; i0 < end; i0 += U * (int64_t)band) {
+      int4 lo[U], hi[U];
+      float4 v[U];
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        const float w = (float)cnt[s];
-        acc[s].x += w * v.x;
-        acc[s].y += w * v.y;
-        acc[s].z += w * v.z;
-        acc[s].w += w * v.w;
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * band;
+        const bool in = i < end;
+        const int4* ec = reinterpret_cast<const int4*>(ecount + (in ? i : beg) * 8);
+        lo[u] = ec[0];
+        hi[u] = ec[1];
+        v[u] = g[(in ? i : beg) * d4 + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + (int64_t)u * band >= end) break;
+        const int cnt[8] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y, hi[u].z, hi[u].w};
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const float w = (float)cnt[s];
+          acc[s].x += w * v[u].x;
+          acc[s].y += w * v[u].y;
+          acc[s].z += w * v[u].z;
+          acc[s].w += w * v[u].w;
+        }
       }
     }
 #pragma unroll

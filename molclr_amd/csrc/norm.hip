@@ -323,20 +323,35 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
   if (live) {
     float4 mu = mean[c], is = invstd[c], sc, sh;
     bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
-#pragma unroll 4
-    for (int64_t i = beg + r; i < end; i += band) {
-      float4 g = dy[i * d4 + c], x = z[i * d4 + c];
-      if (relu) {
-        g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
-        g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
-        g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
-        g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
+    // eight rows' loads in flight per round trip (few waves per CU here);
+    // the sums stay in row order
+    constexpr int U = 8;
+    for (int64_t i0 = beg + r; i0 < end; i0 += U * (int64_t)band) {
+      float4 gv[U], xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * band;
+        const int64_t ii = i < end ? i : i0;
+        gv[u] = dy[ii * d4 + c];
+        xv[u] = z[ii * d4 + c];
       }
-      s1 = f4add(s1, g);
-      s2.x += g.x * ((x.x - mu.x) * is.x);
-      s2.y += g.y * ((x.y - mu.y) * is.y);
-      s2.z += g.z * ((x.z - mu.z) * is.z);
-      s2.w += g.w * ((x.w - mu.w) * is.w);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + (int64_t)u * band >= end) break;
+        float4 g = gv[u];
+        const float4 x = xv[u];
+        if (relu) {
+          g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
+          g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
+          g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
+          g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
+        }
+        s1 = f4add(s1, g);
+        s2.x += g.x * ((x.x - mu.x) * is.x);
+        s2.y += g.y * ((x.y - mu.y) * is.y);
+        s2.z += g.z * ((x.z - mu.z) * is.z);
+        s2.w += g.w * ((x.w - mu.w) * is.w);
+      }
     }
     red[r * d4 + c] = s1;
     red[(band + r) * d4 + c] = s2;
