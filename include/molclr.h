@@ -449,6 +449,58 @@ int molclr_gin_encoder_bwd(const molclr_gin_encoder* enc, const molclr_gin_encod
                            const float* dh_out, const void* arena, size_t arena_bytes,
                            void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
+/* GCN encoder executor: GCN's node-embedding stack (models/gcn_molclr.py:140-151:
+ * atom embedding, per layer GCNConv -> BatchNorm1d (+ReLU but the last)) in one
+ * host call per direction, issuing the same entry points as the per-op path
+ * (molclr_amd.ops: gemm_w, molclr_gcn_aggregate_fwd/_bwd, batchnorm, gemm) in
+ * its order, so the results are identical.  weight[l] is GCNConv.weight
+ * [D_in, D_out] (not transposed, gcn_molclr.py:45); weight_planes[l] its planes
+ * as the B operand of x W (molclr_bplanes_make(W, D, D, D, b_kmajor=1)),
+ * weight_planes_t[l] as the B operand of dxw W^T (b_kmajor=0). */
+typedef struct molclr_gcn_encoder {
+  int32_t num_layer;
+  int32_t training;
+  int64_t dim;
+  int64_t n_atom;
+  int64_t n_chiral;
+  double momentum, eps;
+  const float* x_embedding1;
+  const float* x_embedding2;
+  const float* weight[MOLCLR_MAX_LAYERS];
+  const float* bias[MOLCLR_MAX_LAYERS];
+  const float* edge_embedding1[MOLCLR_MAX_LAYERS]; /* [5,1] */
+  const float* edge_embedding2[MOLCLR_MAX_LAYERS]; /* [3,1] */
+  const float* bn_weight[MOLCLR_MAX_LAYERS];
+  const float* bn_bias[MOLCLR_MAX_LAYERS];
+  float* bn_running_mean[MOLCLR_MAX_LAYERS];
+  float* bn_running_var[MOLCLR_MAX_LAYERS];
+  int64_t* bn_num_batches_tracked[MOLCLR_MAX_LAYERS];
+  const uint16_t* weight_planes[MOLCLR_MAX_LAYERS];
+  const uint16_t* weight_planes_t[MOLCLR_MAX_LAYERS];
+} molclr_gcn_encoder;
+
+typedef struct molclr_gcn_encoder_grads {
+  float* x_embedding1;
+  float* x_embedding2;
+  float* weight[MOLCLR_MAX_LAYERS];
+  float* bias[MOLCLR_MAX_LAYERS];
+  float* edge_embedding1[MOLCLR_MAX_LAYERS];
+  float* edge_embedding2[MOLCLR_MAX_LAYERS];
+  float* bn_weight[MOLCLR_MAX_LAYERS];
+  float* bn_bias[MOLCLR_MAX_LAYERS];
+} molclr_gcn_encoder_grads;
+
+size_t molclr_gcn_encoder_arena_bytes(int num_layer, int64_t num_nodes, int64_t dim);
+size_t molclr_gcn_encoder_workspace_bytes(int num_layer, int64_t num_nodes, int64_t dim);
+int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* enc, const int64_t* x,
+                           const molclr_device_graph* graph, float* h_out, void* arena,
+                           size_t arena_bytes, void* workspace, size_t workspace_bytes,
+                           molclr_stream_t stream);
+int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* enc, const molclr_gcn_encoder_grads* grads,
+                           const int64_t* x, const molclr_device_graph* graph,
+                           const float* dh_out, const void* arena, size_t arena_bytes,
+                           void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
 /* ---- Benchmark instrumentation (no reference counterpart) -------------------
  * Opt-in kernel timer.  While a kind is enabled, its launches go through
  * hipExtLaunchKernelGGL with a start/stop event pair recorded by the dispatch

@@ -86,6 +86,10 @@ SIGNATURES = {
     "molclr_gin_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
     "molclr_gin_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_gin_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
+    "molclr_gcn_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_gcn_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_gcn_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
+    "molclr_gcn_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_ktimer_start": (c_int, [c_int]),
     "molclr_ktimer_read": (c_int, [c_int, _P, _P]),
     "molclr_ktimer_stop": (c_int, []),
@@ -118,6 +122,23 @@ class GinEncoderGrads(ctypes.Structure):
     _fields_ = [("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
         (f, _L16) for f in ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias",
                             "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias")]
+
+
+class GcnEncoder(ctypes.Structure):
+    """struct molclr_gcn_encoder (include/molclr.h)."""
+    _fields_ = [("num_layer", ctypes.c_int32), ("training", ctypes.c_int32), ("dim", c_int64),
+                ("n_atom", c_int64), ("n_chiral", c_int64), ("momentum", c_double),
+                ("eps", c_double), ("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
+        (f, _L16) for f in ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight",
+                            "bn_bias", "bn_running_mean", "bn_running_var",
+                            "bn_num_batches_tracked", "weight_planes", "weight_planes_t")]
+
+
+class GcnEncoderGrads(ctypes.Structure):
+    """struct molclr_gcn_encoder_grads."""
+    _fields_ = [("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
+        (f, _L16) for f in ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight",
+                            "bn_bias")]
 
 
 class DeviceGraphC(ctypes.Structure):

@@ -205,3 +205,169 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   }
   return MOLCLR_OK;
 }
+
+// ---------------------------------------------------------------------------
+// GCN encoder executor (models/gcn_molclr.py:140-151), same scheme: per layer
+// xw = x W (scratch), z = gcn_aggregate(xw) + bias (BatchNorm input, saved),
+// h = BatchNorm(z) (+ReLU but the last; the next layer's input, saved).
+// Arena: per layer z_l, h_l [N,D], mean_l / invstd_l [D]; then h0 [N,D].
+// Workspace: xw / dxw, dz, dh [N,D] x 3, then the entry points' largest.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct GcnArena {
+  size_t z[MOLCLR_MAX_LAYERS], h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS],
+      invstd[MOLCLR_MAX_LAYERS];
+  size_t h0, total;
+  GcnArena(int L, int64_t N, int64_t D) {
+    size_t used = 0;
+    auto off = [&](size_t count) {
+      const size_t o = used;
+      used += (count + 63) / 64 * 64;
+      return o;
+    };
+    for (int l = 0; l < L; ++l) {
+      z[l] = off(N * D);
+      h[l] = off(N * D);
+      mean[l] = off(D);
+      invstd[l] = off(D);
+    }
+    h0 = off(N * D);
+    total = used * sizeof(float);
+  }
+};
+
+size_t gcn_kernels_ws(int64_t N, int64_t D) {
+  size_t m = 0;
+  auto mx = [&](size_t v) { m = v > m ? v : m; };
+  mx(molclr_gemm_f32_workspace_bytes(N, D, D));  // x W, dxw W^T
+  mx(molclr_gemm_f32_workspace_bytes(D, D, N));  // dW = x^T dxw
+  mx(molclr_batchnorm_workspace_bytes(N, D));
+  mx(molclr_gcn_aggregate_bwd_workspace_bytes(N, D));
+  mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
+  return m;
+}
+size_t gcn_scratch_floats(int64_t N, int64_t D) { return (size_t)N * D * 3; }
+
+int check_gcn(const molclr_gcn_encoder* e, const molclr_device_graph* g) {
+  MOLCLR_REQUIRE(e && g, "gcn_encoder: null encoder / graph");
+  MOLCLR_REQUIRE(e->num_layer >= 1 && e->num_layer <= MOLCLR_MAX_LAYERS,
+                 "gcn_encoder: num_layer %d", e->num_layer);
+  MOLCLR_REQUIRE(e->dim > 0 && e->dim % 4 == 0, "gcn_encoder: dim %lld", (long long)e->dim);
+  MOLCLR_REQUIRE(e->n_atom == MOLCLR_NUM_ATOM_TYPE && e->n_chiral == MOLCLR_NUM_CHIRALITY,
+                 "gcn_encoder: embedding tables must be [%d,D] and [%d,D]",
+                 MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY);
+  for (int l = 0; l < e->num_layer; ++l)
+    MOLCLR_REQUIRE(e->weight_planes[l] && e->weight_planes_t[l] && e->bias[l] &&
+                       e->edge_embedding1[l] && e->edge_embedding2[l] && e->bn_weight[l] &&
+                       e->bn_bias[l],
+                   "gcn_encoder: layer %d: missing planes, bias, edge tables or BatchNorm", l);
+  return MOLCLR_OK;
+}
+
+}  // namespace
+
+MOLCLR_API size_t molclr_gcn_encoder_arena_bytes(int L, int64_t N, int64_t D) {
+  if (L < 1 || L > MOLCLR_MAX_LAYERS) return 0;
+  return GcnArena(L, N, D).total;
+}
+
+MOLCLR_API size_t molclr_gcn_encoder_workspace_bytes(int L, int64_t N, int64_t D) {
+  (void)L;
+  return gcn_scratch_floats(N, D) * sizeof(float) + 256 + gcn_kernels_ws(N, D) + 256;
+}
+
+MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t* x,
+                                      const molclr_device_graph* g, float* h_out, void* arena,
+                                      size_t arena_bytes, void* workspace, size_t workspace_bytes,
+                                      molclr_stream_t stream) {
+  MOLCLR_TRY(check_gcn(e, g));
+  const int L = e->num_layer;
+  const int64_t N = g->num_nodes, D = e->dim;
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && h_out && arena, "gcn_encoder_fwd: null pointer");
+  const GcnArena lay(L, N, D);
+  MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gcn_encoder_workspace_bytes(L, N, D));
+  float* A = (float*)arena;
+  float* xw = (float*)workspace;
+  void* kws = (char*)workspace + molclr::align_up(gcn_scratch_floats(N, D) * sizeof(float), 256);
+  const size_t kws_bytes = gcn_kernels_ws(N, D);
+
+  float* h = A + lay.h0;
+  MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, h, N, D, e->n_atom,
+                                   e->n_chiral, stream));
+  for (int l = 0; l < L; ++l) {
+    float* z = A + lay.z[l];
+    const bool last = l == L - 1;
+    float* y = last ? h_out : A + lay.h[l];
+    // x W, W [in, out] as a K-major B (ops.gemm_w(x, W, N, D, D, D, D, False, True))
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(h, e->weight_planes[l], xw, N, D, D, D, D, 0,
+                                       MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
+                                       stream));
+    MOLCLR_TRY(molclr_gcn_aggregate_fwd(xw, g->rowptr, g->col, g->ecode, g->nbr,
+                                        e->edge_embedding1[l], e->edge_embedding2[l], e->bias[l],
+                                        z, N, D, stream));
+    MOLCLR_TRY(molclr_batchnorm_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                    e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                    A + lay.mean[l], A + lay.invstd[l], N, D, e->momentum, e->eps,
+                                    e->training, last ? 0 : 1, kws, kws_bytes, stream));
+    h = y;
+  }
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
+                                      const molclr_gcn_encoder_grads* gr, const int64_t* x,
+                                      const molclr_device_graph* g, const float* dh_out,
+                                      const void* arena, size_t arena_bytes, void* workspace,
+                                      size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_TRY(check_gcn(e, g));
+  MOLCLR_REQUIRE(gr, "gcn_encoder_bwd: null grads");
+  MOLCLR_REQUIRE(e->training, "gcn_encoder_bwd: backward through eval-mode BatchNorm");
+  const int L = e->num_layer;
+  const int64_t N = g->num_nodes, D = e->dim;
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && dh_out && arena, "gcn_encoder_bwd: null pointer");
+  const GcnArena lay(L, N, D);
+  MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gcn_encoder_workspace_bytes(L, N, D));
+  const float* A = (const float*)arena;
+  float* S = (float*)workspace;
+  float* dxw = S;
+  float* dz = S + N * D;
+  float* dh = S + 2 * N * D;
+  void* kws = (char*)workspace + molclr::align_up(gcn_scratch_floats(N, D) * sizeof(float), 256);
+  const size_t kws_bytes = gcn_kernels_ws(N, D);
+
+  const float* dy = dh_out;
+  for (int l = L - 1; l >= 0; --l) {
+    const float* z = A + lay.z[l];
+    const float* xin = l == 0 ? A + lay.h0 : A + lay.h[l - 1];
+    const bool last = l == L - 1;
+    MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gcn_encoder_bwd: BatchNorm grads needed");
+    MOLCLR_TRY(molclr_batchnorm_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
+                                    A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], N, D,
+                                    last ? 0 : 1, 1, kws, kws_bytes, stream));
+    // ops._GCNConv.backward order: aggregation (dxw, edge tables, bias), dW, dx
+    MOLCLR_TRY(molclr_gcn_aggregate_bwd(dz, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dxw,
+                                        gr->edge_embedding1[l], gr->edge_embedding2[l],
+                                        gr->bias[l], N, D, 1, kws, kws_bytes, stream));
+    if (gr->weight[l])  // dW [in, out] = x^T dxw
+      MOLCLR_TRY(molclr_gemm_f32(xin, dxw, gr->weight[l], D, D, N, D, D, D, 1, 1,
+                                 MOLCLR_EPI_NONE | MOLCLR_EPI_ACCUMULATE, nullptr, nullptr, 0, kws,
+                                 kws_bytes, stream));
+    // dx = dxw W^T  (ops.gemm_w(dxw, W, N, D, D, D, D, False, False))
+    MOLCLR_TRY(molclr_gemm_f32_bplanes(dxw, e->weight_planes_t[l], dh, N, D, D, D, D, 0,
+                                       MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
+                                       stream));
+    dy = dh;
+  }
+  if (gr->x_embedding1 || gr->x_embedding2) {
+    MOLCLR_REQUIRE(gr->x_embedding1 && gr->x_embedding2,
+                   "gcn_encoder_bwd: both atom-embedding grads or neither");
+    MOLCLR_TRY(molclr_atom_embed_bwd(x, dh, gr->x_embedding1, gr->x_embedding2, N, D, e->n_atom,
+                                     e->n_chiral, 1, kws, kws_bytes, stream));
+  }
+  return MOLCLR_OK;
+}

@@ -107,8 +107,29 @@ class GCN(nn.Module):
             nn.Linear(self.feat_dim, self.feat_dim // 2),
         )
 
+    # Run the node-embedding stack through the native encoder executor
+    # (ops.gcn_encoder, one host call per direction) when its BatchNorm and
+    # dropout settings are the ones it implements; else op by op.
+    use_executor = True
+
+    def _executor_ok(self) -> bool:
+        if not self.use_executor or self.num_layer > 16 or self.emb_dim % 4:
+            return False
+        if self.drop_ratio > 0 and self.training:
+            return False
+        bn0 = self.batch_norms[0]
+        return all(bn.track_running_stats and bn.affine and bn.momentum is not None
+                   and bn.training == bn0.training and bn.momentum == bn0.momentum
+                   and bn.eps == bn0.eps for bn in self.batch_norms)
+
     def encode(self, data, graph: DeviceGraph | None = None):
         graph = graph or device_graph(data)
+        if self._executor_ok():
+            params = [self.x_embedding1.weight, self.x_embedding2.weight]
+            for g, bn in zip(self.gnns, self.batch_norms):
+                params += [g.weight, g.bias, g.edge_embedding1.weight, g.edge_embedding2.weight,
+                           bn.weight, bn.bias]
+            return ops.gcn_encoder(data.x, graph, list(self.batch_norms), params), graph
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         for layer in range(self.num_layer):
             h = self.gnns[layer].conv(h, graph)

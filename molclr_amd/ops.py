@@ -772,6 +772,99 @@ class _GINEncoder(torch.autograd.Function):
         return (None, None, None, *ret)
 
 
+GCN_PARAMS_PER_LAYER = 6  # weight, bias, edge_emb1, edge_emb2, bn.W, bn.b
+
+
+class _GCNEncoder(torch.autograd.Function):
+    """GCN's node-embedding stack (gcn_molclr.py:140-151) through
+    molclr_gcn_encoder_fwd / _bwd (encoder.hip): the per-op path's kernels in
+    its order, one host call each way.
+    params: x_embedding1, x_embedding2, then per layer GCN_PARAMS_PER_LAYER."""
+
+    @staticmethod
+    def forward(ctx, x_idx, graph: DeviceGraph, bns, *params):
+        _check(x_idx, *params)
+        L = len(bns)
+        D = params[0].shape[1]
+        x_idx = _c(x_idx.to(torch.long))
+        N = graph.num_nodes
+        training = bool(bns[0].training)
+        enc = _lib.GcnEncoder()
+        enc.num_layer, enc.training, enc.dim = L, int(training), D
+        enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
+        enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
+        enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
+        for l in range(L):
+            W, b, E1, E2, g, bb = params[2 + GCN_PARAMS_PER_LAYER * l:
+                                         2 + GCN_PARAMS_PER_LAYER * (l + 1)]
+            bn = bns[l]
+            enc.weight[l], enc.bias[l] = W.data_ptr(), b.data_ptr()
+            enc.edge_embedding1[l], enc.edge_embedding2[l] = E1.data_ptr(), E2.data_ptr()
+            enc.bn_weight[l], enc.bn_bias[l] = g.data_ptr(), bb.data_ptr()
+            enc.bn_running_mean[l] = bn.running_mean.data_ptr()
+            enc.bn_running_var[l] = bn.running_var.data_ptr()
+            nbt = bn.num_batches_tracked
+            enc.bn_num_batches_tracked[l] = nbt.data_ptr() if training and nbt is not None else None
+            # the planes (and cache entries) _GCNConv's gemm_w calls use
+            enc.weight_planes[l] = weight_planes(W, D, D, D, 1).data_ptr()
+            enc.weight_planes_t[l] = weight_planes(W, D, D, D, 0).data_ptr()
+        dev = x_idx.device
+        arena_bytes = _wsq("molclr_gcn_encoder_arena_bytes", L, N, D)
+        arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)
+        ws_bytes = _wsq("molclr_gcn_encoder_workspace_bytes", L, N, D)
+        ws = _ws(ws_bytes, dev)
+        h = torch.empty(N, D, dtype=torch.float32, device=dev)
+        gc = graph.cstruct()
+        _lib.call("molclr_gcn_encoder_fwd", ctypes.addressof(enc), x_idx.data_ptr(),
+                  ctypes.addressof(gc), h.data_ptr(), arena.data_ptr(), arena_bytes,
+                  ws.data_ptr(), ws_bytes, _stream(x_idx))
+        if _TIMER is not None:
+            for _ in range(L):
+                _TIMER.add("gemm_f32", 2.0 * N * D * D)
+        ctx.enc, ctx.graph, ctx.arena, ctx.arena_bytes = enc, graph, arena, arena_bytes
+        ctx.x_idx, ctx.params, ctx.training = x_idx, params, training
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        if not ctx.training:
+            raise NotImplementedError("molclr_amd: backward through eval-mode BatchNorm")
+        dh = _c(dh)
+        params = ctx.params
+        L = ctx.enc.num_layer
+        N, D = dh.shape
+        owned = all(getattr(p, "_molclr_fused_grad", False) and p.grad is not None
+                    for p in params)
+        if owned:  # FusedAdam: add straight into the flat gradient buffer
+            bufs = [p.grad for p in params]
+            ret = [None] * len(params)
+        else:
+            bufs = [torch.zeros_like(p) for p in params]
+            ret = bufs
+        gr = _lib.GcnEncoderGrads()
+        gr.x_embedding1, gr.x_embedding2 = bufs[0].data_ptr(), bufs[1].data_ptr()
+        names = ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias")
+        for l in range(L):
+            for j, nm in enumerate(names):
+                getattr(gr, nm)[l] = bufs[2 + GCN_PARAMS_PER_LAYER * l + j].data_ptr()
+        ws_bytes = _wsq("molclr_gcn_encoder_workspace_bytes", L, N, D)
+        ws = _ws(ws_bytes, dh.device)
+        gc = ctx.graph.cstruct()
+        _lib.call("molclr_gcn_encoder_bwd", ctypes.addressof(ctx.enc), ctypes.addressof(gr),
+                  ctx.x_idx.data_ptr(), ctypes.addressof(gc), dh.data_ptr(), ctx.arena.data_ptr(),
+                  ctx.arena_bytes, ws.data_ptr(), ws_bytes, _stream(dh))
+        if _TIMER is not None:
+            for _ in range(L):
+                _TIMER.add("gemm_f32", 2 * 2.0 * N * D * D)
+        ctx.arena = None
+        return (None, None, None, *ret)
+
+
+def gcn_encoder(x_idx, graph, bns, params):
+    """GCN.encode through the encoder executor (see _GCNEncoder)."""
+    return _GCNEncoder.apply(x_idx, graph, bns, *params)
+
+
 def gin_encoder(x_idx, graph, bns, params):
     """GINet.encode through the encoder executor (see _GINEncoder)."""
     return _GINEncoder.apply(x_idx, graph, bns, *params)

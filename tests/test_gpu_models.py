@@ -259,3 +259,36 @@ def test_encoder_executor_matches_per_op_path(dev, L, D, B):
     b.eval()
     with torch.no_grad():
         assert torch.equal(a.encode(xi)[0], b.encode(xi)[0])
+
+
+@pytest.mark.parametrize("L,D,B", [(5, 300, 64), (2, 16, 4), (3, 128, 33)])
+def test_gcn_encoder_executor_matches_per_op_path(dev, L, D, B):
+    """molclr_gcn_encoder_fwd/_bwd runs the per-op GCN path's kernels in the
+    same order: node embeddings, every parameter gradient and the BatchNorm
+    running statistics are bit-identical; eval mode too."""
+    from molclr_amd.gcn_molclr import GCN
+    torch.manual_seed(2)
+    a = GCN(L, D, 256).to(dev)
+    b = copy.deepcopy(a)
+    b.use_executor = False
+    assert a._executor_ok() and not b._executor_ok()
+    xi, _ = SyntheticPairBatches(B, seed=L + D + 1).next()
+    xi = xi.to(dev)
+    g = torch.randn(xi.x.shape[0], D, device=dev)
+    outs = []
+    for m in (a, b):
+        h, _ = m.encode(xi)
+        (h * g).sum().backward()
+        outs.append(h.detach())
+    assert torch.equal(outs[0], outs[1])
+    pa, pb = dict(a.named_parameters()), dict(b.named_parameters())
+    for n in pa:
+        assert (pa[n].grad is None) == (pb[n].grad is None), n
+        assert pa[n].grad is None or torch.equal(pa[n].grad, pb[n].grad), n
+    assert sum(p.grad is not None for p in pa.values()) == 2 + 6 * L
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        assert torch.equal(ba, bb), n
+    a.eval()
+    b.eval()
+    with torch.no_grad():
+        assert torch.equal(a.encode(xi)[0], b.encode(xi)[0])
