@@ -341,16 +341,27 @@ __global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __r
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int64_t i = wave; i < N; i += nwaves) {
-    double s = 0.0;
+  // two rows per trip: both rows' loads are issued before either reduction
+  for (int64_t i = wave; i < N; i += 2 * nwaves) {
+    const int64_t i2 = i + nwaves;
+    double s = 0.0, s2 = 0.0;
     for (int c = lane; c < d4; c += 64) {
-      float4 v = g[i * d4 + c];
+      const float4 v = g[i * d4 + c];
+      const float4 v2 = i2 < N ? g[i2 * d4 + c] : f4zero();
       s += ((double)v.x + (double)v.y) + ((double)v.z + (double)v.w);
+      s2 += ((double)v2.x + (double)v2.y) + ((double)v2.z + (double)v2.w);
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    for (int o = 32; o > 0; o >>= 1) {
+      s += __shfl_xor(s, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] += (double)ecount[i * 8 + q] * s;
+    if (i2 < N) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += (double)ecount[i2 * 8 + q] * s2;
+    }
   }
   if (lane < 8) {
     double v = acc[0];
@@ -361,13 +372,32 @@ __global__ __launch_bounds__(256) void k_rowsum_ecount_partial(const float4* __r
   }
 }
 
-__global__ void k_reduce_rowsum_partial(const double* __restrict__ partial, int64_t nparts,
-                                        float* __restrict__ dE1, float* __restrict__ dE2,
-                                        int accumulate) {
-  int q = threadIdx.x;
-  if (q >= 8) return;
-  double acc = 0.0;
-  for (int64_t p = 0; p < nparts; ++p) acc += partial[p * 8 + q];
+// 64 groups of 8 lanes (one per table entry) fold strided partials with four
+// in flight, then a fixed-order tree through LDS (deterministic).
+__global__ __launch_bounds__(512) void k_reduce_rowsum_partial(
+    const double* __restrict__ partial, int64_t nparts, float* __restrict__ dE1,
+    float* __restrict__ dE2, int accumulate) {
+  constexpr int G = 64;
+  __shared__ double red[G][8];
+  const int q = threadIdx.x & 7, r = threadIdx.x >> 3;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int64_t p = r;
+  for (; p + 3 * G < nparts; p += 4 * G) {
+    a0 += partial[p * 8 + q];
+    a1 += partial[(p + G) * 8 + q];
+    a2 += partial[(p + 2 * G) * 8 + q];
+    a3 += partial[(p + 3 * G) * 8 + q];
+  }
+  for (; p < nparts; p += G) a0 += partial[p * 8 + q];
+  double acc = (a0 + a1) + (a2 + a3);
+  red[r][q] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int stride = G / 2; stride > 0; stride >>= 1) {
+    if (r < stride) red[r][q] = acc = acc + red[r + stride][q];
+    __syncthreads();
+  }
+  if (r != 0) return;
   float* o = q < 5 ? (dE1 ? dE1 + q : nullptr) : (dE2 ? dE2 + (q - 5) : nullptr);
   if (o) *o = accumulate ? *o + (float)acc : (float)acc;
 }
@@ -384,7 +414,7 @@ int64_t ecount_parts(int64_t N, int band) {
   if (P < 1) P = 1;
   return P;
 }
-constexpr int64_t kRowsumBlocks = 128;
+constexpr int64_t kRowsumBlocks = 1024;  // 4096 waves, ~2 trips of two rows each at c3
 
 }  // namespace
 
@@ -552,7 +582,7 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
   if (dE1 || dE2) {
     hipLaunchKernelGGL(k_rowsum_ecount_partial, dim3(kRowsumBlocks), dim3(256), 0, s,
                        (const float4*)g, ecount, N, d4, partial);
-    hipLaunchKernelGGL(k_reduce_rowsum_partial, dim3(1), dim3(64), 0, s, partial,
+    hipLaunchKernelGGL(k_reduce_rowsum_partial, dim3(1), dim3(512), 0, s, partial,
                        kRowsumBlocks * 4, dE1, dE2, accumulate);
   }
   MOLCLR_LAUNCHED();
