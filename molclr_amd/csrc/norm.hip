@@ -171,7 +171,7 @@ __global__ void k_bn_stats_partial(const float4* __restrict__ z, int64_t rows, i
 __device__ __forceinline__ void bn_coeffs(float gamma, float beta, float mean, float invstd,
                                           float& scale, float& shift) {
   scale = gamma * invstd;
-  shift = beta - mean * scale;
+  shift = __fmaf_rn(-mean, scale, beta);  // explicit: molclr_gine_aggregate_bn_fwd repeats it
 }
 
 __device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb, float mb, float qb) {
@@ -279,7 +279,7 @@ __global__ void k_bn_saved_coeffs(const float* __restrict__ gamma, const float* 
   shift[c] = sh;
 }
 
-__device__ __forceinline__ float bn_apply1(float z, float sc, float sh) { return z * sc + sh; }
+__device__ __forceinline__ float bn_apply1(float z, float sc, float sh) { return __fmaf_rn(z, sc, sh); }
 
 __global__ __launch_bounds__(kT) void k_bn_apply(const float4* __restrict__ z,
                                                  const float4* __restrict__ scale,
@@ -570,7 +570,7 @@ MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const fl
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_fwd: dim must be a multiple of 4");
   MOLCLR_REQUIRE(!training || rows > 1, "batchnorm_fwd: need more than 1 row when training");
   MOLCLR_REQUIRE(training || (running_mean && running_var), "batchnorm_fwd: eval needs running stats");
-  MOLCLR_REQUIRE(save_mean && save_invstd && y && z, "batchnorm_fwd: null pointer");
+  MOLCLR_REQUIRE(save_mean && save_invstd && z, "batchnorm_fwd: null pointer");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_batchnorm_workspace_bytes(rows, D));
   hipStream_t s = molclr::as_stream(stream);
   molclr::Band b = molclr::make_band(D);
@@ -595,7 +595,7 @@ MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const fl
                        scale, shift);
   }
   int64_t total4 = rows * (D / 4);
-  if (total4 > 0)
+  if (total4 > 0 && y)  // y == NULL: statistics only (the consumer applies them)
     hipLaunchKernelGGL(k_bn_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
                        (const float4*)z, (const float4*)scale, (const float4*)shift, (float4*)y,
                        total4, (int)(D / 4), relu);

@@ -554,3 +554,50 @@ def test_fused_adam_matches_torch_adam(dev):
     for a, b in zip(mine, ref):
         assert rel(a.detach(), b.detach()) < TOL
     assert o_mine.steps_taken == 5
+
+
+@pytest.mark.parametrize("training,relu,D", [(1, 1, 300), (1, 0, 128), (0, 1, 300)])
+def test_gine_aggregate_bn_fwd_matches_materialised(dev, training, relu, D):
+    """molclr_gine_aggregate_bn_fwd(z) == molclr_gine_aggregate_fwd(BatchNorm(z)),
+    bit for bit (the executor's fused path)."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    b = batch(96, 4)
+    g = dgraph(b, dev)
+    N = b.x.shape[0]
+    torch.manual_seed(D + relu)
+    z = (torch.randn(N, D) * 3 + 1).to(dev)
+    gamma = torch.randn(D).to(dev)
+    beta = torch.randn(D).to(dev)
+    rm, rv = torch.randn(D).to(dev), (torch.rand(D) + 0.5).to(dev)
+    y = torch.empty(N, D, device=dev)
+    mean, invstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    wsb = lib.molclr_batchnorm_workspace_bytes(N, D)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    assert lib.molclr_batchnorm_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
+                                    rv.data_ptr(), None, y.data_ptr(), mean.data_ptr(),
+                                    invstd.data_ptr(), N, D, 0.1, 1e-5, training, relu,
+                                    ws.data_ptr(), wsb, None) == 0
+    Ec = torch.randn(15, D).to(dev)
+    ref = torch.empty(N, D, device=dev)
+    out = torch.empty(N, D, device=dev)
+    assert lib.molclr_gine_aggregate_fwd(y.data_ptr(), g.rowptr.data_ptr(), g.col.data_ptr(),
+                                         g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                                         ref.data_ptr(), N, D, None) == 0
+    assert lib.molclr_gine_aggregate_bn_fwd(z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                            gamma.data_ptr(), beta.data_ptr(), relu,
+                                            g.rowptr.data_ptr(), g.col.data_ptr(),
+                                            g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                                            out.data_ptr(), N, D, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    # statistics only (y = NULL) gives the same saved statistics
+    m2, i2 = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    rm2, rv2 = torch.randn(D).to(dev), (torch.rand(D) + 0.5).to(dev)
+    if not training:
+        rm2, rv2 = rm, rv
+    assert lib.molclr_batchnorm_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                    rm2.data_ptr(), rv2.data_ptr(), None, None, m2.data_ptr(),
+                                    i2.data_ptr(), N, D, 0.1, 1e-5, training, relu,
+                                    ws.data_ptr(), wsb, None) == 0
+    assert torch.equal(m2, mean) and torch.equal(i2, invstd)
