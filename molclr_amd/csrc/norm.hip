@@ -426,7 +426,17 @@ __global__ void k_pool_fwd(const float4* __restrict__ h, const int32_t* __restri
   int c = (int)(t - g * d4);
   int32_t beg = ptr[g], end = ptr[g + 1];
   float4 acc = f4zero();
-  for (int32_t i = beg; i < end; ++i) acc = f4add(acc, h[(int64_t)i * d4 + c]);
+  // eight rows' loads in flight (a graph's ~30 rows were a serial load chain);
+  // the adds stay in row order
+  int32_t i = beg;
+  for (; i + 8 <= end; i += 8) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = h[(int64_t)(i + u) * d4 + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = f4add(acc, v[u]);
+  }
+  for (; i < end; ++i) acc = f4add(acc, h[(int64_t)i * d4 + c]);
   if (mode == 0) {
     float cnt = (float)(end - beg > 1 ? end - beg : 1);
     acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
