@@ -449,7 +449,7 @@ int64_t atom_parts(int64_t N) {
   return P;
 }
 int64_t ecount_parts(int64_t N, int band) {
-  int64_t P = molclr::ceil_div(N, (int64_t)band * 16);
+  int64_t P = molclr::ceil_div(N, (int64_t)band * 8);
   if (P > 1024) P = 1024;
   if (P < 1) P = 1;
   return P;
