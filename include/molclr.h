@@ -323,6 +323,31 @@ int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
                          int64_t rows, int64_t dim, int relu, int accumulate, void* workspace,
                          size_t workspace_bytes, molclr_stream_t stream);
 
+/* Segmented BatchNorm: the rows are `nseg` consecutive segments of
+ * seg_rows[s] rows (host array), each normalised with its own batch statistics
+ * -- the reference's two encoder calls per step (molclr.py:57,60) run as ONE
+ * pass over both views -- and the running statistics updated once per
+ * segment in segment order (num_batches_tracked += nseg).  Every segment's
+ * outputs are bit-identical to a molclr_batchnorm_fwd / _bwd call over its
+ * rows alone.  save_mean / save_invstd are [nseg, D].  dgamma / dbeta are the
+ * sums over the segments (in segment order).  dtype: MOLCLR_DTYPE_F32 or
+ * MOLCLR_DTYPE_BF16 storage of z / y / dy / dz (statistics always fp32). */
+#define MOLCLR_MAX_SEGMENTS 8
+enum { MOLCLR_DTYPE_F32 = 0, MOLCLR_DTYPE_BF16 = 1 };
+size_t molclr_batchnorm_seg_workspace_bytes(int nseg, const int64_t* seg_rows, int64_t dim);
+int molclr_batchnorm_seg_fwd(const void* z, const float* gamma, const float* beta,
+                             float* running_mean, float* running_var,
+                             int64_t* num_batches_tracked, void* y, float* save_mean,
+                             float* save_invstd, int nseg, const int64_t* seg_rows, int64_t dim,
+                             int dtype, double momentum, double eps, int training, int relu,
+                             void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const float* gamma,
+                             const float* beta, const float* save_mean, const float* save_invstd,
+                             void* dz, float* dgamma, float* dbeta, int nseg,
+                             const int64_t* seg_rows, int64_t dim, int dtype, int relu,
+                             int accumulate, void* workspace, size_t workspace_bytes,
+                             molclr_stream_t stream);
+
 /* Segment pooling over graph_ptr (PyG global_mean_pool / global_add_pool):
  * mode 0 = mean (sum / max(count,1)), 1 = add. */
 int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr, float* out,

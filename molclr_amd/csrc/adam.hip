@@ -40,25 +40,32 @@ void timer_record(int kind, hipEvent_t e0, hipEvent_t e1) {
 
 namespace {
 
+// torch.optim.Adam's multi-tensor (GPU) update, op for op:
+//   g' = g + wd p;  m = lerp(m, g', 1 - b1);  v = v b2 + (1 - b2) g'^2;
+//   p = p + (-lr / bc1) (m / (sqrt(v) / sqrt(bc2) + eps))
+// with bc1 = 1 - b1^t, bc2 = 1 - b2^t, step_size and sqrt(bc2) evaluated in
+// double (torch does them in Python floats on the host) and rounded to fp32
+// once, as torch's scalar arguments are.  The step count t lives on the device.
 __global__ void k_adam_step(float4* __restrict__ p, const float4* __restrict__ g,
                             float4* __restrict__ m, float4* __restrict__ v, int64_t n4,
                             const float* __restrict__ lr_ptr, const int32_t* __restrict__ step_ptr,
-                            float b1, float b2, float eps, float wd) {
+                            double b1, double b2, float eps, float wd) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n4) return;
   const int step = *step_ptr + 1;  // the counter is advanced by k_adam_tick afterwards
-  const float lr = *lr_ptr;
-  const float bc1 = 1.f - powf(b1, (float)step);
-  const float bc2s = sqrtf(1.f - powf(b2, (float)step));
-  const float step_size = lr / bc1;
+  const double bc1 = 1.0 - pow(b1, (double)step);
+  const double bc2 = 1.0 - pow(b2, (double)step);
+  const float neg_step_size = (float)(-((double)*lr_ptr / bc1));
+  const float bc2s = (float)sqrt(bc2);
+  const float w1 = (float)(1.0 - b1), fb2 = (float)b2, w2 = (float)(1.0 - b2);
   float4 pp = p[t], gg = g[t], mm = m[t], vv = v[t];
-#define MOLCLR_ADAM_LANE(c)                                   \
-  {                                                           \
-    float gr = gg.c + wd * pp.c;                              \
-    mm.c = b1 * mm.c + (1.f - b1) * gr;                       \
-    vv.c = b2 * vv.c + (1.f - b2) * gr * gr;                  \
-    float den = sqrtf(vv.c) / bc2s + eps;                     \
-    pp.c = pp.c - step_size * (mm.c / den);                   \
+#define MOLCLR_ADAM_LANE(c)                                                   \
+  {                                                                           \
+    const float gr = gg.c + wd * pp.c;                                        \
+    mm.c = fabsf(w1) < 0.5f ? mm.c + w1 * (gr - mm.c) : gr - (gr - mm.c) * (1.f - w1); \
+    vv.c = vv.c * fb2 + w2 * gr * gr;                                         \
+    const float den = sqrtf(vv.c) / bc2s + eps;                               \
+    pp.c = pp.c + neg_step_size * (mm.c / den);                               \
   }
   MOLCLR_ADAM_LANE(x)
   MOLCLR_ADAM_LANE(y)
@@ -89,7 +96,7 @@ MOLCLR_API int molclr_adam_step(float* param, const float* grad, float* exp_avg,
   if (n4 > 0)
     hipLaunchKernelGGL(k_adam_step, dim3(molclr::ceil_div(n4, 256)), dim3(256), 0, s,
                        (float4*)param, (const float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
-                       n4, lr, step, (float)beta1, (float)beta2, (float)eps, (float)weight_decay);
+                       n4, lr, step, beta1, beta2, (float)eps, (float)weight_decay);
   hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;

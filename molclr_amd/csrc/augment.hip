@@ -29,7 +29,18 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// key of item i of one (view, kind, molecule) stream; kind 0 = atoms, 1 = bonds
+// Stream of one (seed, view, kind, molecule): a chain of splitmix64 over the
+// four fields, so distinct tuples give unrelated streams (a flat
+// seed ^ (2 view + kind) would make view 1 at seed s replay view 0 at s ^ 2).
+// kind 0 = atoms, 1 = bonds.
+__device__ __forceinline__ uint64_t subset_stream(uint64_t seed, int view, int kind, int64_t id) {
+  uint64_t z = splitmix64(seed);
+  z = splitmix64(z ^ (uint64_t)view);
+  z = splitmix64(z ^ (uint64_t)kind);
+  return splitmix64(z ^ (uint64_t)id);
+}
+
+// key of item i of one stream
 __device__ __forceinline__ uint64_t item_key(uint64_t stream, int64_t i) {
   return splitmix64(stream ^ (uint64_t)i);
 }
@@ -129,9 +140,8 @@ __global__ __launch_bounds__(64 * kMolsPerBlock) void k_mask_views(
   if (aoff + n > num_nodes || eoff + 2 * (M - M / 4) > num_edges) return;
   const int64_t k_atoms = n > 0 ? (n / 4 > 1 ? n / 4 : 1) : 0;  // max(1, floor(0.25 N))
   const int64_t k_bonds = M / 4;                                // floor(0.25 M)
-  const uint64_t vs = splitmix64(seed ^ (uint64_t)(2 * view));
-  const uint64_t atom_stream = splitmix64(vs ^ (uint64_t)id);
-  const uint64_t bond_stream = splitmix64(splitmix64(seed ^ (uint64_t)(2 * view + 1)) ^ (uint64_t)id);
+  const uint64_t atom_stream = subset_stream(seed, view, 0, id);
+  const uint64_t bond_stream = subset_stream(seed, view, 1, id);
 
   for (int64_t i = lane; i < n; i += 64) {
     const bool masked = chosen(atom_stream, n, k_atoms, i);

@@ -127,6 +127,47 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
+// ---------------------------------------------------------------------------
+// Storage types of node-feature matrices.  Kernels over [rows, D] matrices are
+// templated on one of these: a "column unit" is 4 consecutive elements, read
+// and written as a float4 of fp32 values (fp32 storage: one 16-byte access;
+// bf16 storage: one 8-byte access, widened / rounded to nearest even).  All
+// arithmetic stays fp32 (the c5 configuration's bf16 storage, fp32 math).
+// ---------------------------------------------------------------------------
+struct StF32 {
+  typedef float T;
+  static constexpr int kBytes = 4;
+  __device__ __forceinline__ static float4 ld(const T* __restrict__ p, int64_t unit) {
+    return reinterpret_cast<const float4*>(p)[unit];
+  }
+  __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
+    reinterpret_cast<float4*>(p)[unit] = v;
+  }
+};
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t bits16) {
+  return __uint_as_float(bits16 << 16);
+}
+// round to nearest even (v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ uint32_t f32x2_to_bf16x2(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+struct StBF16 {
+  typedef uint16_t T;
+  static constexpr int kBytes = 2;
+  __device__ __forceinline__ static float4 ld(const T* __restrict__ p, int64_t unit) {
+    const uint2 u = reinterpret_cast<const uint2*>(p)[unit];
+    return make_float4(bf16_to_f32(u.x & 0xFFFFu), bf16_to_f32(u.x >> 16),
+                       bf16_to_f32(u.y & 0xFFFFu), bf16_to_f32(u.y >> 16));
+  }
+  __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
+    reinterpret_cast<uint2*>(p)[unit] = make_uint2(f32x2_to_bf16x2(v.x, v.y), f32x2_to_bf16x2(v.z, v.w));
+  }
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

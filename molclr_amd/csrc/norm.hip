@@ -100,7 +100,34 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_colsum_final(
 
 // ---------------------------------------------------------------------------
 // BatchNorm
+//
+// Segmented: the rows are `nseg` consecutive segments (the two contrastive
+// views of a step run through one encoder pass), each normalised with its
+// OWN batch statistics -- exactly as the reference's two separate forward
+// calls (molclr.py:57,60) -- and the running statistics are updated once per
+// segment, in segment order.  A segment is partitioned exactly as a
+// one-segment call over its rows would be, so every per-segment result is
+// bit-identical to that call.  Storage of z / y / dy / dz is fp32 or bf16
+// (StF32 / StBF16); the statistics are always fp32.
 // ---------------------------------------------------------------------------
+struct Segs {
+  int n;
+  int64_t row0[MOLCLR_MAX_SEGMENTS + 1];   // segment s: rows [row0[s], row0[s+1])
+  int64_t part0[MOLCLR_MAX_SEGMENTS + 1];  // its partitions: [part0[s], part0[s+1])
+  int64_t rpp[MOLCLR_MAX_SEGMENTS];        // rows per partition
+};
+
+__device__ __forceinline__ int seg_of_part(const Segs& sg, int64_t b) {
+  int s = 0;
+  while (s + 1 < sg.n && b >= sg.part0[s + 1]) ++s;
+  return s;
+}
+__device__ __forceinline__ int seg_of_row(const Segs& sg, int64_t i) {
+  int s = 0;
+  while (s + 1 < sg.n && i >= sg.row0[s + 1]) ++s;
+  return s;
+}
+
 struct Welford4 {
   float n;
   float4 mean, m2;
@@ -125,22 +152,24 @@ __device__ __forceinline__ void chan_merge(float& na, float4& ma, float4& qa, fl
 }
 
 // partial layout: mean [P][d4] float4, m2 [P][d4] float4, n [P]
-__global__ void k_bn_stats_partial(const float4* __restrict__ z, int64_t rows, int d4, int band,
-                                   int64_t rows_per_part, float4* __restrict__ pmean,
-                                   float4* __restrict__ pm2, float* __restrict__ pn) {
+template <typename St>
+__global__ void k_bn_stats_partial(const typename St::T* __restrict__ z, int d4, int band, Segs sg,
+                                   float4* __restrict__ pmean, float4* __restrict__ pm2,
+                                   float* __restrict__ pn) {
   extern __shared__ __attribute__((aligned(16))) float4 red[];  // [2][band][d4]
   const int tid = threadIdx.x;
   const bool live = tid < band * d4;
   const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
-  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
-  int64_t end = beg + rows_per_part;
-  if (end > rows) end = rows;
+  const int s = seg_of_part(sg, blockIdx.x);
+  const int64_t beg = sg.row0[s] + (blockIdx.x - sg.part0[s]) * sg.rpp[s];
+  int64_t end = beg + sg.rpp[s];
+  if (end > sg.row0[s + 1]) end = sg.row0[s + 1];
   float n = 0.f;
   float4 mean = f4zero(), m2 = f4zero();
   if (live) {
 #pragma unroll 4
     for (int64_t i = beg + r; i < end; i += band) {
-      float4 x = z[i * d4 + c];
+      float4 x = St::ld(z, i * d4 + c);
       n += 1.f;
       float inv = 1.f / n;
       float4 d = make_float4(x.x - mean.x, x.y - mean.y, x.z - mean.z, x.w - mean.w);
@@ -189,111 +218,115 @@ __device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb
   n = nn;
 }
 
-// Per column: Chan-merge the P partials (kRedLanes strided lanes, four
-// partials in flight, then a fixed-order tree over the lanes), update running
-// stats, write save_mean/save_invstd and the apply coefficients.
+// Per segment and column: Chan-merge the segment's partials (kRedLanes
+// strided lanes, four partials in flight, then a fixed-order tree over the
+// lanes), update the running stats (segments in order), write save_mean /
+// save_invstd and the apply coefficients [seg][D].
 // grid = ceil(D/kRedCols), block = kRedCols * kRedLanes.
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
     const float* __restrict__ pmean, const float* __restrict__ pm2, const float* __restrict__ pn,
-    int64_t P, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
+    Segs sg, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
     float* __restrict__ running_mean, float* __restrict__ running_var,
     float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ scale,
     float* __restrict__ shift, float momentum, float eps, int64_t* __restrict__ nbt) {
   __shared__ float rn[kRedLanes][kRedCols], rm[kRedLanes][kRedCols], rq[kRedLanes][kRedCols];
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += sg.n;  // num_batches_tracked
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < D) {
-    int64_t p = rl;
-    for (; p + 3 * kRedLanes < P; p += 4 * kRedLanes) {
-      float bn[4], bm[4], bq[4];
+  for (int s = 0; s < sg.n; ++s) {
+    const int64_t P = sg.part0[s + 1] - sg.part0[s];
+    const float* sm = pmean + sg.part0[s] * D;
+    const float* sq = pm2 + sg.part0[s] * D;
+    const float* sn = pn + sg.part0[s];
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    if (c < D) {
+      int64_t p = rl;
+      for (; p + 3 * kRedLanes < P; p += 4 * kRedLanes) {
+        float bn[4], bm[4], bq[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t q = p + u * kRedLanes;
-        bn[u] = pn[q];
-        bm[u] = pmean[q * D + c];
-        bq[u] = pm2[q * D + c];
+        for (int u = 0; u < 4; ++u) {
+          const int64_t q = p + u * kRedLanes;
+          bn[u] = sn[q];
+          bm[u] = sm[q * D + c];
+          bq[u] = sq[q * D + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) chan1(n, mean, m2, bn[u], bm[u], bq[u]);
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) chan1(n, mean, m2, bn[u], bm[u], bq[u]);
+      for (; p < P; p += kRedLanes) chan1(n, mean, m2, sn[p], sm[p * D + c], sq[p * D + c]);
     }
-    for (; p < P; p += kRedLanes) chan1(n, mean, m2, pn[p], pmean[p * D + c], pm2[p * D + c]);
-  }
-  rn[rl][cl] = n;
-  rm[rl][cl] = mean;
-  rq[rl][cl] = m2;
-  __syncthreads();
-#pragma unroll
-  for (int stride = kRedLanes / 2; stride > 0; stride >>= 1) {
-    if (rl < stride) {
-      chan1(n, mean, m2, rn[rl + stride][cl], rm[rl + stride][cl], rq[rl + stride][cl]);
-      rn[rl][cl] = n;
-      rm[rl][cl] = mean;
-      rq[rl][cl] = m2;
-    }
+    __syncthreads();  // the previous segment's tree is done with the arrays
+    rn[rl][cl] = n;
+    rm[rl][cl] = mean;
+    rq[rl][cl] = m2;
     __syncthreads();
+#pragma unroll
+    for (int stride = kRedLanes / 2; stride > 0; stride >>= 1) {
+      if (rl < stride) {
+        chan1(n, mean, m2, rn[rl + stride][cl], rm[rl + stride][cl], rq[rl + stride][cl]);
+        rn[rl][cl] = n;
+        rm[rl][cl] = mean;
+        rq[rl][cl] = m2;
+      }
+      __syncthreads();
+    }
+    if (rl == 0 && c < D) {
+      float var = m2 / n;
+      float invstd = 1.0f / sqrtf(var + eps);
+      save_mean[s * D + c] = mean;
+      save_invstd[s * D + c] = invstd;
+      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      if (running_var) {
+        float unbiased = n > 1.f ? m2 / (n - 1.f) : var;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+      }
+      float sc, sh;
+      bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
+      scale[s * D + c] = sc;
+      shift[s * D + c] = sh;
+    }
   }
-  if (rl != 0 || c >= D) return;
-  float var = m2 / n;
-  float invstd = 1.0f / sqrtf(var + eps);
-  save_mean[c] = mean;
-  save_invstd[c] = invstd;
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-  if (running_var) {
-    float unbiased = n > 1.f ? m2 / (n - 1.f) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
-  }
-  float sc, sh;
-  bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
-  scale[c] = sc;
-  shift[c] = sh;
 }
 
+// eval: running statistics, the same coefficients for every segment
 __global__ void k_bn_eval_coeffs(const float* __restrict__ gamma, const float* __restrict__ beta,
                                  const float* __restrict__ running_mean,
-                                 const float* __restrict__ running_var, int64_t D, float eps,
-                                 float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                                 float* __restrict__ scale, float* __restrict__ shift) {
+                                 const float* __restrict__ running_var, int64_t D, int nseg,
+                                 float eps, float* __restrict__ save_mean,
+                                 float* __restrict__ save_invstd, float* __restrict__ scale,
+                                 float* __restrict__ shift) {
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= D) return;
   float mean = running_mean[c];
   float invstd = 1.0f / sqrtf(running_var[c] + eps);
-  if (save_mean) save_mean[c] = mean;
-  if (save_invstd) save_invstd[c] = invstd;
   float sc, sh;
   bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
-  scale[c] = sc;
-  shift[c] = sh;
-}
-
-__global__ void k_bn_saved_coeffs(const float* __restrict__ gamma, const float* __restrict__ beta,
-                                  const float* __restrict__ save_mean,
-                                  const float* __restrict__ save_invstd, int64_t D,
-                                  float* __restrict__ scale, float* __restrict__ shift) {
-  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float sc, sh;
-  bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, save_mean[c], save_invstd[c], sc, sh);
-  scale[c] = sc;
-  shift[c] = sh;
+  for (int s = 0; s < nseg; ++s) {
+    if (save_mean) save_mean[s * D + c] = mean;
+    if (save_invstd) save_invstd[s * D + c] = invstd;
+    scale[s * D + c] = sc;
+    shift[s * D + c] = sh;
+  }
 }
 
 __device__ __forceinline__ float bn_apply1(float z, float sc, float sh) { return __fmaf_rn(z, sc, sh); }
 
-__global__ __launch_bounds__(kT) void k_bn_apply(const float4* __restrict__ z,
+template <typename St>
+__global__ __launch_bounds__(kT) void k_bn_apply(const typename St::T* __restrict__ z,
                                                  const float4* __restrict__ scale,
                                                  const float4* __restrict__ shift,
-                                                 float4* __restrict__ y, int64_t total4, int d4,
-                                                 int relu) {
+                                                 typename St::T* __restrict__ y, int64_t total4,
+                                                 int d4, int relu, Segs sg) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total4) return;
-  int c = (int)(t % d4);
-  float4 v = z[t], sc = scale[c], sh = shift[c];
+  const int64_t i = t / d4;
+  const int c = (int)(t - i * d4);
+  const int s = seg_of_row(sg, i);
+  float4 v = St::ld(z, t), sc = scale[s * d4 + c], sh = shift[s * d4 + c];
   float4 o = make_float4(bn_apply1(v.x, sc.x, sh.x), bn_apply1(v.y, sc.y, sh.y),
                          bn_apply1(v.z, sc.z, sh.z), bn_apply1(v.w, sc.w, sh.w));
   if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
-  y[t] = o;
+  St::st(y, t, o);
 }
 
 // BN backward pass 1: per-column Σ dyr and Σ dyr * xhat (fixed order).
@@ -307,21 +340,24 @@ __device__ __forceinline__ void bn_coeffs4(const float* gamma, const float* beta
   bn_coeffs(g.w, b.w, mu.w, is.w, sc.w, sh.w);
 }
 
-__global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __restrict__ z,
+template <typename St>
+__global__ void k_bn_bwd_partial(const typename St::T* __restrict__ dy,
+                                 const typename St::T* __restrict__ z,
                                  const float4* __restrict__ mean, const float4* __restrict__ invstd,
                                  const float* __restrict__ gamma, const float* __restrict__ beta,
-                                 int64_t rows, int d4, int band, int64_t rows_per_part, int relu,
-                                 float4* __restrict__ p1, float4* __restrict__ p2) {
+                                 int d4, int band, Segs sg, int relu, float4* __restrict__ p1,
+                                 float4* __restrict__ p2) {
   extern __shared__ __attribute__((aligned(16))) float4 red[];  // [2][band][d4]
   const int tid = threadIdx.x;
   const bool live = tid < band * d4;
   const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
-  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
-  int64_t end = beg + rows_per_part;
-  if (end > rows) end = rows;
+  const int s = seg_of_part(sg, blockIdx.x);
+  const int64_t beg = sg.row0[s] + (blockIdx.x - sg.part0[s]) * sg.rpp[s];
+  int64_t end = beg + sg.rpp[s];
+  if (end > sg.row0[s + 1]) end = sg.row0[s + 1];
   float4 s1 = f4zero(), s2 = f4zero();
   if (live) {
-    float4 mu = mean[c], is = invstd[c], sc, sh;
+    float4 mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
     bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
     // eight rows' loads in flight per round trip (few waves per CU here);
     // the sums stay in row order
@@ -332,8 +368,8 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * band;
         const int64_t ii = i < end ? i : i0;
-        gv[u] = dy[ii * d4 + c];
-        xv[u] = z[ii * d4 + c];
+        gv[u] = St::ld(dy, ii * d4 + c);
+        xv[u] = St::ld(z, ii * d4 + c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -368,38 +404,51 @@ __global__ void k_bn_bwd_partial(const float4* __restrict__ dy, const float4* __
   }
 }
 
+// dgamma / dbeta: Σ over segments in segment order (added to the existing
+// value when accumulate); k1 / k2 [seg][D] per segment.
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
-    const float* __restrict__ p1, const float* __restrict__ p2, int64_t P, int64_t D,
+    const float* __restrict__ p1, const float* __restrict__ p2, Segs sg, int64_t D,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
-    float* __restrict__ k2, float inv_rows, int accumulate) {
+    float* __restrict__ k2, int accumulate) {
   __shared__ float ra[kRedLanes][kRedCols], rb[kRedLanes][kRedCols];
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
-  float a = 0.f, b = 0.f;
-  if (c < D) {
-    a = lane_fold(p1, P, D, c, rl);
-    b = lane_fold(p2, P, D, c, rl);
+  for (int s = 0; s < sg.n; ++s) {
+    const int64_t P = sg.part0[s + 1] - sg.part0[s];
+    float a = 0.f, b = 0.f;
+    if (c < D) {
+      a = lane_fold(p1 + sg.part0[s] * D, P, D, c, rl);
+      b = lane_fold(p2 + sg.part0[s] * D, P, D, c, rl);
+    }
+    __syncthreads();
+    a = lane_tree_sum(ra, rl, cl, a);
+    b = lane_tree_sum(rb, rl, cl, b);
+    if (rl == 0 && c < D) {
+      const float inv_rows = 1.0f / (float)(sg.row0[s + 1] - sg.row0[s]);
+      const bool add = accumulate || s > 0;
+      if (dbeta) dbeta[c] = add ? dbeta[c] + a : a;
+      if (dgamma) dgamma[c] = add ? dgamma[c] + b : b;
+      k1[s * D + c] = a * inv_rows;
+      k2[s * D + c] = b * inv_rows;
+    }
   }
-  a = lane_tree_sum(ra, rl, cl, a);
-  b = lane_tree_sum(rb, rl, cl, b);
-  if (rl != 0 || c >= D) return;
-  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + a : a;
-  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + b : b;
-  k1[c] = a * inv_rows;
-  k2[c] = b * inv_rows;
 }
 
+template <typename St>
 __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
-    const float4* __restrict__ dy, const float4* __restrict__ z, const float4* __restrict__ mean,
-    const float4* __restrict__ invstd, const float* __restrict__ gamma,
-    const float* __restrict__ beta, const float4* __restrict__ k1,
-    const float4* __restrict__ k2, float4* __restrict__ dz, int64_t total4, int d4, int relu) {
+    const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
+    const float4* __restrict__ mean, const float4* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
+    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t total4, int d4,
+    int relu, Segs sg) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total4) return;
-  int c = (int)(t % d4);
-  float4 g = dy[t], x = z[t], mu = mean[c], is = invstd[c], sc, sh;
+  const int64_t i = t / d4;
+  const int c = (int)(t - i * d4);
+  const int s = seg_of_row(sg, i);
+  float4 g = St::ld(dy, t), x = St::ld(z, t), mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
   bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
-  float4 a = k1[c], b = k2[c];
+  float4 a = k1[s * d4 + c], b = k2[s * d4 + c];
   if (relu) {
     g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
     g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
@@ -412,9 +461,8 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
   o.y = (g.y - a.y - ((x.y - mu.y) * is.y) * b.y) * sc.y;
   o.z = (g.z - a.z - ((x.z - mu.z) * is.z) * b.z) * sc.z;
   o.w = (g.w - a.w - ((x.w - mu.w) * is.w) * b.w) * sc.w;
-  dz[t] = o;
+  St::st(dz, t, o);
 }
-
 // ---------------------------------------------------------------------------
 // segment pooling over graph_ptr
 // ---------------------------------------------------------------------------
@@ -556,18 +604,176 @@ MOLCLR_API int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64
   return molclr_colsum_impl(X, out, rows, cols, ld, accumulate, w, molclr::as_stream(stream));
 }
 
-MOLCLR_API size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t D) {
-  molclr::Band b = molclr::make_band(D);
-  int64_t P = band_parts(rows, b.band);
+namespace {
+
+// host-side segment plan: partitions of every segment exactly as a one-segment
+// call over its rows would have them
+int make_segs(int nseg, const int64_t* seg_rows, int64_t D, Segs& sg, int64_t& P, int64_t& rows) {
+  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && seg_rows,
+                 "batchnorm: %d segments (1..%d)", nseg, MOLCLR_MAX_SEGMENTS);
+  const molclr::Band b = molclr::make_band(D);
+  sg.n = nseg;
+  sg.row0[0] = 0;
+  sg.part0[0] = 0;
+  for (int s = 0; s < nseg; ++s) {
+    MOLCLR_REQUIRE(seg_rows[s] >= 0, "batchnorm: negative segment rows");
+    const int64_t Ps = band_parts(seg_rows[s], b.band);
+    sg.row0[s + 1] = sg.row0[s] + seg_rows[s];
+    sg.part0[s + 1] = sg.part0[s] + Ps;
+    sg.rpp[s] = molclr::ceil_div(seg_rows[s] > 0 ? seg_rows[s] : 1, Ps);
+  }
+  for (int s = nseg; s < MOLCLR_MAX_SEGMENTS; ++s) {
+    sg.row0[s + 1] = sg.row0[nseg];
+    sg.part0[s + 1] = sg.part0[nseg];
+    sg.rpp[s] = 1;
+  }
+  P = sg.part0[nseg];
+  rows = sg.row0[nseg];
+  return MOLCLR_OK;
+}
+
+size_t bn_ws_bytes(int64_t P, int64_t D, int nseg) {
   molclr::Workspace w(nullptr, 0);
-  w.take<float>(P * D);  // partial mean / s1
-  w.take<float>(P * D);  // partial m2 / s2
-  w.take<float>(P);      // partial n
-  w.take<float>(D);      // scale
-  w.take<float>(D);      // shift
-  w.take<float>(D);      // k1
-  w.take<float>(D);      // k2
+  w.take<float>(P * D);     // partial mean / s1
+  w.take<float>(P * D);     // partial m2 / s2
+  w.take<float>(P);         // partial n
+  w.take<float>(nseg * D);  // scale
+  w.take<float>(nseg * D);  // shift
+  w.take<float>(nseg * D);  // k1
+  w.take<float>(nseg * D);  // k2
   return w.used + 256;
+}
+
+template <typename St>
+int bn_fwd(const void* zv, const float* gamma, const float* beta, float* running_mean,
+           float* running_var, int64_t* nbt, void* yv, float* save_mean, float* save_invstd,
+           int nseg, const int64_t* seg_rows, int64_t D, double momentum, double eps, int training,
+           int relu, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  Segs sg;
+  int64_t P = 0, rows = 0;
+  if (int rc = make_segs(nseg, seg_rows, D, sg, P, rows)) return rc;
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_fwd: dim must be a multiple of 4");
+  for (int q = 0; q < nseg; ++q)
+    MOLCLR_REQUIRE(!training || seg_rows[q] > 1,
+                   "batchnorm_fwd: need more than 1 row per segment when training");
+  MOLCLR_REQUIRE(training || (running_mean && running_var), "batchnorm_fwd: eval needs running stats");
+  MOLCLR_REQUIRE(save_mean && save_invstd && (rows == 0 || zv), "batchnorm_fwd: null pointer");
+  MOLCLR_REQUIRE_WS(workspace_bytes, bn_ws_bytes(P, D, nseg));
+  const auto* z = static_cast<const typename St::T*>(zv);
+  auto* y = static_cast<typename St::T*>(yv);
+  const molclr::Band b = molclr::make_band(D);
+  molclr::Workspace w(workspace, workspace_bytes);
+  float* pmean = w.take<float>(P * D);
+  float* pm2 = w.take<float>(P * D);
+  float* pn = w.take<float>(P);
+  float* scale = w.take<float>(nseg * D);
+  float* shift = w.take<float>(nseg * D);
+  if (training) {
+    const size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
+    hipLaunchKernelGGL(k_bn_stats_partial<St>, dim3((unsigned)P), dim3(b.threads), lds, s, z, b.d4,
+                       b.band, sg, (float4*)pmean, (float4*)pm2, pn);
+    hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kRedCols)),
+                       dim3(kRedCols * kRedLanes), 0, s, pmean, pm2, pn, sg, D, gamma, beta,
+                       running_mean, running_var, save_mean, save_invstd, scale, shift,
+                       (float)momentum, (float)eps, nbt);
+  } else {
+    hipLaunchKernelGGL(k_bn_eval_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma,
+                       beta, running_mean, running_var, D, nseg, (float)eps, save_mean,
+                       save_invstd, scale, shift);
+  }
+  const int64_t total4 = rows * (D / 4);
+  if (total4 > 0 && y)  // y == NULL: statistics only (the consumer applies them)
+    hipLaunchKernelGGL(k_bn_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, z,
+                       (const float4*)scale, (const float4*)shift, y, total4, (int)(D / 4), relu,
+                       sg);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+template <typename St>
+int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* beta,
+           const float* save_mean, const float* save_invstd, void* dzv, float* dgamma,
+           float* dbeta, int nseg, const int64_t* seg_rows, int64_t D, int relu, int accumulate,
+           void* workspace, size_t workspace_bytes, hipStream_t s) {
+  Segs sg;
+  int64_t P = 0, rows = 0;
+  if (int rc = make_segs(nseg, seg_rows, D, sg, P, rows)) return rc;
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_bwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(rows > 0 && dyv && zv && save_mean && save_invstd && dzv, "batchnorm_bwd: bad args");
+  for (int q = 0; q < nseg; ++q) MOLCLR_REQUIRE(seg_rows[q] > 0, "batchnorm_bwd: empty segment");
+  MOLCLR_REQUIRE_WS(workspace_bytes, bn_ws_bytes(P, D, nseg));
+  const auto* dy = static_cast<const typename St::T*>(dyv);
+  const auto* z = static_cast<const typename St::T*>(zv);
+  auto* dz = static_cast<typename St::T*>(dzv);
+  const molclr::Band b = molclr::make_band(D);
+  molclr::Workspace w(workspace, workspace_bytes);
+  float* p1 = w.take<float>(P * D);
+  float* p2 = w.take<float>(P * D);
+  w.take<float>(P);
+  w.take<float>(nseg * D);  // scale
+  w.take<float>(nseg * D);  // shift
+  float* k1 = w.take<float>(nseg * D);
+  float* k2 = w.take<float>(nseg * D);
+  // the forward's coefficient expression is recomputed in-kernel (same ReLU mask)
+  const size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
+  hipLaunchKernelGGL(k_bn_bwd_partial<St>, dim3((unsigned)P), dim3(b.threads), lds, s, dy, z,
+                     (const float4*)save_mean, (const float4*)save_invstd, gamma, beta, b.d4,
+                     b.band, sg, relu, (float4*)p1, (float4*)p2);
+  hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes),
+                     0, s, p1, p2, sg, D, dgamma, dbeta, k1, k2, accumulate);
+  const int64_t total4 = rows * (D / 4);
+  hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy, z,
+                     (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
+                     (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+}  // namespace
+
+MOLCLR_API size_t molclr_batchnorm_seg_workspace_bytes(int nseg, const int64_t* seg_rows,
+                                                       int64_t D) {
+  Segs sg;
+  int64_t P = 0, rows = 0;
+  if (make_segs(nseg, seg_rows, D > 0 ? D : 4, sg, P, rows)) return 0;
+  return bn_ws_bytes(P, D, nseg);
+}
+
+MOLCLR_API size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t D) {
+  return molclr_batchnorm_seg_workspace_bytes(1, &rows, D);
+}
+
+MOLCLR_API int molclr_batchnorm_seg_fwd(const void* z, const float* gamma, const float* beta,
+                                        float* running_mean, float* running_var,
+                                        int64_t* num_batches_tracked, void* y, float* save_mean,
+                                        float* save_invstd, int nseg, const int64_t* seg_rows,
+                                        int64_t D, int dtype, double momentum, double eps,
+                                        int training, int relu, void* workspace,
+                                        size_t workspace_bytes, molclr_stream_t stream) {
+  hipStream_t s = molclr::as_stream(stream);
+  if (dtype == MOLCLR_DTYPE_F32)
+    return bn_fwd<StF32>(z, gamma, beta, running_mean, running_var, num_batches_tracked, y,
+                         save_mean, save_invstd, nseg, seg_rows, D, momentum, eps, training, relu,
+                         workspace, workspace_bytes, s);
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_BF16, "batchnorm_seg_fwd: dtype %d", dtype);
+  return bn_fwd<StBF16>(z, gamma, beta, running_mean, running_var, num_batches_tracked, y,
+                        save_mean, save_invstd, nseg, seg_rows, D, momentum, eps, training, relu,
+                        workspace, workspace_bytes, s);
+}
+
+MOLCLR_API int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const float* gamma,
+                                        const float* beta, const float* save_mean,
+                                        const float* save_invstd, void* dz, float* dgamma,
+                                        float* dbeta, int nseg, const int64_t* seg_rows, int64_t D,
+                                        int dtype, int relu, int accumulate, void* workspace,
+                                        size_t workspace_bytes, molclr_stream_t stream) {
+  hipStream_t s = molclr::as_stream(stream);
+  if (dtype == MOLCLR_DTYPE_F32)
+    return bn_bwd<StF32>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
+                         seg_rows, D, relu, accumulate, workspace, workspace_bytes, s);
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_BF16, "batchnorm_seg_bwd: dtype %d", dtype);
+  return bn_bwd<StBF16>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
+                        seg_rows, D, relu, accumulate, workspace, workspace_bytes, s);
 }
 
 MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
@@ -577,40 +783,9 @@ MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const fl
                                     int64_t D, double momentum, double eps, int training,
                                     int relu, void* workspace, size_t workspace_bytes,
                                     molclr_stream_t stream) {
-  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_fwd: dim must be a multiple of 4");
-  MOLCLR_REQUIRE(!training || rows > 1, "batchnorm_fwd: need more than 1 row when training");
-  MOLCLR_REQUIRE(training || (running_mean && running_var), "batchnorm_fwd: eval needs running stats");
-  MOLCLR_REQUIRE(save_mean && save_invstd && z, "batchnorm_fwd: null pointer");
-  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_batchnorm_workspace_bytes(rows, D));
-  hipStream_t s = molclr::as_stream(stream);
-  molclr::Band b = molclr::make_band(D);
-  int64_t P = band_parts(rows, b.band);
-  molclr::Workspace w(workspace, workspace_bytes);
-  float* pmean = w.take<float>(P * D);
-  float* pm2 = w.take<float>(P * D);
-  float* pn = w.take<float>(P);
-  float* scale = w.take<float>(D);
-  float* shift = w.take<float>(D);
-  if (training) {
-    int64_t rpp = molclr::ceil_div(rows, P);
-    size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
-    hipLaunchKernelGGL(k_bn_stats_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)z, rows,
-                       b.d4, b.band, rpp, (float4*)pmean, (float4*)pm2, pn);
-    hipLaunchKernelGGL(k_bn_stats_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, pmean, pm2,
-                       pn, P, D, gamma, beta, running_mean, running_var, save_mean, save_invstd,
-                       scale, shift, (float)momentum, (float)eps, num_batches_tracked);
-  } else {
-    hipLaunchKernelGGL(k_bn_eval_coeffs, dim3(molclr::ceil_div(D, kT)), dim3(kT), 0, s, gamma,
-                       beta, running_mean, running_var, D, (float)eps, save_mean, save_invstd,
-                       scale, shift);
-  }
-  int64_t total4 = rows * (D / 4);
-  if (total4 > 0 && y)  // y == NULL: statistics only (the consumer applies them)
-    hipLaunchKernelGGL(k_bn_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
-                       (const float4*)z, (const float4*)scale, (const float4*)shift, (float4*)y,
-                       total4, (int)(D / 4), relu);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
+  return molclr_batchnorm_seg_fwd(z, gamma, beta, running_mean, running_var, num_batches_tracked,
+                                  y, save_mean, save_invstd, 1, &rows, D, MOLCLR_DTYPE_F32,
+                                  momentum, eps, training, relu, workspace, workspace_bytes, stream);
 }
 
 MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
@@ -619,35 +794,9 @@ MOLCLR_API int molclr_batchnorm_bwd(const float* dy, const float* z, const float
                                     float* dbeta, int64_t rows, int64_t D, int relu,
                                     int accumulate, void* workspace, size_t workspace_bytes,
                                     molclr_stream_t stream) {
-  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_bwd: dim must be a multiple of 4");
-  MOLCLR_REQUIRE(rows > 0 && dy && z && save_mean && save_invstd && dz, "batchnorm_bwd: bad args");
-  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_batchnorm_workspace_bytes(rows, D));
-  hipStream_t s = molclr::as_stream(stream);
-  molclr::Band b = molclr::make_band(D);
-  int64_t P = band_parts(rows, b.band);
-  molclr::Workspace w(workspace, workspace_bytes);
-  float* p1 = w.take<float>(P * D);
-  float* p2 = w.take<float>(P * D);
-  w.take<float>(P);
-  float* scale = w.take<float>(D);
-  float* shift = w.take<float>(D);
-  float* k1 = w.take<float>(D);
-  float* k2 = w.take<float>(D);
-  // the forward's coefficient expression is recomputed in-kernel (same ReLU mask)
-  int64_t rpp = molclr::ceil_div(rows, P);
-  size_t lds = 2 * (size_t)b.band * b.d4 * sizeof(float4);
-  hipLaunchKernelGGL(k_bn_bwd_partial, dim3(P), dim3(b.threads), lds, s, (const float4*)dy,
-                     (const float4*)z, (const float4*)save_mean, (const float4*)save_invstd, gamma,
-                     beta, rows, b.d4, b.band, rpp, relu, (float4*)p1, (float4*)p2);
-  hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes), 0, s, p1, p2, P, D,
-                     dgamma, dbeta, k1, k2, 1.0f / (float)rows, accumulate);
-  int64_t total4 = rows * (D / 4);
-  hipLaunchKernelGGL(k_bn_bwd_apply, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
-                     (const float4*)dy, (const float4*)z, (const float4*)save_mean,
-                     (const float4*)save_invstd, gamma, beta, (const float4*)k1, (const float4*)k2,
-                     (float4*)dz, total4, (int)(D / 4), relu);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
+  return molclr_batchnorm_seg_bwd(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta,
+                                  1, &rows, D, MOLCLR_DTYPE_F32, relu, accumulate, workspace,
+                                  workspace_bytes, stream);
 }
 
 MOLCLR_API int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr, float* out,

@@ -169,19 +169,23 @@ class SyntheticPairBatches:
 
 class MoleculeDataset(torch.utils.data.Dataset):
     """Map-style dataset of synthetic molecules with the reference's
-    ``__getitem__ -> (Data_i, Data_j)`` contract (dataset/dataset.py:56-150)."""
+    ``__getitem__ -> (Data_i, Data_j)`` contract (dataset/dataset.py:56-150).
 
-    def __init__(self, num_molecules: int, seed: int = 0, shape: str = "uniform"):
+    Views are drawn from ``SeedSequence([seed, rank, index, call])``: every
+    (rank, molecule, epoch) pair gets its own augmentation stream."""
+
+    def __init__(self, num_molecules: int, seed: int = 0, shape: str = "uniform", rank: int = 0):
         super().__init__()
         rng = np.random.default_rng(seed)
         self.mols = [random_molecule(rng, shape) for _ in range(num_molecules)]
         self.seed = seed
+        self.rank = rank
         self._calls = 0
 
     def __getitem__(self, index):
         # per-item, per-call view streams: reproducible yet different each epoch
         self._calls += 1
-        ss = np.random.SeedSequence([self.seed, index, self._calls])
+        ss = np.random.SeedSequence([self.seed, self.rank, index, self._calls])
         ri, rj = (np.random.default_rng(s) for s in ss.spawn(2))
         return augment_pair(self.mols[index], ri, rj)
 
@@ -189,19 +193,63 @@ class MoleculeDataset(torch.utils.data.Dataset):
         return len(self.mols)
 
 
+class ShardedSubsetSampler(torch.utils.data.Sampler):
+    """SubsetRandomSampler for data parallelism: every epoch, one permutation of
+    ``indices`` seeded by (seed, epoch) -- the same on every rank -- is dealt
+    round-robin, rank r taking positions r, r + world, ...; the tail that does
+    not divide evenly is dropped, so every rank sees the same number of
+    molecules (and of full batches, drop_last) and no molecule is seen by two
+    ranks in one epoch.  world == 1 is SubsetRandomSampler with a seeded,
+    per-epoch permutation (the reference's dataset/dataset.py:176-177)."""
+
+    def __init__(self, indices, rank: int = 0, world: int = 1, seed: int = 0):
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world size {world}")
+        self.indices = list(indices)
+        self.rank, self.world, self.seed = rank, world, seed
+        self.epoch = 0
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = epoch
+
+    def __iter__(self):
+        per = len(self.indices) // self.world
+        order = np.random.default_rng([self.seed, self.epoch]).permutation(len(self.indices))
+        self.epoch += 1
+        mine = order[self.rank:per * self.world:self.world]
+        return iter([self.indices[i] for i in mine])
+
+    def __len__(self):
+        return len(self.indices) // self.world
+
+
 class MoleculeDatasetWrapper:
     """dataset/dataset.py:153-185: shuffled train/valid split, DataLoaders with
     ``drop_last=True`` (NT-Xent needs full batches).  ``data_path`` is read as
-    ``synthetic:<num_molecules>`` (SMILES featurisation needs RDKit, absent)."""
+    ``synthetic:<num_molecules>`` (SMILES featurisation needs RDKit, absent) or
+    a binary graph shard (molclr_amd.shards).
+
+    Data parallel: with ``torch.distributed`` initialised (or ``rank`` /
+    ``world`` given), each rank draws a disjoint, equally sized shard of the
+    train and valid index sets every epoch (ShardedSubsetSampler)."""
 
     def __init__(self, batch_size, num_workers, valid_size, data_path, seed: int = 0,
-                 shape: str = "uniform"):
+                 shape: str = "uniform", rank: int | None = None, world: int | None = None):
         self.batch_size = batch_size
         self.num_workers = num_workers
         self.valid_size = valid_size
         self.data_path = data_path
         self.seed = seed
         self.shape = shape
+        self.rank, self.world = rank, world
+
+    def _rank_world(self) -> tuple[int, int]:
+        if self.rank is not None and self.world is not None:
+            return int(self.rank), int(self.world)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
 
     def _num_molecules(self) -> int:
         p = str(self.data_path)
@@ -209,19 +257,26 @@ class MoleculeDatasetWrapper:
             return int(p.split(":", 1)[1])
         raise NotImplementedError(
             f"data_path {p!r}: SMILES featurisation needs RDKit, which is not available; "
-            "use 'synthetic:<num_molecules>'")
+            "use 'synthetic:<num_molecules>' or a binary graph shard")
 
     def get_data_loaders(self):
-        train_dataset = MoleculeDataset(self._num_molecules(), self.seed, self.shape)
+        rank, _ = self._rank_world()
+        p = str(self.data_path)
+        if p.startswith("synthetic:"):
+            train_dataset = MoleculeDataset(self._num_molecules(), self.seed, self.shape, rank=rank)
+        else:
+            from .shards import ShardMoleculeDataset
+            train_dataset = ShardMoleculeDataset(p, seed=self.seed, rank=rank)
         return self.get_train_validation_data_loaders(train_dataset)
 
     def get_train_validation_data_loaders(self, train_dataset):
+        rank, world = self._rank_world()
         num_train = len(train_dataset)
         indices = np.random.default_rng(self.seed).permutation(num_train).tolist()
         split = int(np.floor(self.valid_size * num_train))
         train_idx, valid_idx = indices[split:], indices[:split]
-        train_sampler = torch.utils.data.SubsetRandomSampler(train_idx)
-        valid_sampler = torch.utils.data.SubsetRandomSampler(valid_idx)
+        train_sampler = ShardedSubsetSampler(train_idx, rank, world, seed=self.seed + 1)
+        valid_sampler = ShardedSubsetSampler(valid_idx, rank, world, seed=self.seed + 2)
         kw = dict(batch_size=self.batch_size, num_workers=self.num_workers, drop_last=True,
                   collate_fn=collate_pairs)
         train_loader = torch.utils.data.DataLoader(train_dataset, sampler=train_sampler, **kw)

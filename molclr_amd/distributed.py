@@ -4,8 +4,9 @@ The reference is single-device (molclr.py:45-53).  Scaling it out needs only
 two exchanges per step, both chosen for a point-to-point xGMI fabric:
 
 1. NT-Xent over the GLOBAL contrastive batch (molclr_amd.ops._NTXent):
-   all-gather of the normalised projections (2 x [B_local, C]) and of the
-   per-row logsumexp (2 x [B_local]).  Because the NT-Xent weight matrix
+   one all-gather of each rank's normalised rows [zj_local; zi_local]
+   ([2 B_local, C]) reordered into the reference's [zj_all; zi_all]
+   (gather_rows), and one of the per-row logsumexp (gather_lse).  Because the NT-Xent weight matrix
    W_rc = P_rc + P_cr - 2[c = p(r)] is symmetric, each rank then computes the
    exact gradient of its own rows locally: no column-gradient reduce-scatter.
 2. One SUM all-reduce of the flat gradient buffer (FusedAdam.flat_grad,
@@ -54,6 +55,43 @@ def init(backend: str | None = None) -> tuple[int, int, torch.device]:
             kw["device_id"] = device
         dist.init_process_group(**kw)
     return rank, world, device
+
+
+def _all_gather_stack(t: torch.Tensor, group=None) -> torch.Tensor:
+    """[world, *t.shape]: every rank's t, in rank order.  One collective
+    (all_gather_into_tensor on RCCL; the list form on backends without it)."""
+    world = dist.get_world_size(group)
+    t = t.contiguous()
+    out = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, t, group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), t, group=group)
+    return out
+
+
+def gather_rows(local_rows: torch.Tensor, group=None) -> torch.Tensor:
+    """Rows [zj_local; zi_local] ([2 B_l, C]) of every rank -> the global
+    R = [zj_all; zi_all] ([2 B, C], B = world * B_l) of utils/nt_xent.py:48,
+    rank r's molecules at [r B_l, (r+1) B_l) of each half."""
+    g = _all_gather_stack(local_rows, group)          # [W, 2 B_l, C]
+    W, two_bl = g.shape[0], g.shape[1]
+    bl = two_bl // 2
+    return torch.cat([g[:, :bl].reshape(W * bl, -1), g[:, bl:].reshape(W * bl, -1)], 0)
+
+
+def gather_lse(local_lse: torch.Tensor, group=None) -> torch.Tensor:
+    """Per-row logsumexp [2 B_l] of every rank -> [2 B] in R's row order."""
+    g = _all_gather_stack(local_lse, group)            # [W, 2 B_l]
+    bl = g.shape[1] // 2
+    return torch.cat([g[:, :bl].reshape(-1), g[:, bl:].reshape(-1)], 0)
+
+
+def global_row_index(b_local: int, rank: int, world: int, device) -> torch.Tensor:
+    """Global R row of each local row [zj_local; zi_local] (int32 [2 B_l])."""
+    B = b_local * world
+    base = torch.arange(b_local, dtype=torch.int32, device=device) + rank * b_local
+    return torch.cat([base, base + B])
 
 
 def allreduce_grads(flat_grad: torch.Tensor, group=None) -> None:

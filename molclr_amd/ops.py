@@ -628,16 +628,15 @@ class _NTXent(torch.autograd.Function):
             gidx = torch.arange(n, dtype=torch.int32, device=dev)
         else:
             import torch.distributed as dist
+
+            from . import distributed as mdist
             world = dist.get_world_size(group)
             rank = dist.get_rank(group)
             B = Bl * world
             if batch_size != B:
                 raise ValueError(f"global batch {B} != NTXentLoss batch_size {batch_size}")
-            cols = torch.empty(2 * B, C, dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(cols[:B], rhat[:Bl].contiguous(), group=group)
-            dist.all_gather_into_tensor(cols[B:], rhat[Bl:].contiguous(), group=group)
-            base = torch.arange(Bl, dtype=torch.int32, device=dev) + rank * Bl
-            gidx = torch.cat([base, base + B])
+            cols = mdist.gather_rows(rhat, group)
+            gidx = mdist.global_row_index(Bl, rank, world, dev)
         lse = torch.empty(n, dtype=torch.float32, device=dev)
         loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
         ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
@@ -650,9 +649,7 @@ class _NTXent(torch.autograd.Function):
         if group is None:
             lse_cols = lse
         else:
-            lse_cols = torch.empty(2 * B, dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(lse_cols[:B], lse[:Bl].contiguous(), group=group)
-            dist.all_gather_into_tensor(lse_cols[B:], lse[Bl:].contiguous(), group=group)
+            lse_cols = mdist.gather_lse(lse, group)
             dist.all_reduce(loss, group=group)
         ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols)
         ctx.meta = (B, Bl, C, float(temperature), int(cosine))

@@ -40,8 +40,11 @@ def splitmix64(z):
 
 
 def _stream(seed: int, view: int, kind: int, mol_id: int) -> np.uint64:
-    s = splitmix64(np.uint64(seed) ^ np.uint64(2 * view + kind))
-    return splitmix64(s ^ np.uint64(mol_id))
+    """augment.hip subset_stream: splitmix64 chained over (seed, view, kind, id)."""
+    z = splitmix64(np.uint64(seed))
+    z = splitmix64(z ^ np.uint64(view))
+    z = splitmix64(z ^ np.uint64(kind))
+    return splitmix64(z ^ np.uint64(mol_id))
 
 
 def chosen_items(seed: int, view: int, kind: int, mol_id: int, n: int, k: int) -> np.ndarray:

@@ -94,3 +94,20 @@ def test_edge_cases():
     assert np.array_equal(out["ptr"], [0, 1, 3, 7])
     empty = mask_views(store, np.zeros(0, np.int64), seed=0, view=0)
     assert empty["x"].shape == (0, 2) and np.array_equal(empty["ptr"], [0])
+
+
+def test_streams_do_not_alias_across_seed_view_kind():
+    """A flat seed ^ (2 view + kind) key made view 1 at seed s replay view 0 at
+    seed s ^ 2 (and the bond stream of one view replay the atom stream of the
+    next seed); the chained splitmix64 keys of augment.hip do not."""
+    from oracle.augment_ref import _stream
+    keys = {}
+    for seed in range(64):
+        for view in (0, 1):
+            for kind in (0, 1):
+                k = int(_stream(seed, view, kind, 7))
+                assert k not in keys, (seed, view, kind, keys.get(k))
+                keys[k] = (seed, view, kind)
+    n, k = 40, 10
+    for s in range(32):
+        assert not np.array_equal(chosen_items(s, 1, 0, 3, n, k), chosen_items(s ^ 2, 0, 0, 3, n, k))

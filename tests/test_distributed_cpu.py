@@ -6,8 +6,14 @@
   gradient of its own rows (symmetric W, no column-gradient exchange) —
   reproduces the single-process reference NTXentLoss on the concatenated
   batch, loss and gradients.
+* The product's exchange helpers (molclr_amd.distributed.gather_rows /
+  gather_lse / global_row_index, what ops._NTXent calls) produce the
+  reference's global order.
 * molclr_amd.distributed: init() from the torchrun environment, the flat
   gradient SUM all-reduce and the parameter broadcast.
+* Data parallel input: MoleculeDatasetWrapper gives each rank a disjoint,
+  equally sized shard, reshuffled every epoch (identical per-rank
+  data made every row meet copies of itself as negatives).
 """
 import os
 import socket
@@ -52,29 +58,46 @@ def _worker(rank, port, out_q):
     # local rows [zj_local; zi_local], global indices
     R_local = np.concatenate([zj[sl], zi[sl]], 0)
     rh, nrm = ntxent_math.prep(R_local, True)
-    gidx = np.concatenate([np.arange(B_LOCAL) + rank * B_LOCAL,
-                           np.arange(B_LOCAL) + rank * B_LOCAL + B])
-    # all-gather into [zj_all; zi_all] (two collectives, as ops._NTXent does)
-    t = torch.from_numpy(rh)
-    cols = torch.empty(2 * B, C, dtype=torch.float64)
-    dist.all_gather(list(cols[:B].chunk(WORLD)), t[:B_LOCAL].contiguous())
-    dist.all_gather(list(cols[B:].chunk(WORLD)), t[B_LOCAL:].contiguous())
-    cols = cols.numpy()
+    # the product's exchange (molclr_amd.distributed, as ops._NTXent calls it):
+    # one gather of [zj_local; zi_local] into [zj_all; zi_all], global row ids
+    gidx = mdist.global_row_index(B_LOCAL, rank, WORLD, "cpu").numpy().astype(np.int64)
+    assert np.array_equal(gidx, np.concatenate([np.arange(B_LOCAL) + rank * B_LOCAL,
+                                                np.arange(B_LOCAL) + rank * B_LOCAL + B]))
+    cols = mdist.gather_rows(torch.from_numpy(rh)).numpy()
+    Rall = np.concatenate([zj, zi], 0)
+    assert np.allclose(cols, ntxent_math.prep(Rall, True)[0])
     lse, loss_rows = ntxent_math.rows_forward(rh, gidx, cols, B, T)
-    lt = torch.from_numpy(lse)
-    lse_cols = torch.empty(2 * B, dtype=torch.float64)
-    dist.all_gather(list(lse_cols[:B].chunk(WORLD)), lt[:B_LOCAL].contiguous())
-    dist.all_gather(list(lse_cols[B:].chunk(WORLD)), lt[B_LOCAL:].contiguous())
+    lse_cols = mdist.gather_lse(torch.from_numpy(lse)).numpy()
+    assert np.allclose(lse_cols, ntxent_math.rows_forward(cols, np.arange(2 * B), cols, B, T)[0])
     loss = torch.tensor([loss_rows.sum()])
     dist.all_reduce(loss)
-    drh = ntxent_math.rows_backward(rh, gidx, cols, lse_cols.numpy(), B, T)
+    drh = ntxent_math.rows_backward(rh, gidx, cols, lse_cols, B, T)
     dR = ntxent_math.prep_bwd(drh, rh, nrm, True)
+    # data sharding: disjoint, equally sized per-rank shards every epoch
+    from molclr_amd.dataset import MoleculeDatasetWrapper
+    w = MoleculeDatasetWrapper(8, 0, 0.2, "synthetic:120", seed=3)
+    tr, va = w.get_data_loaders()
+    ids = []
+    for epoch in range(2):
+        ids.append(list(tr.sampler))
+    first = next(iter(tr))[0]
+    nb = torch.tensor([len(tr), len(va)])
+    nbs = [torch.zeros(2, dtype=torch.long) for _ in range(WORLD)]
+    dist.all_gather(nbs, nb)
+    shard = torch.tensor(sorted(ids[0]))
+    shards = [torch.zeros_like(shard) for _ in range(WORLD)]
+    dist.all_gather(shards, shard)
+    xs = torch.tensor([first.x.shape[0]])
+    sizes = [torch.zeros_like(xs) for _ in range(WORLD)]
+    dist.all_gather(sizes, xs)
+    sharding = ([n.tolist() for n in nbs], [s.tolist() for s in shards], ids[0] != ids[1])
     # gradient reduction + broadcast helpers on flat buffers
     flat = torch.full((10,), float(rank + 1))
     mdist.allreduce_grads(flat)
     p = torch.full((4,), float(rank))
     mdist.broadcast_params(p)
-    out_q.put((rank, float(loss.item()), dR[B_LOCAL:], dR[:B_LOCAL], flat.tolist(), p.tolist()))
+    out_q.put((rank, float(loss.item()), dR[B_LOCAL:], dR[:B_LOCAL], flat.tolist(), p.tolist(),
+               sharding))
     dist.destroy_process_group()
 
 
@@ -101,5 +124,9 @@ def test_sharded_ntxent_matches_single_process_reference():
         assert abs(r[1] - ref.item()) < 1e-5 * ref.item()
         assert r[4] == [3.0] * 10        # SUM over ranks 1 + 2
         assert r[5] == [0.0] * 4         # rank 0's values broadcast
+    nbs, shards, reshuffled = res[0][6]
+    assert nbs[0] == nbs[1] and nbs[0][0] > 0       # equal batch counts per rank
+    assert not set(shards[0]) & set(shards[1])      # disjoint molecule shards
+    assert reshuffled                                 # a new permutation every epoch
     assert np.linalg.norm(dzi - a.grad.numpy()) <= 1e-5 * np.linalg.norm(a.grad.numpy())
     assert np.linalg.norm(dzj - b.grad.numpy()) <= 1e-5 * np.linalg.norm(b.grad.numpy())

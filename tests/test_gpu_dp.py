@@ -1,0 +1,168 @@
+"""Data-parallel NT-Xent on the GPU (BASELINE config c4).
+
+* c4 as W = 8 simulated ranks through the C ABI: every rank owns its rows
+  [zj_local; zi_local] (2 x 512) and sees the gathered columns (8192 x 256)
+  and gathered logsumexp -- molclr_ntxent_fwd / _bwd with nrows != ncols and
+  the global row offsets of molclr_amd.distributed.global_row_index.  The
+  assembled loss and gradients must equal the single-process NT-Xent of the
+  global batch 4096 (utils/nt_xent.py:47-65; oracle/ntxent_math in float64,
+  itself pinned by the reference's goldens) at 1e-5 norm-wise.
+* The product's ``group=`` branch (ops._NTXent: gather_rows / gather_lse /
+  loss all-reduce, the gradient all-reduce) under RCCL with world size 1: the
+  collectives run for real and the result is bit-identical to the
+  single-process path.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from molclr_amd import _lib
+from molclr_amd import distributed as mdist
+from oracle import ntxent_math
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def rel(a, b):
+    a = np.asarray(torch.as_tensor(a).detach().double().cpu())
+    b = np.asarray(b, dtype=np.float64)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def _prep(lib, R, cosine, dev):
+    n, C = R.shape
+    rh = torch.empty_like(R)
+    nrm = torch.empty(n, device=dev)
+    assert lib.molclr_ntxent_prep(R.data_ptr(), rh.data_ptr(), nrm.data_ptr(), n, C, int(cosine),
+                                  None) == 0
+    return rh, nrm
+
+
+@pytest.mark.parametrize("W,Bl,C,cosine", [(8, 512, 256, True), (3, 37, 64, False)])
+def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine):
+    lib = _lib.load()
+    B = W * Bl
+    T = 0.1
+    rng = np.random.default_rng(W * Bl)
+    zi = rng.standard_normal((B, C)).astype(np.float32)
+    zj = (0.5 * zi + rng.standard_normal((B, C))).astype(np.float32)
+    if not cosine:  # dot similarity needs tame logits: unit rows, as after F.normalize
+        zi /= np.linalg.norm(zi, axis=1, keepdims=True)
+        zj /= np.linalg.norm(zj, axis=1, keepdims=True)
+    loss_ref, dzi_ref, dzj_ref = ntxent_math.ntxent(zi, zj, T, cosine)
+    zid, zjd = torch.from_numpy(zi).to(dev), torch.from_numpy(zj).to(dev)
+    # each rank: local rows, prep (row scaling), then what gather_rows returns
+    ranks = []
+    for r in range(W):
+        sl = slice(r * Bl, (r + 1) * Bl)
+        rows, nrm = _prep(lib, torch.cat([zjd[sl], zid[sl]]).contiguous(), cosine, dev)
+        ranks.append((rows, nrm, mdist.global_row_index(Bl, r, W, dev)))
+    g = torch.stack([rk[0] for rk in ranks])                  # all_gather stack
+    cols = torch.cat([g[:, :Bl].reshape(B, C), g[:, Bl:].reshape(B, C)]).contiguous()
+    ws_bytes = lib.molclr_ntxent_workspace_bytes(2 * Bl, 2 * B, C)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    lses, loss = [], 0.0
+    for rows, _, gidx in ranks:
+        lse = torch.empty(2 * Bl, device=dev)
+        lr = torch.empty(2 * Bl, device=dev)
+        assert lib.molclr_ntxent_fwd(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(), 2 * Bl,
+                                     2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(), ws.data_ptr(),
+                                     ws_bytes, None) == 0
+        lses.append(lse)
+        loss += lr.double().sum().item()
+    lg = torch.stack(lses)
+    lse_cols = torch.cat([lg[:, :Bl].reshape(-1), lg[:, Bl:].reshape(-1)]).contiguous()
+    gl = torch.ones((), device=dev)
+    dzi, dzj = [], []
+    for rows, nrm, gidx in ranks:
+        drh = torch.empty_like(rows)
+        assert lib.molclr_ntxent_bwd(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                                     lse_cols.data_ptr(), gl.data_ptr(), 2 * Bl, 2 * B, C, B, T,
+                                     drh.data_ptr(), ws.data_ptr(), ws_bytes, None) == 0
+        dR = torch.empty_like(rows)
+        assert lib.molclr_ntxent_prep_bwd(drh.data_ptr(), rows.data_ptr(), nrm.data_ptr(),
+                                          dR.data_ptr(), 2 * Bl, C, int(cosine), None) == 0
+        dzj.append(dR[:Bl])
+        dzi.append(dR[Bl:])
+    torch.cuda.synchronize()
+    assert abs(loss - loss_ref) <= TOL * abs(loss_ref), (loss, loss_ref)
+    assert rel(torch.cat(dzi), dzi_ref) < TOL
+    assert rel(torch.cat(dzj), dzj_ref) < TOL
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture()
+def rccl_world1(dev):
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    yield dist.group.WORLD
+    dist.destroy_process_group()
+
+
+def test_ntxent_group_branch_rccl_world1(dev, rccl_world1):
+    """ops._NTXent's group branch and the gradient all-reduce with real RCCL
+    collectives (world size 1): bit-identical to the single-process path."""
+    from molclr_amd.nt_xent import NTXentLoss
+    torch.manual_seed(0)
+    B, C = 512, 256
+    zi = torch.randn(B, C, device=dev)
+    zj = zi + 0.8 * torch.randn(B, C, device=dev)
+    outs = []
+    for group in (None, rccl_world1):
+        a = zi.clone().requires_grad_(True)
+        b = zj.clone().requires_grad_(True)
+        loss = NTXentLoss(dev, B, 0.1, True, group=group)(a, b)
+        loss.backward()
+        outs.append((loss.detach(), a.grad, b.grad))
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    flat = torch.arange(8, dtype=torch.float32, device=dev)
+    mdist.allreduce_grads(flat)
+    assert torch.equal(flat, torch.arange(8, dtype=torch.float32, device=dev))
+    rows = torch.randn(2 * 4, 3, device=dev)
+    assert torch.equal(mdist.gather_rows(rows), rows)          # world 1: identity order
+    assert torch.equal(mdist.gather_lse(rows[:, 0].contiguous()), rows[:, 0])
+
+
+def test_training_step_under_rccl_world1(dev, rccl_world1):
+    """A product training step through the data-parallel code path (group NT-Xent,
+    gradient all-reduce, parameter broadcast) equals the single-process step."""
+    import copy
+
+    from molclr_amd.dataset import SyntheticPairBatches
+    from molclr_amd.ginet_molclr import GINet
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from molclr_amd.optim import FusedAdam
+    torch.manual_seed(3)
+    m0 = GINet(2, 64, 128).to(dev)
+    m1 = copy.deepcopy(m0)
+    xi, xj = SyntheticPairBatches(32, seed=9).next()
+    xi, xj = xi.to(dev), xj.to(dev)
+    res = []
+    for m, group in ((m0, None), (m1, rccl_world1)):
+        opt = FusedAdam(m.parameters(), 5e-4, weight_decay=1e-5)
+        mdist.broadcast_params(opt.flat)
+        opt.zero_grad()
+        loss = NTXentLoss(dev, 32, 0.1, True, group=group)(l2_normalize(m(xi)[1]),
+                                                            l2_normalize(m(xj)[1]))
+        loss.backward()
+        if group is not None:
+            mdist.allreduce_grads(opt.flat_grad)
+        opt.step()
+        res.append(opt.flat.clone())
+    assert torch.equal(res[0], res[1])

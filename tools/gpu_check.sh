@@ -14,8 +14,10 @@ run() {
 steps="${STEPS:-kernels models bench}"
 for s in $steps; do
   case $s in
-    kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
-    models)  run models 900 python -m pytest tests/test_gpu_models.py -m gpu -q --maxfail=200 -rf; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    kernels) run kernels 900 python -m pytest tests/test_gpu_kernels.py -m gpu -q --maxfail=200 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    models)  MOLCLR_RECORD_ERRS=gpurun_out/errs run models 900 python -m pytest tests/test_gpu_models.py -m gpu -q --maxfail=200 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    dp)      run dp 600 python -m pytest tests/test_gpu_dp.py -m gpu -q --maxfail=200 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    rest)    run rest 900 python -m pytest tests -m gpu -q --maxfail=200 -rf --timeout 300 --timeout-method thread --deselect tests/test_gpu_kernels.py --deselect tests/test_gpu_models.py --deselect tests/test_gpu_dp.py; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
     pmc)     export TMPDIR=/tmp; rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
              run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
