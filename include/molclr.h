@@ -110,6 +110,25 @@ int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
                        int32_t* ecount, int32_t* graph_ptr, int32_t* status,
                        void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
+/* molclr_graph_build over `nseg` (<= MOLCLR_MAX_SEGMENTS) PyG batches taken as
+ * one: segment s's nodes / edges / graphs follow those of segments 0..s-1
+ * (edge_index values stay local to their segment).  The two contrastive
+ * views of a step are built as ONE graph this way and run through one
+ * encoder pass (molclr_batchnorm_seg_fwd keeps their statistics apart).
+ * Workspace: molclr_graph_build_workspace_bytes(total nodes, total edges). */
+#define MOLCLR_MAX_SEGMENTS 8
+typedef struct molclr_graph_segment {
+  const int64_t* edge_index; /* [2, num_edges] */
+  const int64_t* edge_attr;  /* [num_edges, 2] */
+  const int64_t* batch;      /* [num_nodes] */
+  int64_t num_nodes, num_edges, num_graphs;
+} molclr_graph_segment;
+int molclr_graph_build_multi(int nseg, const molclr_graph_segment* segs, int32_t* rowptr,
+                             int32_t* col, uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t,
+                             uint32_t* nbr, uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
+                             int32_t* status, void* workspace, size_t workspace_bytes,
+                             molclr_stream_t stream);
+
 /* On-device node-mask augmentation + collate: one contrastive view of a batch
  * of molecules, replacing MoleculeDataset.__getitem__'s masking
  * (dataset/dataset.py:111-145) and the DataLoader's PyG collate
@@ -332,7 +351,6 @@ int molclr_batchnorm_bwd(const float* dy, const float* z, const float* gamma,
  * rows alone.  save_mean / save_invstd are [nseg, D].  dgamma / dbeta are the
  * sums over the segments (in segment order).  dtype: MOLCLR_DTYPE_F32 or
  * MOLCLR_DTYPE_BF16 storage of z / y / dy / dz (statistics always fp32). */
-#define MOLCLR_MAX_SEGMENTS 8
 enum { MOLCLR_DTYPE_F32 = 0, MOLCLR_DTYPE_BF16 = 1 };
 size_t molclr_batchnorm_seg_workspace_bytes(int nseg, const int64_t* seg_rows, int64_t dim);
 int molclr_batchnorm_seg_fwd(const void* z, const float* gamma, const float* beta,
@@ -467,11 +485,17 @@ typedef struct molclr_gin_encoder_grads {
 } molclr_gin_encoder_grads;
 
 /* The graph of one batch as molclr_graph_build produced it. */
+/* num_segments > 1: the graph is molclr_graph_build_multi's union of that many
+ * batches with segment_nodes[s] nodes each; the executors keep the
+ * BatchNorm statistics of every segment apart (molclr_batchnorm_seg_fwd).
+ * num_segments 0 or 1: one batch. */
 typedef struct molclr_device_graph {
   int64_t num_nodes, num_edges, num_graphs;
   const int32_t *rowptr, *col, *rowptr_t, *col_t, *ecount, *graph_ptr;
   const uint8_t* ecode;
   const uint32_t *nbr, *nbr_t;
+  int32_t num_segments;
+  int64_t segment_nodes[MOLCLR_MAX_SEGMENTS];
 } molclr_device_graph;
 
 /* Saved activations of one forward (kept for the backward): arena of

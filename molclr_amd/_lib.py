@@ -30,6 +30,8 @@ SIGNATURES = {
     "molclr_graph_build_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_graph_build": (c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                    _P, _P, _P, c_size_t, _P]),
+    "molclr_graph_build_multi": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                         c_size_t, _P]),
     "molclr_mask_views_workspace_bytes": (c_size_t, [_I64]),
     "molclr_mask_views": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, c_uint64, c_int, _P, _P,
                                   _P, _P, _P, _I64, _I64, _P, _P, c_size_t, _P]),
@@ -70,6 +72,11 @@ SIGNATURES = {
                                      c_double, c_int, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, c_int,
                                      _P, c_size_t, _P]),
+    "molclr_batchnorm_seg_workspace_bytes": (c_size_t, [c_int, _P, _I64]),
+    "molclr_batchnorm_seg_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P, _I64, c_int,
+                                         c_double, c_double, c_int, c_int, _P, c_size_t, _P]),
+    "molclr_batchnorm_seg_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P, _I64, c_int,
+                                         c_int, c_int, _P, c_size_t, _P]),
     "molclr_segment_pool_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
     "molclr_segment_pool_bwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_l2norm_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_double, _P]),
@@ -101,6 +108,8 @@ EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK = 0, 1, 2, 3
 EPI_ACCUMULATE = 16
 NUM_ECOMB = 15  # combined edge-table rows (bond type * 3 + bond dir)
 MAX_LAYERS = 16
+MAX_SEGMENTS = 8
+DTYPE_F32, DTYPE_BF16 = 0, 1
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
 
@@ -147,7 +156,14 @@ class DeviceGraphC(ctypes.Structure):
     """struct molclr_device_graph."""
     _fields_ = [("num_nodes", c_int64), ("num_edges", c_int64), ("num_graphs", c_int64)] + [
         (f, c_void_p) for f in ("rowptr", "col", "rowptr_t", "col_t", "ecount", "graph_ptr",
-                                "ecode", "nbr", "nbr_t")]
+                                "ecode", "nbr", "nbr_t")] + [
+        ("num_segments", ctypes.c_int32), ("segment_nodes", c_int64 * 8)]
+
+
+class GraphSegmentC(ctypes.Structure):
+    """struct molclr_graph_segment."""
+    _fields_ = [("edge_index", c_void_p), ("edge_attr", c_void_p), ("batch", c_void_p),
+                ("num_nodes", c_int64), ("num_edges", c_int64), ("num_graphs", c_int64)]
 
 
 class MolclrError(RuntimeError):

@@ -81,6 +81,9 @@ void launch_timed(int kind, F kernel, dim3 grid, dim3 block, uint32_t shmem,
 
 }  // namespace molclr
 
+// norm.hip: BatchNorm workspace for any split of `rows` into segments
+size_t molclr_batchnorm_ws_bound(int64_t rows, int64_t D);
+
 #define MOLCLR_REQUIRE(cond, ...)        \
   do {                                   \
     if (!(cond)) {                       \

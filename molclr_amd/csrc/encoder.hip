@@ -33,8 +33,8 @@ struct ArenaLayout {
       a1[l] = off(N * 2 * D);
       z[l] = off(N * D);
       h[l] = off(N * D);
-      mean[l] = off(D);
-      invstd[l] = off(D);
+      mean[l] = off(MOLCLR_MAX_SEGMENTS * D);  // [segment][D]
+      invstd[l] = off(MOLCLR_MAX_SEGMENTS * D);
     }
     h0 = off(N * D);
     ec = off((size_t)L * MOLCLR_NUM_ECOMB * D);
@@ -52,7 +52,7 @@ size_t kernels_ws(int64_t N, int64_t D) {
   mx(molclr_colsum_f32_workspace_bytes(N, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, D, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, 2 * D, D));
-  mx(molclr_batchnorm_workspace_bytes(N, D));
+  mx(molclr_batchnorm_ws_bound(N, D));
   mx(molclr_gine_aggregate_bwd_workspace_bytes(N, D));
   mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
   return m;
@@ -72,6 +72,26 @@ int check_encoder(const molclr_gin_encoder* e, const molclr_device_graph* g) {
     MOLCLR_REQUIRE(e->mlp0_planes[l] && e->mlp0_planes_t[l] && e->mlp2_planes[l] &&
                        e->mlp2_planes_t[l] && e->bn_weight[l] && e->bn_bias[l],
                    "gin_encoder: layer %d: missing planes or BatchNorm affine", l);
+  return MOLCLR_OK;
+}
+
+// BatchNorm segments of a graph (the views of a paired forward), checked
+struct SegRows {
+  int n;
+  const int64_t* rows;
+};
+int graph_segments(const molclr_device_graph* g, const int64_t* N, SegRows& out) {
+  if (g->num_segments <= 1) {
+    out = {1, N};
+    return MOLCLR_OK;
+  }
+  MOLCLR_REQUIRE(g->num_segments <= MOLCLR_MAX_SEGMENTS, "encoder: %d graph segments",
+                 g->num_segments);
+  int64_t tot = 0;
+  for (int s = 0; s < g->num_segments; ++s) tot += g->segment_nodes[s];
+  MOLCLR_REQUIRE(tot == *N, "encoder: segment nodes sum to %lld, graph has %lld", (long long)tot,
+                 (long long)*N);
+  out = {g->num_segments, g->segment_nodes};
   return MOLCLR_OK;
 }
 
@@ -101,6 +121,8 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   const int L = e->num_layer;
   const int64_t N = g->num_nodes, D = e->dim;
   if (N == 0) return MOLCLR_OK;
+  SegRows seg;
+  MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && h_out && arena, "gin_encoder_fwd: null pointer");
   const ArenaLayout lay(L, N, D);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
@@ -129,10 +151,11 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
     MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
                                        MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
                                        kws_bytes, stream));
-    MOLCLR_TRY(molclr_batchnorm_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                    e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                    A + lay.mean[l], A + lay.invstd[l], N, D, e->momentum, e->eps,
-                                    e->training, last ? 0 : 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                        e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                        A + lay.mean[l], A + lay.invstd[l], seg.n, seg.rows, D,
+                                        MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
+                                        last ? 0 : 1, kws, kws_bytes, stream));
     h = y;
   }
   return MOLCLR_OK;
@@ -149,6 +172,8 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   const int L = e->num_layer;
   const int64_t N = g->num_nodes, D = e->dim;
   if (N == 0) return MOLCLR_OK;
+  SegRows seg;
+  MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && dh_out && arena, "gin_encoder_bwd: null pointer");
   const ArenaLayout lay(L, N, D);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
@@ -169,9 +194,10 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     const float* z = A + lay.z[l];
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
-    MOLCLR_TRY(molclr_batchnorm_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
-                                    A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], N, D,
-                                    last ? 0 : 1, 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
+                                        A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l],
+                                        seg.n, seg.rows, D, MOLCLR_DTYPE_F32, last ? 0 : 1, 1,
+                                        kws, kws_bytes, stream));
     // second Linear (ops.linear_bwd order: dW with db, dx with the ReLU mask of a1)
     if (gr->mlp2_weight[l])
       MOLCLR_TRY(molclr_linear_wgrad(dz, a1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D, 2 * D, D,
@@ -229,8 +255,8 @@ struct GcnArena {
     for (int l = 0; l < L; ++l) {
       z[l] = off(N * D);
       h[l] = off(N * D);
-      mean[l] = off(D);
-      invstd[l] = off(D);
+      mean[l] = off(MOLCLR_MAX_SEGMENTS * D);  // [segment][D]
+      invstd[l] = off(MOLCLR_MAX_SEGMENTS * D);
     }
     h0 = off(N * D);
     total = used * sizeof(float);
@@ -242,7 +268,7 @@ size_t gcn_kernels_ws(int64_t N, int64_t D) {
   auto mx = [&](size_t v) { m = v > m ? v : m; };
   mx(molclr_gemm_f32_workspace_bytes(N, D, D));  // x W, dxw W^T
   mx(molclr_gemm_f32_workspace_bytes(D, D, N));  // dW = x^T dxw
-  mx(molclr_batchnorm_workspace_bytes(N, D));
+  mx(molclr_batchnorm_ws_bound(N, D));
   mx(molclr_gcn_aggregate_bwd_workspace_bytes(N, D));
   mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
   return m;
@@ -285,6 +311,8 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
   const int L = e->num_layer;
   const int64_t N = g->num_nodes, D = e->dim;
   if (N == 0) return MOLCLR_OK;
+  SegRows seg;
+  MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && h_out && arena, "gcn_encoder_fwd: null pointer");
   const GcnArena lay(L, N, D);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
@@ -308,10 +336,11 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
     MOLCLR_TRY(molclr_gcn_aggregate_fwd(xw, g->rowptr, g->col, g->ecode, g->nbr,
                                         e->edge_embedding1[l], e->edge_embedding2[l], e->bias[l],
                                         z, N, D, stream));
-    MOLCLR_TRY(molclr_batchnorm_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                    e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                    A + lay.mean[l], A + lay.invstd[l], N, D, e->momentum, e->eps,
-                                    e->training, last ? 0 : 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                        e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                        A + lay.mean[l], A + lay.invstd[l], seg.n, seg.rows, D,
+                                        MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
+                                        last ? 0 : 1, kws, kws_bytes, stream));
     h = y;
   }
   return MOLCLR_OK;
@@ -328,6 +357,8 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
   const int L = e->num_layer;
   const int64_t N = g->num_nodes, D = e->dim;
   if (N == 0) return MOLCLR_OK;
+  SegRows seg;
+  MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && dh_out && arena, "gcn_encoder_bwd: null pointer");
   const GcnArena lay(L, N, D);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
@@ -346,9 +377,10 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
     const float* xin = l == 0 ? A + lay.h0 : A + lay.h[l - 1];
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gcn_encoder_bwd: BatchNorm grads needed");
-    MOLCLR_TRY(molclr_batchnorm_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
-                                    A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], N, D,
-                                    last ? 0 : 1, 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
+                                        A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l],
+                                        seg.n, seg.rows, D, MOLCLR_DTYPE_F32, last ? 0 : 1, 1,
+                                        kws, kws_bytes, stream));
     // ops._GCNConv.backward order: aggregation (dxw, edge tables, bias), dW, dx
     MOLCLR_TRY(molclr_gcn_aggregate_bwd(dz, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dxw,
                                         gr->edge_embedding1[l], gr->edge_embedding2[l],

@@ -17,6 +17,23 @@ namespace {
 
 constexpr int kScanThreads = 1024;
 
+// The inputs as up to MOLCLR_MAX_SEGMENTS concatenated PyG batches (the two
+// contrastive views of a step built as one graph): segment s's nodes, edges
+// and graphs follow those of segments 0..s-1.
+struct GSegs {
+  int n;
+  const int64_t* ei[MOLCLR_MAX_SEGMENTS];
+  const int64_t* ea[MOLCLR_MAX_SEGMENTS];
+  const int64_t* batch[MOLCLR_MAX_SEGMENTS];
+  int64_t n0[MOLCLR_MAX_SEGMENTS + 1], e0[MOLCLR_MAX_SEGMENTS + 1], g0[MOLCLR_MAX_SEGMENTS + 1];
+};
+
+__device__ __forceinline__ int gseg(const int64_t* off, int n, int64_t k) {
+  int s = 0;
+  while (s + 1 < n && k >= off[s + 1]) ++s;
+  return s;
+}
+
 __global__ void k_graph_init(int32_t* __restrict__ ecount, int32_t* __restrict__ counters,
                              int64_t n_counters, int64_t N, int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -29,20 +46,24 @@ __global__ void k_graph_init(int32_t* __restrict__ ecount, int32_t* __restrict__
   }
 }
 
-__global__ void k_graph_count(const int64_t* __restrict__ ei, const int64_t* __restrict__ ea,
-                              int64_t N, int64_t E, int32_t* __restrict__ src32,
+__global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
                               int32_t* __restrict__ dst32, uint8_t* __restrict__ code8,
                               int32_t* __restrict__ indeg, int32_t* __restrict__ outdeg,
                               int32_t* __restrict__ ecount, int32_t* __restrict__ status) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= E) return;
-  int64_t s = ei[k], d = ei[E + k];
-  int64_t bt = ea[2 * k], bd = ea[2 * k + 1];
+  const int g = gseg(sg.e0, sg.n, k);
+  const int64_t kk = k - sg.e0[g], Eg = sg.e0[g + 1] - sg.e0[g];
+  const int64_t Ng = sg.n0[g + 1] - sg.n0[g];
+  const int64_t* ei = sg.ei[g];
+  const int64_t* ea = sg.ea[g];
+  int64_t s = ei[kk], d = ei[Eg + kk];
+  int64_t bt = ea[2 * kk], bd = ea[2 * kk + 1];
   int bad = 0;
-  if (s < 0 || s >= N || d < 0 || d >= N) {
+  if (s < 0 || s >= Ng || d < 0 || d >= Ng) {
     bad |= 1;
-    s = s < 0 ? 0 : (s >= N ? N - 1 : s);
-    d = d < 0 ? 0 : (d >= N ? N - 1 : d);
+    s = s < 0 ? 0 : (s >= Ng ? Ng - 1 : s);
+    d = d < 0 ? 0 : (d >= Ng ? Ng - 1 : d);
   }
   if (bt < 0 || bt >= MOLCLR_NUM_BOND_TYPE || bd < 0 || bd >= MOLCLR_NUM_BOND_DIR) {
     bad |= 2;
@@ -50,6 +71,8 @@ __global__ void k_graph_count(const int64_t* __restrict__ ei, const int64_t* __r
     bd = bd < 0 ? 0 : (bd >= MOLCLR_NUM_BOND_DIR ? MOLCLR_NUM_BOND_DIR - 1 : bd);
   }
   if (bad) atomicOr(status, bad);
+  s += sg.n0[g];
+  d += sg.n0[g];
   src32[k] = (int32_t)s;
   dst32[k] = (int32_t)d;
   code8[k] = (uint8_t)(bt | (bd << 3));
@@ -168,22 +191,32 @@ __global__ void k_graph_rows(int64_t N, const int32_t* __restrict__ src32,
   (csc ? nbr_t : nbr)[i] = make_uint4(slot[0], slot[1], slot[2], slot[3]);
 }
 
-__global__ void k_graph_ptr(const int64_t* __restrict__ batch, int64_t N, int64_t G,
-                            int32_t* __restrict__ graph_ptr, int32_t* __restrict__ status) {
+__global__ void k_graph_ptr(GSegs sg, int64_t N, int64_t G, int32_t* __restrict__ graph_ptr,
+                            int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < N) {
-    int64_t b = batch[t];
-    if (b < 0 || b >= G || (t > 0 && batch[t - 1] > b)) atomicOr(status, 4);
+    const int g = gseg(sg.n0, sg.n, t);
+    const int64_t* batch = sg.batch[g];
+    const int64_t i = t - sg.n0[g], Gg = sg.g0[g + 1] - sg.g0[g];
+    const int64_t b = batch[i];
+    if (b < 0 || b >= Gg || (i > 0 && batch[i - 1] > b)) atomicOr(status, 4);
   }
   if (t <= G) {
-    // lower_bound(batch, t)
-    int64_t lo = 0, hi = N;
-    while (lo < hi) {
-      int64_t mid = (lo + hi) >> 1;
-      if (batch[mid] < t) lo = mid + 1;
-      else hi = mid;
+    if (t == G) {
+      graph_ptr[t] = (int32_t)N;
+    } else {
+      // lower_bound(batch of t's segment, local graph id) + the segment's first node
+      const int g = gseg(sg.g0, sg.n, t);
+      const int64_t* batch = sg.batch[g];
+      const int64_t want = t - sg.g0[g];
+      int64_t lo = 0, hi = sg.n0[g + 1] - sg.n0[g];
+      while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (batch[mid] < want) lo = mid + 1;
+        else hi = mid;
+      }
+      graph_ptr[t] = (int32_t)(sg.n0[g] + lo);
     }
-    graph_ptr[t] = (int32_t)(t == G ? N : lo);
   }
 }
 
@@ -200,22 +233,45 @@ MOLCLR_API size_t molclr_graph_build_workspace_bytes(int64_t N, int64_t E) {
   return w.used + 256;
 }
 
-MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
-                                  const int64_t* batch, int64_t N, int64_t E, int64_t G,
-                                  int32_t* rowptr, int32_t* col, uint8_t* ecode,
-                                  int32_t* rowptr_t, int32_t* col_t, uint32_t* nbr,
-                                  uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
-                                  int32_t* status, void* workspace,
-                                  size_t workspace_bytes, molclr_stream_t stream) {
-  MOLCLR_REQUIRE(N >= 0 && E >= 0 && G >= 0, "graph_build: negative size");
+MOLCLR_API int molclr_graph_build_multi(int nseg, const molclr_graph_segment* segs,
+                                        int32_t* rowptr, int32_t* col, uint8_t* ecode,
+                                        int32_t* rowptr_t, int32_t* col_t, uint32_t* nbr,
+                                        uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
+                                        int32_t* status, void* workspace, size_t workspace_bytes,
+                                        molclr_stream_t stream) {
+  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && segs,
+                 "graph_build: %d segments (1..%d)", nseg, MOLCLR_MAX_SEGMENTS);
+  GSegs sg{};
+  sg.n = nseg;
+  for (int g = 0; g < nseg; ++g) {
+    const molclr_graph_segment& q = segs[g];
+    MOLCLR_REQUIRE(q.num_nodes >= 0 && q.num_edges >= 0 && q.num_graphs >= 0,
+                   "graph_build: negative size in segment %d", g);
+    sg.ei[g] = q.edge_index;
+    sg.ea[g] = q.edge_attr;
+    sg.batch[g] = q.batch;
+    sg.n0[g + 1] = sg.n0[g] + q.num_nodes;
+    sg.e0[g + 1] = sg.e0[g] + q.num_edges;
+    sg.g0[g + 1] = sg.g0[g] + q.num_graphs;
+  }
+  for (int g = nseg; g < MOLCLR_MAX_SEGMENTS; ++g) {
+    sg.n0[g + 1] = sg.n0[nseg];
+    sg.e0[g + 1] = sg.e0[nseg];
+    sg.g0[g + 1] = sg.g0[nseg];
+  }
+  const int64_t N = sg.n0[nseg], E = sg.e0[nseg], G = sg.g0[nseg];
   MOLCLR_REQUIRE(N <= MOLCLR_NBR_MAX_NODES && E < (int64_t)1 << 31,
                  "graph_build: %lld nodes exceed the neighbour-slot limit %d (or E > int32)",
                  (long long)N, MOLCLR_NBR_MAX_NODES);
+  for (int g = 0; g < nseg; ++g) {
+    MOLCLR_REQUIRE(segs[g].num_edges == 0 || (segs[g].edge_index && segs[g].edge_attr),
+                   "graph_build: null edge input in segment %d", g);
+    MOLCLR_REQUIRE(segs[g].num_nodes == 0 || segs[g].batch, "graph_build: null batch in segment %d",
+                   g);
+  }
   MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status && (N == 0 || (nbr && nbr_t)),
                  "graph_build: null output");
-  MOLCLR_REQUIRE(E == 0 || (edge_index && edge_attr && col && ecode && col_t),
-                 "graph_build: null edge buffer");
-  MOLCLR_REQUIRE(N == 0 || batch, "graph_build: null batch");
+  MOLCLR_REQUIRE(E == 0 || (col && ecode && col_t), "graph_build: null edge buffer");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_graph_build_workspace_bytes(N, E));
   hipStream_t s = molclr::as_stream(stream);
   molclr::Workspace w(workspace, workspace_bytes);
@@ -236,8 +292,8 @@ MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge
   hipLaunchKernelGGL(k_graph_init, dim3(molclr::ceil_div(n_init, T)), dim3(T), 0, s, ecount,
                      counters, 4 * N, N, status);
   if (E > 0) {
-    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, edge_index,
-                       edge_attr, N, E, src32, dst32, code8, indeg, outdeg, ecount, status);
+    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, sg, E, src32,
+                       dst32, code8, indeg, outdeg, ecount, status);
   }
   hipLaunchKernelGGL(k_scan2, dim3(2), dim3(kScanThreads), 0, s, indeg, rowptr, outdeg, rowptr_t,
                      N);
@@ -251,8 +307,20 @@ MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge
                        (uint4*)nbr, (uint4*)nbr_t);
   }
   int64_t n_ptr = N > G + 1 ? N : G + 1;
-  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, batch, N, G,
+  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, sg, N, G,
                      graph_ptr, status);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
+                                  const int64_t* batch, int64_t N, int64_t E, int64_t G,
+                                  int32_t* rowptr, int32_t* col, uint8_t* ecode,
+                                  int32_t* rowptr_t, int32_t* col_t, uint32_t* nbr,
+                                  uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
+                                  int32_t* status, void* workspace,
+                                  size_t workspace_bytes, molclr_stream_t stream) {
+  const molclr_graph_segment seg{edge_index, edge_attr, batch, N, E, G};
+  return molclr_graph_build_multi(1, &seg, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount,
+                                  graph_ptr, status, workspace, workspace_bytes, stream);
 }

@@ -731,6 +731,15 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
 
 }  // namespace
 
+// Workspace that covers any split of `rows` rows into <= MOLCLR_MAX_SEGMENTS
+// segments (the encoder executors size their scratch before knowing it).
+size_t molclr_batchnorm_ws_bound(int64_t rows, int64_t D) {
+  const molclr::Band b = molclr::make_band(D > 0 ? D : 4);
+  int64_t P = molclr::ceil_div(rows, (int64_t)b.band * 16) + MOLCLR_MAX_SEGMENTS;
+  if (P > (int64_t)MOLCLR_MAX_SEGMENTS * 1024) P = (int64_t)MOLCLR_MAX_SEGMENTS * 1024;
+  return bn_ws_bytes(P, D, MOLCLR_MAX_SEGMENTS);
+}
+
 MOLCLR_API size_t molclr_batchnorm_seg_workspace_bytes(int nseg, const int64_t* seg_rows,
                                                        int64_t D) {
   Segs sg;

@@ -10,6 +10,7 @@ PyG's per-layer ``add_self_loops`` + scatter bookkeeping.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Iterable, Sequence
 
 import torch
@@ -111,24 +112,49 @@ def _num_graphs_of(data) -> int:
 
 class DeviceGraph:
     """Destination CSR / source CSC / bond-type counts / graph offsets of one
-    batch, built on the GPU by ``molclr_graph_build`` (graph.hip)."""
+    batch, built on the GPU by ``molclr_graph_build`` (graph.hip).
+
+    :meth:`union` builds the graph of several batches taken as one
+    (``molclr_graph_build_multi``): the two contrastive views of a step run
+    through one encoder pass, ``segment_nodes`` telling the executors where
+    each view's rows start (their BatchNorm statistics stay per view)."""
 
     def __init__(self, edge_index: torch.Tensor, edge_attr: torch.Tensor, num_nodes: int,
                  batch: torch.Tensor | None = None, num_graphs: int | None = None):
         dev = edge_index.device
+        if batch is None:
+            batch = torch.zeros(int(num_nodes), dtype=torch.long, device=dev)
+            num_graphs = 1 if int(num_nodes) > 0 else 0
+        self._build([(edge_index, edge_attr, batch, int(num_nodes), int(num_graphs))])
+
+    @classmethod
+    def union(cls, parts) -> "DeviceGraph":
+        """parts: (edge_index, edge_attr, batch, num_nodes, num_graphs) per batch."""
+        g = cls.__new__(cls)
+        g._build(list(parts))
+        return g
+
+    def _build(self, parts):
+        dev = parts[0][0].device
         if dev.type != "cuda":
             raise RuntimeError("DeviceGraph: molclr_amd runs on the GPU only (got %s)" % dev)
-        N = int(num_nodes)
-        E = int(edge_index.shape[1])
-        if batch is None:
-            batch = torch.zeros(N, dtype=torch.long, device=dev)
-            num_graphs = 1 if N > 0 else 0
-        G = int(num_graphs)
-        edge_index = edge_index.to(torch.long).contiguous()
-        edge_attr = edge_attr.to(torch.long).contiguous()
-        batch = batch.to(torch.long).contiguous()
+        if not 1 <= len(parts) <= _lib.MAX_SEGMENTS:
+            raise ValueError(f"DeviceGraph: {len(parts)} segments (1..{_lib.MAX_SEGMENTS})")
+        keep = []  # the int64 inputs must outlive the (asynchronous) build
+        segs = (_lib.GraphSegmentC * len(parts))()
+        for q, (ei, ea, b, n, G) in enumerate(parts):
+            ei = ei.to(torch.long).contiguous()
+            ea = ea.to(torch.long).contiguous()
+            b = b.to(torch.long).contiguous()
+            keep += [ei, ea, b]
+            segs[q] = _lib.GraphSegmentC(ei.data_ptr(), ea.data_ptr(), b.data_ptr(), int(n),
+                                         int(ei.shape[1]), int(G))
+        N = sum(int(p[3]) for p in parts)
+        E = sum(int(segs[q].num_edges) for q in range(len(parts)))
+        G = sum(int(p[4]) for p in parts)
         i32 = dict(dtype=torch.int32, device=dev)
         self.num_nodes, self.num_edges, self.num_graphs = N, E, G
+        self.segment_nodes = [int(p[3]) for p in parts]
         self.rowptr = torch.empty(N + 1, **i32)
         self.col = torch.empty(max(E, 1), **i32)
         self.ecode = torch.empty(max(E, 1), dtype=torch.uint8, device=dev)
@@ -141,11 +167,11 @@ class DeviceGraph:
         self.status = torch.empty(1, **i32)
         ws_bytes = _lib.query("molclr_graph_build_workspace_bytes", N, E)
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        _lib.call("molclr_graph_build", edge_index.data_ptr(), edge_attr.data_ptr(),
-                  batch.data_ptr(), N, E, G, self.rowptr.data_ptr(), self.col.data_ptr(),
-                  self.ecode.data_ptr(), self.rowptr_t.data_ptr(), self.col_t.data_ptr(),
-                  self.nbr.data_ptr(), self.nbr_t.data_ptr(), self.ecount.data_ptr(), self.graph_ptr.data_ptr(), self.status.data_ptr(),
-                  ws.data_ptr(), ws_bytes, _lib.stream_of(dev))
+        _lib.call("molclr_graph_build_multi", len(parts), ctypes.addressof(segs),
+                  self.rowptr.data_ptr(), self.col.data_ptr(), self.ecode.data_ptr(),
+                  self.rowptr_t.data_ptr(), self.col_t.data_ptr(), self.nbr.data_ptr(),
+                  self.nbr_t.data_ptr(), self.ecount.data_ptr(), self.graph_ptr.data_ptr(),
+                  self.status.data_ptr(), ws.data_ptr(), ws_bytes, _lib.stream_of(dev))
         self.device = dev
 
     def cstruct(self):
@@ -156,6 +182,9 @@ class DeviceGraph:
                 t.data_ptr() for t in (self.rowptr, self.col, self.rowptr_t, self.col_t,
                                        self.ecount, self.graph_ptr, self.ecode, self.nbr,
                                        self.nbr_t)])
+            c.num_segments = len(self.segment_nodes)
+            for q, n in enumerate(self.segment_nodes):
+                c.segment_nodes[q] = n
             self._cstruct = c
         return c
 
@@ -171,6 +200,26 @@ class DeviceGraph:
             if st & 4:
                 what.append("batch not ascending / out of range")
             raise ValueError("invalid graph batch: " + ", ".join(what))
+
+
+def pair_graph(xi, xj) -> DeviceGraph:
+    """The graph of both views of a step as one (view i first), cached on xi."""
+    g = getattr(xi, "_molclr_pair_graph", None)
+    if g is not None and g[0] is xj and g[1].device == xi.edge_index.device:
+        return g[1]
+    parts = []
+    for d in (xi, xj):
+        b = getattr(d, "batch", None)
+        n = int(d.x.shape[0])
+        if b is None:
+            b = torch.zeros(n, dtype=torch.long, device=d.edge_index.device)
+        parts.append((d.edge_index, d.edge_attr, b, n, _num_graphs_of(d)))
+    g = DeviceGraph.union(parts)
+    try:
+        xi._molclr_pair_graph = (xj, g)
+    except AttributeError:
+        pass
+    return g
 
 
 def device_graph(data) -> DeviceGraph:

@@ -20,7 +20,7 @@ from torch import nn
 from torch.nn import Parameter
 
 from . import ops
-from .data import DeviceGraph, device_graph
+from .data import DeviceGraph, device_graph, pair_graph
 
 num_atom_type = 119  # including the extra mask tokens
 num_chirality_tag = 3
@@ -122,14 +122,18 @@ class GCN(nn.Module):
                    and bn.training == bn0.training and bn.momentum == bn0.momentum
                    and bn.eps == bn0.eps for bn in self.batch_norms)
 
+    def _encoder_params(self):
+        params = [self.x_embedding1.weight, self.x_embedding2.weight]
+        for g, bn in zip(self.gnns, self.batch_norms):
+            params += [g.weight, g.bias, g.edge_embedding1.weight, g.edge_embedding2.weight,
+                       bn.weight, bn.bias]
+        return params
+
     def encode(self, data, graph: DeviceGraph | None = None):
         graph = graph or device_graph(data)
         if self._executor_ok():
-            params = [self.x_embedding1.weight, self.x_embedding2.weight]
-            for g, bn in zip(self.gnns, self.batch_norms):
-                params += [g.weight, g.bias, g.edge_embedding1.weight, g.edge_embedding2.weight,
-                           bn.weight, bn.bias]
-            return ops.gcn_encoder(data.x, graph, list(self.batch_norms), params), graph
+            return ops.gcn_encoder(data.x, graph, list(self.batch_norms),
+                                   self._encoder_params()), graph
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         for layer in range(self.num_layer):
             h = self.gnns[layer].conv(h, graph)
@@ -139,10 +143,25 @@ class GCN(nn.Module):
                 h = F.dropout(h, self.drop_ratio, training=True)
         return h, graph
 
-    def forward(self, data):
-        h, graph = self.encode(data)
+    def _readout(self, h, graph):
         h = ops.segment_pool(h, graph, self.pool)
         h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
         out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
                                   self.out_lin[2].weight, self.out_lin[2].bias)
         return h, out
+
+    def forward(self, data):
+        h, graph = self.encode(data)
+        return self._readout(h, graph)
+
+    def forward_pair(self, xi, xj):
+        """Both views in one pass, per-view BatchNorm statistics (see
+        GINet.forward_pair): rows of forward(xi) then forward(xj)."""
+        if not self._executor_ok():
+            hi, oi = self(xi)
+            hj, oj = self(xj)
+            return torch.cat([hi, hj], 0), torch.cat([oi, oj], 0)
+        graph = pair_graph(xi, xj)
+        x = torch.cat([xi.x, xj.x], 0)
+        h = ops.gcn_encoder(x, graph, list(self.batch_norms), self._encoder_params())
+        return self._readout(h, graph)

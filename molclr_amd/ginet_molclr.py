@@ -14,7 +14,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import ops
-from .data import DeviceGraph, device_graph
+from .data import DeviceGraph, device_graph, pair_graph
 
 num_atom_type = 119  # including the extra mask tokens
 num_chirality_tag = 3
@@ -112,15 +112,19 @@ class GINet(nn.Module):
                    and bn.training == bn0.training and bn.momentum == bn0.momentum
                    and bn.eps == bn0.eps for bn in self.batch_norms)
 
+    def _encoder_params(self):
+        params = [self.x_embedding1.weight, self.x_embedding2.weight]
+        for g, bn in zip(self.gnns, self.batch_norms):
+            params += [g.mlp[0].weight, g.mlp[0].bias, g.mlp[2].weight, g.mlp[2].bias,
+                       g.edge_embedding1.weight, g.edge_embedding2.weight, bn.weight, bn.bias]
+        return params
+
     def encode(self, data, graph: DeviceGraph | None = None):
         """Node embeddings after the last layer (ginet_molclr.py:103-111)."""
         graph = graph or device_graph(data)
         if self._executor_ok():
-            params = [self.x_embedding1.weight, self.x_embedding2.weight]
-            for g, bn in zip(self.gnns, self.batch_norms):
-                params += [g.mlp[0].weight, g.mlp[0].bias, g.mlp[2].weight, g.mlp[2].bias,
-                           g.edge_embedding1.weight, g.edge_embedding2.weight, bn.weight, bn.bias]
-            return ops.gin_encoder(data.x, graph, list(self.batch_norms), params), graph
+            return ops.gin_encoder(data.x, graph, list(self.batch_norms),
+                                   self._encoder_params()), graph
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         # per-edge embeddings E1[bt] + E2[bd] of every layer, tabulated in one launch
         Ec = ops.edge_tables_combine([g.edge_embedding1.weight for g in self.gnns],
@@ -133,10 +137,30 @@ class GINet(nn.Module):
                 h = F.dropout(h, self.drop_ratio, training=True)
         return h, graph
 
-    def forward(self, data):
-        h, graph = self.encode(data)
+    def _readout(self, h, graph):
         h = ops.segment_pool(h, graph, self.pool)
         h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
         out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
                                   self.out_lin[2].weight, self.out_lin[2].bias)
         return h, out
+
+    def forward(self, data):
+        h, graph = self.encode(data)
+        return self._readout(h, graph)
+
+    def forward_pair(self, xi, xj):
+        """Both contrastive views of a step in ONE pass: ``(h, out)`` with the
+        rows of ``forward(xi)`` followed by those of ``forward(xj)``
+        (molclr.py:57,60).  The views' graphs are built as one
+        (molclr_graph_build_multi) and every BatchNorm keeps per-view batch
+        statistics, updating its running statistics for view i, then view j
+        (molclr_batchnorm_seg_fwd) -- the two-call semantics, with half the
+        launches and twice the rows per GEMM / aggregation launch."""
+        if not self._executor_ok():
+            hi, oi = self(xi)
+            hj, oj = self(xj)
+            return torch.cat([hi, hj], 0), torch.cat([oi, oj], 0)
+        graph = pair_graph(xi, xj)
+        x = torch.cat([xi.x, xj.x], 0)
+        h = ops.gin_encoder(x, graph, list(self.batch_norms), self._encoder_params())
+        return self._readout(h, graph)

@@ -89,6 +89,12 @@ class MolCLR(object):
         return rank, world, device
 
     def _step(self, model, xis, xjs, n_iter):
+        """molclr.py:55-67.  Both views go through ONE encoder pass
+        (model.forward_pair: per-view BatchNorm statistics, the reference's
+        two-call semantics); F.normalize and NT-Xent on the stacked [zis; zjs]."""
+        if getattr(self, "paired", True) and hasattr(model, "forward_pair"):
+            _, z = model.forward_pair(xis, xjs)
+            return self.nt_xent_criterion.forward_pair(l2_normalize(z))
         ris, zis = model(xis)  # [N,C]
         rjs, zjs = model(xjs)  # [N,C]
         zis = l2_normalize(zis)

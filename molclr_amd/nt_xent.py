@@ -43,3 +43,9 @@ class NTXentLoss(torch.nn.Module):
     def forward(self, zis, zjs):
         return ops.nt_xent(zis, zjs, self.batch_size, self.temperature,
                            self.use_cosine_similarity, self.group)
+
+    def forward_pair(self, z):
+        """The loss of a paired forward's projections z = [zis; zjs]
+        (GINet.forward_pair): the same value as forward(z[:B], z[B:])."""
+        return ops.nt_xent_pair(z, self.batch_size, self.temperature,
+                                self.use_cosine_similarity, self.group)

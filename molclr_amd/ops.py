@@ -604,16 +604,17 @@ class _L2Normalize(torch.autograd.Function):
 
 
 class _NTXent(torch.autograd.Function):
-    """NT-Xent over R = [zj; zi].  With a ``group`` (torch.distributed) the
-    batch is the global one: rows are this rank's, columns are gathered."""
+    """NT-Xent over this process's rows R = [zj; zi] (utils/nt_xent.py:48).
+    With a ``group`` (torch.distributed) the batch is the global one: rows
+    are this rank's, columns are gathered (molclr_amd.distributed)."""
 
     @staticmethod
-    def forward(ctx, zis, zjs, batch_size, temperature, cosine, group):
-        _check(zis, zjs)
-        dev = zis.device
-        Bl, C = zis.shape
-        R = torch.cat([_c(zjs), _c(zis)], 0)
-        n = R.shape[0]
+    def forward(ctx, R, batch_size, temperature, cosine, group):
+        _check(R)
+        dev = R.device
+        R = _c(R)
+        n, C = R.shape
+        Bl = n // 2
         rhat = torch.empty_like(R)
         norm = torch.empty(n, dtype=torch.float32, device=dev)
         st = _lib.stream_of(dev)
@@ -652,13 +653,13 @@ class _NTXent(torch.autograd.Function):
             lse_cols = mdist.gather_lse(lse, group)
             dist.all_reduce(loss, group=group)
         ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols)
-        ctx.meta = (B, Bl, C, float(temperature), int(cosine))
+        ctx.meta = (B, C, float(temperature), int(cosine))
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
         rhat, norm, cols, gidx, lse_cols = ctx.saved_tensors
-        B, Bl, C, T, cosine = ctx.meta
+        B, C, T, cosine = ctx.meta
         dev = rhat.device
         n = rhat.shape[0]
         gloss = gloss.to(torch.float32).contiguous()
@@ -672,7 +673,7 @@ class _NTXent(torch.autograd.Function):
         dR = torch.empty_like(rhat)
         _lib.call("molclr_ntxent_prep_bwd", drhat.data_ptr(), rhat.data_ptr(), norm.data_ptr(),
                   dR.data_ptr(), n, C, cosine, st)
-        return dR[Bl:], dR[:Bl], None, None, None, None
+        return dR, None, None, None, None
 
 
 GIN_PARAMS_PER_LAYER = 8  # mlp0.W, mlp0.b, mlp2.W, mlp2.b, edge_emb1, edge_emb2, bn.W, bn.b
@@ -922,4 +923,15 @@ def l2_normalize(z, eps: float = 1e-12):
 
 
 def nt_xent(zis, zjs, batch_size, temperature, use_cosine_similarity=True, group=None):
-    return _NTXent.apply(zis, zjs, batch_size, temperature, bool(use_cosine_similarity), group)
+    """NTXentLoss.forward(zis, zjs): R = [zjs; zis] (utils/nt_xent.py:48)."""
+    _check(zis, zjs)
+    return _NTXent.apply(torch.cat([zjs, zis], 0), batch_size, temperature,
+                         bool(use_cosine_similarity), group)
+
+
+def nt_xent_pair(z, batch_size, temperature, use_cosine_similarity=True, group=None):
+    """NT-Xent of a paired forward's projections z = [zis; zjs] (one tensor)."""
+    _check(z)
+    B = z.shape[0] // 2
+    return _NTXent.apply(torch.cat([z[B:], z[:B]], 0), batch_size, temperature,
+                         bool(use_cosine_similarity), group)

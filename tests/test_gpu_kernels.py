@@ -612,3 +612,91 @@ def test_gine_aggregate_bn_fwd_matches_materialised(dev, training, relu, D):
                                     i2.data_ptr(), N, D, 0.1, 1e-5, training, relu,
                                     ws.data_ptr(), wsb, None) == 0
     assert torch.equal(m2, mean) and torch.equal(i2, invstd)
+
+
+# ---------------------------------------------------------------------------
+# the paired (both views in one pass) building blocks
+def test_graph_build_multi_equals_concatenated_batch(dev):
+    """molclr_graph_build_multi over (view i, view j) == molclr_graph_build over
+    the PyG collate of the two batches (node / graph offsets), bit for bit."""
+    from molclr_amd.data import Batch, DeviceGraph
+    bi, bj = SyntheticPairBatches(37, seed=3).next()
+    g2 = DeviceGraph.union([(b.edge_index.to(dev), b.edge_attr.to(dev), b.batch.to(dev),
+                             b.x.shape[0], b.num_graphs) for b in (bi, bj)])
+    g2.check()
+    Ni = bi.x.shape[0]
+    cat = Batch(x=torch.cat([bi.x, bj.x]), edge_index=torch.cat([bi.edge_index, bj.edge_index + Ni], 1),
+                edge_attr=torch.cat([bi.edge_attr, bj.edge_attr]),
+                batch=torch.cat([bi.batch, bj.batch + bi.num_graphs]))
+    g1 = DeviceGraph(cat.edge_index.to(dev), cat.edge_attr.to(dev), cat.x.shape[0],
+                     cat.batch.to(dev), 74)
+    E = cat.edge_index.shape[1]
+    for name in ("rowptr", "rowptr_t", "nbr", "nbr_t", "ecount", "graph_ptr"):
+        assert torch.equal(getattr(g1, name), getattr(g2, name)), name
+    for name in ("col", "ecode", "col_t"):
+        assert torch.equal(getattr(g1, name)[:E], getattr(g2, name)[:E]), name
+    assert g2.segment_nodes == [Ni, bj.x.shape[0]]
+    # an out-of-range index in the second segment is flagged
+    bad = bj.edge_index.clone()
+    bad[0, 0] = bj.x.shape[0]
+    g3 = DeviceGraph.union([(bi.edge_index.to(dev), bi.edge_attr.to(dev), bi.batch.to(dev), Ni, 37),
+                            (bad.to(dev), bj.edge_attr.to(dev), bj.batch.to(dev), bj.x.shape[0], 37)])
+    with pytest.raises(ValueError, match="edge_index"):
+        g3.check()
+
+
+@pytest.mark.parametrize("rows,D", [((15300, 15256), 300), ((7, 3), 64), ((1950, 2001, 40), 128)])
+def test_batchnorm_segments_equal_separate_calls(dev, rows, D):
+    """Segmented BatchNorm == one call per segment, bit for bit: outputs, saved
+    statistics, running statistics (updated in segment order), num_batches_tracked,
+    and the backward (dz, dgamma / dbeta summed over the segments in order)."""
+    import ctypes
+    from molclr_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(sum(rows))
+    N = sum(rows)
+    z = (torch.randn(N, D) * 2 + 0.5).to(dev)
+    dy = torch.randn(N, D).to(dev)
+    gamma, beta = (torch.rand(D) + 0.5).to(dev), torch.randn(D).to(dev)
+    S = len(rows)
+    seg = (ctypes.c_int64 * S)(*rows)
+    wsb = lib.molclr_batchnorm_seg_workspace_bytes(S, seg, D)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    rm, rv = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+    y = torch.empty(N, D, device=dev)
+    sm, si = torch.empty(S, D, device=dev), torch.empty(S, D, device=dev)
+    assert lib.molclr_batchnorm_seg_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
+                                        rv.data_ptr(), nbt.data_ptr(), y.data_ptr(), sm.data_ptr(),
+                                        si.data_ptr(), S, seg, D, 0, 0.1, 1e-5, 1, 1, ws.data_ptr(),
+                                        wsb, None) == 0
+    dz = torch.empty(N, D, device=dev)
+    dg, db = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    assert lib.molclr_batchnorm_seg_bwd(dy.data_ptr(), z.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                        sm.data_ptr(), si.data_ptr(), dz.data_ptr(), dg.data_ptr(),
+                                        db.data_ptr(), S, seg, D, 0, 1, 0, ws.data_ptr(), wsb,
+                                        None) == 0
+    # one call per segment
+    rm2, rv2 = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    nbt2 = torch.zeros(1, dtype=torch.int64, device=dev)
+    y2, dz2 = torch.empty(N, D, device=dev), torch.empty(N, D, device=dev)
+    dg2, db2 = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    r0 = 0
+    for s, r in enumerate(rows):
+        m1, i1 = torch.empty(D, device=dev), torch.empty(D, device=dev)
+        w1 = lib.molclr_batchnorm_workspace_bytes(r, D)
+        ws1 = torch.empty(w1, dtype=torch.uint8, device=dev)
+        assert lib.molclr_batchnorm_fwd(z[r0:].data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                        rm2.data_ptr(), rv2.data_ptr(), nbt2.data_ptr(),
+                                        y2[r0:].data_ptr(), m1.data_ptr(), i1.data_ptr(), r, D, 0.1,
+                                        1e-5, 1, 1, ws1.data_ptr(), w1, None) == 0
+        assert torch.equal(m1, sm[s]) and torch.equal(i1, si[s])
+        assert lib.molclr_batchnorm_bwd(dy[r0:].data_ptr(), z[r0:].data_ptr(), gamma.data_ptr(),
+                                        beta.data_ptr(), m1.data_ptr(), i1.data_ptr(),
+                                        dz2[r0:].data_ptr(), dg2.data_ptr(), db2.data_ptr(), r, D,
+                                        1, int(s > 0), ws1.data_ptr(), w1, None) == 0
+        r0 += r
+    torch.cuda.synchronize()
+    for a, b in ((y, y2), (rm, rm2), (rv, rv2), (nbt, nbt2), (dz, dz2), (dg, dg2), (db, db2)):
+        assert torch.equal(a, b)
+    assert int(nbt) == S

@@ -4,9 +4,12 @@ same augmented batches; fp32 norm-wise relative tolerance 1e-5.
 
 The oracle is evaluated in fp64 as well as fp32: the fp64 evaluation is the
 exact result of the reference algorithm, while the fp32 CPU result depends on
-the host (on the GPU box's host the fp32 oracle's backward lands 4e-4 away from
-fp64 for GIN layers below the last, on the build container's host 2e-6; the HIP
-path lands ~1e-6 away on both).  Gradients are therefore judged against fp64."""
+the host.  Gradients are therefore judged against fp64: at the c1 shape the
+HIP path lands ~1e-6 away; at c2 / c3 the step's gradients are
+ill-conditioned (F.normalize + NT-Xent at random init and five BatchNorm
+backwards cancel most of every term), the reference's own fp32 gradients land
+up to 3e-3 from fp64 and the HIP path 1.5e-3 (gpurun_out/errs from a -m gpu
+run with MOLCLR_RECORD_ERRS set)."""
 import copy
 import json
 import os
@@ -322,3 +325,62 @@ def test_gcn_encoder_executor_matches_per_op_path(dev, L, D, B):
     b.eval()
     with torch.no_grad():
         assert torch.equal(a.encode(xi)[0], b.encode(xi)[0])
+
+
+@pytest.mark.parametrize("kind,L,D,B", [("gin", 5, 300, 512), ("gcn", 5, 300, 512),
+                                        ("gin", 3, 128, 33), ("gcn", 2, 64, 8)])
+def test_paired_forward_matches_two_calls(dev, kind, L, D, B):
+    """forward_pair(xi, xj) -- both views in ONE encoder pass, per-view
+    (segmented) BatchNorm statistics -- against the reference's two calls
+    model(xi), model(xj) (molclr.py:57,60): outputs, loss, running statistics
+    and every gradient within 1e-5.  (Not bitwise: with twice the rows a GEMM
+    may pick another K-group split -- k_gemm_q6 sums K in two in-block groups
+    for narrow launches -- and the weight gradients sum over both views at
+    once; both are fp32 reorderings.)"""
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    _, _, a = pair_models(kind, L, D, 512, seed=4)
+    a = a.to(dev)
+    b = copy.deepcopy(a)
+    xi, xj = SyntheticPairBatches(B, seed=B + L).next()
+    xi, xj = xi.to(dev), xj.to(dev)
+    crit = NTXentLoss(dev, B, 0.1, True)
+    hi, oi = a(xi)
+    hj, oj = a(xj)
+    la = crit(l2_normalize(oi), l2_normalize(oj))
+    la.backward()
+    hp, op = b.forward_pair(xi, xj)
+    lb = crit.forward_pair(l2_normalize(op))
+    lb.backward()
+    assert rel(hp, torch.cat([hi, hj])) < TOL and rel(op, torch.cat([oi, oj])) < TOL
+    assert abs(la.item() - lb.item()) <= TOL * abs(la.item())
+    ba = dict(a.named_buffers())
+    for n, buf in b.named_buffers():
+        if n.endswith("num_batches_tracked"):
+            assert int(buf) == int(ba[n]) == 2
+        else:
+            assert rel(buf, ba[n]) < TOL, n
+    pa = dict(a.named_parameters())
+    total = torch.cat([p.grad.flatten() for p in pa.values()]).norm().item()
+    for n, p in b.named_parameters():
+        if pre_bn_bias(n):
+            assert p.grad.norm().item() <= 1e-5 * total, n
+        else:
+            assert rel(p.grad, pa[n].grad) < 1e-5, n
+
+
+def test_paired_step_trainer_and_eval(dev):
+    """MolCLR._step uses the paired pass; in eval mode (validation) the paired
+    pass equals the two-call pass with running statistics."""
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(0)
+    m = GINet(3, 64, 128).to(dev)
+    xi, xj = SyntheticPairBatches(16, seed=2).next()
+    xi, xj = xi.to(dev), xj.to(dev)
+    m(xi), m(xj)  # populate running statistics
+    m.eval()
+    with torch.no_grad():
+        hp, op = m.forward_pair(xi, xj)
+        hi, oi = m(xi)
+        hj, oj = m(xj)
+    assert rel(op, torch.cat([oi, oj])) < 1e-6 and rel(hp, torch.cat([hi, hj])) < 1e-6
