@@ -48,7 +48,12 @@ CONFIGS = {
                shape="uniform", desc="c2: GIN 5x300 feat 512, batch 512/GPU, 10-50 atom graphs"),
     "c3": dict(model_type="gcn", num_layer=5, emb_dim=300, feat_dim=512, batch=512,
                shape="uniform", desc="c3: GCN 5x300 feat 512, batch 512/GPU, 10-50 atom graphs"),
+    "c5": dict(model_type="gin", num_layer=5, emb_dim=512, feat_dim=512, batch=1024,
+               shape="pubchem", precision="bf16",
+               desc="c5: GIN 5x512 feat 512, bf16 (fp32 accumulation), batch 1024/GPU, "
+                    "PubChem-shaped graphs (atoms ~ N(27, 9) clipped to [6, 80])"),
 }
+BF16_MFMA_PEAK_TFS = 2500.0
 
 
 def parse():
@@ -132,11 +137,14 @@ def main():
 
     # ---- model / optimiser / loss ---------------------------------------------
     torch.manual_seed(0)
+    precision = cfg.get("precision", "fp32")
     if cfg["model_type"] == "gin":
-        from molclr_amd.ginet_molclr import GINet as M
+        from molclr_amd.ginet_molclr import GINet
+        model = GINet(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"],
+                      precision=precision).to(dev)
     else:
-        from molclr_amd.gcn_molclr import GCN as M
-    model = M(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"]).to(dev)
+        from molclr_amd.gcn_molclr import GCN
+        model = GCN(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"]).to(dev)
     opt = FusedAdam(model.parameters(), 5e-4, weight_decay=1e-5)
     mdist.broadcast_params(opt.flat)
     group = torch.distributed.group.WORLD if world > 1 else None
@@ -238,10 +246,11 @@ def main():
             per_launch_s = agg["ms"] / agg["launches"] / 1e3
             per_launch_bytes = agg["work"] / agg["launches"]
             achieved = per_launch_bytes / per_launch_s / 1e9
-            roofline = {"kernel": "molclr_gine_aggregate_fwd (k_gine_agg_fwd)", "bound": "hbm",
+            roofline = {"kernel": ("molclr_gine_aggregate_fwd_bf16" if precision == "bf16" else
+                                   "molclr_gine_aggregate_fwd") + " (k_gine_agg_fwd)", "bound": "hbm",
                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": load_pmc_traffic(),
+                        "traffic": load_pmc_traffic(args.config, args.two_pass),
                         "bytes_per_launch": int(per_launch_bytes),
                         "us_per_launch": round(per_launch_s * 1e6, 2),
                         "launches": agg["launches"],
@@ -249,9 +258,12 @@ def main():
         gm = s.get("gemm_f32")
         if gm:
             tfs = gm["work"] / (gm["ms"] / 1e3) / 1e12
-            roofline_mfma = {"kernel": "molclr_gemm_f32 (all launches)", "bound": "mfma",
-                             "achieved": round(tfs, 2), "peak": FP32_MFMA_PEAK_TFS,
-                             "unit": "TFLOP/s", "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
+            peak = BF16_MFMA_PEAK_TFS if precision == "bf16" else FP32_MFMA_PEAK_TFS
+            roofline_mfma = {"kernel": ("molclr_gemm_bf16 / _linear_wgrad_bf16 encoder GEMMs + "
+                                        "the fp32 head GEMMs" if precision == "bf16" else
+                                        "molclr_gemm_f32 (all launches)"), "bound": "mfma",
+                             "achieved": round(tfs, 2), "peak": peak,
+                             "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
                              "traffic": None, "launches": gm["launches"],
                              "ms_per_step": round(gm["ms"] / args.mfma_steps, 3),
                              "timing": f"dispatch events over {args.mfma_steps} extra steps "
@@ -260,7 +272,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(rank, "timing the CPU baseline (oracle) ...")
-        cpu = cpu_baseline(cfg, batches_cpu, args.cpu_steps)
+        # c5's oracle step (fp32, 2B = 2048 broadcast cosine) takes tens of
+        # seconds: one timed step after the warm-up bounds the sample
+        cpu = cpu_baseline(cfg, batches_cpu, 1 if args.config == "c5" else args.cpu_steps)
 
     if rank == 0:
         line = {
@@ -268,7 +282,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
             "median_ms_per_step": round(median_ms, 3),
             "median_value": round(B * world / (median_ms / 1e3), 1),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16" if precision == "bf16" else "f32",
             "data": f"synthetic: {args.batches} resident pre-built batch pairs per rank "
                     f"(SURVEY §8d generator, node-mask views), random-init weights",
             "config": {"workload": cfg["desc"], "model": f"{cfg['model_type']} "
@@ -289,10 +304,12 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def load_pmc_traffic():
-    """HBM bytes per aggregation launch from the committed PMC summary
-    (profiles/*pmc_gine_agg*.json, written by tools/pmc_traffic.py), or None."""
-    cands = sorted((ROOT / "profiles").glob("*pmc_gine_agg*.json"))
+def load_pmc_traffic(config: str, two_pass: bool):
+    """HBM bytes per aggregation launch from the committed PMC summary of the
+    same workload (profiles/*pmc_gine_agg_<config>[_pair].json, written by
+    tools/pmc_traffic.py), or None."""
+    tag = f"{config}{'' if two_pass else '_pair'}"
+    cands = sorted((ROOT / "profiles").glob(f"*pmc_gine_agg_{tag}.json"))
     if not cands:
         return None
     try:

@@ -252,15 +252,17 @@ int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t
                     int64_t ldaux, void* workspace, size_t workspace_bytes,
                     molclr_stream_t stream);
 
-/* Implementation switch (process-wide, not thread-safe): 0 = f32-input MFMA
- * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 1 = split-bf16 ("x6": each fp32
+/* molclr_gemm_f32 with the implementation chosen per call (tests and
+ * benchmarks; molclr_gemm_f32 is impl = -1): -1 = automatic (split-bf16 "p6",
+ * or "w6" for a long-K weight gradient), 0 = f32-input MFMA
+ * (v_mfma_f32_32x32x2_f32), 64x64 tiles; 5 / 6 = split-bf16 "p6" (each fp32
  * operand split into 3 round-to-nearest bf16 parts, six bf16 MFMA products,
- * fp32 accumulation; fp32-GEMM accuracy), 64x64 tiles; 2 = split-bf16, 128x64;
- * 3 = split-bf16, 128x128; 4 = split-bf16 with all nine products, 64x64;
- * 5 (default) / 6 = split-bf16 with the second-generation staging ("p6"),
- * 64x64 / 128x64. */
-int molclr_gemm_set_impl(int impl);
-int molclr_gemm_get_impl(void);
+ * fp32 accumulation; fp32-GEMM accuracy), 64x64 / 128x64 tiles. */
+int molclr_gemm_f32_impl(const float* A, const float* B, float* C, int64_t M, int64_t N,
+                         int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                         int b_kmajor, int epilogue_flags, const float* bias, const float* aux,
+                         int64_t ldaux, void* workspace, size_t workspace_bytes,
+                         molclr_stream_t stream, int impl);
 
 /* Pre-split weight operand.  A Linear layer's weight is the B operand of the
  * forward (y = x W^T) and data-gradient (dx = dy W) GEMMs of every row tile;
@@ -287,16 +289,17 @@ int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, in
                             int epilogue_flags, const float* bias, const float* aux,
                             int64_t ldaux, void* workspace, size_t workspace_bytes,
                             molclr_stream_t stream);
-/* tile of molclr_gemm_f32_bplanes: 0 (default) = automatic (9 for a row-major A
- * whose 128-row tiles number >= 128, else 64x128 for N >= 512, else 64x64),
- * 5 = 64x64, 6 = 128x64, 7 = 64x128, 8 = 128x128, 9 = "q6": 128 x 160 (or
- * 128 / 64 wide) tiles with A streamed through registers, one wave per 32
- * rows, for K <= 1024 (a K-major A or a longer K falls back to 5 / 7) */
-int molclr_gemm_bplanes_set_impl(int impl);
-/* K groups per block of the weight-gradient kernel (both operands K-major,
- * long K): 2 (default) = two 4-wave groups per block, half as many split-K
- * partial tiles; 1 = one group per block, two blocks per CU. */
-int molclr_gemm_w6_set_groups(int kg);
+/* molclr_gemm_f32_bplanes with the tile chosen per call (molclr_gemm_f32_bplanes
+ * is tile = 0): 0 = automatic (9 for a row-major A whose 128-row tiles number
+ * >= 128, else 64x128 for N >= 512, else 64x64), 5 = 64x64, 6 = 128x64,
+ * 7 = 64x128, 8 = 128x128, 9 = "q6": 128 x 160 (or 128 / 64 wide) tiles with A
+ * streamed through registers, one wave per 32 rows, for K <= 1024 (a K-major A
+ * or a longer K falls back to 5 / 7). */
+int molclr_gemm_f32_bplanes_tile(const float* A, const uint16_t* planes, float* C, int64_t M,
+                                 int64_t N, int64_t K, int64_t lda, int64_t ldc, int a_kmajor,
+                                 int epilogue_flags, const float* bias, const float* aux,
+                                 int64_t ldaux, void* workspace, size_t workspace_bytes,
+                                 molclr_stream_t stream, int tile);
 
 /* Weight and bias gradients of y = x W^T + b (nn.Linear backward):
  *   dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i],   db[n_out] (+)= Σ_r dy[r][o]
@@ -309,6 +312,13 @@ size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_out, int64_t 
 int molclr_linear_wgrad(const float* dy, const float* x, float* dW, float* db, int64_t rows,
                         int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
                         void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+/* molclr_linear_wgrad with the K groups per block of the long-K kernel chosen
+ * per call (molclr_linear_wgrad is groups = 2): 2 = two 4-wave groups per block,
+ * half as many split-K partial tiles; 1 = one group per block. */
+int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float* db,
+                               int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                               int64_t ld_x, int accumulate, void* workspace,
+                               size_t workspace_bytes, molclr_stream_t stream, int groups);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
@@ -468,6 +478,14 @@ typedef struct molclr_gin_encoder {
   const uint16_t* mlp0_planes_t[MOLCLR_MAX_LAYERS];
   const uint16_t* mlp2_planes[MOLCLR_MAX_LAYERS];
   const uint16_t* mlp2_planes_t[MOLCLR_MAX_LAYERS];
+  /* MOLCLR_DTYPE_F32: fp32 node features, split-bf16 GEMMs (fp32 accuracy).
+   * MOLCLR_DTYPE_BF16 (dim % 8 == 0): bf16 node features and activation
+   * gradients, one bf16 MFMA per product with fp32 accumulation (plane 0 of
+   * the *_planes images is the bf16 weight), fp32 statistics, tables, and
+   * parameter gradients: the c5 configuration / the reference's
+   * mixed-precision switch (molclr.py:16-24,93-96,121-123).  h_out / dh_out
+   * are then bf16. */
+  int32_t dtype;
 } molclr_gin_encoder;
 
 /* Gradient buffers, same shapes as the parameters; NULL = not needed. */
@@ -500,17 +518,19 @@ typedef struct molclr_device_graph {
 
 /* Saved activations of one forward (kept for the backward): arena of
  * molclr_gin_encoder_arena_bytes; scratch: molclr_gin_encoder_workspace_bytes. */
-size_t molclr_gin_encoder_arena_bytes(int num_layer, int64_t num_nodes, int64_t dim);
-size_t molclr_gin_encoder_workspace_bytes(int num_layer, int64_t num_nodes, int64_t dim);
-/* x int64 [N,2] (atom type, chirality); h_out [N,D]: the last BatchNorm's output. */
+size_t molclr_gin_encoder_arena_bytes(int num_layer, int64_t num_nodes, int64_t dim, int dtype);
+size_t molclr_gin_encoder_workspace_bytes(int num_layer, int64_t num_nodes, int64_t dim,
+                                          int dtype);
+/* x int64 [N,2] (atom type, chirality); h_out [N,D] (enc->dtype): the last
+ * BatchNorm's output. */
 int molclr_gin_encoder_fwd(const molclr_gin_encoder* enc, const int64_t* x,
-                           const molclr_device_graph* graph, float* h_out, void* arena,
+                           const molclr_device_graph* graph, void* h_out, void* arena,
                            size_t arena_bytes, void* workspace, size_t workspace_bytes,
                            molclr_stream_t stream);
-/* dh_out [N,D]: gradient w.r.t. h_out; grads are accumulated (+=). */
+/* dh_out [N,D] (enc->dtype): gradient w.r.t. h_out; grads are accumulated (+=). */
 int molclr_gin_encoder_bwd(const molclr_gin_encoder* enc, const molclr_gin_encoder_grads* grads,
                            const int64_t* x, const molclr_device_graph* graph,
-                           const float* dh_out, const void* arena, size_t arena_bytes,
+                           const void* dh_out, const void* arena, size_t arena_bytes,
                            void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
 /* GCN encoder executor: GCN's node-embedding stack (models/gcn_molclr.py:140-151:
@@ -564,6 +584,55 @@ int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* enc, const molclr_gcn_encod
                            const int64_t* x, const molclr_device_graph* graph,
                            const float* dh_out, const void* arena, size_t arena_bytes,
                            void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * bf16 storage (BASELINE config c5: GIN 5 x 512, bf16, batch 1024 / GPU).
+ * Node features and activation gradients are bf16 ([N,D] of uint16 bit
+ * patterns, round-to-nearest-even); all arithmetic, tables, statistics and
+ * parameter gradients are fp32.  Same semantics as the fp32 entry points.
+ * ------------------------------------------------------------------------ */
+int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, const float* X2, uint16_t* h,
+                               int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,
+                               molclr_stream_t stream);
+/* workspace: molclr_atom_embed_bwd_workspace_bytes */
+int molclr_atom_embed_bwd_bf16(const int64_t* x, const uint16_t* dh, float* dX1, float* dX2,
+                               int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,
+                               int accumulate, void* workspace, size_t workspace_bytes,
+                               molclr_stream_t stream);
+int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* rowptr, const int32_t* col,
+                                   const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
+                                   uint16_t* out, int64_t num_nodes, int64_t dim,
+                                   molclr_stream_t stream);
+/* workspace: molclr_gine_aggregate_bwd_workspace_bytes */
+int molclr_gine_aggregate_bwd_bf16(const uint16_t* g, const int32_t* rowptr_t,
+                                   const int32_t* col_t, const uint32_t* nbr_t,
+                                   const int32_t* ecount, uint16_t* dx, float* dE1, float* dE2,
+                                   int64_t num_nodes, int64_t dim, int accumulate, void* workspace,
+                                   size_t workspace_bytes, molclr_stream_t stream);
+/* h bf16 -> out fp32 [G,D]; dout fp32 -> dh bf16 */
+int molclr_segment_pool_fwd_bf16(const uint16_t* h, const int32_t* graph_ptr, float* out,
+                                 int64_t num_graphs, int64_t dim, int mode,
+                                 molclr_stream_t stream);
+int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* graph_ptr, uint16_t* dh,
+                                 int64_t num_nodes, int64_t num_graphs, int64_t dim, int mode,
+                                 molclr_stream_t stream);
+/* C[M,N] (bf16) = epilogue(Σ_k A[m][k] B(k,n)), A bf16 row-major (lda), B the
+ * weight operand as molclr_bplanes_make planes (plane 0 = bf16(B) is read),
+ * one v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation.  Epilogues:
+ * NONE / BIAS / BIAS_RELU (bias fp32) / RELU_MASK (aux bf16, ldaux % 4 == 0);
+ * no accumulate.  K and lda multiples of 8, ldc a multiple of 4. */
+int molclr_gemm_bf16(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M, int64_t N,
+                     int64_t K, int64_t lda, int64_t ldc, int epilogue, const float* bias,
+                     const uint16_t* aux, int64_t ldaux, molclr_stream_t stream);
+/* Linear weight / bias gradients from bf16 operands into fp32:
+ * dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i], db (+)= Σ_r dy[r][o] (db may be
+ * NULL); n_out, n_in, ld_dy, ld_x multiples of 8.  Split-K partials summed in
+ * a fixed order (deterministic). */
+size_t molclr_linear_wgrad_bf16_workspace_bytes(int64_t rows, int64_t n_out, int64_t n_in);
+int molclr_linear_wgrad_bf16(const uint16_t* dy, const uint16_t* x, float* dW, float* db,
+                             int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                             int64_t ld_x, int accumulate, void* workspace,
+                             size_t workspace_bytes, molclr_stream_t stream);
 
 /* ---- Benchmark instrumentation (no reference counterpart) -------------------
  * Opt-in kernel timer.  While a kind is enabled, its launches go through

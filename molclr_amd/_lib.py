@@ -53,18 +53,20 @@ SIGNATURES = {
     "molclr_gemm_f32_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_gemm_f32": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, c_int, c_int, c_int,
                                 _P, _P, _I64, _P, c_size_t, _P]),
-    "molclr_gemm_set_impl": (c_int, [c_int]),
-    "molclr_gemm_bplanes_set_impl": (c_int, [c_int]),
-    "molclr_gemm_w6_set_groups": (c_int, [c_int]),
+    "molclr_gemm_f32_impl": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, _I64, c_int, c_int,
+                                     c_int, _P, _P, _I64, _P, c_size_t, _P, c_int]),
     "molclr_bplanes_bytes": (c_size_t, [_I64, _I64]),
     "molclr_bplanes_make": (c_int, [_P, _I64, _I64, _I64, c_int, _P, _P]),
     "molclr_bplanes_make_batch": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P]),
     "molclr_gemm_f32_bplanes": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, c_int, _P,
                                         _P, _I64, _P, c_size_t, _P]),
-    "molclr_gemm_get_impl": (c_int, []),
+    "molclr_gemm_f32_bplanes_tile": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
+                                             c_int, _P, _P, _I64, _P, c_size_t, _P, c_int]),
     "molclr_linear_wgrad_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_linear_wgrad": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
                                     _P]),
+    "molclr_linear_wgrad_groups": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
+                                           c_size_t, _P, c_int]),
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),
@@ -91,14 +93,27 @@ SIGNATURES = {
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
-    "molclr_gin_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64]),
-    "molclr_gin_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_gin_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64, c_int]),
+    "molclr_gin_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64, c_int]),
     "molclr_gin_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_gin_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_gcn_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64]),
     "molclr_gcn_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
     "molclr_gcn_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_gcn_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
+    "molclr_atom_embed_fwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "molclr_atom_embed_bwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P,
+                                           c_size_t, _P]),
+    "molclr_gine_aggregate_fwd_bf16": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_gine_aggregate_bwd_bf16": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int,
+                                               _P, c_size_t, _P]),
+    "molclr_segment_pool_fwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_segment_pool_bwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
+    "molclr_gemm_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P, _I64,
+                                 _P]),
+    "molclr_linear_wgrad_bf16_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_linear_wgrad_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
+                                         c_size_t, _P]),
     "molclr_ktimer_start": (c_int, [c_int]),
     "molclr_ktimer_read": (c_int, [c_int, _P, _P]),
     "molclr_ktimer_stop": (c_int, []),
@@ -125,7 +140,8 @@ class GinEncoder(ctypes.Structure):
         (f, _L16) for f in ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias",
                             "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias",
                             "bn_running_mean", "bn_running_var", "bn_num_batches_tracked",
-                            "mlp0_planes", "mlp0_planes_t", "mlp2_planes", "mlp2_planes_t")]
+                            "mlp0_planes", "mlp0_planes_t", "mlp2_planes", "mlp2_planes_t")] + [
+        ("dtype", ctypes.c_int32)]
 
 
 class GinEncoderGrads(ctypes.Structure):

@@ -26,9 +26,10 @@ constexpr int kT = 256;
 // ---------------------------------------------------------------------------
 // atom embedding
 // ---------------------------------------------------------------------------
+template <typename St>
 __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __restrict__ X1,
-                                 const float4* __restrict__ X2, float4* __restrict__ h, int64_t N,
-                                 int d4, int64_t n1, int64_t n2) {
+                                 const float4* __restrict__ X2, typename St::T* __restrict__ h,
+                                 int64_t N, int d4, int64_t n1, int64_t n2) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
@@ -36,13 +37,14 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
   int64_t a = x[2 * i], b = x[2 * i + 1];
   a = a < 0 ? 0 : (a >= n1 ? n1 - 1 : a);
   b = b < 0 ? 0 : (b >= n2 ? n2 - 1 : b);
-  h[t] = f4add(X1[a * d4 + c], X2[b * d4 + c]);
+  St::st(h, t, f4add(X1[a * d4 + c], X2[b * d4 + c]));
 }
 
 // Partial per-type column sums of dh.  grid = (P partitions, ceil(D/64)),
 // block = 64 threads (one column each), LDS table [n1+n2][64].
+template <typename St>
 __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
-    const int64_t* __restrict__ x, const float* __restrict__ dh, int64_t N, int64_t D,
+    const int64_t* __restrict__ x, const typename St::T* __restrict__ dh, int64_t N, int64_t D,
     int64_t n1, int64_t n2, int64_t rows_per_part, double* __restrict__ partial) {
   // fp32 table within a partition (<= 128 rows), fp64 partials across partitions
   extern __shared__ __attribute__((aligned(16))) float tab[];  // [(n1+n2)][64]
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
     for (int u = 0; u < 4; ++u) {
       a[u] = x[2 * (i + u)];
       b[u] = x[2 * (i + u) + 1];
-      v[u] = active ? dh[(i + u) * D + c] : 0.f;
+      v[u] = active ? St::ld1(dh, (i + u) * D + c) : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
     int64_t aa = x[2 * i], bb = x[2 * i + 1];
     aa = aa < 0 ? 0 : (aa >= n1 ? n1 - 1 : aa);
     bb = bb < 0 ? 0 : (bb >= n2 ? n2 - 1 : bb);
-    float v = active ? dh[i * D + c] : 0.f;
+    float v = active ? St::ld1(dh, i * D + c) : 0.f;
     tab[aa * 64 + lane] += v;
     tab[(n1 + bb) * 64 + lane] += v;
   }
@@ -175,11 +177,11 @@ __device__ __forceinline__ float bn_shift1(float b, float m, float sc) { return 
 
 // BN = true: x holds z, and every x element read goes through BatchNorm
 // (+ReLU) first (molclr_gine_aggregate_bn_fwd); the adds are unchanged.
-template <bool BN>
+template <bool BN, typename St = StF32>
 __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
-    const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+    const typename St::T* __restrict__ x, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
-    const uint4* __restrict__ nbr, const float4* __restrict__ Ec, float4* __restrict__ out,
+    const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
     int64_t N, int d4, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, int relu) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     bn.relu = relu != 0;
   }
   auto X = [&](int64_t idx) {
-    const float4 v = x[idx];
+    const float4 v = St::ld(x, idx);
     if constexpr (BN) return bn(v);
     return v;
   };
@@ -226,18 +228,19 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
       acc = f4add(acc, f4add(X((int64_t)col[k] * d4 + c), Ec[MOLCLR_ECOMB(ecode[k]) * d4 + c]));
   }
   acc = f4add(acc, f4add(self, es));
-  out[t] = acc;
+  St::st(out, t, acc);
 }
 
 // dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC).
 // Unlike the forward, the self row is read last and the gathers stay in
 // branches: measured 14.0 us against 17.3 us for the forward's structure here
 // (tools/agg_bench.py transpose).
-__global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restrict__ g,
+template <typename St = StF32>
+__global__ __launch_bounds__(kT) void k_transpose_gather(const typename St::T* __restrict__ g,
                                                          const int32_t* __restrict__ rowptr_t,
                                                          const int32_t* __restrict__ col_t,
                                                          const uint4* __restrict__ nbr_t,
-                                                         float4* __restrict__ dx, int64_t N,
+                                                         typename St::T* __restrict__ dx, int64_t N,
                                                          int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
@@ -247,21 +250,22 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const float4* __restric
   const uint32_t deg = nbr_degree(s.x);
   float4 acc = f4zero();
   if (deg <= MOLCLR_NBR_SLOTS) {
-    if (deg > 0) acc = f4add(acc, g[(int64_t)nbr_node(s.x) * d4 + c]);
-    if (deg > 1) acc = f4add(acc, g[(int64_t)nbr_node(s.y) * d4 + c]);
-    if (deg > 2) acc = f4add(acc, g[(int64_t)nbr_node(s.z) * d4 + c]);
-    if (deg > 3) acc = f4add(acc, g[(int64_t)nbr_node(s.w) * d4 + c]);
+    if (deg > 0) acc = f4add(acc, St::ld(g, (int64_t)nbr_node(s.x) * d4 + c));
+    if (deg > 1) acc = f4add(acc, St::ld(g, (int64_t)nbr_node(s.y) * d4 + c));
+    if (deg > 2) acc = f4add(acc, St::ld(g, (int64_t)nbr_node(s.z) * d4 + c));
+    if (deg > 3) acc = f4add(acc, St::ld(g, (int64_t)nbr_node(s.w) * d4 + c));
   } else {
     for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k)
-      acc = f4add(acc, g[(int64_t)col_t[k] * d4 + c]);
+      acc = f4add(acc, St::ld(g, (int64_t)col_t[k] * d4 + c));
   }
-  dx[t] = f4add(acc, g[t]);
+  St::st(dx, t, f4add(acc, St::ld(g, t)));
 }
 
 // Edge-table gradient partials: partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c].
 // Band layout (a block covers `band` rows x all D/4 float4 columns, 1 KiB
 // contiguous per wave); fp32 within a partition, fp64 partials across.
-__global__ void k_ecount_weighted_partial(const float4* __restrict__ g,
+template <typename St = StF32>
+__global__ void k_ecount_weighted_partial(const typename St::T* __restrict__ g,
                                           const int32_t* __restrict__ ecount, int64_t N, int d4,
                                           int band, int64_t rows_per_part,
                                           double* __restrict__ partial) {
@@ -290,7 +294,7 @@ __global__ void k_ecount_weighted_partial(const float4* __restrict__ g,
         const int4* ec = reinterpret_cast<const int4*>(ecount + (in ? i : beg) * 8);
         lo[u] = ec[0];
         hi[u] = ec[1];
-        v[u] = g[(in ? i : beg) * d4 + c];
+        v[u] = St::ld(g, (in ? i : beg) * d4 + c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -472,9 +476,9 @@ MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const fl
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && X1 && X2 && h, "atom_embed_fwd: null pointer");
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_atom_embed_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2,
-                     (float4*)h, N, d4, n1, n2);
+  hipLaunchKernelGGL(k_atom_embed_fwd<StF32>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N, d4,
+                     n1, n2);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -496,8 +500,8 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
   int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
   double* partial = (double*)workspace;
   size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
-  hipLaunchKernelGGL(k_atom_embed_bwd_partial, dim3(P, molclr::ceil_div(D, 64)), dim3(64), lds, s,
-                     x, dh, N, D, n1, n2, rpp, partial);
+  hipLaunchKernelGGL(k_atom_embed_bwd_partial<StF32>, dim3(P, molclr::ceil_div(D, 64)), dim3(64),
+                     lds, s, x, dh, N, D, n1, n2, rpp, partial);
   hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 16)), dim3(1024),
                      0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
   MOLCLR_LAUNCHED();
@@ -535,10 +539,10 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
   MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
   const float* nf = nullptr;
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false>,
+  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StF32>,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       (const float4*)x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec,
-                       (float4*)out, N, d4, nf, nf, nf, nf, 0);
+                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, nf,
+                       nf, nf, nf, 0);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -555,10 +559,10 @@ MOLCLR_API int molclr_gine_aggregate_bn_fwd(const float* z, const float* mean,
   MOLCLR_REQUIRE(z && mean && invstd && rowptr && nbr && Ec && out,
                  "gine_aggregate_bn_fwd: null pointer");
   int d4 = (int)(D / 4);
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<true>,
+  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<true, StF32>,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       (const float4*)z, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec,
-                       (float4*)out, N, d4, mean, invstd, gamma, beta, relu);
+                       z, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, mean,
+                       invstd, gamma, beta, relu);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -578,9 +582,8 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
   int d4 = (int)(D / 4);
   if (dx && N > 0) {
     MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gine_aggregate_bwd: null pointer");
-    hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
-                       (const float4*)g, rowptr_t, col_t, (const uint4*)nbr_t, (float4*)dx, N,
-                       d4);
+    hipLaunchKernelGGL(k_transpose_gather<StF32>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                       s, g, rowptr_t, col_t, (const uint4*)nbr_t, dx, N, d4);
   }
   if (dE1 || dE2) {
     MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
@@ -590,8 +593,8 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
     double* partial = (double*)workspace;
     size_t lds = (size_t)b.band * 8 * b.d4 * sizeof(float4);
     MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd: dim too large for the edge-table reduction");
-    hipLaunchKernelGGL(k_ecount_weighted_partial, dim3(P), dim3(b.threads), lds, s,
-                       (const float4*)g, ecount, N, d4, b.band, rpp, partial);
+    hipLaunchKernelGGL(k_ecount_weighted_partial<StF32>, dim3(P), dim3(b.threads), lds, s, g,
+                       ecount, N, d4, b.band, rpp, partial);
     hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 16)), dim3(1024), 0, s,
                        partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2, accumulate);
   }
@@ -634,9 +637,8 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
   int d4 = (int)(D / 4);
   if (dxw && N > 0) {
     MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gcn_aggregate_bwd: null pointer");
-    hipLaunchKernelGGL(k_transpose_gather, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, s,
-                       (const float4*)g, rowptr_t, col_t, (const uint4*)nbr_t, (float4*)dxw, N,
-                       d4);
+    hipLaunchKernelGGL(k_transpose_gather<StF32>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                       s, g, rowptr_t, col_t, (const uint4*)nbr_t, dxw, N, d4);
   }
   molclr::Workspace w(workspace, workspace_bytes);
   double* partial = w.take<double>(kRowsumBlocks * 4 * 8);
@@ -651,5 +653,92 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
     int rc = molclr_colsum_impl(g, dbias, N, D, D, accumulate, w, s);
     if (rc) return rc;
   }
+  return MOLCLR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// bf16 storage (the c5 configuration): the same kernels over bf16 node
+// features, fp32 arithmetic, fp32 tables and table gradients.
+// ---------------------------------------------------------------------------
+MOLCLR_API int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, const float* X2,
+                                          uint16_t* h, int64_t N, int64_t D, int64_t n1,
+                                          int64_t n2, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "atom_embed_fwd_bf16: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(n1 > 0 && n2 > 0, "atom_embed_fwd_bf16: empty table");
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && X1 && X2 && h, "atom_embed_fwd_bf16: null pointer");
+  const int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_atom_embed_fwd<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N, d4,
+                     n1, n2);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_atom_embed_bwd_bf16(const int64_t* x, const uint16_t* dh, float* dX1,
+                                          float* dX2, int64_t N, int64_t D, int64_t n1, int64_t n2,
+                                          int accumulate, void* workspace, size_t workspace_bytes,
+                                          molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd_bf16: bad sizes");
+  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd_bf16: tables too large");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
+  hipStream_t s = molclr::as_stream(stream);
+  const int64_t P = atom_parts(N);
+  const int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
+  double* partial = (double*)workspace;
+  const size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
+  hipLaunchKernelGGL(k_atom_embed_bwd_partial<StBF16>, dim3(P, molclr::ceil_div(D, 64)), dim3(64),
+                     lds, s, x, dh, N, D, n1, n2, rpp, partial);
+  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 16)), dim3(1024),
+                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* rowptr,
+                                              const int32_t* col, const uint8_t* ecode,
+                                              const uint32_t* nbr, const float* Ec, uint16_t* out,
+                                              int64_t N, int64_t D, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_fwd_bf16: dim must be a multiple of 4");
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd_bf16: null pointer");
+  const int d4 = (int)(D / 4);
+  const float* nf = nullptr;
+  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StBF16>,
+                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
+                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, nf,
+                       nf, nf, nf, 0);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gine_aggregate_bwd_bf16(const uint16_t* g, const int32_t* rowptr_t,
+                                              const int32_t* col_t, const uint32_t* nbr_t,
+                                              const int32_t* ecount, uint16_t* dx, float* dE1,
+                                              float* dE2, int64_t N, int64_t D, int accumulate,
+                                              void* workspace, size_t workspace_bytes,
+                                              molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_bwd_bf16: dim must be a multiple of 4");
+  hipStream_t s = molclr::as_stream(stream);
+  const int d4 = (int)(D / 4);
+  if (dx && N > 0) {
+    MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gine_aggregate_bwd_bf16: null pointer");
+    hipLaunchKernelGGL(k_transpose_gather<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
+                       s, g, rowptr_t, col_t, (const uint4*)nbr_t, dx, N, d4);
+  }
+  if (dE1 || dE2) {
+    MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));
+    const molclr::Band b = molclr::make_band(D);
+    const int64_t P = ecount_parts(N, b.band);
+    const int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
+    double* partial = (double*)workspace;
+    const size_t lds = (size_t)b.band * 8 * b.d4 * sizeof(float4);
+    MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd_bf16: dim too large for the edge-table reduction");
+    hipLaunchKernelGGL(k_ecount_weighted_partial<StBF16>, dim3(P), dim3(b.threads), lds, s, g,
+                       ecount, N, d4, b.band, rpp, partial);
+    hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div(8 * D, 16)), dim3(1024), 0, s,
+                       partial, P, (int64_t)8, D, (int64_t)5, dE1, dE2, accumulate);
+  }
+  MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

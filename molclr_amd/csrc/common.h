@@ -146,6 +146,7 @@ struct StF32 {
   __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
     reinterpret_cast<float4*>(p)[unit] = v;
   }
+  __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) { return p[i]; }
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t bits16) {
@@ -168,6 +169,9 @@ struct StBF16 {
   }
   __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
     reinterpret_cast<uint2*>(p)[unit] = make_uint2(f32x2_to_bf16x2(v.x, v.y), f32x2_to_bf16x2(v.z, v.w));
+  }
+  __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) {
+    return bf16_to_f32(p[i]);
   }
 };
 

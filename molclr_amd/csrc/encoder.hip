@@ -17,30 +17,34 @@
 
 namespace {
 
+// byte offsets; node-feature buffers in the encoder's storage type (fp32 or
+// bf16), statistics and edge tables fp32; every buffer 256-byte aligned
 struct ArenaLayout {
   size_t agg[MOLCLR_MAX_LAYERS], a1[MOLCLR_MAX_LAYERS], z[MOLCLR_MAX_LAYERS],
       h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS], invstd[MOLCLR_MAX_LAYERS];
   size_t h0, ec, total;
-  ArenaLayout(int L, int64_t N, int64_t D) {
-    size_t used = 0;  // floats; every buffer 256-byte aligned
-    auto off = [&](size_t count) {
+  ArenaLayout(int L, int64_t N, int64_t D, size_t es) {
+    size_t used = 0;
+    auto off = [&](size_t bytes) {
       const size_t o = used;
-      used += (count + 63) / 64 * 64;
+      used += (bytes + 255) / 256 * 256;
       return o;
     };
     for (int l = 0; l < L; ++l) {
-      agg[l] = off(N * D);
-      a1[l] = off(N * 2 * D);
-      z[l] = off(N * D);
-      h[l] = off(N * D);
-      mean[l] = off(MOLCLR_MAX_SEGMENTS * D);  // [segment][D]
-      invstd[l] = off(MOLCLR_MAX_SEGMENTS * D);
+      agg[l] = off(N * D * es);
+      a1[l] = off(N * 2 * D * es);
+      z[l] = off(N * D * es);
+      h[l] = off(N * D * es);
+      mean[l] = off(MOLCLR_MAX_SEGMENTS * D * sizeof(float));  // [segment][D]
+      invstd[l] = off(MOLCLR_MAX_SEGMENTS * D * sizeof(float));
     }
-    h0 = off(N * D);
-    ec = off((size_t)L * MOLCLR_NUM_ECOMB * D);
-    total = used * sizeof(float);
+    h0 = off(N * D * es);
+    ec = off((size_t)L * MOLCLR_NUM_ECOMB * D * sizeof(float));
+    total = used;
   }
 };
+
+size_t elem_bytes(int dtype) { return dtype == MOLCLR_DTYPE_BF16 ? 2 : 4; }
 
 size_t kernels_ws(int64_t N, int64_t D) {
   size_t m = 0;
@@ -52,19 +56,24 @@ size_t kernels_ws(int64_t N, int64_t D) {
   mx(molclr_colsum_f32_workspace_bytes(N, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, D, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, 2 * D, D));
+  mx(molclr_linear_wgrad_bf16_workspace_bytes(N, D, 2 * D));
+  mx(molclr_linear_wgrad_bf16_workspace_bytes(N, 2 * D, D));
   mx(molclr_batchnorm_ws_bound(N, D));
   mx(molclr_gine_aggregate_bwd_workspace_bytes(N, D));
   mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
   return m;
 }
 
-size_t scratch_floats(int64_t N, int64_t D) { return (size_t)N * D * 3 + (size_t)N * 2 * D; }
+// backward scratch dh, dz, dagg [N,D] + dz1 [N,2D], in the storage type
+size_t scratch_bytes(int64_t N, int64_t D, size_t es) { return ((size_t)N * D * 3 + (size_t)N * 2 * D) * es; }
 
 int check_encoder(const molclr_gin_encoder* e, const molclr_device_graph* g) {
   MOLCLR_REQUIRE(e && g, "gin_encoder: null encoder / graph");
   MOLCLR_REQUIRE(e->num_layer >= 1 && e->num_layer <= MOLCLR_MAX_LAYERS,
                  "gin_encoder: num_layer %d", e->num_layer);
   MOLCLR_REQUIRE(e->dim > 0 && e->dim % 4 == 0, "gin_encoder: dim %lld", (long long)e->dim);
+  MOLCLR_REQUIRE(e->dtype == MOLCLR_DTYPE_F32 || (e->dtype == MOLCLR_DTYPE_BF16 && e->dim % 8 == 0),
+                 "gin_encoder: dtype %d (bf16 needs dim %% 8 == 0)", e->dtype);
   MOLCLR_REQUIRE(e->n_atom == MOLCLR_NUM_ATOM_TYPE && e->n_chiral == MOLCLR_NUM_CHIRALITY,
                  "gin_encoder: embedding tables must be [%d,D] and [%d,D]",
                  MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY);
@@ -103,18 +112,18 @@ int graph_segments(const molclr_device_graph* g, const int64_t* N, SegRows& out)
 
 }  // namespace
 
-MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D) {
+MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, int dtype) {
   if (L < 1 || L > MOLCLR_MAX_LAYERS) return 0;
-  return ArenaLayout(L, N, D).total;
+  return ArenaLayout(L, N, D, elem_bytes(dtype)).total;
 }
 
-MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D) {
+MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
   (void)L;
-  return scratch_floats(N, D) * sizeof(float) + 256 + kernels_ws(N, D) + 256;
+  return scratch_bytes(N, D, elem_bytes(dtype)) + 256 + kernels_ws(N, D) + 256;
 }
 
 MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t* x,
-                                      const molclr_device_graph* g, float* h_out, void* arena,
+                                      const molclr_device_graph* g, void* h_out, void* arena,
                                       size_t arena_bytes, void* workspace, size_t workspace_bytes,
                                       molclr_stream_t stream) {
   MOLCLR_TRY(check_encoder(e, g));
@@ -124,38 +133,61 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   SegRows seg;
   MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && h_out && arena, "gin_encoder_fwd: null pointer");
-  const ArenaLayout lay(L, N, D);
+  const bool bf = e->dtype == MOLCLR_DTYPE_BF16;
+  const size_t es = elem_bytes(e->dtype);
+  const ArenaLayout lay(L, N, D, es);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
-  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D));
-  float* A = (float*)arena;
-  void* kws = (char*)workspace + molclr::align_up(scratch_floats(N, D) * sizeof(float), 256);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D, e->dtype));
+  char* A = (char*)arena;
+  auto F = [&](size_t off) { return (float*)(A + off); };
+  auto H = [&](size_t off) { return (uint16_t*)(A + off); };
+  void* kws = (char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256);
   const size_t kws_bytes = kernels_ws(N, D);
 
-  float* h = A + lay.h0;
-  MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, h, N, D, e->n_atom,
-                                   e->n_chiral, stream));
-  float* Ec = A + lay.ec;
+  void* h = A + lay.h0;
+  if (bf)
+    MOLCLR_TRY(molclr_atom_embed_fwd_bf16(x, e->x_embedding1, e->x_embedding2, (uint16_t*)h, N, D,
+                                          e->n_atom, e->n_chiral, stream));
+  else
+    MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, (float*)h, N, D,
+                                     e->n_atom, e->n_chiral, stream));
+  float* Ec = F(lay.ec);
   MOLCLR_TRY(molclr_edge_tables_combine(L, e->edge_embedding1, e->edge_embedding2, Ec, D, stream));
   for (int l = 0; l < L; ++l) {
-    float* agg = A + lay.agg[l];
-    float* a1 = A + lay.a1[l];
-    float* z = A + lay.z[l];
     const bool last = l == L - 1;
-    float* y = last ? h_out : A + lay.h[l];
-    MOLCLR_TRY(molclr_gine_aggregate_fwd(h, g->rowptr, g->col, g->ecode, g->nbr,
-                                         Ec + (size_t)l * MOLCLR_NUM_ECOMB * D, agg, N, D, stream));
-    // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
-                                       MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
-                                       kws_bytes, stream));
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
-                                       MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
-                                       kws_bytes, stream));
-    MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                        e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                        A + lay.mean[l], A + lay.invstd[l], seg.n, seg.rows, D,
-                                        MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
-                                        last ? 0 : 1, kws, kws_bytes, stream));
+    void* y = last ? h_out : A + lay.h[l];
+    const float* Ecl = Ec + (size_t)l * MOLCLR_NUM_ECOMB * D;
+    if (bf) {
+      uint16_t *agg = H(lay.agg[l]), *a1 = H(lay.a1[l]), *z = H(lay.z[l]);
+      MOLCLR_TRY(molclr_gine_aggregate_fwd_bf16((const uint16_t*)h, g->rowptr, g->col, g->ecode,
+                                                g->nbr, Ecl, agg, N, D, stream));
+      // GINEConv.update in bf16: one MFMA per product, fp32 accumulation
+      MOLCLR_TRY(molclr_gemm_bf16(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
+                                  MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, stream));
+      MOLCLR_TRY(molclr_gemm_bf16(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D,
+                                  MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, stream));
+      MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                          e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                          F(lay.mean[l]), F(lay.invstd[l]), seg.n, seg.rows, D,
+                                          MOLCLR_DTYPE_BF16, e->momentum, e->eps, e->training,
+                                          last ? 0 : 1, kws, kws_bytes, stream));
+    } else {
+      float *agg = F(lay.agg[l]), *a1 = F(lay.a1[l]), *z = F(lay.z[l]);
+      MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
+                                           Ecl, agg, N, D, stream));
+      // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
+                                         MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
+                                         kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
+                                         MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
+                                         kws_bytes, stream));
+      MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                                          e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
+                                          F(lay.mean[l]), F(lay.invstd[l]), seg.n, seg.rows, D,
+                                          MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
+                                          last ? 0 : 1, kws, kws_bytes, stream));
+    }
     h = y;
   }
   return MOLCLR_OK;
@@ -163,7 +195,7 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
 
 MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                       const molclr_gin_encoder_grads* gr, const int64_t* x,
-                                      const molclr_device_graph* g, const float* dh_out,
+                                      const molclr_device_graph* g, const void* dh_out,
                                       const void* arena, size_t arena_bytes, void* workspace,
                                       size_t workspace_bytes, molclr_stream_t stream) {
   MOLCLR_TRY(check_encoder(e, g));
@@ -175,59 +207,94 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   SegRows seg;
   MOLCLR_TRY(graph_segments(g, &g->num_nodes, seg));
   MOLCLR_REQUIRE(x && dh_out && arena, "gin_encoder_bwd: null pointer");
-  const ArenaLayout lay(L, N, D);
+  const bool bf = e->dtype == MOLCLR_DTYPE_BF16;
+  const size_t es = elem_bytes(e->dtype);
+  const ArenaLayout lay(L, N, D, es);
   MOLCLR_REQUIRE_WS(arena_bytes, lay.total);
-  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D));
-  const float* A = (const float*)arena;
-  float* S = (float*)workspace;
-  float* dh = S;                 // gradient w.r.t. the current layer's output
-  float* dz = S + N * D;         // w.r.t. the BatchNorm input z
-  float* dagg = S + 2 * N * D;   // w.r.t. the aggregation output
-  float* dz1 = S + 3 * N * D;    // w.r.t. the first Linear's pre-activation [N,2D]
-  void* kws = (char*)workspace + molclr::align_up(scratch_floats(N, D) * sizeof(float), 256);
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gin_encoder_workspace_bytes(L, N, D, e->dtype));
+  const char* A = (const char*)arena;
+  auto F = [&](size_t off) { return (const float*)(A + off); };
+  char* S = (char*)workspace;
+  void* dh = S;                              // gradient w.r.t. the current layer's output
+  void* dz = S + (size_t)N * D * es;         // w.r.t. the BatchNorm input z
+  void* dagg = S + 2 * (size_t)N * D * es;   // w.r.t. the aggregation output
+  void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
+  void* kws = S + molclr::align_up(scratch_bytes(N, D, es), 256);
   const size_t kws_bytes = kernels_ws(N, D);
+  const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
 
-  const float* dy = dh_out;
+  const void* dy = dh_out;
   for (int l = L - 1; l >= 0; --l) {
-    const float* agg = A + lay.agg[l];
-    const float* a1 = A + lay.a1[l];
-    const float* z = A + lay.z[l];
+    const void* agg = A + lay.agg[l];
+    const void* a1 = A + lay.a1[l];
+    const void* z = A + lay.z[l];
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
-    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
-                                        A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l],
-                                        seg.n, seg.rows, D, MOLCLR_DTYPE_F32, last ? 0 : 1, 1,
-                                        kws, kws_bytes, stream));
-    // second Linear (ops.linear_bwd order: dW with db, dx with the ReLU mask of a1)
-    if (gr->mlp2_weight[l])
-      MOLCLR_TRY(molclr_linear_wgrad(dz, a1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D, 2 * D, D,
-                                     2 * D, 1, kws, kws_bytes, stream));
-    else if (gr->mlp2_bias[l])
-      MOLCLR_TRY(molclr_colsum_f32(dz, gr->mlp2_bias[l], N, D, D, 1, kws, kws_bytes, stream));
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(dz, e->mlp2_planes_t[l], dz1, N, 2 * D, D, D, 2 * D, 0,
-                                       MOLCLR_EPI_RELU_MASK, nullptr, a1, 2 * D, kws, kws_bytes,
+    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
+                                        F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l],
+                                        seg.n, seg.rows, D, dt, last ? 0 : 1, 1, kws, kws_bytes,
+                                        stream));
+    if (bf) {
+      const uint16_t *hz = (const uint16_t*)dz, *ha1 = (const uint16_t*)a1;
+      // second Linear: dW2, db2 from dz and a1; dz1 = (dz W2) * (a1 > 0)
+      if (gr->mlp2_weight[l] || gr->mlp2_bias[l]) {
+        MOLCLR_REQUIRE(gr->mlp2_weight[l], "gin_encoder_bwd: bf16 needs the weight gradient");
+        MOLCLR_TRY(molclr_linear_wgrad_bf16(hz, ha1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D,
+                                            2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
+      }
+      MOLCLR_TRY(molclr_gemm_bf16(hz, e->mlp2_planes_t[l], (uint16_t*)dz1, N, 2 * D, D, D, 2 * D,
+                                  MOLCLR_EPI_RELU_MASK, nullptr, ha1, 2 * D, stream));
+      if (gr->mlp0_weight[l] || gr->mlp0_bias[l]) {
+        MOLCLR_REQUIRE(gr->mlp0_weight[l], "gin_encoder_bwd: bf16 needs the weight gradient");
+        MOLCLR_TRY(molclr_linear_wgrad_bf16((const uint16_t*)dz1, (const uint16_t*)agg,
+                                            gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D,
+                                            2 * D, D, 1, kws, kws_bytes, stream));
+      }
+      MOLCLR_TRY(molclr_gemm_bf16((const uint16_t*)dz1, e->mlp0_planes_t[l], (uint16_t*)dagg, N,
+                                  D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE, nullptr, nullptr, 0, stream));
+      MOLCLR_TRY(molclr_gine_aggregate_bwd_bf16((const uint16_t*)dagg, g->rowptr_t, g->col_t,
+                                                g->nbr_t, g->ecount, (uint16_t*)dh,
+                                                gr->edge_embedding1[l], gr->edge_embedding2[l], N,
+                                                D, 1, kws, kws_bytes, stream));
+    } else {
+      const float *fz = (const float*)dz, *fa1 = (const float*)a1;
+      // second Linear (ops.linear_bwd order: dW with db, dx with the ReLU mask of a1)
+      if (gr->mlp2_weight[l])
+        MOLCLR_TRY(molclr_linear_wgrad(fz, fa1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D, 2 * D,
+                                       D, 2 * D, 1, kws, kws_bytes, stream));
+      else if (gr->mlp2_bias[l])
+        MOLCLR_TRY(molclr_colsum_f32(fz, gr->mlp2_bias[l], N, D, D, 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(fz, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
+                                         2 * D, 0, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D, kws,
+                                         kws_bytes, stream));
+      // first Linear
+      if (gr->mlp0_weight[l])
+        MOLCLR_TRY(molclr_linear_wgrad((const float*)dz1, (const float*)agg, gr->mlp0_weight[l],
+                                       gr->mlp0_bias[l], N, 2 * D, D, 2 * D, D, 1, kws, kws_bytes,
                                        stream));
-    // first Linear
-    if (gr->mlp0_weight[l])
-      MOLCLR_TRY(molclr_linear_wgrad(dz1, agg, gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D,
-                                     2 * D, D, 1, kws, kws_bytes, stream));
-    else if (gr->mlp0_bias[l])
-      MOLCLR_TRY(molclr_colsum_f32(dz1, gr->mlp0_bias[l], N, 2 * D, 2 * D, 1, kws, kws_bytes,
-                                   stream));
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(dz1, e->mlp0_planes_t[l], dagg, N, D, 2 * D, 2 * D, D, 0,
-                                       MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
-                                       stream));
-    // aggregation: dh of the layer input, edge-table gradients
-    MOLCLR_TRY(molclr_gine_aggregate_bwd(dagg, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dh,
-                                         gr->edge_embedding1[l], gr->edge_embedding2[l], N, D, 1,
-                                         kws, kws_bytes, stream));
+      else if (gr->mlp0_bias[l])
+        MOLCLR_TRY(molclr_colsum_f32((const float*)dz1, gr->mlp0_bias[l], N, 2 * D, 2 * D, 1, kws,
+                                     kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_bplanes((const float*)dz1, e->mlp0_planes_t[l], (float*)dagg, N,
+                                         D, 2 * D, 2 * D, D, 0, MOLCLR_EPI_NONE, nullptr, nullptr,
+                                         0, kws, kws_bytes, stream));
+      // aggregation: dh of the layer input, edge-table gradients
+      MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
+                                           g->ecount, (float*)dh, gr->edge_embedding1[l],
+                                           gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));
+    }
     dy = dh;
   }
   if (gr->x_embedding1 || gr->x_embedding2) {
     MOLCLR_REQUIRE(gr->x_embedding1 && gr->x_embedding2,
                    "gin_encoder_bwd: both atom-embedding grads or neither");
-    MOLCLR_TRY(molclr_atom_embed_bwd(x, dh, gr->x_embedding1, gr->x_embedding2, N, D, e->n_atom,
-                                     e->n_chiral, 1, kws, kws_bytes, stream));
+    if (bf)
+      MOLCLR_TRY(molclr_atom_embed_bwd_bf16(x, (const uint16_t*)dh, gr->x_embedding1,
+                                            gr->x_embedding2, N, D, e->n_atom, e->n_chiral, 1, kws,
+                                            kws_bytes, stream));
+    else
+      MOLCLR_TRY(molclr_atom_embed_bwd(x, (const float*)dh, gr->x_embedding1, gr->x_embedding2, N,
+                                       D, e->n_atom, e->n_chiral, 1, kws, kws_bytes, stream));
   }
   return MOLCLR_OK;
 }

@@ -22,13 +22,12 @@
 // Workgroups are remapped so that the tiles sharing an A row-slab land on the
 // same XCD (blocks b and b+8 share an L2): the A slab is then read from HBM
 // once per XCD rather than once per column tile.
-#include "common.h"
+#include "mfma.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using namespace molclr;
 
-constexpr int BK = 32;
 constexpr int LDK = BK + 4;  // [row][k] image pitch (floats): conflict-free ds_read_b128
 constexpr int RPAD = 4;      // [k][row] image pad (floats)
 
@@ -246,348 +245,25 @@ __global__ __launch_bounds__(WM* WN * 64) void k_gemm_f32(
 }
 
 // ---------------------------------------------------------------------------
-// Split-bf16 variant ("x6") on v_mfma_f32_32x32x16_bf16.
+// Split-bf16 fp32 GEMM on v_mfma_f32_32x32x16_bf16.
 //
 // Every fp32 operand element is split into three bf16 parts, each the
-// round-to-nearest bf16 of what is left:
+// round-to-nearest bf16 of what is left (mfma.h split2):
 //   x = hi + mid + lo + t,  |mid| <= 2^-8 |x|,  |lo| <= 2^-16 |x|,  |t| <= 2^-24 |x|
 // and C = Σ_k a b is accumulated in fp32 from the six products down to order
 // 2^-16: hi·lo + lo·hi + mid·mid + hi·mid + mid·hi + hi·hi.  What is left out
 // (mid·lo, lo·mid, lo·lo and the tails t) is below 4·2^-24 |a b| per product,
 // of random sign: the order of one fp32 rounding of the product.  Every
 // bf16 x bf16 product is exact in the fp32 accumulator.  The result has fp32
-// GEMM accuracy (tests/test_gpu_kernels.py compares both implementations
-// against float64).  bf16 MFMA runs at 16x the f32-input MFMA rate, so six
-// of them cost 3/8 of one f32 MFMA chain.  (Inputs beyond the bf16 range,
-// |x| > 3.39e38, are not supported.)
+// GEMM accuracy (tests/test_gpu_kernels.py compares against float64 and the
+// f32-input MFMA kernel above).  bf16 MFMA runs at 16x the f32-input MFMA
+// rate, so six of them cost 3/8 of one f32 MFMA chain.  (Inputs beyond the
+// bf16 range, |x| > 3.39e38, are not supported.)
 //
-// The split happens once per element while staging (global -> registers ->
-// split -> LDS), into a [plane][row][k] bf16 image of 64-byte rows whose four
-// 16-byte chunks are XOR-swizzled by (row >> 2) & 3: a lane's 8 consecutive k
-// of one row (the A/B fragment of the 32x32x16 MFMA: lane (r, h) holds
-// k = 8h .. 8h+7) are one ds_read_b128, conflict-free over every 16-lane
-// group, with no padding.
-// Staging works on 4-row x 4-k blocks, so a K-major operand (dY^T, X^T of a
-// weight gradient) is transposed in registers for free.
-// ---------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int XK = 32;  // bf16 per image row (64 B, unpadded, chunk-swizzled)
-
-// bf16 offset of k = 8 * chunk (+ 4 * half) in image row `row`
-__device__ __forceinline__ int xoff(int row, int chunk) {
-  return row * XK + ((chunk ^ ((row >> 2) & 3)) << 3);
-}
-
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
-// Two floats -> packed hi / mid / lo bf16 pairs, each part the round-to-nearest
-// bf16 of the remaining residual (v_cvt_pk_bf16_f32); both subtractions are
-// exact (Sterbenz), so a = hi + mid + lo + t with |t| <= 2^-24 |a|.
-__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
-  const bf16x2 hh = {(__bf16)a, (__bf16)b};
-  const float ra = a - (float)hh[0], rb = b - (float)hh[1];
-  const bf16x2 mm = {(__bf16)ra, (__bf16)rb};
-  const float sa = ra - (float)mm[0], sb = rb - (float)mm[1];
-  const bf16x2 ll = {(__bf16)sa, (__bf16)sb};
-  h = __builtin_bit_cast(uint32_t, hh);
-  m = __builtin_bit_cast(uint32_t, mm);
-  l = __builtin_bit_cast(uint32_t, ll);
-}
-
-__device__ __forceinline__ void split4(float4 v, uint2& hi, uint2& mid, uint2& lo) {
-  split2(v.x, v.y, hi.x, mid.x, lo.x);
-  split2(v.z, v.w, hi.y, mid.y, lo.y);
-}
-
-// One operand's K-slice (ROWS x BK) as ROWS/4 x BK/4 blocks of 4 rows x 4 k.
-// Block b: k group kb = b % 8 (fastest: 8 lanes read 128 contiguous bytes of a
-// K-contiguous row, and the LDS writes of 16 lanes hit 32 distinct banks),
-// row group rb = b / 8.  `off` rotates the thread->block map so that two
-// operands with fewer blocks than threads are staged by different waves.
-template <bool KMAJOR, int ROWS, int T>
-struct XStager {
-  static constexpr int BLOCKS = (ROWS / 4) * (BK / 4);
-  static constexpr int PER = (BLOCKS + T - 1) / T;
-  float4 r[PER][4];
-  uint32_t ok;  // bit 4j+i: load i of block j in range
-
-  __device__ __forceinline__ void load(const float* __restrict__ src, int64_t ld, int64_t row0,
-                                       int64_t rows, int64_t k0, int64_t K, int t) {
-    ok = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int b = t + j * T;
-      const int kb = b % (BK / 4), rb = b / (BK / 4);
-      const bool bin = b < BLOCKS;
-      if (!bin) continue;  // wave-uniform: BLOCKS is a multiple of 64
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (!KMAJOR) {  // load i = row 4rb+i, k = 4kb .. 4kb+3
-          const int64_t gr = row0 + 4 * rb + i, gk = k0 + 4 * kb;
-          const bool in = bin && gr < rows && gk < K;
-          r[j][i] = *reinterpret_cast<const float4*>(src + (gr < rows ? gr : rows - 1) * ld +
-                                                     (gk < K ? gk : 0));
-          ok |= (uint32_t)in << (4 * j + i);
-        } else {  // load i = k 4kb+i, rows 4rb .. 4rb+3 (rows % 4 == 0)
-          const int64_t gk = k0 + 4 * kb + i, gr = row0 + 4 * rb;
-          const bool in = bin && gk < K && gr < rows;
-          r[j][i] = *reinterpret_cast<const float4*>(src + (gk < K ? gk : K - 1) * ld +
-                                                     (gr < rows ? gr : 0));
-          ok |= (uint32_t)in << (4 * j + i);
-        }
-      }
-    }
-  }
-
-  // image: 3 planes of [ROWS][XK] bf16
-  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int b = t + j * T;
-      if (b >= BLOCKS) continue;
-      const int kb = b % (BK / 4), rb = b / (BK / 4);
-      float4 v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        v[i] = ((ok >> (4 * j + i)) & 1u) ? r[j][i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 row[4];
-      if (!KMAJOR) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) row[i] = v[i];
-      } else {  // register transpose: row i takes component i of the 4 k loads
-        row[0] = make_float4(v[0].x, v[1].x, v[2].x, v[3].x);
-        row[1] = make_float4(v[0].y, v[1].y, v[2].y, v[3].y);
-        row[2] = make_float4(v[0].z, v[1].z, v[2].z, v[3].z);
-        row[3] = make_float4(v[0].w, v[1].w, v[2].w, v[3].w);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint2 hi, mid, lo;
-        split4(row[i], hi, mid, lo);
-        const int o = xoff(4 * rb + i, kb >> 1) + 4 * (kb & 1);
-        *reinterpret_cast<uint2*>(img + o) = hi;
-        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
-        *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
-      }
-    }
-  }
-};
-
-__device__ __forceinline__ bf16x8 xfrag(const uint16_t* __restrict__ img, int row, int chunk) {
-  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + xoff(row, chunk)));
-}
-
-// 2 x 2 waves, wave tile (32 TM) x (32 TN), workgroup tile (64 TM) x (64 TN).
-// NP = 6 or 9 products per element pair.  hi·hi goes to its own accumulator and
-// the smaller products to a second one, added at the end: the correction terms
-// then accumulate with ~2^-8 of the rounding error they would pick up in the
-// large running sum.
-template <int TM, int TN, int NP, bool AK, bool BKM, int EPI, bool SPLIT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TM * TN == 1 ? 3 : 1))) void k_gemm_x6(
-    const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ C, int64_t M,
-    int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const float* __restrict__ bias,
-    const float* __restrict__ aux, int64_t ldaux, int ktiles_per_split, int accumulate) {
-  constexpr int T = 256;
-  constexpr int BM = 64 * TM, BN = 64 * TN;
-  constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (AI + BI)];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int li = lane & 31, lh = lane >> 5;
-
-  const int ntn = (int)((N + BN - 1) / BN);
-  const int ntm = (int)((M + BM - 1) / BM);
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int64_t m0 = (int64_t)(tile / ntn) * BM;
-  const int64_t n0 = (int64_t)(tile % ntn) * BN;
-
-  const int nk_total = (int)((K + BK - 1) / BK);
-  const int kt_beg = SPLIT ? blockIdx.y * ktiles_per_split : 0;
-  int kt_end = SPLIT ? kt_beg + ktiles_per_split : nk_total;
-  if (kt_end > nk_total) kt_end = nk_total;
-
-  f32x16 acc[TM][TN], acl[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = acl[a][b][r] = 0.f;
-
-  XStager<AK, BM, T> sa0, sa1;
-  XStager<BKM, BN, T> sb0, sb1;
-  // B blocks go to the threads A leaves idle (A has 2 BM blocks, B 2 BN)
-  const int tb = (tid + (2 * BM) % T) % T;
-  uint16_t* buf0 = lds;
-  uint16_t* buf1 = lds + (AI + BI);
-
-  auto compute = [&](const uint16_t* As) {
-    const uint16_t* Bs = As + AI;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int ch = ks * 2 + lh;
-      bf16x8 bh[TN], bm[TN], bl[TN];
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int bro = wn * TN * 32 + b * 32 + li;
-        bh[b] = xfrag(Bs, bro, ch);
-        bm[b] = xfrag(Bs + BN * XK, bro, ch);
-        bl[b] = xfrag(Bs + 2 * BN * XK, bro, ch);
-      }
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const int aro = wm * TM * 32 + a * 32 + li;
-        const bf16x8 ah = xfrag(As, aro, ch);
-        const bf16x8 am = xfrag(As + BM * XK, aro, ch);
-        const bf16x8 al = xfrag(As + 2 * BM * XK, aro, ch);
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          if (NP == 9) {
-            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bl[b], acl[a][b], 0, 0, 0);
-            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bl[b], acl[a][b], 0, 0, 0);
-            acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bm[b], acl[a][b], 0, 0, 0);
-          }
-          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[b], acl[a][b], 0, 0, 0);
-          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[b], acl[a][b], 0, 0, 0);
-          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm[b], acl[a][b], 0, 0, 0);
-          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm[b], acl[a][b], 0, 0, 0);
-          acl[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[b], acl[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[b], acc[a][b], 0, 0, 0);
-        }
-      }
-    }
-  };
-
-  const int nsteps = kt_end - kt_beg;
-  if (nsteps > 0) {
-    sa0.load(A, lda, m0, M, (int64_t)kt_beg * BK, K, tid);
-    sb0.load(B, ldb, n0, N, (int64_t)kt_beg * BK, K, tb);
-    if (nsteps > 1) {
-      sa1.load(A, lda, m0, M, (int64_t)(kt_beg + 1) * BK, K, tid);
-      sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + 1) * BK, K, tb);
-    }
-    sa0.store(buf0, tid);
-    sb0.store(buf0 + AI, tb);
-    __syncthreads();
-  }
-  int i = 0;
-  for (; i + 2 <= nsteps; i += 2) {
-    sa0.load(A, lda, m0, M, (int64_t)(kt_beg + i + 2) * BK, K, tid);
-    sb0.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 2) * BK, K, tb);
-    compute(buf0);
-    sa1.store(buf1, tid);
-    sb1.store(buf1 + AI, tb);
-    __syncthreads();
-    sa1.load(A, lda, m0, M, (int64_t)(kt_beg + i + 3) * BK, K, tid);
-    sb1.load(B, ldb, n0, N, (int64_t)(kt_beg + i + 3) * BK, K, tb);
-    compute(buf1);
-    sa0.store(buf0, tid);
-    sb0.store(buf0 + AI, tb);
-    __syncthreads();
-  }
-  if (i < nsteps) compute(buf0);
-
-  float* Cout = SPLIT ? C + (int64_t)blockIdx.y * M * N : C;
-  const int64_t ldo = SPLIT ? N : ldc;
-  // Epilogue through LDS: each wave writes its accumulators as a row-major
-  // [32 TM][32 TN] fp32 tile, then stores 16-byte row pieces (4 store
-  // instructions per 32 x 32 instead of 16 dword stores: the store tail is
-  // issue-bound).  Needs 16-byte aligned rows; otherwise the dword path.
-  constexpr int WR = 32 * TM, WC = 32 * TN;
-  static_assert(4 * WR * WC * (int)sizeof(float) <= (int)sizeof(lds), "epilogue tile > LDS");
-  const bool vec = ((ldo & 3) == 0) && ((reinterpret_cast<uintptr_t>(Cout) & 15) == 0) &&
-                   (SPLIT || EPI != MOLCLR_EPI_RELU_MASK ||
-                    (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
-                   (SPLIT || (EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
-                    (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
-  if (vec) {
-    __syncthreads();  // every wave is done reading the K images
-    float* tw = reinterpret_cast<float*>(lds) + wave * WR * WC;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          tw[(a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * WC + b * 32 + li] =
-              acc[a][b][r] + acl[a][b][r];
-    __syncthreads();
-    constexpr int C4 = WC / 4;
-    const int64_t mw = m0 + wm * WR, nw = n0 + wn * WC;
-#pragma unroll
-    for (int it = 0; it < WR * C4 / 64; ++it) {
-      const int idx = it * 64 + lane;
-      const int row = idx / C4, c4 = idx - row * C4;
-      const int64_t m = mw + row, n = nw + 4 * c4;
-      if (m >= M || n >= N) continue;
-      float4 v = *reinterpret_cast<const float4*>(tw + row * WC + 4 * c4);
-      float* o = Cout + m * ldo + n;
-      if (n + 4 <= N) {
-        if (!SPLIT) {
-          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
-            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
-            v = f4add(v, bv);
-            if (EPI == MOLCLR_EPI_BIAS_RELU)
-              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-          }
-          if (EPI == MOLCLR_EPI_RELU_MASK) {
-            const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
-            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
-                            x.w > 0.f ? v.w : 0.f);
-          }
-          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
-        }
-        *reinterpret_cast<float4*>(o) = v;
-      } else {  // the last, partial piece of a row (N % 4 != 0)
-        const float e[4] = {v.x, v.y, v.z, v.w};
-        for (int j = 0; j < 4 && n + j < N; ++j) {
-          float x = e[j];
-          if (!SPLIT) {
-            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
-            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
-            if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
-            if (accumulate) x += o[j];
-          }
-          o[j] = x;
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int64_t n = n0 + wn * TN * 32 + b * 32 + li;
-    if (n >= N) continue;
-    float bv = 0.f;
-    if (!SPLIT && (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU)) bv = bias[n];
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t m = m0 + wm * TM * 32 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= M) continue;
-        float v = acc[a][b][r] + acl[a][b][r];
-        if (!SPLIT) {
-          if (EPI == MOLCLR_EPI_BIAS) v = v + bv;
-          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bv, 0.f);
-          if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
-          if (accumulate) v += Cout[m * ldo + n];
-        }
-        Cout[m * ldo + n] = v;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Split-bf16 GEMM, second generation ("p6"): the same six-product scheme and
-// LDS image as k_gemm_x6, with the staging cost cut down — that, not the
-// MFMA, bounds k_gemm_x6 (rocprofv3: ~20 VALU instructions per MFMA, MFMA
-// busy 22 %).
+// "p6": a 64 x 64 (or 128 x 64 / 64 x 128) tile of 2 x 2 waves with both
+// operands staged as split [plane][row][k] images (xoff swizzle).  The first
+// version split both operands while staging 4 x 4 blocks and was bound by it
+// (rocprofv3: ~20 VALU instructions per MFMA, MFMA busy 22 %); here:
 //  * Operand sources (template AMODE / BMODE):
 //      0 fp32, K contiguous ([rows][K]): a thread stages 8 consecutive k of
 //        one row (two float4 loads) and writes one 16-byte chunk per plane;
@@ -601,18 +277,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TM * TN == 
 //    offsets, and only the last, partial K tile takes the masked path.
 // ---------------------------------------------------------------------------
 constexpr int kPlanesRowPad = 128;  // Npad multiple (covers every BN)
-
-__device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4& hi, u32x4& mid,
-                                       u32x4& lo) {
-  uint32_t h[4], m[4], l[4];
-  split2(a.x, a.y, h[0], m[0], l[0]);
-  split2(a.z, a.w, h[1], m[1], l[1]);
-  split2(b.x, b.y, h[2], m[2], l[2]);
-  split2(b.z, b.w, h[3], m[3], l[3]);
-  hi = u32x4{h[0], h[1], h[2], h[3]};
-  mid = u32x4{m[0], m[1], m[2], m[3]};
-  lo = u32x4{l[0], l[1], l[2], l[3]};
-}
 
 // fp32, K contiguous: unit = (row, 8-k chunk); ROWS*4 units over T threads.
 template <int ROWS, int T>
@@ -672,16 +336,6 @@ struct PStageK {
 // 4 x 4 blocks transposed in registers into the [row][k] image, spent 60 % of
 // its LDS cycles in bank conflicts: rows 4 apart share banks.)
 // Needs ROWS == 64, rows % 4 == 0 and ld % 4 == 0.
-// 32-element XOR of k-row k: separates the 4 k-rows one transposed read
-// touches (64-row rows are 32 dwords: rows k and k+2 share banks; 128-row
-// rows are 64 dwords: all four do).
-// 160-row rows are 80 dwords (16 mod 64 banks apart): the four k-rows of a
-// transposed read already fall on distinct banks, no XOR.
-template <int ROWS>
-__device__ __forceinline__ int kswz(int k) {
-  return ROWS == 64 ? ((k >> 1) & 1) << 5 : ROWS == 128 ? (k & 3) << 5 : 0;
-}
-
 template <int ROWS, int T>
 struct PStageM {
   static_assert(ROWS == 64 || ROWS == 128 || ROWS == 160,
@@ -741,28 +395,6 @@ struct PStageM {
     }
   }
 };
-
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-// MFMA 32x32x16 operand fragment of rows row0 .. row0+31 (lane: row row0 + li,
-// k = 16 ks + 8 lh .. +7) from a [k][ROWS] K-major image plane: two transposed
-// reads, each giving 4 consecutive k of one row.  Lane 4q+p of a 16-lane group
-// addresses k-row q, rows 4p .. 4p+3 of the group's 16 (ISA ds_read_b64_tr_b16).
-template <int ROWS>
-__device__ __forceinline__ bf16x8 kmfrag(const uint16_t* __restrict__ plane, int row0, int ks,
-                                         int lane) {
-  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
-  const int m = row0 + (g & 1) * 16 + 4 * pp;
-  const int k = 16 * ks + 8 * (g >> 1) + q;
-  const uint16_t* a0 = plane + k * ROWS + (m ^ kswz<ROWS>(k));
-  const uint16_t* a1 = plane + (k + 4) * ROWS + (m ^ kswz<ROWS>(k + 4));
-  const v4i16 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
-  const v4i16 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
-  typedef short v8i16 __attribute__((ext_vector_type(8)));
-  const v8i16 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // pre-split planes [3][Npad][Kp] bf16: unit = (plane, row, 16-byte chunk)
 template <int ROWS, int T>
@@ -850,7 +482,7 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
   using SA = typename PStageSel<AMODE, BM, T>::type;
   using SB = typename PStageSel<BMODE, BN, T>::type;
   // a K-major operand with fewer units than threads leaves threads idle: give
-  // the other operand's units to those threads (as k_gemm_x6 does)
+  // the other operand's units to those threads
   const int ta = tid;
   const int tb = (AMODE == 1 && SA::UNITS < T) ? (tid + SA::UNITS) % T : tid;
   SA sa0, sa1;
@@ -1623,29 +1255,24 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   C[m * ldc + n] = v;
 }
 
-// 0 = f32-input MFMA, 64 x 64 tiles; split-bf16 with 6 products and 1 = 64 x 64,
-// 2 = 128 x 64, 3 = 128 x 128 tiles; 4 = split-bf16 with all 9 products, 64 x 64;
-// 5 / 6 = split-bf16 "p6" staging, 64 x 64 / 128 x 64 (molclr_gemm_set_impl).
-// The split-bf16 kernels stage K-major operands 4 rows at a time, so they need
-// rows % 4 == 0 and ld % 4 == 0 there; other shapes take impl 0.
-int g_impl = 5;
-// tile of molclr_gemm_f32_bplanes: 0 = automatic (64 x 128 for N >= 512, else
-// 64 x 64: measured best on the step's shapes, tools/gemm_bench.py), 5 = 64 x 64,
-// 6 = 128 x 64, 7 = 64 x 128, 8 = 128 x 128
-int g_bplanes_impl = 0;
-int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk) {
-  if (g_impl == 0) return 0;
+// Implementations of molclr_gemm_f32 (per call, molclr_gemm_f32_impl):
+// 0 = f32-input MFMA, 64 x 64 tiles; 5 (automatic) / 6 = split-bf16 "p6",
+// 64 x 64 / 128 x 64.  The split-bf16 kernels stage K-major operands 4 rows
+// at a time, so they need rows % 4 == 0 and ld % 4 == 0 there; other shapes
+// take impl 0.
+int impl_for(int64_t M, int64_t N, int64_t lda, int64_t ldb, int ak, int bk, int want) {
+  if (want < 0) want = 5;
+  if (want == 0) return 0;
   if (ak && (M % 4 || lda % 4)) return 0;
   if (bk && (N % 4 || ldb % 4)) return 0;
-  if (g_impl == 6 && ak) return 5;  // the K-major image is laid out for 64-row tiles
-  return g_impl;
+  if (want == 6 && ak) return 5;  // the K-major image is laid out for 64-row tiles
+  return want;
 }
 // p6 tiles of a weight-gradient product (both operands K-major): 128 along the
 // longer of M / N (8.9 -> ~6 VALU per MFMA: half the B or A split work)
 bool p6_wide(int impl, int ak, int bk) { return impl == 5 && ak && bk; }
 int tiles_for(int impl, int64_t M, int64_t N, int ak = 0, int bk = 0) {
-  int64_t bm = (impl == 2 || impl == 3 || impl == 6 || impl == 8) ? 128 : 64,
-          bn = (impl == 3 || impl == 7 || impl == 8) ? 128 : 64;
+  int64_t bm = (impl == 6 || impl == 8) ? 128 : 64, bn = (impl == 7 || impl == 8) ? 128 : 64;
   if (p6_wide(impl, ak, bk)) {
     bm = M >= N ? 128 : 64;
     bn = M >= N ? 64 : 128;
@@ -1704,30 +1331,6 @@ void launch_t(dim3 grid, hipStream_t s, const Args& a) {
   }
   if (a.impl == 6) {
     launch_p6<(AK ? 1 : 2), AK ? 1 : 0, BKM ? 1 : 0, EPI, SPLIT>(grid, s, a);
-    return;
-  }
-  if (a.impl == 1) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, 1, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
-                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.kps, a.accumulate);
-    return;
-  }
-  if (a.impl == 2) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, 1, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
-                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.kps, a.accumulate);
-    return;
-  }
-  if (a.impl == 4) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<1, 1, 9, AK, BKM, EPI, SPLIT>), grid, dim3(256),
-                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.kps, a.accumulate);
-    return;
-  }
-  if (a.impl == 3) {
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_x6<2, 2, 6, AK, BKM, EPI, SPLIT>), grid, dim3(256),
-                         0, s, a.A, a.B, a.C, a.M, a.N, a.K, a.lda, a.ldb, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.kps, a.accumulate);
     return;
   }
   molclr::launch_timed(molclr::kTimeGemm, (k_gemm_f32<WM, WN, TM, TN, AK, BKM, EPI, SPLIT>), grid,
@@ -1860,15 +1463,14 @@ int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s) {
 // single-group blocks measured 8 % / 40 % slower with the partial reduction
 // included), each group at least 4 K tiles deep.  kg = 2 (default): two
 // groups per block, ~256 blocks; kg = 1: ~512 one-group blocks.
-int g_w6_groups = 2;
 struct W6Plan {
   int tn, splits, kps, kg;
   int64_t ntiles;
 };
-W6Plan w6_plan(int64_t M, int64_t N, int64_t K) {
+W6Plan w6_plan(int64_t M, int64_t N, int64_t K, int kg) {
   W6Plan p;
   p.tn = wide_tn(N);
-  p.kg = g_w6_groups;
+  p.kg = kg;
   p.ntiles = ((M + kW6BM - 1) / kW6BM) * ((N + 32 * p.tn - 1) / (32 * p.tn));
   const int64_t nk = (K + BK - 1) / BK;
   // whole waves of blocks only: a block past 512 / kg (one per CU at kg = 2)
@@ -1885,18 +1487,15 @@ W6Plan w6_plan(int64_t M, int64_t N, int64_t K) {
 bool w6_shape_ok(int64_t M, int64_t N, int64_t K) {
   return M % 4 == 0 && N % 4 == 0 && K >= 1024 && M * N < (1ll << 28);
 }
-// sized for the larger of the two group settings (the setting may change
-// between a workspace query and the launch)
+// sized for the larger of the two group settings (molclr_linear_wgrad_groups
+// takes either with the same workspace query)
 size_t w6_ws_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
-  const int keep = g_w6_groups;
   size_t need = 0;
   for (int kg = 1; kg <= 2; ++kg) {
-    g_w6_groups = kg;
-    const W6Plan p = w6_plan(M, N, K);
+    const W6Plan p = w6_plan(M, N, K, kg);
     const size_t b = (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
     need = b > need ? b : need;
   }
-  g_w6_groups = keep;
   return need;
 }
 
@@ -1922,8 +1521,8 @@ void launch_w6(const W6Plan& p, hipStream_t s, const float* A, const float* B, f
 // when non-null.  Partial tiles in the workspace, then the fixed-order reduce.
 int run_w6(const float* A, const float* B, float* C, float* colsum, int64_t M, int64_t N,
            int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int accumulate, void* ws,
-           size_t ws_bytes, hipStream_t s) {
-  const W6Plan p = w6_plan(M, N, K);
+           size_t ws_bytes, hipStream_t s, int kg = 2) {
+  const W6Plan p = w6_plan(M, N, K, kg);
   MOLCLR_REQUIRE_WS(ws_bytes, w6_ws_bytes(M, N, K, colsum != nullptr));
   float* part = static_cast<float*>(ws);
   float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
@@ -2011,10 +1610,20 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
 
 }  // namespace
 
+void molclr_splitk_reduce_none(const float* partial, int splits, int64_t M, int64_t N, float* C,
+                               int64_t ldc, int accumulate, const float* cs_partial,
+                               float* colsum, hipStream_t s) {
+  const float* no_f = nullptr;
+  molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>,
+                       dim3((unsigned)molclr::ceil_div(M * N > M ? M * N : M, 256)), dim3(256), 0,
+                       s, partial, splits, M, N, C, ldc, no_f, no_f, (int64_t)0, accumulate,
+                       cs_partial, colsum);
+}
+
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {
   // sized for the largest split count any implementation would pick
   int sp = pick_splits(0, M, N, K);
-  for (int impl = 1; impl <= 8; ++impl) {
+  for (int impl = 5; impl <= 8; ++impl) {
     const int s2 = pick_splits(impl, M, N, K);
     sp = s2 > sp ? s2 : sp;
   }
@@ -2028,13 +1637,15 @@ MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t 
   return need;
 }
 
-MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
-                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
-                               int b_kmajor, int epilogue_flags, const float* bias, const float* aux,
-                               int64_t ldaux, void* workspace, size_t workspace_bytes,
-                               molclr_stream_t stream) {
+MOLCLR_API int molclr_gemm_f32_impl(const float* A, const float* B, float* C, int64_t M, int64_t N,
+                                    int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                                    int b_kmajor, int epilogue_flags, const float* bias,
+                                    const float* aux, int64_t ldaux, void* workspace,
+                                    size_t workspace_bytes, molclr_stream_t stream, int impl_req) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
+  MOLCLR_REQUIRE(impl_req == -1 || impl_req == 0 || impl_req == 5 || impl_req == 6,
+                 "gemm_f32: impl %d (-1 automatic, 0, 5, 6)", impl_req);
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32: negative size");
   MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
                  "gemm_f32: bad epilogue %d", epilogue);
@@ -2054,14 +1665,24 @@ MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t
     molclr::set_error("gemm_f32: K == 0 unsupported");
     return MOLCLR_ERR_UNSUPPORTED;
   }
-  const int impl = impl_for(M, N, lda, ldb, a_kmajor, b_kmajor);
+  const int impl = impl_for(M, N, lda, ldb, a_kmajor, b_kmajor, impl_req);
   // a weight-gradient product (both operands K-major, long K): k_gemm_w6
-  if (impl == 5 && a_kmajor && b_kmajor && epilogue == MOLCLR_EPI_NONE && w6_shape_ok(M, N, K) &&
-      lda % 4 == 0 && ldb % 4 == 0 && workspace_bytes >= w6_ws_bytes(M, N, K, false))
+  if (impl_req == -1 && impl == 5 && a_kmajor && b_kmajor && epilogue == MOLCLR_EPI_NONE &&
+      w6_shape_ok(M, N, K) && lda % 4 == 0 && ldb % 4 == 0 &&
+      workspace_bytes >= w6_ws_bytes(M, N, K, false))
     return run_w6(A, B, C, nullptr, M, N, K, lda, ldb, ldc, accumulate, workspace,
                   workspace_bytes, s);
   Args a{A, B, C, M, N, K, lda, ldb, ldc, bias, aux, ldaux, 0, accumulate, impl};
   return run_gemm(a, impl, false, a_kmajor, b_kmajor, epilogue, workspace, workspace_bytes, s);
+}
+
+MOLCLR_API int molclr_gemm_f32(const float* A, const float* B, float* C, int64_t M, int64_t N,
+                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                               int b_kmajor, int epilogue_flags, const float* bias, const float* aux,
+                               int64_t ldaux, void* workspace, size_t workspace_bytes,
+                               molclr_stream_t stream) {
+  return molclr_gemm_f32_impl(A, B, C, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor, epilogue_flags,
+                              bias, aux, ldaux, workspace, workspace_bytes, stream, -1);
 }
 
 MOLCLR_API size_t molclr_bplanes_bytes(int64_t N, int64_t K) {
@@ -2107,13 +1728,16 @@ MOLCLR_API int molclr_bplanes_make_batch(int count, const float* const* B, const
   return MOLCLR_OK;
 }
 
-MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
-                                       int64_t N, int64_t K, int64_t lda, int64_t ldc,
-                                       int a_kmajor, int epilogue_flags, const float* bias,
-                                       const float* aux, int64_t ldaux, void* workspace,
-                                       size_t workspace_bytes, molclr_stream_t stream) {
+MOLCLR_API int molclr_gemm_f32_bplanes_tile(const float* A, const uint16_t* planes, float* C,
+                                            int64_t M, int64_t N, int64_t K, int64_t lda,
+                                            int64_t ldc, int a_kmajor, int epilogue_flags,
+                                            const float* bias, const float* aux, int64_t ldaux,
+                                            void* workspace, size_t workspace_bytes,
+                                            molclr_stream_t stream, int tile) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
+  MOLCLR_REQUIRE(tile == 0 || (tile >= 5 && tile <= 9),
+                 "gemm_f32_bplanes: tile %d (0 automatic, 5..9)", tile);
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_bplanes: negative size");
   MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
                  "gemm_f32_bplanes: bad epilogue %d", epilogue);
@@ -2130,7 +1754,7 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   const int64_t npad = planes_npad(N), kp = planes_kp(K);
   // automatic: q6 for a row-major A whose row tiles fill the chip, else p6
   // (64 x 128 for N >= 512, else 64 x 64; split-K when it pays)
-  int impl = g_bplanes_impl;
+  int impl = tile;
   if (impl == 0) impl = (!a_kmajor && q6_blocks(M, N) >= 128) ? 9 : (N >= 512 ? 7 : 5);
   if (impl == 9 && (a_kmajor || K > kQ6MaxK || 3 * npad * kp >= (1ll << 31) ||
                     q6_blocks(M, N) >= (1ll << 31)))
@@ -2142,6 +1766,15 @@ MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, f
   if (impl == 9) return run_q6(a, npad, epilogue, molclr::as_stream(stream));
   return run_gemm(a, impl, true, a_kmajor, 0, epilogue, workspace, workspace_bytes,
                   molclr::as_stream(stream));
+}
+
+MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
+                                       int64_t N, int64_t K, int64_t lda, int64_t ldc,
+                                       int a_kmajor, int epilogue_flags, const float* bias,
+                                       const float* aux, int64_t ldaux, void* workspace,
+                                       size_t workspace_bytes, molclr_stream_t stream) {
+  return molclr_gemm_f32_bplanes_tile(A, planes, C, M, N, K, lda, ldc, a_kmajor, epilogue_flags,
+                                      bias, aux, ldaux, workspace, workspace_bytes, stream, 0);
 }
 
 size_t molclr_colsum_ws(int64_t rows, int64_t cols);  // norm.hip
@@ -2160,10 +1793,12 @@ MOLCLR_API size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_ou
   return cs > need ? cs : need;
 }
 
-MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, float* db,
-                                   int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
-                                   int64_t ld_x, int accumulate, void* workspace,
-                                   size_t workspace_bytes, molclr_stream_t stream) {
+MOLCLR_API int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float* db,
+                                          int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                                          int64_t ld_x, int accumulate, void* workspace,
+                                          size_t workspace_bytes, molclr_stream_t stream,
+                                          int groups) {
+  MOLCLR_REQUIRE(groups == 1 || groups == 2, "linear_wgrad: groups must be 1 or 2");
   MOLCLR_REQUIRE(rows >= 0 && n_out > 0 && n_in > 0, "linear_wgrad: bad sizes");
   MOLCLR_REQUIRE(dy && x && dW, "linear_wgrad: null pointer");
   MOLCLR_REQUIRE(ld_dy >= n_out && ld_x >= n_in, "linear_wgrad: leading dimension too small");
@@ -2180,10 +1815,10 @@ MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, f
     return MOLCLR_OK;
   }
   // dW = dy^T x: A = dy (K-major, lda = ld_dy), B = x (K-major, ldb = ld_x)
-  if (g_impl == 5 && w6_shape_ok(n_out, n_in, rows) && ld_dy % 4 == 0 && ld_x % 4 == 0)
+  if (w6_shape_ok(n_out, n_in, rows) && ld_dy % 4 == 0 && ld_x % 4 == 0)
     return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
-                  workspace_bytes, molclr::as_stream(stream));
-  if (!db || impl_for(n_out, n_in, ld_dy, ld_x, 1, 1) != 5) {
+                  workspace_bytes, molclr::as_stream(stream), groups);
+  if (!db || impl_for(n_out, n_in, ld_dy, ld_x, 1, 1, -1) != 5) {
     int rc = molclr_gemm_f32(dy, x, dW, n_out, n_in, rows, ld_dy, ld_x, n_in, 1, 1, flags,
                              nullptr, nullptr, 0, workspace, workspace_bytes, stream);
     if (rc || !db) return rc;
@@ -2196,23 +1831,10 @@ MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, f
                   molclr::as_stream(stream));
 }
 
-MOLCLR_API int molclr_gemm_get_impl(void) { return g_impl; }
-
-MOLCLR_API int molclr_gemm_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl >= 0 && impl <= 6, "gemm_set_impl: impl must be 0..6");
-  g_impl = impl;
-  return MOLCLR_OK;
-}
-
-MOLCLR_API int molclr_gemm_w6_set_groups(int kg) {
-  MOLCLR_REQUIRE(kg == 1 || kg == 2, "gemm_w6_set_groups: groups must be 1 or 2");
-  g_w6_groups = kg;
-  return MOLCLR_OK;
-}
-
-MOLCLR_API int molclr_gemm_bplanes_set_impl(int impl) {
-  MOLCLR_REQUIRE(impl == 0 || (impl >= 5 && impl <= 9),
-                 "gemm_bplanes_set_impl: impl must be 0 (automatic) or 5..9");
-  g_bplanes_impl = impl;
-  return MOLCLR_OK;
+MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, float* db,
+                                   int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                                   int64_t ld_x, int accumulate, void* workspace,
+                                   size_t workspace_bytes, molclr_stream_t stream) {
+  return molclr_linear_wgrad_groups(dy, x, dW, db, rows, n_out, n_in, ld_dy, ld_x, accumulate,
+                                    workspace, workspace_bytes, stream, 2);
 }

@@ -1,0 +1,107 @@
+// MFMA operand helpers shared by the GEMM kernels (gemm.hip: split-bf16 fp32
+// GEMMs; gemm_bf16.hip: the native bf16 GEMMs of the c5 configuration).
+//
+// v_mfma_f32_32x32x16_bf16: lane l (r = l & 31, h = l >> 5) holds A[row r][k =
+// 8h + j] and B[k = 8h + j][col r] in element j = 0..7 of its fragment; the
+// 32 x 32 fp32 result has its column on the lane and rows (reg & 3) +
+// 8 (reg >> 2) + 4 h in the 16 registers.
+#pragma once
+
+#include "common.h"
+
+namespace molclr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int BK = 32;  // K per staged slice
+constexpr int XK = 32;  // bf16 per [row][k] image row (64 B, unpadded, chunk-swizzled)
+
+// [row][k] images: bf16 offset of k = 8 * chunk in image row `row`; the four
+// 16-byte chunks of a row are XOR-swizzled by (row >> 2) & 3, so a lane's
+// 8 consecutive k of one row (one MFMA fragment) are one ds_read_b128,
+// conflict-free over every 16-lane group, with no padding.
+__device__ __forceinline__ int xoff(int row, int chunk) {
+  return row * XK + ((chunk ^ ((row >> 2) & 3)) << 3);
+}
+
+__device__ __forceinline__ bf16x8 xfrag(const uint16_t* __restrict__ img, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + xoff(row, chunk)));
+}
+
+// Two floats -> packed hi / mid / lo bf16 pairs, each part the round-to-nearest
+// bf16 of the remaining residual (v_cvt_pk_bf16_f32); both subtractions are
+// exact (Sterbenz), so a = hi + mid + lo + t with |t| <= 2^-24 |a|.
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const bf16x2 hh = {(__bf16)a, (__bf16)b};
+  const float ra = a - (float)hh[0], rb = b - (float)hh[1];
+  const bf16x2 mm = {(__bf16)ra, (__bf16)rb};
+  const float sa = ra - (float)mm[0], sb = rb - (float)mm[1];
+  const bf16x2 ll = {(__bf16)sa, (__bf16)sb};
+  h = __builtin_bit_cast(uint32_t, hh);
+  m = __builtin_bit_cast(uint32_t, mm);
+  l = __builtin_bit_cast(uint32_t, ll);
+}
+
+__device__ __forceinline__ void split4(float4 v, uint2& hi, uint2& mid, uint2& lo) {
+  split2(v.x, v.y, hi.x, mid.x, lo.x);
+  split2(v.z, v.w, hi.y, mid.y, lo.y);
+}
+
+__device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4& hi, u32x4& mid,
+                                       u32x4& lo) {
+  uint32_t h[4], m[4], l[4];
+  split2(a.x, a.y, h[0], m[0], l[0]);
+  split2(a.z, a.w, h[1], m[1], l[1]);
+  split2(b.x, b.y, h[2], m[2], l[2]);
+  split2(b.z, b.w, h[3], m[3], l[3]);
+  hi = u32x4{h[0], h[1], h[2], h[3]};
+  mid = u32x4{m[0], m[1], m[2], m[3]};
+  lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+// K-major [k][ROWS] image planes (the dY^T / X^T operands of a weight
+// gradient), read with the gfx950 transposed LDS read.  32-element XOR of
+// k-row k: separates the 4 k-rows one transposed read touches (64-row rows
+// are 32 dwords: rows k and k+2 share banks; 128-row rows are 64 dwords: all
+// four do, as on any multiple of 128 rows); 160-row rows are 80 dwords
+// (16 mod 64 banks apart): no XOR.
+template <int ROWS>
+__device__ __forceinline__ int kswz(int k) {
+  return ROWS == 64 ? ((k >> 1) & 1) << 5 : (ROWS % 128 == 0) ? (k & 3) << 5 : 0;
+}
+
+// MFMA 32x32x16 operand fragment of rows row0 .. row0+31 (lane: row row0 + li,
+// k = 16 ks + 8 lh .. +7) from a [k][ROWS] K-major image plane: two transposed
+// reads, each giving 4 consecutive k of one row.  Lane 4q+p of a 16-lane group
+// addresses k-row q, rows 4p .. 4p+3 of the group's 16 (ISA ds_read_b64_tr_b16).
+template <int ROWS>
+__device__ __forceinline__ bf16x8 kmfrag(const uint16_t* __restrict__ plane, int row0, int ks,
+                                         int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int m = row0 + (g & 1) * 16 + 4 * pp;
+  const int k = 16 * ks + 8 * (g >> 1) + q;
+  const uint16_t* a0 = plane + k * ROWS + (m ^ kswz<ROWS>(k));
+  const uint16_t* a1 = plane + (k + 4) * ROWS + (m ^ kswz<ROWS>(k + 4));
+  const v4i16 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+  const v4i16 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// row of register r of a 32x32 MFMA accumulator, lane half lh
+__device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
+
+}  // namespace molclr
+
+// split-K partial reduction of the fp32 GEMMs (gemm.hip), shared with the bf16
+// weight-gradient GEMM: C (+)= Σ_z partial[z] (fixed order), colsum (+)= Σ_z
+// cs_partial[z] when cs_partial is given.
+void molclr_splitk_reduce_none(const float* partial, int splits, int64_t M, int64_t N, float* C,
+                               int64_t ldc, int accumulate, const float* cs_partial,
+                               float* colsum, hipStream_t s);

@@ -466,7 +466,8 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
 // ---------------------------------------------------------------------------
 // segment pooling over graph_ptr
 // ---------------------------------------------------------------------------
-__global__ void k_pool_fwd(const float4* __restrict__ h, const int32_t* __restrict__ ptr,
+template <typename St = StF32>
+__global__ void k_pool_fwd(const typename St::T* __restrict__ h, const int32_t* __restrict__ ptr,
                            float4* __restrict__ out, int64_t G, int d4, int mode) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= G * d4) return;
@@ -480,11 +481,11 @@ __global__ void k_pool_fwd(const float4* __restrict__ h, const int32_t* __restri
   for (; i + 8 <= end; i += 8) {
     float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = h[(int64_t)(i + u) * d4 + c];
+    for (int u = 0; u < 8; ++u) v[u] = St::ld(h, (int64_t)(i + u) * d4 + c);
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc = f4add(acc, v[u]);
   }
-  for (; i < end; ++i) acc = f4add(acc, h[(int64_t)i * d4 + c]);
+  for (; i < end; ++i) acc = f4add(acc, St::ld(h, (int64_t)i * d4 + c));
   if (mode == 0) {
     float cnt = (float)(end - beg > 1 ? end - beg : 1);
     acc = make_float4(acc.x / cnt, acc.y / cnt, acc.z / cnt, acc.w / cnt);
@@ -492,8 +493,9 @@ __global__ void k_pool_fwd(const float4* __restrict__ h, const int32_t* __restri
   out[t] = acc;
 }
 
+template <typename St = StF32>
 __global__ void k_pool_bwd(const float4* __restrict__ dout, const int32_t* __restrict__ ptr,
-                           float4* __restrict__ dh, int64_t G, int d4, int mode) {
+                           typename St::T* __restrict__ dh, int64_t G, int d4, int mode) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= G * d4) return;
   int64_t g = t / d4;
@@ -504,7 +506,7 @@ __global__ void k_pool_bwd(const float4* __restrict__ dout, const int32_t* __res
     float cnt = (float)(end - beg > 1 ? end - beg : 1);
     v = make_float4(v.x / cnt, v.y / cnt, v.z / cnt, v.w / cnt);
   }
-  for (int32_t i = beg; i < end; ++i) dh[(int64_t)i * d4 + c] = v;
+  for (int32_t i = beg; i < end; ++i) St::st(dh, (int64_t)i * d4 + c, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -817,9 +819,8 @@ MOLCLR_API int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr,
   }
   if (G == 0) return MOLCLR_OK;
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_pool_fwd, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), (const float4*)h, graph_ptr, (float4*)out, G, d4,
-                     mode);
+  hipLaunchKernelGGL(k_pool_fwd<StF32>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), h, graph_ptr, (float4*)out, G, d4, mode);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -840,8 +841,39 @@ MOLCLR_API int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_p
   }
   if (G == 0) return MOLCLR_OK;
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_pool_bwd, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
-                     (const float4*)dout, graph_ptr, (float4*)dh, G, d4, mode);
+  hipLaunchKernelGGL(k_pool_bwd<StF32>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
+                     (const float4*)dout, graph_ptr, dh, G, d4, mode);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_segment_pool_fwd_bf16(const uint16_t* h, const int32_t* graph_ptr,
+                                            float* out, int64_t G, int64_t D, int mode,
+                                            molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_fwd_bf16: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(mode == 0 || mode == 1, "segment_pool_fwd_bf16: mode %d (0 mean, 1 add)", mode);
+  if (G == 0) return MOLCLR_OK;
+  const int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_pool_fwd<StBF16>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), h, graph_ptr, (float4*)out, G, d4, mode);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* graph_ptr,
+                                            uint16_t* dh, int64_t N, int64_t G, int64_t D, int mode,
+                                            molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_bwd_bf16: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(mode == 0 || mode == 1, "segment_pool_bwd_bf16: mode %d (0 mean, 1 add)", mode);
+  hipStream_t s = molclr::as_stream(stream);
+  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * sizeof(uint16_t), s) != hipSuccess) {
+    molclr::set_error("segment_pool_bwd_bf16: memset failed");
+    return MOLCLR_ERR_ARG;
+  }
+  if (G == 0) return MOLCLR_OK;
+  const int d4 = (int)(D / 4);
+  hipLaunchKernelGGL(k_pool_bwd<StBF16>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
+                     (const float4*)dout, graph_ptr, dh, G, d4, mode);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

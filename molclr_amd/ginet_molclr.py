@@ -61,8 +61,16 @@ class GINet(nn.Module):
     """models/ginet_molclr.py:50-117.  ``forward(data) -> (h [B, feat_dim],
     out [B, feat_dim // 2])``."""
 
-    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean'):
+    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean',
+                 precision='fp32'):
         super().__init__()
+        if precision not in ('fp32', 'bf16'):
+            raise ValueError(f"precision {precision!r}: 'fp32' or 'bf16'")
+        # 'bf16': the c5 configuration (BASELINE.json) / the reference's
+        # fp16_precision switch (molclr.py:16-24,93-96): bf16 node features and
+        # bf16 MFMA GEMMs with fp32 accumulation; fp32 master weights, BatchNorm
+        # statistics, pooled features, heads and NT-Xent
+        self.precision = precision
         self.num_layer = num_layer
         self.emb_dim = emb_dim
         self.feat_dim = feat_dim
@@ -105,6 +113,8 @@ class GINet(nn.Module):
     def _executor_ok(self) -> bool:
         if not self.use_executor or self.num_layer > 16 or self.emb_dim % 4:
             return False
+        if self.precision == 'bf16' and self.emb_dim % 8:
+            return False
         if self.drop_ratio > 0 and self.training:
             return False
         bn0 = self.batch_norms[0]
@@ -124,7 +134,10 @@ class GINet(nn.Module):
         graph = graph or device_graph(data)
         if self._executor_ok():
             return ops.gin_encoder(data.x, graph, list(self.batch_norms),
-                                   self._encoder_params()), graph
+                                   self._encoder_params(), self.precision), graph
+        if self.precision != 'fp32':
+            raise NotImplementedError("bf16 runs through the encoder executor only "
+                                      "(dropout 0, tracked BatchNorm statistics)")
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         # per-edge embeddings E1[bt] + E2[bd] of every layer, tabulated in one launch
         Ec = ops.edge_tables_combine([g.edge_embedding1.weight for g in self.gnns],
@@ -162,5 +175,6 @@ class GINet(nn.Module):
             return torch.cat([hi, hj], 0), torch.cat([oi, oj], 0)
         graph = pair_graph(xi, xj)
         x = torch.cat([xi.x, xj.x], 0)
-        h = ops.gin_encoder(x, graph, list(self.batch_norms), self._encoder_params())
+        h = ops.gin_encoder(x, graph, list(self.batch_norms), self._encoder_params(),
+                            self.precision)
         return self._readout(h, graph)

@@ -104,7 +104,10 @@ class MolCLR(object):
     def build_model(self):
         if self.config['model_type'] == 'gin':
             from .ginet_molclr import GINet
-            model = GINet(**self.config["model"]).to(self.device)
+            # fp16_precision (apex O2 in the reference, molclr.py:16-24,93-96):
+            # the bf16 encoder path here, fp32 master weights
+            prec = 'bf16' if self.config.get('fp16_precision', False) else 'fp32'
+            model = GINet(**self.config["model"], precision=prec).to(self.device)
         elif self.config['model_type'] == 'gcn':
             from .gcn_molclr import GCN
             model = GCN(**self.config["model"]).to(self.device)

@@ -128,8 +128,9 @@ def set_kernel_timer(timer: KernelTimer | None) -> None:
 # GEMM helpers
 # ---------------------------------------------------------------------------
 def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
-         out=None, accumulate=0):
-    """C[M,N] = op(A) op(B) (+ epilogue, + C if accumulate), see molclr_gemm_f32."""
+         out=None, accumulate=0, impl=-1):
+    """C[M,N] = op(A) op(B) (+ epilogue, + C if accumulate), see molclr_gemm_f32
+    (``impl``: molclr_gemm_f32_impl's choice, -1 = automatic)."""
     dev = A.device
     if out is None:
         out = torch.empty(M, N, dtype=torch.float32, device=dev)
@@ -137,9 +138,10 @@ def gemm(A, B, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, a
         epi |= EPI_ACCUMULATE
     ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, N, K)
     ws = _ws(ws_bytes, dev) if ws_bytes else None
-    _lib.call("molclr_gemm_f32", A.data_ptr(), B.data_ptr(), out.data_ptr(), M, N, K, lda, ldb,
-              out.stride(0), int(a_kmajor), int(b_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
-              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A))
+    _lib.call("molclr_gemm_f32_impl", A.data_ptr(), B.data_ptr(), out.data_ptr(), M, N, K, lda,
+              ldb, out.stride(0), int(a_kmajor), int(b_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A),
+              int(impl))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -211,9 +213,9 @@ def _refresh_planes(gen: int) -> None:
 
 
 def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
-           out=None, accumulate=0):
+           out=None, accumulate=0, tile=0):
     """gemm() whose B operand is a weight: through its cached pre-split planes
-    (molclr_gemm_f32_bplanes) when enabled."""
+    (molclr_gemm_f32_bplanes; ``tile``: molclr_gemm_f32_bplanes_tile's choice)."""
     if not USE_BPLANES:
         return gemm(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi, bias, aux, out, accumulate)
     _check(A, W)
@@ -225,9 +227,10 @@ def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None,
         epi |= EPI_ACCUMULATE
     ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, N, K)
     ws = _ws(ws_bytes, dev) if ws_bytes else None
-    _lib.call("molclr_gemm_f32_bplanes", A.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
-              lda, out.stride(0), int(a_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
-              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A))
+    _lib.call("molclr_gemm_f32_bplanes_tile", A.data_ptr(), planes.data_ptr(), out.data_ptr(), M,
+              N, K, lda, out.stride(0), int(a_kmajor), epi, _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, _lib.ptr(ws), ws_bytes, _stream(A),
+              int(tile))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -287,13 +290,14 @@ def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=No
     return dx, dW, db
 
 
-def gine_aggregate_bytes(N: int, D: int, E: int) -> int:
+def gine_aggregate_bytes(N: int, D: int, E: int, elem_bytes: int = 4) -> int:
     """Compulsory HBM bytes of one molclr_gine_aggregate_fwd launch: read x and
-    write the output once (2*N*D*4) and the 16-byte neighbour slots of every
-    node (16N); the 15 x D combined edge table is cache-resident, and the CSR
-    tail of the few rows of degree > 4 is not counted.  (E is kept for the
-    signature: the slot layout makes the compulsory bytes independent of it.)"""
-    return 2 * N * D * 4 + 16 * N
+    write the output once (2*N*D*s, s = 4 fp32 / 2 bf16) and the 16-byte
+    neighbour slots of every node (16N); the 15 x D combined edge table is
+    cache-resident, and the CSR tail of the few rows of degree > 4 is not
+    counted.  (E is kept for the signature: the slot layout makes the
+    compulsory bytes independent of it.)"""
+    return 2 * N * D * elem_bytes + 16 * N
 
 
 def edge_tables_combine(E1s, E2s) -> torch.Tensor:
@@ -502,6 +506,9 @@ POOL_MODES = {"mean": 0, "add": 1}
 
 
 class _SegmentPool(torch.autograd.Function):
+    """Pooling over graph_ptr; bf16 node embeddings pool into fp32 (the
+    projection heads stay fp32) and receive a bf16 gradient."""
+
     @staticmethod
     def forward(ctx, h, graph: DeviceGraph, mode: int):
         _check(h)
@@ -509,18 +516,23 @@ class _SegmentPool(torch.autograd.Function):
         N, D = h.shape
         G = graph.num_graphs
         out = torch.empty(G, D, dtype=torch.float32, device=h.device)
-        _lib.call("molclr_segment_pool_fwd", h.data_ptr(), graph.graph_ptr.data_ptr(),
-                  out.data_ptr(), G, D, mode, _stream(h))
-        ctx.graph, ctx.mode, ctx.N = graph, mode, N
+        bf = h.dtype == torch.bfloat16
+        if not bf and h.dtype != torch.float32:
+            raise TypeError(f"segment_pool: {h.dtype} node embeddings (fp32 / bf16)")
+        _lib.call("molclr_segment_pool_fwd_bf16" if bf else "molclr_segment_pool_fwd", h.data_ptr(),
+                  graph.graph_ptr.data_ptr(), out.data_ptr(), G, D, mode, _stream(h))
+        ctx.graph, ctx.mode, ctx.N, ctx.dtype = graph, mode, N, h.dtype
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        dout = _c(dout)
+        dout = _c(dout.to(torch.float32))
         G, D = dout.shape
-        dh = torch.empty(ctx.N, D, dtype=torch.float32, device=dout.device)
-        _lib.call("molclr_segment_pool_bwd", dout.data_ptr(), ctx.graph.graph_ptr.data_ptr(),
-                  dh.data_ptr(), ctx.N, G, D, ctx.mode, _stream(dout))
+        dh = torch.empty(ctx.N, D, dtype=ctx.dtype, device=dout.device)
+        bf = ctx.dtype == torch.bfloat16
+        _lib.call("molclr_segment_pool_bwd_bf16" if bf else "molclr_segment_pool_bwd",
+                  dout.data_ptr(), ctx.graph.graph_ptr.data_ptr(), dh.data_ptr(), ctx.N, G, D,
+                  ctx.mode, _stream(dout))
         return dh, None, None
 
 
@@ -686,7 +698,7 @@ class _GINEncoder(torch.autograd.Function):
     params: x_embedding1, x_embedding2, then per layer GIN_PARAMS_PER_LAYER."""
 
     @staticmethod
-    def forward(ctx, x_idx, graph: DeviceGraph, bns, *params):
+    def forward(ctx, x_idx, graph: DeviceGraph, bns, dtype, *params):
         _check(x_idx, *params)
         L = len(bns)
         D = params[0].shape[1]
@@ -695,6 +707,7 @@ class _GINEncoder(torch.autograd.Function):
         training = bool(bns[0].training)
         enc = _lib.GinEncoder()
         enc.num_layer, enc.training, enc.dim = L, int(training), D
+        enc.dtype = dtype
         enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
         enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
@@ -717,18 +730,19 @@ class _GINEncoder(torch.autograd.Function):
             enc.mlp2_planes[l] = weight_planes(W2, D, twoD, twoD, 0).data_ptr()
             enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1).data_ptr()
         dev = x_idx.device
-        arena_bytes = _wsq("molclr_gin_encoder_arena_bytes", L, N, D)
+        arena_bytes = _wsq("molclr_gin_encoder_arena_bytes", L, N, D, dtype)
         arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)
-        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D)
+        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D, dtype)
         ws = _ws(ws_bytes, dev)
-        h = torch.empty(N, D, dtype=torch.float32, device=dev)
+        h = torch.empty(N, D, dtype=TORCH_DTYPE[dtype], device=dev)
         gc = graph.cstruct()
         _lib.call("molclr_gin_encoder_fwd", ctypes.addressof(enc), x_idx.data_ptr(),
                   ctypes.addressof(gc), h.data_ptr(), arena.data_ptr(), arena_bytes,
                   ws.data_ptr(), ws_bytes, _stream(x_idx))
         if _TIMER is not None:
+            es = 2 if dtype == _lib.DTYPE_BF16 else 4
             for _ in range(L):
-                _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges))
+                _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges, es))
                 _TIMER.add("gemm_f32", 2 * 2.0 * N * D * (2 * D))
         ctx.enc, ctx.graph, ctx.arena, ctx.arena_bytes = enc, graph, arena, arena_bytes
         ctx.x_idx, ctx.params, ctx.training = x_idx, params, training
@@ -738,7 +752,8 @@ class _GINEncoder(torch.autograd.Function):
     def backward(ctx, dh):
         if not ctx.training:
             raise NotImplementedError("molclr_amd: backward through eval-mode BatchNorm")
-        dh = _c(dh)
+        dtype = int(ctx.enc.dtype)
+        dh = _c(dh.to(TORCH_DTYPE[dtype]))
         params = ctx.params
         L = ctx.enc.num_layer
         N, D = dh.shape
@@ -757,7 +772,7 @@ class _GINEncoder(torch.autograd.Function):
         for l in range(L):
             for j, nm in enumerate(names):
                 getattr(gr, nm)[l] = bufs[2 + GIN_PARAMS_PER_LAYER * l + j].data_ptr()
-        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D)
+        ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D, dtype)
         ws = _ws(ws_bytes, dh.device)
         gc = ctx.graph.cstruct()
         _lib.call("molclr_gin_encoder_bwd", ctypes.addressof(ctx.enc), ctypes.addressof(gr),
@@ -767,7 +782,7 @@ class _GINEncoder(torch.autograd.Function):
             for _ in range(L):
                 _TIMER.add("gemm_f32", 4 * 2.0 * N * D * (2 * D))
         ctx.arena = None
-        return (None, None, None, *ret)
+        return (None, None, None, None, *ret)
 
 
 GCN_PARAMS_PER_LAYER = 6  # weight, bias, edge_emb1, edge_emb2, bn.W, bn.b
@@ -863,9 +878,15 @@ def gcn_encoder(x_idx, graph, bns, params):
     return _GCNEncoder.apply(x_idx, graph, bns, *params)
 
 
-def gin_encoder(x_idx, graph, bns, params):
-    """GINet.encode through the encoder executor (see _GINEncoder)."""
-    return _GINEncoder.apply(x_idx, graph, bns, *params)
+DTYPES = {"fp32": _lib.DTYPE_F32, "bf16": _lib.DTYPE_BF16}
+TORCH_DTYPE = {_lib.DTYPE_F32: torch.float32, _lib.DTYPE_BF16: torch.bfloat16}
+
+
+def gin_encoder(x_idx, graph, bns, params, precision: str = "fp32"):
+    """GINet.encode through the encoder executor (see _GINEncoder); precision
+    "bf16" runs the c5 configuration's bf16 storage / bf16 MFMA path and
+    returns bf16 node embeddings."""
+    return _GINEncoder.apply(x_idx, graph, bns, DTYPES[precision], *params)
 
 
 # public functional API -------------------------------------------------------

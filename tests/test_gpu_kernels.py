@@ -218,16 +218,10 @@ GEMM_SHAPES = [
 ]
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6],
-                ids=["f32", "x6_64x64", "x6_128x64", "x6_128x128", "x9_64x64", "p6_64x64", "p6_128x64"])
+@pytest.fixture(params=[-1, 0, 5, 6], ids=["auto", "f32", "p6_64x64", "p6_128x64"])
 def gemm_impl(request, dev):
-    """Run a GEMM test under each implementation of molclr_gemm_f32."""
-    from molclr_amd import _lib
-    lib = _lib.load()
-    prev = lib.molclr_gemm_get_impl()
-    lib.molclr_gemm_set_impl(request.param)
-    yield request.param
-    lib.molclr_gemm_set_impl(prev)
+    """Each implementation of molclr_gemm_f32 (molclr_gemm_f32_impl's argument)."""
+    return request.param
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
@@ -241,7 +235,7 @@ def test_gemm_layouts(dev, gemm_impl, M, N, K, ak, bk):
     Bt = (Bm if bk else Bm.t()).contiguous().float().to(dev)
     lda = M if ak else K
     ldb = N if bk else K
-    out = ops.gemm(A, Bt, M, N, K, lda, ldb, ak, bk)
+    out = ops.gemm(A, Bt, M, N, K, lda, ldb, ak, bk, impl=gemm_impl)
     assert rel(out, ref) < TOL
 
 
@@ -255,64 +249,58 @@ def test_gemm_epilogues(dev, gemm_impl):
     aux = torch.randn(M, N)
     y = x.double() @ W.double().t()
     xd, Wd, bd, auxd = (t.to(dev) for t in (x, W, b, aux))
-    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS, bias=bd), y + b.double()) < TOL
-    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS_RELU, bias=bd),
+    im = dict(impl=gemm_impl)
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS, bias=bd, **im), y + b.double()) < TOL
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_BIAS_RELU, bias=bd, **im),
                (y + b.double()).clamp(min=0)) < TOL
-    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_RELU_MASK, aux=auxd),
+    assert rel(ops.gemm(xd, Wd, M, N, K, K, K, 0, 0, EPI_RELU_MASK, aux=auxd, **im),
                y * (aux > 0).double()) < TOL
 
 
 @pytest.mark.parametrize("ak,bk", [(0, 0), (0, 1), (1, 1), (1, 0)])
 def test_gemm_split_bf16_accuracy(dev, ak, bk):
-    """The split-bf16 GEMM is as accurate as the f32-input MFMA one: its
+    """The split-bf16 GEMMs are as accurate as the f32-input MFMA one: their
     error against float64 stays within 2x of the f32 kernel's, elementwise-
     max and norm-wise, including a long K (the weight-gradient shape)."""
     from molclr_amd import _lib
     lib = _lib.load()
-    prev = lib.molclr_gemm_get_impl()
-    try:
-        for M, N, K, positive in ((1000, 600, 300, False), (300, 600, 15700, False),
-                                  (1000, 600, 300, True), (300, 600, 15700, True)):
-            torch.manual_seed(K)
-            if positive:  # no cancellation: elementwise relative error is meaningful
-                Am = torch.rand(M, K, dtype=torch.float64)
-                Bm = torch.rand(K, N, dtype=torch.float64)
+    for M, N, K, positive in ((1000, 600, 300, False), (300, 600, 15700, False),
+                              (1000, 600, 300, True), (300, 600, 15700, True)):
+        torch.manual_seed(K)
+        if positive:  # no cancellation: elementwise relative error is meaningful
+            Am = torch.rand(M, K, dtype=torch.float64)
+            Bm = torch.rand(K, N, dtype=torch.float64)
+        else:
+            Am = torch.randn(M, K, dtype=torch.float64) * torch.logspace(-3, 3, K).double()
+            Bm = torch.randn(K, N, dtype=torch.float64)
+        A = (Am.t() if ak else Am).contiguous().float()
+        Bt = (Bm if bk else Bm.t()).contiguous().float()
+        # reference on the fp32-rounded inputs: only the GEMM's own error counts
+        ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
+        errs = {}
+        for impl in (0, -1, 5, 6, "bplanes", "q6"):
+            if impl in ("bplanes", "q6"):
+                planes = ops.weight_planes(Bt.to(dev), N, K, N if bk else K, bk)
+                out = torch.empty(M, N, device=dev)
+                ws_bytes = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
+                ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+                Ad = A.to(dev)
+                rc = lib.molclr_gemm_f32_bplanes_tile(
+                    Ad.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
+                    M if ak else K, N, ak, 0, None, None, 0, ws.data_ptr(), ws_bytes,
+                    None, 9 if impl == "q6" else 0)
+                assert rc == 0
+                out = out.double().cpu()
             else:
-                Am = torch.randn(M, K, dtype=torch.float64) * torch.logspace(-3, 3, K).double()
-                Bm = torch.randn(K, N, dtype=torch.float64)
-            A = (Am.t() if ak else Am).contiguous().float()
-            Bt = (Bm if bk else Bm.t()).contiguous().float()
-            # reference on the fp32-rounded inputs: only the GEMM's own error counts
-            ref = (A.double().t() if ak else A.double()) @ (Bt.double() if bk else Bt.double().t())
-            errs = {}
-            for impl in (0, 1, 2, 3, 4, 5, 6, "bplanes", "q6"):
-                if impl in ("bplanes", "q6"):
-                    lib.molclr_gemm_bplanes_set_impl(9 if impl == "q6" else 0)
-                    planes = ops.weight_planes(Bt.to(dev), N, K, N if bk else K, bk)
-                    out = torch.empty(M, N, device=dev)
-                    ws_bytes = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
-                    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-                    Ad = A.to(dev)
-                    rc = lib.molclr_gemm_f32_bplanes(
-                        Ad.data_ptr(), planes.data_ptr(), out.data_ptr(), M, N, K,
-                        M if ak else K, N, ak, 0, None, None, 0, ws.data_ptr(), ws_bytes,
-                        None)
-                    lib.molclr_gemm_bplanes_set_impl(0)
-                    assert rc == 0
-                    out = out.double().cpu()
-                else:
-                    lib.molclr_gemm_set_impl(impl)
-                    out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K,
-                                   N if bk else K, ak, bk).double().cpu()
-                errs[impl] = (rel(out, ref), (out - ref).abs().max().item(),
-                              ((out - ref).abs() / ref.abs().clamp(min=1e-30)).max().item())
-            for impl in (1, 2, 3, 4, 5, 6, "bplanes", "q6"):
-                assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
-                assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
-                if positive:
-                    assert errs[impl][2] <= 2 * errs[0][2], errs
-    finally:
-        lib.molclr_gemm_set_impl(prev)
+                out = ops.gemm(A.to(dev), Bt.to(dev), M, N, K, M if ak else K,
+                               N if bk else K, ak, bk, impl=impl).double().cpu()
+            errs[impl] = (rel(out, ref), (out - ref).abs().max().item(),
+                          ((out - ref).abs() / ref.abs().clamp(min=1e-30)).max().item())
+        for impl in (-1, 5, 6, "bplanes", "q6"):
+            assert errs[impl][0] <= 2 * errs[0][0] + 1e-9, errs
+            assert errs[impl][1] <= 2 * errs[0][1] + 1e-9, errs
+            if positive:
+                assert errs[impl][2] <= 2 * errs[0][2], errs
 
 
 @pytest.mark.parametrize("tile", [0, 5, 6, 7, 8, 9])
@@ -322,41 +310,36 @@ def test_gemm_split_bf16_accuracy(dev, ak, bk):
 def test_gemm_bplanes(dev, tile, M, N, K, ak, bk):
     """molclr_gemm_f32_bplanes (pre-split weight planes) against float64, all
     epilogues, both B storage orders, both A layouts and both tiles."""
-    from molclr_amd import _lib
     from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_RELU_MASK
     if ak and M % 4:
         pytest.skip("K-major A needs M % 4 == 0")
-    lib = _lib.load()
-    lib.molclr_gemm_bplanes_set_impl(tile)
-    try:
-        torch.manual_seed(M * 7 + N + K)
-        Am = torch.randn(M, K, dtype=torch.float64)
-        Bm = torch.randn(K, N, dtype=torch.float64)
-        b = torch.randn(N, dtype=torch.float64)
-        aux = torch.randn(M, N)
-        A = (Am.t() if ak else Am).contiguous().float().to(dev)
-        W = (Bm if bk else Bm.t()).contiguous().float().to(dev)
-        y = (Am.float().double()) @ (Bm.float().double())
-        lda, ldb = (M if ak else K), (N if bk else K)
-        bd, auxd = b.float().to(dev), aux.to(dev)
-        got = ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk)
-        assert rel(got, y) < TOL
-        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS, bias=bd),
-                   y + b.float().double()) < TOL
-        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS_RELU, bias=bd),
-                   (y + b.float().double()).clamp(min=0)) < TOL
-        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_RELU_MASK, aux=auxd),
-                   y * (aux > 0).double()) < TOL
-        acc = torch.randn(M, N)
-        out = acc.to(dev)
-        ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, out=out, accumulate=1)
-        assert rel(out, y + acc.double()) < TOL
-        # the cached planes follow in-place changes of the weight
-        with torch.no_grad():
-            W.mul_(2.0)
-        assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk), 2 * y) < TOL
-    finally:
-        lib.molclr_gemm_bplanes_set_impl(0)
+    torch.manual_seed(M * 7 + N + K)
+    Am = torch.randn(M, K, dtype=torch.float64)
+    Bm = torch.randn(K, N, dtype=torch.float64)
+    b = torch.randn(N, dtype=torch.float64)
+    aux = torch.randn(M, N)
+    A = (Am.t() if ak else Am).contiguous().float().to(dev)
+    W = (Bm if bk else Bm.t()).contiguous().float().to(dev)
+    y = (Am.float().double()) @ (Bm.float().double())
+    lda, ldb = (M if ak else K), (N if bk else K)
+    bd, auxd = b.float().to(dev), aux.to(dev)
+    t = dict(tile=tile)
+    got = ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, **t)
+    assert rel(got, y) < TOL
+    assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS, bias=bd, **t),
+               y + b.float().double()) < TOL
+    assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_BIAS_RELU, bias=bd, **t),
+               (y + b.float().double()).clamp(min=0)) < TOL
+    assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, EPI_RELU_MASK, aux=auxd, **t),
+               y * (aux > 0).double()) < TOL
+    acc = torch.randn(M, N)
+    out = acc.to(dev)
+    ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, out=out, accumulate=1, **t)
+    assert rel(out, y + acc.double()) < TOL
+    # the cached planes follow in-place changes of the weight
+    with torch.no_grad():
+        W.mul_(2.0)
+    assert rel(ops.gemm_w(A, W, M, N, K, lda, ldb, ak, bk, **t), 2 * y) < TOL
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(15278, 300, 600), (15278, 600, 300), (512, 512, 300),
@@ -368,15 +351,10 @@ def test_linear_wgrad(dev, rows, n_out, n_in, acc, groups):
     4-aligned shapes, gemm + colsum otherwise), against float64; both K-group
     settings of the long-K weight-gradient kernel."""
     from molclr_amd import _lib
-    lib = _lib.load()
-    assert lib.molclr_gemm_w6_set_groups(groups) == 0
-    try:
-        _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc)
-    finally:
-        lib.molclr_gemm_w6_set_groups(2)
+    _check_linear_wgrad(_lib.load(), dev, rows, n_out, n_in, acc, groups)
 
 
-def _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc):
+def _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc, groups):
     torch.manual_seed(rows + n_out)
     dy = torch.randn(rows, n_out)
     x = torch.randn(rows, n_in)
@@ -387,8 +365,9 @@ def _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc):
     ws_bytes = lib.molclr_linear_wgrad_workspace_bytes(rows, n_out, n_in)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     dyd, xd = dy.to(dev), x.to(dev)
-    rc = lib.molclr_linear_wgrad(dyd.data_ptr(), xd.data_ptr(), dW.data_ptr(), db.data_ptr(),
-                                 rows, n_out, n_in, n_out, n_in, acc, ws.data_ptr(), ws_bytes, None)
+    rc = lib.molclr_linear_wgrad_groups(dyd.data_ptr(), xd.data_ptr(), dW.data_ptr(), db.data_ptr(),
+                                        rows, n_out, n_in, n_out, n_in, acc, ws.data_ptr(), ws_bytes,
+                                        None, groups)
     if n_out % 4:
         assert rc == -1 and b"multiples of 4" in lib.molclr_last_error()
     else:
@@ -399,8 +378,9 @@ def _check_linear_wgrad(lib, dev, rows, n_out, n_in, acc):
         assert rel(db, refb) < TOL
     # without db: the weight gradient alone
     dW2 = torch.empty(n_out, n_in, device=dev)
-    assert lib.molclr_linear_wgrad(dyd.data_ptr(), xd.data_ptr(), dW2.data_ptr(), None, rows,
-                                   n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_bytes, None) == 0
+    assert lib.molclr_linear_wgrad_groups(dyd.data_ptr(), xd.data_ptr(), dW2.data_ptr(), None, rows,
+                                          n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_bytes, None,
+                                          groups) == 0
     assert rel(dW2, dy.double().t() @ x.double()) < TOL
 
 

@@ -55,46 +55,29 @@ def main():
           f"{torch.backends.cuda.matmul.allow_tf32})")
     from molclr_amd import _lib
     lib = _lib.load()
-    impls = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,1,5,6".split(","))]
+    impls = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else "-1,0,5,6".split(","))]
     for name, A, B, M, N, K, lda, ldb, ak, bk, epi, kw, weight, ref in cases:
         flops = 2 * M * N * K
         res = []
         for impl in impls:
-            lib.molclr_gemm_set_impl(impl)
-            tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+            tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, impl=impl, **kw))
             res.append(f"i{impl} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
         if ak and bk:  # weight gradient: the long-K kernel with one / two K groups
-            lib.molclr_gemm_set_impl(5)
+            ws_bytes = lib.molclr_linear_wgrad_workspace_bytes(K, M, N)
+            ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+            out = torch.empty(M, N, device=dev)
             for kg in (1, 2):
-                lib.molclr_gemm_w6_set_groups(kg)
-                tm = timeit(lambda: ops.gemm(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+                tm = timeit(lambda: lib.molclr_linear_wgrad_groups(
+                    A.data_ptr(), B.data_ptr(), out.data_ptr(), None, K, M, N, lda, ldb, 0,
+                    ws.data_ptr(), ws_bytes, _lib.stream_of(dev), kg))
                 res.append(f"w6/kg{kg} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
-            lib.molclr_gemm_w6_set_groups(2)
         if weight:
             for t in (5, 7, 9):
-                lib.molclr_gemm_bplanes_set_impl(t)
-                tm = timeit(lambda: ops.gemm_w(A, B, M, N, K, lda, ldb, ak, bk, epi, **kw))
+                tm = timeit(lambda: ops.gemm_w(A, B, M, N, K, lda, ldb, ak, bk, epi, tile=t, **kw))
                 res.append(f"bp{t} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
-        lib.molclr_gemm_set_impl(5)
         tr = timeit(ref)
         print(f"{name:24s} " + " | ".join(res) + f" | torch {tr*1e6:5.1f}us {flops/tr/1e12:5.1f}TF",
               flush=True)
-    # correctness of every impl on one shape per layout
-    torch.manual_seed(1)
-    for impl in (1, 2, 3, 4, 5, 6):
-        lib.molclr_gemm_set_impl(impl)
-        for (ak, bk) in ((0, 0), (0, 1), (1, 1), (1, 0)):
-            M, N, K = 333, 300, 1000
-            Am = torch.randn(M, K, dtype=torch.float64)
-            Bm = torch.randn(K, N, dtype=torch.float64)
-            A = (Am.t() if ak else Am).contiguous().float().to(dev)
-            Bt = (Bm if bk else Bm.t()).contiguous().float().to(dev)
-            out = ops.gemm(A, Bt, M, N, K, M if ak else K, N if bk else K, ak, bk)
-            ref = Am @ Bm
-            err = ((out.double().cpu() - ref).norm() / ref.norm()).item()
-            print(f"impl{impl} ak={ak} bk={bk} rel err {err:.2e}", flush=True)
-            assert err < 1e-5
-    lib.molclr_gemm_set_impl(5)
 
 
 if __name__ == "__main__":

@@ -25,6 +25,8 @@ for s in $steps; do
     smoke)   run smoke 300 python __graft_entry__.py smoke; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench)   run bench 600 python bench.py --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench2)  run bench2 600 python bench.py --no-cpu-baseline --two-pass; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    bf16)    run bf16 900 python -m pytest tests/test_gpu_bf16.py -m gpu -q --maxfail=200 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    bench5)  run bench5 600 python bench.py --no-cpu-baseline --config c5; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench3)  run bench3 600 python bench.py --no-cpu-baseline --config c3; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchfull) run benchfull 900 python bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     prof)    export TMPDIR=/tmp; rm -rf gpurun_out/prof
