@@ -624,6 +624,14 @@ int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* graph_ptr, ui
 int molclr_gemm_bf16(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M, int64_t N,
                      int64_t K, int64_t lda, int64_t ldc, int epilogue, const float* bias,
                      const uint16_t* aux, int64_t ldaux, molclr_stream_t stream);
+/* The same with the tile shape chosen per call (tests and benchmarks; -1 =
+ * automatic, as molclr_gemm_bf16): output tiles 0 = 128 x 128, 1 = 128 x 256,
+ * 2 = 128 x 512, 3 = 64 x 512, 4 = 128 x 256 (8 waves), 5 = 128 x 128 (shallow
+ * A prefetch).  Every shape gives the same result bits. */
+int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M,
+                          int64_t N, int64_t K, int64_t lda, int64_t ldc, int epilogue,
+                          const float* bias, const uint16_t* aux, int64_t ldaux,
+                          molclr_stream_t stream, int impl);
 /* Linear weight / bias gradients from bf16 operands into fp32:
  * dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i], db (+)= Σ_r dy[r][o] (db may be
  * NULL); n_out, n_in, ld_dy, ld_x multiples of 8.  Split-K partials summed in
@@ -633,6 +641,13 @@ int molclr_linear_wgrad_bf16(const uint16_t* dy, const uint16_t* x, float* dW, f
                              int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
                              int64_t ld_x, int accumulate, void* workspace,
                              size_t workspace_bytes, molclr_stream_t stream);
+/* The same with the tile shape chosen per call (-1 = automatic): 0 = 128 x 128,
+ * 1 = 256 x 256, 2 = 128 x 256 output tiles; each has its own split-K plan
+ * (the workspace query covers all). */
+int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t* x, float* dW, float* db,
+                                  int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
+                                  int64_t ld_x, int accumulate, void* workspace,
+                                  size_t workspace_bytes, molclr_stream_t stream, int impl);
 
 /* ---- Benchmark instrumentation (no reference counterpart) -------------------
  * Opt-in kernel timer.  While a kind is enabled, its launches go through

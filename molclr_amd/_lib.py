@@ -111,7 +111,11 @@ SIGNATURES = {
     "molclr_segment_pool_bwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_gemm_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P, _I64,
                                  _P]),
+    "molclr_gemm_bf16_impl": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P,
+                                      _I64, _P, c_int]),
     "molclr_linear_wgrad_bf16_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_linear_wgrad_bf16_impl": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
+                                              _P, c_size_t, _P, c_int]),
     "molclr_linear_wgrad_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
                                          c_size_t, _P]),
     "molclr_ktimer_start": (c_int, [c_int]),

@@ -446,6 +446,89 @@ __global__ __launch_bounds__(512) void k_reduce_rowsum_partial(
   if (o) *o = accumulate ? *o + (float)acc : (float)acc;
 }
 
+// bf16 storage with 16-byte units: a thread owns 8 consecutive columns (one
+// uint4 of a bf16 row), so a wave moves the same 1 KiB per load instruction as
+// the fp32 kernels' float4 units.  Per element the adds are the fp32 kernels'
+// (same order), rounded once to bf16 at the store.
+struct F8 {
+  float4 a, b;
+};
+__device__ __forceinline__ F8 ld8(const uint16_t* __restrict__ p, int64_t unit) {
+  const uint4 u = reinterpret_cast<const uint4*>(p)[unit];
+  return {make_float4(bf16_to_f32(u.x & 0xFFFFu), bf16_to_f32(u.x >> 16), bf16_to_f32(u.y & 0xFFFFu),
+                      bf16_to_f32(u.y >> 16)),
+          make_float4(bf16_to_f32(u.z & 0xFFFFu), bf16_to_f32(u.z >> 16), bf16_to_f32(u.w & 0xFFFFu),
+                      bf16_to_f32(u.w >> 16))};
+}
+__device__ __forceinline__ void st8(uint16_t* __restrict__ p, int64_t unit, F8 v) {
+  reinterpret_cast<uint4*>(p)[unit] =
+      make_uint4(f32x2_to_bf16x2(v.a.x, v.a.y), f32x2_to_bf16x2(v.a.z, v.a.w),
+                 f32x2_to_bf16x2(v.b.x, v.b.y), f32x2_to_bf16x2(v.b.z, v.b.w));
+}
+__device__ __forceinline__ F8 f8add(F8 x, F8 y) { return {f4add(x.a, y.a), f4add(x.b, y.b)}; }
+__device__ __forceinline__ F8 ec8(const float4* __restrict__ Ec, int comb, int d8, int c) {
+  const float4* e = Ec + (int64_t)comb * 2 * d8 + 2 * c;
+  return {e[0], e[1]};
+}
+
+__global__ __launch_bounds__(kT) void k_gine_agg_fwd_b8(
+    const uint16_t* __restrict__ x, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+    const uint4* __restrict__ nbr, const float4* __restrict__ Ec, uint16_t* __restrict__ out,
+    int64_t N, int d8) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d8) return;
+  const int64_t i = t / d8;
+  const int c = (int)(t - i * d8);
+  auto msg = [&](uint32_t w) {
+    return f8add(ld8(x, (int64_t)nbr_node(w) * d8 + c), ec8(Ec, nbr_ecomb(w), d8, c));
+  };
+  const uint4 s = nbr[i];
+  const F8 self = ld8(x, t);
+  const F8 es = ec8(Ec, MOLCLR_SELF_LOOP_ECOMB, d8, c);
+  const uint32_t deg = nbr_degree(s.x);
+  F8 acc = {f4zero(), f4zero()};
+  if (deg <= MOLCLR_NBR_SLOTS) {
+    const F8 m0 = deg > 0 ? msg(s.x) : acc;
+    const F8 m1 = deg > 1 ? msg(s.y) : acc;
+    const F8 m2 = deg > 2 ? msg(s.z) : acc;
+    const F8 m3 = deg > 3 ? msg(s.w) : acc;
+    if (deg > 0) acc = f8add(acc, m0);
+    if (deg > 1) acc = f8add(acc, m1);
+    if (deg > 2) acc = f8add(acc, m2);
+    if (deg > 3) acc = f8add(acc, m3);
+  } else {
+    for (int32_t k = rowptr[i], e = rowptr[i + 1]; k < e; ++k)
+      acc = f8add(acc, f8add(ld8(x, (int64_t)col[k] * d8 + c), ec8(Ec, MOLCLR_ECOMB(ecode[k]), d8, c)));
+  }
+  st8(out, t, f8add(acc, f8add(self, es)));
+}
+
+__global__ __launch_bounds__(kT) void k_transpose_gather_b8(const uint16_t* __restrict__ g,
+                                                            const int32_t* __restrict__ rowptr_t,
+                                                            const int32_t* __restrict__ col_t,
+                                                            const uint4* __restrict__ nbr_t,
+                                                            uint16_t* __restrict__ dx, int64_t N,
+                                                            int d8) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if (t >= N * d8) return;
+  const int64_t j = t / d8;
+  const int c = (int)(t - j * d8);
+  const uint4 s = nbr_t[j];
+  const uint32_t deg = nbr_degree(s.x);
+  F8 acc = {f4zero(), f4zero()};
+  if (deg <= MOLCLR_NBR_SLOTS) {
+    if (deg > 0) acc = f8add(acc, ld8(g, (int64_t)nbr_node(s.x) * d8 + c));
+    if (deg > 1) acc = f8add(acc, ld8(g, (int64_t)nbr_node(s.y) * d8 + c));
+    if (deg > 2) acc = f8add(acc, ld8(g, (int64_t)nbr_node(s.z) * d8 + c));
+    if (deg > 3) acc = f8add(acc, ld8(g, (int64_t)nbr_node(s.w) * d8 + c));
+  } else {
+    for (int32_t k = rowptr_t[j], e = rowptr_t[j + 1]; k < e; ++k)
+      acc = f8add(acc, ld8(g, (int64_t)col_t[k] * d8 + c));
+  }
+  st8(dx, t, f8add(acc, ld8(g, t)));
+}
+
 int64_t atom_parts(int64_t N) {
   int64_t P = molclr::ceil_div(N, 128);
   if (P > 128) P = 128;
@@ -702,12 +785,19 @@ MOLCLR_API int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* 
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_fwd_bf16: dim must be a multiple of 4");
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd_bf16: null pointer");
-  const int d4 = (int)(D / 4);
-  const float* nf = nullptr;
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StBF16>,
-                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, nf,
-                       nf, nf, nf, 0);
+  if (D % 8 == 0) {
+    const int d8 = (int)(D / 8);
+    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd_b8, dim3(molclr::ceil_div(N * d8, kT)),
+                         dim3(kT), 0, molclr::as_stream(stream), x, rowptr, col, ecode,
+                         (const uint4*)nbr, (const float4*)Ec, out, N, d8);
+  } else {
+    const int d4 = (int)(D / 4);
+    const float* nf = nullptr;
+    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StBF16>,
+                         dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
+                         x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
+                         nf, nf, nf, nf, 0);
+  }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -723,8 +813,12 @@ MOLCLR_API int molclr_gine_aggregate_bwd_bf16(const uint16_t* g, const int32_t* 
   const int d4 = (int)(D / 4);
   if (dx && N > 0) {
     MOLCLR_REQUIRE(g && rowptr_t && nbr_t, "gine_aggregate_bwd_bf16: null pointer");
-    hipLaunchKernelGGL(k_transpose_gather<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                       s, g, rowptr_t, col_t, (const uint4*)nbr_t, dx, N, d4);
+    if (D % 8 == 0)
+      hipLaunchKernelGGL(k_transpose_gather_b8, dim3(molclr::ceil_div(N * (D / 8), kT)), dim3(kT), 0,
+                         s, g, rowptr_t, col_t, (const uint4*)nbr_t, dx, N, (int)(D / 8));
+    else
+      hipLaunchKernelGGL(k_transpose_gather<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT),
+                         0, s, g, rowptr_t, col_t, (const uint4*)nbr_t, dx, N, d4);
   }
   if (dE1 || dE2) {
     MOLCLR_REQUIRE_WS(workspace_bytes, molclr_gine_aggregate_bwd_workspace_bytes(N, D));

@@ -298,7 +298,7 @@ struct PStageK {
     const bool full = k0 + BK <= K;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (UNITS % T && t + j * T >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && t + j * T >= UNITS) continue;
       const float* q = p[j] + k0;
       if (full) {
         r[j][0] = *reinterpret_cast<const float4*>(q);
@@ -315,7 +315,7 @@ struct PStageK {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
-      if (UNITS % T && u >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
       u32x4 hi, mid, lo;
       split8(r[j][0], r[j][1], hi, mid, lo);
       const int o = xoff(u >> 2, u & 3);
@@ -362,7 +362,7 @@ struct PStageM {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
-      if (UNITS % T && u >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
       const float* q = p[j] + base;
       if (full) {
         r[j] = *reinterpret_cast<const float4*>(q);
@@ -376,7 +376,7 @@ struct PStageM {
   __device__ __forceinline__ void colsum_add(float4* cs, int t) const {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (UNITS % T && t + j * T >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && t + j * T >= UNITS) continue;
       cs[j] = f4add(cs[j], r[j]);
     }
   }
@@ -384,7 +384,7 @@ struct PStageM {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
-      if (UNITS % T && u >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
       const int rb = u % (ROWS / 4), k = u / (ROWS / 4);
       uint2 hi, mid, lo;
       split4(r[j], hi, mid, lo);
@@ -417,14 +417,14 @@ struct PStageP {
   __device__ __forceinline__ void load(int64_t k0, int64_t, int t) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (UNITS % T && t + j * T >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && t + j * T >= UNITS) continue;
       r[j] = *reinterpret_cast<const u32x4*>(p[j] + k0);
     }
   }
   __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (UNITS % T && t + j * T >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && t + j * T >= UNITS) continue;
       *reinterpret_cast<u32x4*>(img + off[j]) = r[j];
     }
   }
@@ -749,7 +749,7 @@ struct QStageB {
   __device__ __forceinline__ void load(const uint16_t* __restrict__ Bp, int64_t k0, int t) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      if (UNITS % T && t + j * T >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && t + j * T >= UNITS) continue;
       r[j] = *reinterpret_cast<const u32x4*>(Bp + goff[j] + k0);
     }
   }
@@ -757,7 +757,7 @@ struct QStageB {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
-      if (UNITS % T && u >= UNITS) continue;
+      if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
       const int pl = u / (BN * 4), rem = u % (BN * 4);
       *reinterpret_cast<u32x4*>(img + pl * BN * XK + xoff(rem >> 2, rem & 3)) = r[j];
     }
@@ -769,7 +769,13 @@ struct QStageB {
 // the other groups' sums (in group order, through LDS) before the epilogue.
 // For the narrow products (N = 300: ~960 waves of 32 x 160 for 1024 SIMDs)
 // this puts two waves on every SIMD instead of one.
-template <int TN, int EPI, int KG>
+// MASK: some K steps of this launch are partial or (KG > 1) beyond the last
+// one; their A values at k >= K are zeroed where they are consumed.  The
+// main loop has no branch: every load is issued from a clamped, in-bounds
+// address, so the compiler keeps counted vmcnt waits and the next steps'
+// loads stay in flight across the MFMAs (a conditional load makes it drain
+// every outstanding load at the top of each step).
+template <int TN, int EPI, int KG, bool MASK>
 __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
@@ -786,7 +792,8 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   __shared__ __attribute__((aligned(16))) uint16_t lds[KG * 2 * BI];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar
   const int grp = wave / kQ6Waves, wm = wave % kQ6Waves, gt = tid - grp * T;
   const int li = lane & 31, lh = lane >> 5;
 
@@ -798,17 +805,24 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 
   int64_t arow_i = m0 + 32 * wm + li;
   arow_i = arow_i < M ? arow_i : M - 1;
-  const float* __restrict__ arow = A + arow_i * lda + 16 * lh;
-  // this lane's 16 k of K step k0 (K % 4 == 0: a float4 is all in or all out)
-  auto load_a = [&](int64_t k0, float4(&r)[4]) {
-    const float* q = arow + k0;
-    if (k0 + BK <= K) {
+  const float* __restrict__ arow = A + arow_i * lda;
+  const int nsteps = (int)(kp / BK);             // K steps of the planes (K rounded up)
+  const int rounds = (nsteps + KG - 1) / KG;     // every group runs as many
+  // this group's round r is K step grp + KG r; B is read from a clamped step
+  // (a step past the last is zeroed through A), A from clamped addresses
+  auto kb = [&](int r) {
+    const int st = grp + KG * r;
+    return (int64_t)(st < nsteps ? st : nsteps - 1) * BK;
+  };
+  // this lane's 16 k of round r: float4 j holds k0 + 16 lh + 4 j .. +3 (K % 4 == 0)
+  auto load_a = [&](int r, float4(&v)[4]) {
+    r = r < rounds ? r : rounds - 1;  // prefetch past the end: never consumed
+    const int64_t k = (int64_t)(grp + KG * r) * BK + 16 * lh;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = *reinterpret_cast<const float4*>(q + 4 * j);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        r[j] = k0 + 16 * lh + 4 * j < K ? *reinterpret_cast<const float4*>(q + 4 * j) : f4zero();
+    for (int j = 0; j < 4; ++j) {
+      int64_t kj = k + 4 * j;
+      if constexpr (MASK) kj = kj < K - 4 ? kj : K - 4;
+      v[j] = *reinterpret_cast<const float4*>(arow + kj);
     }
   };
 
@@ -818,11 +832,20 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
-  auto compute = [&](const uint16_t* Bs, const float4(&a)[4]) {
+  auto compute = [&](const uint16_t* Bs, const float4(&a)[4], int r) {
+    float4 am4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      am4[j] = a[j];
+      if constexpr (MASK) {
+        const int64_t kj = (int64_t)(grp + KG * r) * BK + 16 * lh + 4 * j;
+        if (kj >= K) am4[j] = f4zero();
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       u32x4 h, m, l;
-      split8(a[2 * s], a[2 * s + 1], h, m, l);
+      split8(am4[2 * s], am4[2 * s + 1], h, m, l);
       const bf16x8 ah = __builtin_bit_cast(bf16x8, h);
       const bf16x8 am = __builtin_bit_cast(bf16x8, m);
       const bf16x8 al = __builtin_bit_cast(bf16x8, l);
@@ -847,44 +870,32 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   sb.init(n0, npad, kp, gt);
   uint16_t* buf0 = lds + grp * 2 * BI;
   uint16_t* buf1 = buf0 + BI;
-  const int nsteps = (int)((K + BK - 1) / BK);
-  const int rounds = (nsteps + KG - 1) / KG;   // group 0's step count; every group runs them
-  const int ns = (nsteps - grp + KG - 1) / KG;  // this group's steps: grp, grp + KG, ...
-  auto kof = [&](int r) { return (int64_t)(grp + KG * r) * BK; };
   float4 a0[4], a1[4];
-  if (ns > 0) {
-    sb.load(Bp, kof(0), gt);
-    load_a(kof(0), a0);
-    sb.store(buf0, gt);
-  }
-  if (ns > 1) {
-    sb.load(Bp, kof(1), gt);
-    load_a(kof(1), a1);
-  }
+  sb.load(Bp, kb(0), gt);
+  load_a(0, a0);
+  sb.store(buf0, gt);
+  sb.load(Bp, kb(1), gt);
+  load_a(1, a1);
   __syncthreads();
   // At the top of an iteration (i even): buf0 holds B(i) (visible), sb holds
   // B(i+1) in flight, a0 = A(i), a1 = A(i+1) in flight.  B(i+1) is written
   // right after the barrier into the buffer the previous step read; one
-  // barrier per K step (per round of the groups).
+  // barrier per K step.  Loads past the last round re-read a clamped step.
   int i = 0;
   for (; i + 2 <= rounds; i += 2) {
-    if (i + 1 < ns) sb.store(buf1, gt);
-    if (i + 2 < ns) sb.load(Bp, kof(i + 2), gt);
-    if (i < ns) compute(buf0, a0);
-    if (i + 2 < ns) load_a(kof(i + 2), a0);
+    sb.store(buf1, gt);
+    sb.load(Bp, kb(i + 2), gt);
+    compute(buf0, a0, i);
+    load_a(i + 2, a0);
     __syncthreads();
-    if (i + 2 < ns) {
-      sb.store(buf0, gt);
-      if (i + 3 < ns) sb.load(Bp, kof(i + 3), gt);
-    }
-    if (i + 1 < ns) compute(buf1, a1);
-    if (i + 3 < ns) load_a(kof(i + 3), a1);
+    sb.store(buf0, gt);
+    sb.load(Bp, kb(i + 3), gt);
+    compute(buf1, a1, i + 1);
+    load_a(i + 3, a1);
     __syncthreads();
   }
-  if (i < rounds) {
-    if (i < ns) compute(buf0, a0);
-    __syncthreads();  // the images are reused below
-  }
+  if (i < rounds) compute(buf0, a0, i);  // odd count: B(i) is in buf0
+  __syncthreads();                       // the images are reused below
 
   if constexpr (KG > 1) {
     // the other groups' sums, added to group 0's in group order
@@ -1421,17 +1432,27 @@ int q6_groups(int64_t M, int64_t N, int64_t K) {
   return (q6_blocks(M, N) < 384 && (K + BK - 1) / BK >= 8) ? 2 : 1;
 }
 
+template <int TN, int EPI, int KG, bool MASK>
+void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK>),
+                       dim3((unsigned)q6_blocks(a.M, a.N)), dim3(KG * 64 * kQ6Waves), 0, s, a.A,
+                       a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux,
+                       a.accumulate);
+}
 template <int TN, int EPI>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
-  const dim3 grid((unsigned)q6_blocks(a.M, a.N));
-  if (q6_groups(a.M, a.N, a.K) == 2)
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, 2>), grid, dim3(2 * 64 * kQ6Waves), 0,
-                         s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.accumulate);
-  else
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, 1>), grid, dim3(64 * kQ6Waves), 0, s,
-                         a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux,
-                         a.ldaux, a.accumulate);
+  const int64_t nsteps = (a.K + BK - 1) / BK;
+  const int kg = q6_groups(a.M, a.N, a.K);
+  // steps that need their A tail zeroed: a partial last step, or rounds past
+  // the end for some K groups
+  const bool mask = a.K % BK != 0 || nsteps % kg != 0;
+  if (kg == 2) {
+    if (mask) launch_q6_t<TN, EPI, 2, true>(a, npad, s);
+    else launch_q6_t<TN, EPI, 2, false>(a, npad, s);
+  } else {
+    if (mask) launch_q6_t<TN, EPI, 1, true>(a, npad, s);
+    else launch_q6_t<TN, EPI, 1, false>(a, npad, s);
+  }
 }
 
 template <int TN>

@@ -48,7 +48,7 @@ def bf(t):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (1000, 512, 1024), (333, 256, 64),
-                                   (4096, 1024, 512), (37, 96, 40)])
+                                   (4096, 1024, 512), (37, 96, 40), (500, 512, 1000)])
 def test_gemm_bf16(dev, M, N, K):
     from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
     lib = _lib.load()
@@ -74,10 +74,23 @@ def test_gemm_bf16(dev, M, N, K):
     assert lib.molclr_gemm_bf16(Ad.data_ptr(), planes_t.data_ptr(), C.data_ptr(), M, N, K, K, N,
                                 EPI_NONE, None, None, 0, None) == 0
     assert rel(C, A.double() @ bf(Wt).double()) < EPS_BF16
+    # every tile shape: the same result bits (one wave's MFMA chain per output
+    # element, in the same k order)
+    for epi in (EPI_BIAS_RELU, EPI_RELU_MASK):
+        outs = []
+        for impl in (-1, 0, 1, 2, 3, 4, 5):
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            assert lib.molclr_gemm_bf16_impl(Ad.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N,
+                                             K, K, N, epi, bd.data_ptr(), auxd.data_ptr(), N, None,
+                                             impl) == 0
+            outs.append(C)
+        assert rel(outs[0], cases[epi]) < EPS_BF16
+        for impl, C in enumerate(outs[1:]):
+            assert torch.equal(C, outs[0]), (epi, impl)
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(55000, 1024, 512), (55000, 512, 1024), (777, 64, 128),
-                                             (8, 8, 16)])
+                                             (8, 8, 16), (4096, 512, 256)])
 @pytest.mark.parametrize("acc", [0, 1])
 def test_linear_wgrad_bf16(dev, rows, n_out, n_in, acc):
     lib = _lib.load()
@@ -99,6 +112,12 @@ def test_linear_wgrad_bf16(dev, rows, n_out, n_in, acc):
                                         n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_bytes,
                                         None) == 0
     assert rel(dW2, dy.double().t() @ x.double()) < TOL
+    for impl in (0, 1, 2):  # every tile shape and its split-K plan
+        dW3, db3 = W0.clone().to(dev), b0.clone().to(dev)
+        assert lib.molclr_linear_wgrad_bf16_impl(dyd.data_ptr(), xd.data_ptr(), dW3.data_ptr(),
+                                                 db3.data_ptr(), rows, n_out, n_in, n_out, n_in,
+                                                 acc, ws.data_ptr(), ws_bytes, None, impl) == 0
+        assert rel(dW3, refW) < TOL and rel(db3, refb) < TOL, impl
 
 
 def test_bf16_aggregation_atom_pool_bit_exact(dev):

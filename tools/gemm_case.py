@@ -1,0 +1,72 @@
+"""Run one GEMM shape of the c2 / c5 step repeatedly (for rocprofv3 PMC passes).
+
+    python tools/gemm_case.py CASE [reps] [impl]
+
+CASE: qb_lin1 qb_lin2 qb_dz1 qb_dagg wb_dW2 wb_dW0 (bf16, c5 shapes, 55k rows)
+      q6_lin1 q6_lin2 q6_dz1 q6_dagg w6_dW2 w6_dW1 (fp32 split-bf16, c2, 30.5k rows)
+"""
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from molclr_amd import _lib, ops  # noqa: E402
+from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK  # noqa: E402
+
+
+def main():
+    case = sys.argv[1]
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    variant = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    st = _lib.stream_of(dev)
+    torch.manual_seed(0)
+    bf16 = case[:2] in ("qb", "wb")
+    M = 55342 if bf16 else 30556
+    D = 512 if bf16 else 300
+    H = 2 * D
+    dt = torch.bfloat16 if bf16 else torch.float32
+    X = {n: torch.randn(M, c, device=dev).to(dt) for n, c in (("agg", D), ("a1", H), ("dz", D),
+                                                             ("dz1", H))}
+    W0 = torch.randn(H, D, device=dev) * 0.05
+    W2 = torch.randn(D, H, device=dev) * 0.05
+    b0, b2 = torch.randn(H, device=dev), torch.randn(D, device=dev)
+    if bf16:
+        p = {"lin1": (ops.weight_planes(W0, H, D, D, 0), "agg", H, D, EPI_BIAS_RELU, b0, None),
+             "lin2": (ops.weight_planes(W2, D, H, H, 0), "a1", D, H, EPI_BIAS, b2, None),
+             "dz1": (ops.weight_planes(W2, H, D, H, 1), "dz", H, D, EPI_RELU_MASK, None, "a1"),
+             "dagg": (ops.weight_planes(W0, D, H, D, 1), "dz1", D, H, EPI_NONE, None, None)}
+        if case.startswith("qb"):
+            P, a, N, K, epi, bias, aux = p[case[3:]]
+            C = torch.empty(M, N, dtype=dt, device=dev)
+            auxt = X[aux] if aux else None
+            fn = lambda: lib.molclr_gemm_bf16_impl(X[a].data_ptr(), P.data_ptr(), C.data_ptr(), M, N,  # noqa: E731
+                                                   K, K, N, epi, _lib.ptr(bias), _lib.ptr(auxt),
+                                                   N if aux else 0, st, variant)
+        else:
+            dy, x, n_out, n_in = (X["dz"], X["a1"], D, H) if case == "wb_dW2" else (X["dz1"], X["agg"], H, D)
+            wsb = lib.molclr_linear_wgrad_bf16_workspace_bytes(M, n_out, n_in)
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+            dW, db = torch.empty(n_out, n_in, device=dev), torch.empty(n_out, device=dev)
+            fn = lambda: lib.molclr_linear_wgrad_bf16_impl(dy.data_ptr(), x.data_ptr(), dW.data_ptr(),  # noqa: E731
+                                                           db.data_ptr(), M, n_out, n_in, n_out, n_in,
+                                                           0, ws.data_ptr(), wsb, st, variant)
+    else:
+        cases = {"q6_lin1": lambda: ops.linear_fwd(X["agg"], W0, b0, relu=True),
+                 "q6_lin2": lambda: ops.linear_fwd(X["a1"], W2, b2),
+                 "q6_dz1": lambda: ops.gemm_w(X["dz"], W2, M, H, D, D, H, False, True,
+                                              EPI_RELU_MASK, aux=X["a1"]),
+                 "q6_dagg": lambda: ops.gemm_w(X["dz1"], W0, M, D, H, H, D, False, True),
+                 "w6_dW2": lambda: ops.linear_bwd(X["dz"], X["a1"], W2, need_x=False),
+                 "w6_dW1": lambda: ops.linear_bwd(X["dz1"], X["agg"], W0, need_x=False)}
+        fn = cases[case]
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    print("done", case, reps)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,11 @@ for s in $steps; do
     pmc)     export TMPDIR=/tmp; rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
              run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
-    gemm)    run gemm 300 python tools/gemm_bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    gemm)    run gemm 300 python tools/gemm_bench.py 30556; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    gemmbf)  run gemmbf 300 python tools/gemm_bf16_bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    gpmc)    for c in ${PMC_CASES:-qb_lin2:1}; do
+               CASE=${c%%:*} VARIANT=${c##*:} run "gpmc_${c%%:*}_${c##*:}" 400 bash tools/gemm_pmc.sh; rc=$?; [ $rc -eq 0 ] || exit $rc
+             done ;;
     smoke)   run smoke 300 python __graft_entry__.py smoke; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench)   run bench 600 python bench.py --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench2)  run bench2 600 python bench.py --no-cpu-baseline --two-pass; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
@@ -29,6 +33,8 @@ for s in $steps; do
     bench5)  run bench5 600 python bench.py --no-cpu-baseline --config c5; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench3)  run bench3 600 python bench.py --no-cpu-baseline --config c3; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchfull) run benchfull 900 python bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    prof5)   export TMPDIR=/tmp; rm -rf gpurun_out/prof5
+             run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     prof)    export TMPDIR=/tmp; rm -rf gpurun_out/prof
              run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
   esac
