@@ -627,7 +627,10 @@ int molclr_gemm_bf16(const uint16_t* A, const uint16_t* planes, uint16_t* C, int
 /* The same with the tile shape chosen per call (tests and benchmarks; -1 =
  * automatic, as molclr_gemm_bf16): output tiles 0 = 128 x 128, 1 = 128 x 256,
  * 2 = 128 x 512, 3 = 64 x 512, 4 = 128 x 256 (8 waves), 5 = 128 x 128 (shallow
- * A prefetch).  Every shape gives the same result bits. */
+ * A prefetch), 6 = 256 x 256 with LDS-DMA staging (K % 64 == 0), 7 = 256 x 256
+ * with a four-stage LDS-DMA ring (K % 32 == 0); 6 and 7 fall back to 2 for
+ * other K.  Every shape gives the same result bits (those of hipBLASLt's bf16
+ * GEMM on the epilogue-free products). */
 int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M,
                           int64_t N, int64_t K, int64_t lda, int64_t ldc, int epilogue,
                           const float* bias, const uint16_t* aux, int64_t ldaux,

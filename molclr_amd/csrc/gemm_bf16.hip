@@ -77,9 +77,10 @@ __device__ __forceinline__ uint2 f4_to_bf16x4(float4 v) {
 // k_gemm_qb: WM x WN waves; wave (wm, wn) owns rows m0 + 32 wm .. +31 and
 // columns n0 + 32 TN wn .. + 32 TN - 1, the block a BM = 32 WM by BN =
 // 32 TN WN tile.  A goes global -> registers -> MFMA operand: per K step of
-// 32 a lane loads the 16 consecutive k (32 bytes) of its row it needs (lane
-// half h: k0 + 16h .. +15; MFMA step s uses k0 + 16h + 8s .. +7, and the B
-// fragment is image chunk 2h + s, the same k).  With BN = N every A row is
+// 32 a lane loads the two 16-byte pieces of its row it needs (lane half h:
+// MFMA step s uses k0 + 16s + 8h .. +7, and the B fragment is image chunk
+// 2s + h, the same k -- the k pairing of hipBLASLt's bf16 GEMM, whose results
+// this kernel reproduces bit for bit on the epilogue-free products).  With BN = N every A row is
 // fetched by one block only; the WN waves of a row slab read it at the same
 // time, from L2.  B (the weight plane) is staged per K step into a [BN][32]
 // image, double-buffered, one barrier per step.
@@ -121,10 +122,10 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_qb(
   auto kstep = [&](int i) { return i < ns ? i : ns - 1; };
   // this lane's 16 k of step i (K % 8 == 0: an 8-element chunk is all in or out)
   auto load_a = [&](int i, u32x4(&r)[2]) {
-    const int64_t k = (int64_t)kstep(i) * BK + 16 * lh;
+    const int64_t k = (int64_t)kstep(i) * BK + 8 * lh;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      int64_t kc = k + 8 * c;
+      int64_t kc = k + 16 * c;
       if constexpr (MASK) kc = kc < K - 8 ? kc : K - 8;
       r[c] = *reinterpret_cast<const u32x4*>(arow + kc);
     }
@@ -144,14 +145,14 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_qb(
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int b = 0; b < TN; ++b) f[s][b] = xfrag(Bs, wn * WC + 32 * b + li, 2 * lh + s);
+      for (int b = 0; b < TN; ++b) f[s][b] = xfrag(Bs, wn * WC + 32 * b + li, 2 * s + lh);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       u32x4 as = a[s];
       if constexpr (MASK) {
         const u32x4 z = {0u, 0u, 0u, 0u};
-        if ((int64_t)i * BK + 16 * lh + 8 * s >= K) as = z;
+        if ((int64_t)i * BK + 16 * s + 8 * lh >= K) as = z;
       }
       const bf16x8 av = __builtin_bit_cast(bf16x8, as);
 #pragma unroll
@@ -238,6 +239,329 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_qb(
       }
     }
     wave_lds_sync();  // the wave's tile is rewritten by the next block
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm_tb: the same product on 256 x 256 output tiles, both operands staged
+// in LDS by global_load_lds (the LDS-DMA path: no VGPR round trip, no
+// ds_write), 64-deep K steps, two stages.  8 waves as 4 (M) x 2 (N), each a
+// 64 x 128 sub-tile (2 x 4 MFMA blocks: 6 fragment reads per 8 MFMAs).  Per
+// stage and operand the image is [256 rows][128 B]; one wave-instruction of
+// the DMA writes 1 KB (8 rows) linearly, so the bank swizzle -- chunk c of
+// row r stored at chunk c ^ ((r >> 1) & 7) -- is applied on the SOURCE
+// address (lane L of a piece fetches the logical chunk its slot holds) and
+// again on the fragment read; every 16-lane group of a ds_read_b128 then
+// hits 16 distinct 16-byte slots.  Requires K % 64 == 0 (the host falls back
+// to k_gemm_qb otherwise).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* lds_as_ptr;
+typedef const __attribute__((address_space(1))) void* gbl_as_ptr;
+
+__device__ __forceinline__ int t128(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
+
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_tb(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bp, uint16_t* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const uint16_t* __restrict__ aux, int64_t ldaux) {
+  constexpr int BM = 256, BN = 256, KT = 64;
+  constexpr int SI = BM * KT * 2;  // bytes per operand image per stage (32 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * SI];  // [stage][A, B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);  // a row slab's column tiles share an XCD
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
+  // DMA sources: wave w fills pieces 4w .. 4w+3 (8 rows each) of both images
+  const uint16_t* asrc[4];
+  const uint16_t* bsrc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 8 * (4 * wave + q) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t gm = m0 + r < M ? m0 + r : M - 1;
+    const int64_t gn = n0 + r < npad ? n0 + r : npad - 1;
+    asrc[q] = A + gm * lda + 8 * c;
+    bsrc[q] = Bp + gn * kp + 8 * c;
+  }
+  const int nt = (int)(K / KT);
+  auto stage = [&](int buf, int t) {
+    const int64_t k0 = (int64_t)(t < nt ? t : nt - 1) * KT;
+    uint8_t* ia = lds + buf * 2 * SI + wave * 4096;
+    uint8_t* ib = ia + SI;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(asrc[q] + k0), (lds_as_ptr)(ia + 1024 * q), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(bsrc[q] + k0), (lds_as_ptr)(ib + 1024 * q), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int ra = 64 * wm + li, rb = 128 * wn + li;  // this lane's fragment rows
+  // 16-deep substeps; substep q+1's six fragments are read before substep q's
+  // eight MFMAs issue, so the LDS latency hides behind them
+  auto compute = [&](int buf) {
+    const uint8_t* ia = lds + buf * 2 * SI;
+    const uint8_t* ib = ia + SI;
+    bf16x8 fa[2][2], fb[2][4];
+    auto read = [&](int q, bf16x8(&a)[2], bf16x8(&b)[4]) {
+      const int c = 2 * q + lh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        a[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ia + t128(ra + 32 * i, c)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ib + t128(rb + 32 * j, c)));
+    };
+    read(0, fa[0], fb[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 3) read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
+                                                               0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  stage(0, 0);
+  __syncthreads();  // (waits for the DMA: vmcnt(0))
+  for (int t = 0; t < nt; ++t) {
+    stage((t + 1) & 1, t + 1);  // past the last step: re-reads it into the idle buffer
+    compute(t & 1);
+    __syncthreads();
+  }
+
+  // epilogue: per 32 x 32 block through the wave's 4 KB of LDS, rows leave as
+  // 8-byte (4 x bf16) pieces
+  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t mb = m0 + 64 * wm + 32 * i, nb = n0 + 128 * wn + 32 * j;
+      if (nb >= N) continue;  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tw[acc_row(r, lh) * 32 + li] = acc[i][j][r];
+      wave_lds_sync();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx >> 3, c4 = idx & 7;
+        const int64_t m = mb + row, n = nb + 4 * c4;
+        if (m >= M || n >= N) continue;
+        float4 v = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+        if (n + 4 <= N) {
+          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+            v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            const float4 x = bf16x4_to_f4(*reinterpret_cast<const uint2*>(aux + m * ldaux + n));
+            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                            x.w > 0.f ? v.w : 0.f);
+          }
+          *reinterpret_cast<uint2*>(C + m * ldc + n) = f4_to_bf16x4(v);
+        } else {
+          const float e[4] = {v.x, v.y, v.z, v.w};
+          for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+            float x = e[jj];
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + jj];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + jj], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK) x = bf16_to_f32(aux[m * ldaux + n + jj]) > 0.f ? x : 0.f;
+            C[m * ldc + n + jj] = (uint16_t)(f32x2_to_bf16x2(x, 0.f) & 0xFFFFu);
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm_tc: k_gemm_tb's tile and wave layout with 32-deep K steps in a ring
+// of four LDS stages (32 KB each: [256 rows][64 B] per operand, the xoff
+// swizzle applied on the DMA source address and on the read).  Three steps
+// are in flight while one is consumed; a step is waited for with a counted
+// vmcnt (the two younger steps' DMAs stay outstanding) and a raw s_barrier,
+// never a full drain, so the loads span the barriers.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ __launch_bounds__(512) void k_gemm_tc(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bp, uint16_t* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const uint16_t* __restrict__ aux, int64_t ldaux) {
+  constexpr int BM = 256, BN = 256, NS = 4;
+  constexpr int SI = BM * BK * 2;  // bytes per operand image per stage (16 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NS * 2 * SI];  // [stage][A, B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + BM - 1) / BM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int64_t m0 = (int64_t)(tile / ntn) * BM;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+
+  // DMA sources: wave w fills pieces 2w, 2w+1 (16 rows x 64 B each) of both
+  // images; lane L of a piece: row 16p + L/4, slot L%4 holds chunk
+  // (L%4) ^ ((row >> 2) & 3)
+  const uint16_t* asrc[2];
+  const uint16_t* bsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 16 * (2 * wave + q) + (lane >> 2);
+    const int c = (lane & 3) ^ ((r >> 2) & 3);
+    const int64_t gm = m0 + r < M ? m0 + r : M - 1;
+    const int64_t gn = n0 + r < npad ? n0 + r : npad - 1;
+    asrc[q] = A + gm * lda + 8 * c;
+    bsrc[q] = Bp + gn * kp + 8 * c;
+  }
+  const int nt = (int)(kp / BK);  // K % 32 == 0 (host)
+  auto issue = [&](int t) {
+    const int64_t k0 = (int64_t)(t < nt ? t : nt - 1) * BK;
+    uint8_t* ia = lds + (t % NS) * 2 * SI + wave * 2048;
+    uint8_t* ib = ia + SI;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(asrc[q] + k0), (lds_as_ptr)(ia + 1024 * q), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(bsrc[q] + k0), (lds_as_ptr)(ib + 1024 * q), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int ra = 64 * wm + li, rb = 128 * wn + li;
+  bf16x8 fa[2][2], fb[2][4];
+  auto read = [&](int t) {
+    const uint16_t* ia = reinterpret_cast<const uint16_t*>(lds + (t % NS) * 2 * SI);
+    const uint16_t* ib = ia + SI / 2;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[s][i] = xfrag(ia, ra + 32 * i, 2 * s + lh);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[s][j] = xfrag(ib, rb + 32 * j, 2 * s + lh);
+    }
+  };
+  auto mfma = [&]() {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // Two wave groups, one wave of each per SIMD, run a barrier apart: while
+  // one group issues MFMAs the other reads its fragments, so a SIMD's MFMA
+  // pipe alternates between its two waves instead of both idling in the
+  // read phase.  Group g's step t: X (barrier) -> DMA of step t+3 -> reads ->
+  // Y (barrier) -> MFMAs.  Global barrier b_k: group 0's X_t = b_2t,
+  // Y_t = b_2t+1; group 1's X_t = b_2t+1, Y_t = b_2t+2 (one extra barrier
+  // first).  Step t is read after b_2t (group 0) / b_2t+1 (group 1), so every
+  // wave retires its own DMA of step t before b_2t: group 0 before X_t,
+  // group 1 before Y_t-1, each with steps t+1 and t+2 still in flight
+  // (vmcnt(8)).  Step t+3 reuses step t-1's buffer, whose last reads (group
+  // 1's, before b_2t) precede both groups' issue points.
+  const bool g1 = wave >= 4;  // wave-uniform (scalar)
+  issue(0);
+  issue(1);
+  issue(2);
+  if (g1) {
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // step 0 (before b_0)
+    barrier();                                         // b_0
+  }
+  for (int t = 0; t < nt; ++t) {
+    if (!g1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    barrier();  // X_t
+    issue(t + 3);  // past the last step: re-reads it (never consumed)
+    read(t);
+    if (g1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // step t+1, before b_2t+2
+    barrier();  // Y_t
+    mfma();
+  }
+  if (!g1) barrier();  // group 0's partner of group 1's last Y
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t mb = m0 + 64 * wm + 32 * i, nb = n0 + 128 * wn + 32 * j;
+      if (nb >= N) continue;  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tw[acc_row(r, lh) * 32 + li] = acc[i][j][r];
+      wave_lds_sync();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx >> 3, c4 = idx & 7;
+        const int64_t m = mb + row, n = nb + 4 * c4;
+        if (m >= M || n >= N) continue;
+        float4 v = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+        if (n + 4 <= N) {
+          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+            v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            const float4 x = bf16x4_to_f4(*reinterpret_cast<const uint2*>(aux + m * ldaux + n));
+            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
+                            x.w > 0.f ? v.w : 0.f);
+          }
+          *reinterpret_cast<uint2*>(C + m * ldc + n) = f4_to_bf16x4(v);
+        } else {
+          const float e[4] = {v.x, v.y, v.z, v.w};
+          for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+            float x = e[jj];
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + jj];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + jj], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK) x = bf16_to_f32(aux[m * ldaux + n + jj]) > 0.f ? x : 0.f;
+            C[m * ldc + n + jj] = (uint16_t)(f32x2_to_bf16x2(x, 0.f) & 0xFFFFu);
+          }
+        }
+      }
+      wave_lds_sync();
+    }
   }
 }
 
@@ -476,6 +800,28 @@ int launch_qb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
 #undef MOLCLR_QB
 }
 
+template <bool RING>
+int launch_tb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,
+              int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc, const float* bias,
+              const uint16_t* aux, int64_t ldaux, hipStream_t s) {
+  const int64_t blocks = ((M + 255) / 256) * ((N + 255) / 256);
+  MOLCLR_REQUIRE(blocks < (1ll << 31), "gemm_bf16: too many tiles");
+  const dim3 g((unsigned)blocks), b(512);
+#define MOLCLR_TB(EPV)                                                                          \
+  molclr::launch_timed(molclr::kTimeGemm, RING ? k_gemm_tc<EPV> : k_gemm_tb<EPV>, g, b, 0, s, A, Bp, \
+                       C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux)
+  switch (epi) {
+    case MOLCLR_EPI_NONE: MOLCLR_TB(MOLCLR_EPI_NONE); return MOLCLR_OK;
+    case MOLCLR_EPI_BIAS: MOLCLR_TB(MOLCLR_EPI_BIAS); return MOLCLR_OK;
+    case MOLCLR_EPI_BIAS_RELU: MOLCLR_TB(MOLCLR_EPI_BIAS_RELU); return MOLCLR_OK;
+    case MOLCLR_EPI_RELU_MASK: MOLCLR_TB(MOLCLR_EPI_RELU_MASK); return MOLCLR_OK;
+    default:
+      molclr::set_error("gemm_bf16: bad epilogue %d", epi);
+      return MOLCLR_ERR_ARG;
+  }
+#undef MOLCLR_TB
+}
+
 template <int WM, int WN, int TN, int D>
 int launch_qb_m(bool mask, int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M,
                 int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
@@ -489,11 +835,19 @@ int launch_qb_m(bool mask, int epi, const uint16_t* A, const uint16_t* Bp, uint1
 // k_gemm_qb tile shapes (molclr_gemm_bf16_impl) and A ring depths:
 // 0 = 128 x 128 (4 waves, 4 steps of A in flight), 1 = 128 x 256 (4 waves, 2),
 // 2 = 128 x 512 (8 waves, 2), 3 = 64 x 512 (8 waves, 4), 4 = 128 x 256 (8
-// waves, 4), 5 = 128 x 128 (4 waves, 2)
-constexpr int kQbImpls = 6;
-// measured at the c5 shapes (55k rows, tools/gemm_bf16_bench.py): 128 x 512
-// for N <= 512, 128 x 128 above
-int qb_default(int64_t N) { return N > 512 ? 5 : 2; }
+// waves, 4), 5 = 128 x 128 (4 waves, 2); 6 = k_gemm_tb (256 x 256, LDS-DMA
+// staging of both operands; K % 64 == 0, else 2), 7 = k_gemm_tc (256 x 256,
+// four-stage LDS-DMA ring; K % 32 == 0, else 2)
+constexpr int kQbImpls = 8;
+// measured at the c5 shapes (55k rows, tools/gemm_bf16_bench.py); k_gemm_qb:
+// 128 x 512 for N <= 512, 128 x 128 above
+// k_gemm_tb whenever K % 64 == 0 (10-15 % faster than the best k_gemm_qb
+// shape on all four c5 products), k_gemm_tc for K % 32 == 0
+int qb_default(int64_t N, int64_t K) {
+  if (K % 64 == 0) return 6;
+  if (K % 32 == 0) return 7;
+  return N > 512 ? 5 : 2;
+}
 
 struct WbPlan {
   int splits, kps;
@@ -564,12 +918,19 @@ MOLCLR_API int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, 
   const int64_t npad = (N + 127) / 128 * 128, kp = (K + BK - 1) / BK * BK;
   hipStream_t s = molclr::as_stream(stream);
   const bool mask = K % BK != 0;
-  const int v = impl < 0 ? qb_default(N) : impl;
+  const int v = impl < 0 ? qb_default(N, K) : impl;
   int rc;
 #define MOLCLR_QBM(WMV, WNV, TNV, DV)                                                            \
   launch_qb_m<WMV, WNV, TNV, DV>(mask, epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, \
                                  aux, ldaux, s)
-  switch (v) {
+  const int vv = ((v == 6 && K % 64 != 0) || (v == 7 && K % 32 != 0)) ? 2 : v;
+  switch (vv) {
+    case 6:
+      rc = launch_tb<false>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, s);
+      break;
+    case 7:
+      rc = launch_tb<true>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, s);
+      break;
     case 1: rc = MOLCLR_QBM(4, 1, 8, 2); break;
     case 2: rc = MOLCLR_QBM(4, 2, 8, 2); break;
     case 3: rc = MOLCLR_QBM(2, 4, 4, 4); break;

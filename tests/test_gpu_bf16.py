@@ -78,7 +78,7 @@ def test_gemm_bf16(dev, M, N, K):
     # element, in the same k order)
     for epi in (EPI_BIAS_RELU, EPI_RELU_MASK):
         outs = []
-        for impl in (-1, 0, 1, 2, 3, 4, 5):
+        for impl in (-1, 0, 1, 2, 3, 4, 5, 6, 7):
             C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             assert lib.molclr_gemm_bf16_impl(Ad.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N,
                                              K, K, N, epi, bd.data_ptr(), auxd.data_ptr(), N, None,

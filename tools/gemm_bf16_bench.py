@@ -61,7 +61,7 @@ def main():
     for name, A, P, C, N, K, epi, bias, aux, ref in cases:
         fl = 2.0 * M * N * K
         res = []
-        for v in (-1, 0, 1, 2, 3, 4, 5):
+        for v in (-1, 2, 5, 6, 7):
             t = timeit(lambda: lib.molclr_gemm_bf16_impl(A.data_ptr(), P.data_ptr(), C.data_ptr(), M,
                                                          N, K, K, N, epi, _lib.ptr(bias),
                                                          _lib.ptr(aux), N if aux is not None else 0,
