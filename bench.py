@@ -21,6 +21,11 @@ The JSON line adds:
                   (molclr_ktimer_*), i.e. the kernel's own execution window.
   roofline_mfma — all molclr_gemm_f32 kernels (GEMM + split-K reduce) in the
                   timed region, against 157.3 TF/s (fp32 dense MFMA peak).
+  roofline_ntxent — every NT-Xent kernel (forward: S = R R^T as a split-bf16
+                  GEMM + the row logsumexp; backward: the weights W from the
+                  kept S and dR = W R), work = the two products' flops, against
+                  157.3 TF/s (fp32 MFMA) and 417 TF/s (the six-product split-bf16
+                  ceiling, 2.5 PF / 6); rows x cols x dim of this rank's share.
   cpu_baseline  — the oracle (CPU restatement of the reference step, incl.
                   the broadcast-cosine NT-Xent) on this host, rank 0, N=1 only,
                   a bounded sample of the same workload.
@@ -231,15 +236,15 @@ def main():
     s = timer.summary() if timer is not None else {}
     # GEMM durations: dispatch events over extra steps after the timed region
     if timer is not None and args.mfma_steps > 0:
-        gemm_timer = ops.KernelTimer(kinds=("gemm_f32",))
+        gemm_timer = ops.KernelTimer(kinds=("gemm_f32", "ntxent"))
         ops.set_kernel_timer(gemm_timer)
         for i in range(args.mfma_steps):
             step(args.warmup + args.steps + 3 + i)
         torch.cuda.synchronize()
         ops.set_kernel_timer(None)
-        s.update({k: v for k, v in gemm_timer.summary().items() if k == "gemm_f32"})
+        s.update({k: v for k, v in gemm_timer.summary().items() if k in ("gemm_f32", "ntxent")})
 
-    roofline = roofline_mfma = None
+    roofline = roofline_mfma = roofline_ntxent = None
     if timer is not None:
         agg = s.get("gine_aggregate_fwd")
         if agg:
@@ -268,6 +273,22 @@ def main():
                              "ms_per_step": round(gm["ms"] / args.mfma_steps, 3),
                              "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                        f"after the timed region"}
+        nx = s.get("ntxent")
+        if nx:
+            tfs = nx["work"] / (nx["ms"] / 1e3) / 1e12
+            roofline_ntxent = {"kernel": "molclr_ntxent_fwd/_bwd: every kernel of both calls (the "
+                                         "similarity GEMM S = R R^T, row logsumexp, weights W, "
+                                         "dR = W R; split-bf16 MFMA)",
+                               "bound": "mfma", "achieved": round(tfs, 2),
+                               "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s (fp32-equivalent)",
+                               "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
+                               "frac_of_split_bf16_ceiling": round(tfs / (BF16_MFMA_PEAK_TFS / 6), 4),
+                               "traffic": None,
+                               "rows": 2 * B,
+                               "cols": 2 * B * world, "dim": cfg["feat_dim"] // 2,
+                               "ms_per_step": round(nx["ms"] / args.mfma_steps, 3),
+                               "timing": f"dispatch events over {args.mfma_steps} extra steps "
+                                         f"after the timed region"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -297,7 +318,8 @@ def main():
                                    "device: molclr_mask_views inside the step")},
             "final_loss": round(final_loss, 5),
             "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
-            "roofline": roofline, "roofline_mfma": roofline_mfma, "cpu_baseline": cpu,
+            "roofline": roofline, "roofline_mfma": roofline_mfma,
+            "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

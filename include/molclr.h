@@ -421,6 +421,28 @@ int molclr_ntxent_bwd(const float* rhat_rows, const int32_t* row_gidx, const flo
                       int64_t ncols, int64_t C, int64_t batch_size, double temperature,
                       float* drhat_rows, void* workspace, size_t workspace_bytes,
                       molclr_stream_t stream);
+/* molclr_ntxent_fwd / _bwd with the formulation chosen per call (tests and
+ * benchmarks; -1 = automatic, as the calls above): 0 = fused f32-MFMA kernels
+ * (similarity tiles recomputed in registers, online logsumexp, no S buffer);
+ * 1 = S = rows cols^T as one split-bf16 GEMM (fp32 accuracy), then the row
+ * logsumexp / the symmetric weights W as elementwise passes and dR = W cols as
+ * a second GEMM (ncols % 4 == 0).  Automatic: 1 from nrows * ncols >= 2^20.
+ * sim (formulation 1 only; may be NULL): the forward writes S [nrows][ncols]
+ * there, and a backward given the same buffer uses it instead of recomputing
+ * S.  molclr_ntxent_sim_bytes: its size, 0 when the formulation chosen for
+ * (nrows, ncols, C, impl) keeps no S. */
+size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl);
+int molclr_ntxent_fwd_impl(const float* rhat_rows, const int32_t* row_gidx,
+                           const float* rhat_cols, int64_t nrows, int64_t ncols, int64_t C,
+                           int64_t batch_size, double temperature, float* lse_rows,
+                           float* loss_rows, float* sim, void* workspace, size_t workspace_bytes,
+                           molclr_stream_t stream, int impl);
+int molclr_ntxent_bwd_impl(const float* rhat_rows, const int32_t* row_gidx,
+                           const float* rhat_cols, const float* lse_cols, const float* grad_loss,
+                           int64_t nrows, int64_t ncols, int64_t C, int64_t batch_size,
+                           double temperature, const float* sim, float* drhat_rows,
+                           void* workspace, size_t workspace_bytes, molclr_stream_t stream,
+                           int impl);
 /* loss = Σ loss_rows (deterministic single-block sum). */
 int molclr_sum_f32(const float* x, float* out, int64_t n, molclr_stream_t stream);
 
@@ -656,10 +678,12 @@ int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t* x, float* 
  * Opt-in kernel timer.  While a kind is enabled, its launches go through
  * hipExtLaunchKernelGGL with a start/stop event pair recorded by the dispatch
  * itself, so each sample is the kernel's own execution window (the figure
- * rocprofv3 --kernel-trace reports).  Kinds: 1 = k_gine_agg_fwd,
- * 2 = every kernel of molclr_gemm_f32 (main GEMM + split-K reduce). */
+ * rocprofv3 --kernel-trace reports).  Kinds (a bit mask): 1 = k_gine_agg_fwd,
+ * 2 = every kernel of molclr_gemm_f32 (main GEMM + split-K reduce), 4 = the
+ * NT-Xent similarity kernels. */
 #define MOLCLR_KTIMER_GINE_AGG 1
 #define MOLCLR_KTIMER_GEMM 2
+#define MOLCLR_KTIMER_NTXENT 4 /* k_ntxent_fwd_partial / k_ntxent_bwd_partial */
 int molclr_ktimer_start(int kinds_mask);
 /* Waits for the recorded launches of `kind`, returns their summed duration
  * and count, and forgets them. */

@@ -90,6 +90,11 @@ SIGNATURES = {
                                   c_size_t, _P]),
     "molclr_ntxent_bwd": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P, _P,
                                   c_size_t, _P]),
+    "molclr_ntxent_sim_bytes": (c_size_t, [_I64, _I64, _I64, c_int]),
+    "molclr_ntxent_fwd_impl": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P, _P,
+                                       _P, _P, c_size_t, _P, c_int]),
+    "molclr_ntxent_bwd_impl": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P,
+                                       _P, _P, c_size_t, _P, c_int]),
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
@@ -131,6 +136,7 @@ MAX_SEGMENTS = 8
 DTYPE_F32, DTYPE_BF16 = 0, 1
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
+KTIMER_NTXENT = 4
 
 
 _L16 = c_void_p * 16

@@ -32,6 +32,10 @@ static int g_tmask = 0;
 static std::vector<TimerRec> g_trecs;
 
 bool timer_wants(int kind) { return (g_tmask & kind) != 0; }
+int& timer_kind_override() {
+  thread_local int k = 0;
+  return k;
+}
 void timer_record(int kind, hipEvent_t e0, hipEvent_t e1) {
   std::lock_guard<std::mutex> lk(g_tmu);
   g_trecs.push_back({kind, e0, e1});

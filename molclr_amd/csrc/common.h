@@ -61,13 +61,22 @@ inline Band make_band(int64_t dim) {
 // written by the kernel dispatch itself: the elapsed time is the kernel's own
 // execution window (what rocprofv3's kernel trace reports), not a bracket of
 // separately queued event packets.
-enum { kTimeGineAgg = MOLCLR_KTIMER_GINE_AGG, kTimeGemm = MOLCLR_KTIMER_GEMM };
+enum { kTimeGineAgg = MOLCLR_KTIMER_GINE_AGG, kTimeGemm = MOLCLR_KTIMER_GEMM, kTimeNtxent = MOLCLR_KTIMER_NTXENT };
 bool timer_wants(int kind);
 void timer_record(int kind, hipEvent_t start, hipEvent_t stop);
+// Launches made while a TimerKindScope is alive on the calling thread are
+// attributed to its kind (NT-Xent's internal GEMMs count as NT-Xent time).
+int& timer_kind_override();
+struct TimerKindScope {
+  int prev;
+  explicit TimerKindScope(int kind) : prev(timer_kind_override()) { timer_kind_override() = kind; }
+  ~TimerKindScope() { timer_kind_override() = prev; }
+};
 
 template <typename... Args, typename F = void (*)(Args...)>
 void launch_timed(int kind, F kernel, dim3 grid, dim3 block, uint32_t shmem,
                   hipStream_t stream, Args... args) {
+  if (timer_kind_override()) kind = timer_kind_override();
   if (timer_wants(kind)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {

@@ -266,6 +266,102 @@ __global__ void k_reduce_splits(const float* __restrict__ partial, int64_t split
   out[t] = acc;
 }
 
+// ---- GEMM formulation (impl 1) ------------------------------------------------
+// S = R_rows R_cols^T is one split-bf16 GEMM (molclr_gemm_f32_bplanes: six
+// bf16 MFMA products per element pair, fp32 accuracy, at the bf16 MFMA rate)
+// into an [nrows][ncols] fp32 buffer; the masked row logsumexp, and in the
+// backward the symmetric weight W, are then elementwise passes over it, and
+// dR = W R_cols a second GEMM.  At the c4 row shard (1024 x 8192 x 256) the
+// buffer is 32 MB.
+
+// one wave per row: lse_r = log Σ_{c != r} exp(S_rc / T), loss_r =
+// (lse_r - S_{r,p(r)} / T) / 2B
+__global__ __launch_bounds__(256) void k_ntxent_row_lse(const float* __restrict__ S, int64_t nrows,
+                                                        int64_t ncols, const int32_t* __restrict__ gidx,
+                                                        int64_t B, float inv_t, float inv_2b,
+                                                        float* __restrict__ lse, float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= nrows) return;
+  const int64_t rg = gidx[r];
+  const float* row = S + r * ncols;
+  float m = -INFINITY, s = 0.f;
+  // one float4 of logits into the running (max, sum)
+  auto take = [&](float4 v, int64_t c0) {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+    float x[4], bm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = c0 + j != rg ? e[j] * inv_t : -INFINITY;
+      bm = fmaxf(bm, x[j]);
+    }
+    if (bm > -INFINITY) {
+      const float nm = fmaxf(m, bm);
+      float acc = s * expf(m - nm);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc += expf(x[j] - nm);
+      m = nm;
+      s = acc;
+    }
+  };
+  int64_t c0 = 4 * lane;  // ncols % 4 == 0 (host)
+  for (; c0 + 768 < ncols; c0 += 1024) {  // four loads in flight
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(row + c0 + 256 * u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) take(v[u], c0 + 256 * u);
+  }
+  for (; c0 < ncols; c0 += 256) take(*reinterpret_cast<const float4*>(row + c0), c0);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
+    const float nm = fmaxf(m, mo);
+    s = nm == -INFINITY ? 0.f : s * expf(m - nm) + so * expf(mo - nm);
+    m = nm;
+  }
+  if (lane == 0) {
+    const float l = m + logf(s);
+    const int64_t pg = (rg + B) % (2 * B);
+    lse[r] = l;
+    loss[r] = (l - row[pg] * inv_t) * inv_2b;
+  }
+}
+
+// W_rc = g/(2B T) (exp(S_rc/T - lse_r) + exp(S_rc/T - lse_c) - 2 [c = p(r)]), 0 on the
+// diagonal c = r (W may be S itself)
+__global__ __launch_bounds__(256) void k_ntxent_weights(const float* S, float* W, int64_t nrows,
+                                                        int64_t ncols, const int32_t* __restrict__ gidx,
+                                                        const float* __restrict__ lse_cols,
+                                                        const float* __restrict__ grad_loss, int64_t B,
+                                                        float inv_t) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // float4 index
+  const int64_t per_row = ncols / 4;
+  if (q >= nrows * per_row) return;
+  const int64_t r = q / per_row, c0 = 4 * (q - r * per_row);
+  const int64_t rg = gidx[r];
+  const int64_t pg = (rg + B) % (2 * B);
+  const float lse_r = lse_cols[rg];
+  const float coef = (*grad_loss) * inv_t / (float)(2 * B);
+  float4 v = *reinterpret_cast<const float4*>(S + r * ncols + c0);
+  const float4 lc = *reinterpret_cast<const float4*>(lse_cols + c0);
+  float e[4] = {v.x, v.y, v.z, v.w};
+  const float l[4] = {lc.x, lc.y, lc.z, lc.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t c = c0 + j;
+    float w = 0.f;
+    if (c != rg) {
+      const float lg = e[j] * inv_t;
+      w = expf(lg - lse_r) + expf(lg - l[j]);
+      if (c == pg) w -= 2.f;
+      w *= coef;
+    }
+    e[j] = w;
+  }
+  *reinterpret_cast<float4*>(W + r * ncols + c0) = make_float4(e[0], e[1], e[2], e[3]);
+}
+
 // rhat = r / max(||r||, 1e-8) (cosine) or r (dot); norm saved for the backward
 __global__ __launch_bounds__(256) void k_ntxent_prep(const float* __restrict__ r,
                                                      float* __restrict__ rhat,
@@ -346,57 +442,151 @@ MOLCLR_API int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, con
 
 constexpr int64_t kBwdWaves = 1024;
 
+namespace {
+
+// workspace of the GEMM formulation: the column planes, S / W, and the two
+// GEMMs' split-K space
+size_t ntx_gemm_ws(int64_t nrows, int64_t ncols, int64_t C) {
+  size_t g1 = molclr_gemm_f32_workspace_bytes(nrows, ncols, C);
+  size_t g2 = molclr_gemm_f32_workspace_bytes(nrows, C, ncols);
+  return molclr_bplanes_bytes(ncols, C) + (size_t)nrows * ncols * sizeof(float) +
+         (g1 > g2 ? g1 : g2) + 3 * 256;
+}
+// automatic choice: the GEMM formulation once S has >= 2^20 elements (c2's
+// 1024 x 1024 and up), the fused kernels below that
+int ntx_impl(int64_t nrows, int64_t ncols, int64_t C, int impl) {
+  if (impl >= 0) return impl;
+  return (nrows * ncols >= (1 << 20) && ncols % 4 == 0 && C % 4 == 0) ? 1 : 0;
+}
+
+// S = rows cols^T into `sim` (or, when null, the workspace; planes of the
+// columns made first); returns the GEMM's error code
+int ntx_similarity(const float* rows, const float* cols, int64_t nrows, int64_t ncols, int64_t C,
+                   molclr::Workspace& w, float* sim, float** S_out, hipStream_t s) {
+  molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+  uint16_t* planes = reinterpret_cast<uint16_t*>(w.take<char>(molclr_bplanes_bytes(ncols, C)));
+  float* S = w.take<float>((size_t)nrows * ncols);
+  if (sim) S = sim;
+  const size_t gws = molclr_gemm_f32_workspace_bytes(nrows, ncols, C);
+  void* g = w.take<char>(gws);
+  int rc = molclr_bplanes_make(cols, ncols, C, C, 0, planes, s);
+  if (rc) return rc;
+  rc = molclr_gemm_f32_bplanes(rows, planes, S, nrows, ncols, C, C, ncols, 0, MOLCLR_EPI_NONE,
+                               nullptr, nullptr, 0, g, gws, s);
+  *S_out = S;
+  return rc;
+}
+
+}  // namespace
+
 MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C) {
   int64_t sp = ntx_splits(nrows, ncols);
   size_t fwd = (size_t)(2 * sp + 1) * nrows * sizeof(float);
   size_t bwd = (size_t)ntx_splits(nrows, ncols, kBwdWaves) * nrows * C * sizeof(float);
-  return (fwd > bwd ? fwd : bwd) + 256;
+  size_t fused = (fwd > bwd ? fwd : bwd) + 256;
+  size_t gemm = ntx_gemm_ws(nrows, ncols, C);
+  return fused > gemm ? fused : gemm;
 }
 
-MOLCLR_API int molclr_ntxent_fwd(const float* rows, const int32_t* gidx, const float* cols,
-                                 int64_t nrows, int64_t ncols, int64_t C, int64_t B, double T,
-                                 float* lse, float* loss, void* workspace, size_t ws_bytes,
-                                 molclr_stream_t stream) {
+MOLCLR_API size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl) {
+  if (nrows <= 0 || ncols <= 0 || C <= 0 || ntx_impl(nrows, ncols, C, impl) != 1) return 0;
+  return (size_t)nrows * ncols * sizeof(float);
+}
+
+MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, const float* cols,
+                                      int64_t nrows, int64_t ncols, int64_t C, int64_t B, double T,
+                                      float* lse, float* loss, float* sim, void* workspace,
+                                      size_t ws_bytes, molclr_stream_t stream, int impl) {
   MOLCLR_REQUIRE(C > 0 && C % 8 == 0, "ntxent_fwd: C=%lld must be a multiple of 8", (long long)C);
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_fwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_fwd: bad nrows");
   MOLCLR_REQUIRE(T > 0, "ntxent_fwd: temperature must be > 0");
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 1, "ntxent_fwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
+  const float inv_t = (float)(1.0 / T);
+  molclr::Workspace w(workspace, ws_bytes);
+  if (ntx_impl(nrows, ncols, C, impl) == 1) {
+    MOLCLR_REQUIRE(ncols % 4 == 0, "ntxent_fwd: the GEMM formulation needs ncols %% 4 == 0");
+    float* S = nullptr;
+    const int rc = ntx_similarity(rows, cols, nrows, ncols, C, w, sim, &S, s);
+    if (rc) return rc;
+    molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_row_lse,
+                         dim3((unsigned)molclr::ceil_div(nrows * 64, 256)), dim3(256), 0, s, S,
+                         nrows, ncols, gidx, B, inv_t, (float)(1.0 / (2.0 * B)), lse, loss);
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   int64_t sp = ntx_splits(nrows, ncols);
   int64_t nch = (ncols + 31) / 32;
   int64_t cps = (nch + sp - 1) / sp;
   sp = (nch + cps - 1) / cps;
-  molclr::Workspace w(workspace, ws_bytes);
   float* pm = w.take<float>(sp * nrows);
   float* ps = w.take<float>(sp * nrows);
   float* pos = w.take<float>(nrows);
   const dim3 grid((unsigned)((nrows + 31) / 32), (unsigned)sp);
-  const float inv_t = (float)(1.0 / T);
-  if (C == 256)
-    hipLaunchKernelGGL(k_ntxent_fwd_partial<32>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
-                       C, B, inv_t, cps, pm, ps, pos);
-  else if (C == 128)
-    hipLaunchKernelGGL(k_ntxent_fwd_partial<16>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
-                       C, B, inv_t, cps, pm, ps, pos);
-  else
-    hipLaunchKernelGGL(k_ntxent_fwd_partial<0>, grid, dim3(64), 0, s, rows, gidx, cols, nrows, ncols,
-                       C, B, inv_t, cps, pm, ps, pos);
+#define MOLCLR_NXF(NQ)                                                                           \
+  molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_fwd_partial<NQ>, grid, dim3(64), 0, s, rows, \
+                       gidx, cols, nrows, ncols, C, B, inv_t, cps, pm, ps, pos)
+  if (C == 256) MOLCLR_NXF(32);
+  else if (C == 128) MOLCLR_NXF(16);
+  else MOLCLR_NXF(0);
+#undef MOLCLR_NXF
   hipLaunchKernelGGL(k_ntxent_fwd_final, dim3(molclr::ceil_div(nrows, 256)), dim3(256), 0, s, pm,
                      ps, pos, sp, nrows, (float)(1.0 / (2.0 * B)), lse, loss);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
 
-MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const float* cols,
-                                 const float* lse_cols, const float* grad_loss, int64_t nrows,
-                                 int64_t ncols, int64_t C, int64_t B, double T, float* drows,
-                                 void* workspace, size_t ws_bytes, molclr_stream_t stream) {
+MOLCLR_API int molclr_ntxent_fwd(const float* rows, const int32_t* gidx, const float* cols,
+                                 int64_t nrows, int64_t ncols, int64_t C, int64_t B, double T,
+                                 float* lse, float* loss, void* workspace, size_t ws_bytes,
+                                 molclr_stream_t stream) {
+  return molclr_ntxent_fwd_impl(rows, gidx, cols, nrows, ncols, C, B, T, lse, loss, nullptr,
+                                workspace, ws_bytes, stream, -1);
+}
+
+MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, const float* cols,
+                                      const float* lse_cols, const float* grad_loss, int64_t nrows,
+                                      int64_t ncols, int64_t C, int64_t B, double T, const float* sim,
+                                      float* drows, void* workspace, size_t ws_bytes,
+                                      molclr_stream_t stream, int impl) {
   MOLCLR_REQUIRE(C > 0 && C % 32 == 0, "ntxent_bwd: C=%lld must be a multiple of 32", (long long)C);
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_bwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_bwd: bad nrows");
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 1, "ntxent_bwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
+  const float inv_t = (float)(1.0 / T);
+  if (ntx_impl(nrows, ncols, C, impl) == 1) {
+    MOLCLR_REQUIRE(ncols % 4 == 0, "ntxent_bwd: the GEMM formulation needs ncols %% 4 == 0");
+    molclr::Workspace w(workspace, ws_bytes);
+    int rc;
+    const float* S = sim;  // the forward's similarities, or recomputed here
+    float* W;
+    if (sim) {
+      W = w.take<float>((size_t)nrows * ncols);
+    } else {
+      float* Sw = nullptr;
+      rc = ntx_similarity(rows, cols, nrows, ncols, C, w, nullptr, &Sw, s);
+      if (rc) return rc;
+      S = W = Sw;  // in place
+    }
+    molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_weights,
+                         dim3((unsigned)molclr::ceil_div(nrows * ncols / 4, 256)), dim3(256), 0, s,
+                         S, W, nrows, ncols, gidx, lse_cols, grad_loss, B, inv_t);
+    // dR[r][k] = Σ_c W[r][c] cols[c][k]: A = W (row-major, K = ncols), B = cols ([K][N])
+    const size_t gws = molclr_gemm_f32_workspace_bytes(nrows, C, ncols);
+    void* g = w.take<char>(gws);
+    {
+      molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+      rc = molclr_gemm_f32(W, cols, drows, nrows, C, ncols, ncols, C, C, 0, 1, MOLCLR_EPI_NONE,
+                           nullptr, nullptr, 0, g, gws, s);
+    }
+    if (rc) return rc;
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   int64_t sp = ntx_splits(nrows, ncols, kBwdWaves);
   int64_t nch = (ncols + 31) / 32;
   int64_t cps = (nch + sp - 1) / sp;
@@ -405,18 +595,24 @@ MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const f
   int64_t kgroups = (C / 32 + KT - 1) / KT;
   float* partial = (float*)workspace;
   const dim3 grid((unsigned)((nrows + 31) / 32), (unsigned)sp, (unsigned)kgroups);
-  const float inv_t = (float)(1.0 / T);
-  if (C == 256)
-    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 32>), grid, dim3(64), 0, s, rows, gidx, cols,
-                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
-  else if (C == 128)
-    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 16>), grid, dim3(64), 0, s, rows, gidx, cols,
-                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
-  else
-    hipLaunchKernelGGL((k_ntxent_bwd_partial<KT, 0>), grid, dim3(64), 0, s, rows, gidx, cols,
-                       lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps, partial);
+#define MOLCLR_NXB(NQ)                                                                       \
+  molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_bwd_partial<KT, NQ>, grid, dim3(64), 0, s, \
+                       rows, gidx, cols, lse_cols, grad_loss, nrows, ncols, C, B, inv_t, cps,   \
+                       partial)
+  if (C == 256) MOLCLR_NXB(32);
+  else if (C == 128) MOLCLR_NXB(16);
+  else MOLCLR_NXB(0);
+#undef MOLCLR_NXB
   hipLaunchKernelGGL(k_reduce_splits, dim3(molclr::ceil_div(nrows * C, 256)), dim3(256), 0, s,
                      partial, sp, nrows * C, drows);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ntxent_bwd(const float* rows, const int32_t* gidx, const float* cols,
+                                 const float* lse_cols, const float* grad_loss, int64_t nrows,
+                                 int64_t ncols, int64_t C, int64_t B, double T, float* drows,
+                                 void* workspace, size_t ws_bytes, molclr_stream_t stream) {
+  return molclr_ntxent_bwd_impl(rows, gidx, cols, lse_cols, grad_loss, nrows, ncols, C, B, T,
+                                nullptr, drows, workspace, ws_bytes, stream, -1);
 }

@@ -81,9 +81,11 @@ class KernelTimer:
     (molclr_ktimer_*, hipExtLaunchKernelGGL): each sample is the kernel's own
     execution window, the same figure rocprofv3's kernel trace reports.  This
     class only counts calls and adds up their algorithmic work (bytes for the
-    scatter-add, 2MNK flops for a GEMM)."""
+    scatter-add, 2MNK flops for a GEMM, the similarity products' flops for
+    NT-Xent: 2 n 2B C forward, twice that backward)."""
 
-    KINDS = {"gine_aggregate_fwd": _lib.KTIMER_GINE_AGG, "gemm_f32": _lib.KTIMER_GEMM}
+    KINDS = {"gine_aggregate_fwd": _lib.KTIMER_GINE_AGG, "gemm_f32": _lib.KTIMER_GEMM,
+             "ntxent": _lib.KTIMER_NTXENT}
 
     def __init__(self, kinds=None):
         """``kinds``: the subset of KINDS to time (default all).  Every timed
@@ -654,9 +656,15 @@ class _NTXent(torch.autograd.Function):
         loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
         ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
         ws = _ws(ws_bytes, dev)
-        _lib.call("molclr_ntxent_fwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n, 2 * B,
-                  C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(), ws.data_ptr(),
-                  ws_bytes, st)
+        # the GEMM formulation keeps S = rows cols^T for the backward
+        sim_bytes = _lib.query("molclr_ntxent_sim_bytes", n, 2 * B, C, -1)
+        sim = (torch.empty(sim_bytes // 4, dtype=torch.float32, device=dev) if sim_bytes
+               else torch.empty(0, dtype=torch.float32, device=dev))
+        _lib.call("molclr_ntxent_fwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n,
+                  2 * B, C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(),
+                  sim.data_ptr() if sim_bytes else None, ws.data_ptr(), ws_bytes, st, -1)
+        if _TIMER is not None:
+            _TIMER.add("ntxent", 2.0 * n * 2 * B * C)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         _lib.call("molclr_sum_f32", loss_rows.data_ptr(), loss.data_ptr(), n, st)
         if group is None:
@@ -664,13 +672,13 @@ class _NTXent(torch.autograd.Function):
         else:
             lse_cols = mdist.gather_lse(lse, group)
             dist.all_reduce(loss, group=group)
-        ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols)
+        ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols, sim)
         ctx.meta = (B, C, float(temperature), int(cosine))
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        rhat, norm, cols, gidx, lse_cols = ctx.saved_tensors
+        rhat, norm, cols, gidx, lse_cols, sim = ctx.saved_tensors
         B, C, T, cosine = ctx.meta
         dev = rhat.device
         n = rhat.shape[0]
@@ -679,9 +687,12 @@ class _NTXent(torch.autograd.Function):
         drhat = torch.empty_like(rhat)
         ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
         ws = _ws(ws_bytes, dev)
-        _lib.call("molclr_ntxent_bwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
-                  lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T, drhat.data_ptr(),
-                  ws.data_ptr(), ws_bytes, st)
+        _lib.call("molclr_ntxent_bwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                  lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T,
+                  sim.data_ptr() if sim.numel() else None, drhat.data_ptr(), ws.data_ptr(),
+                  ws_bytes, st, -1)
+        if _TIMER is not None:  # dR = W R (and S again when the forward kept none)
+            _TIMER.add("ntxent", (2.0 if sim.numel() else 4.0) * n * 2 * B * C)
         dR = torch.empty_like(rhat)
         _lib.call("molclr_ntxent_prep_bwd", drhat.data_ptr(), rhat.data_ptr(), norm.data_ptr(),
                   dR.data_ptr(), n, C, cosine, st)

@@ -43,8 +43,11 @@ def _prep(lib, R, cosine, dev):
     return rh, nrm
 
 
-@pytest.mark.parametrize("W,Bl,C,cosine", [(8, 512, 256, True), (3, 37, 64, False)])
-def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine):
+@pytest.mark.parametrize("W,Bl,C,cosine,impl", [(8, 512, 256, True, 0), (8, 512, 256, True, 1),
+                                                (8, 512, 256, True, -1), (3, 37, 64, False, 0),
+                                                (3, 36, 64, False, 1), (3, 37, 64, False, -1)])
+def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine, impl):
+    """impl: 0 fused kernels, 1 GEMM formulation, -1 automatic."""
     lib = _lib.load()
     B = W * Bl
     T = 0.1
@@ -66,24 +69,31 @@ def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine):
     cols = torch.cat([g[:, :Bl].reshape(B, C), g[:, Bl:].reshape(B, C)]).contiguous()
     ws_bytes = lib.molclr_ntxent_workspace_bytes(2 * Bl, 2 * B, C)
     ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    # formulation 1 keeps S from the forward for rank 0's backward (the others
+    # recompute it): both paths are checked
+    sim_bytes = lib.molclr_ntxent_sim_bytes(2 * Bl, 2 * B, C, impl)
+    sims = [torch.empty(max(sim_bytes, 4), dtype=torch.uint8, device=dev) if r == 0 and sim_bytes
+            else None for r in range(W)]
     lses, loss = [], 0.0
-    for rows, _, gidx in ranks:
+    for (rows, _, gidx), sim in zip(ranks, sims):
         lse = torch.empty(2 * Bl, device=dev)
         lr = torch.empty(2 * Bl, device=dev)
-        assert lib.molclr_ntxent_fwd(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(), 2 * Bl,
-                                     2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(), ws.data_ptr(),
-                                     ws_bytes, None) == 0
+        assert lib.molclr_ntxent_fwd_impl(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                                          2 * Bl, 2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(),
+                                          _lib.ptr(sim), ws.data_ptr(), ws_bytes, None,
+                                          impl) == 0
         lses.append(lse)
         loss += lr.double().sum().item()
     lg = torch.stack(lses)
     lse_cols = torch.cat([lg[:, :Bl].reshape(-1), lg[:, Bl:].reshape(-1)]).contiguous()
     gl = torch.ones((), device=dev)
     dzi, dzj = [], []
-    for rows, nrm, gidx in ranks:
+    for (rows, nrm, gidx), sim in zip(ranks, sims):
         drh = torch.empty_like(rows)
-        assert lib.molclr_ntxent_bwd(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
-                                     lse_cols.data_ptr(), gl.data_ptr(), 2 * Bl, 2 * B, C, B, T,
-                                     drh.data_ptr(), ws.data_ptr(), ws_bytes, None) == 0
+        assert lib.molclr_ntxent_bwd_impl(rows.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                                          lse_cols.data_ptr(), gl.data_ptr(), 2 * Bl, 2 * B, C, B,
+                                          T, _lib.ptr(sim), drh.data_ptr(), ws.data_ptr(),
+                                          ws_bytes, None, impl) == 0
         dR = torch.empty_like(rows)
         assert lib.molclr_ntxent_prep_bwd(drh.data_ptr(), rows.data_ptr(), nrm.data_ptr(),
                                           dR.data_ptr(), 2 * Bl, C, int(cosine), None) == 0

@@ -22,6 +22,9 @@ for s in $steps; do
              run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     gemm)    run gemm 300 python tools/gemm_bench.py 30556; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    ntx)     run ntx 300 python tools/ntxent_scale.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    ntxprof) export TMPDIR=/tmp; rm -rf gpurun_out/ntxprof
+             run ntxprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/ntxprof -o run --output-format csv -- python tools/ntxent_scale.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     gemmbf)  run gemmbf 300 python tools/gemm_bf16_bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     gpmc)    for c in ${PMC_CASES:-qb_lin2:1}; do
                CASE=${c%%:*} VARIANT=${c##*:} run "gpmc_${c%%:*}_${c##*:}" 400 bash tools/gemm_pmc.sh; rc=$?; [ $rc -eq 0 ] || exit $rc

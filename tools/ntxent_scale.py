@@ -29,20 +29,26 @@ def main():
         ws_bytes = _lib.query("molclr_ntxent_workspace_bytes", n, 2 * B, C)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
 
-        def fwd():
-            _lib.call("molclr_ntxent_fwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n,
-                      2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(), ws.data_ptr(), ws_bytes, st)
+        for impl in (0, 1):
+            sb = _lib.query("molclr_ntxent_sim_bytes", n, 2 * B, C, impl)
+            sim = torch.empty(max(sb, 4), dtype=torch.uint8, device=dev) if sb else None
 
-        def bwd():
-            _lib.call("molclr_ntxent_bwd", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
-                      lse_cols.data_ptr(), gl.data_ptr(), n, 2 * B, C, B, T, dr.data_ptr(),
-                      ws.data_ptr(), ws_bytes, st)
-        from tools_gemm import timeit  # noqa: F401
-        tf = timeit(fwd)
-        tb = timeit(bwd)
-        flops = 2.0 * n * 2 * B * C
-        print(f"W={W}: cols {2 * B:5d}  fwd {tf * 1e6:7.1f} us ({flops / tf / 1e12:5.1f} TF)  "
-              f"bwd {tb * 1e6:7.1f} us ({3 * flops / tb / 1e12:5.1f} TF)", flush=True)
+            def fwd():
+                _lib.call("molclr_ntxent_fwd_impl", rhat.data_ptr(), gidx.data_ptr(),
+                          cols.data_ptr(), n, 2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(),
+                          _lib.ptr(sim), ws.data_ptr(), ws_bytes, st, impl)
+
+            def bwd():  # with the forward's S kept (formulation 1)
+                _lib.call("molclr_ntxent_bwd_impl", rhat.data_ptr(), gidx.data_ptr(),
+                          cols.data_ptr(), lse_cols.data_ptr(), gl.data_ptr(), n, 2 * B, C, B, T,
+                          _lib.ptr(sim), dr.data_ptr(), ws.data_ptr(), ws_bytes, st, impl)
+            from tools_gemm import timeit  # noqa: F401
+            tf = timeit(fwd)
+            tb = timeit(bwd)
+            flops = 2.0 * n * 2 * B * C
+            print(f"W={W} impl {impl}: cols {2 * B:5d}  fwd {tf * 1e6:7.1f} us "
+                  f"({flops / tf / 1e12:5.1f} TF)  bwd {tb * 1e6:7.1f} us "
+                  f"({2 * flops / tb / 1e12:5.1f} TF)", flush=True)
 
 
 if __name__ == "__main__":
