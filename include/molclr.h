@@ -384,6 +384,16 @@ int molclr_segment_pool_fwd(const float* h, const int32_t* graph_ptr, float* out
 int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_ptr, float* dh,
                             int64_t num_nodes, int64_t num_graphs, int64_t dim, int mode,
                             molclr_stream_t stream);
+/* global_max_pool (models/ginet_molclr.py:85-86, gcn_molclr.py:125-126: PyG
+ * 1.6.3 -> torch_scatter 2.0.6 scatter_max).  out[g][d] = max over the nodes
+ * of graph g, argmax[g][d] = that node (the first in node order among equal
+ * values; -1 and out = 0 for a graph without nodes).  h is fp32 or bf16
+ * (dtype MOLCLR_DTYPE_*), out / dout fp32; the backward writes dout[g][d] to
+ * dh[argmax[g][d]][d] and zero elsewhere (dh in h's dtype).  D % 4 == 0. */
+int molclr_segment_max_fwd(const void* h, const int32_t* graph_ptr, float* out, int32_t* argmax,
+                           int64_t num_graphs, int64_t dim, int dtype, molclr_stream_t stream);
+int molclr_segment_max_bwd(const float* dout, const int32_t* argmax, void* dh, int64_t num_nodes,
+                           int64_t num_graphs, int64_t dim, int dtype, molclr_stream_t stream);
 
 /* F.normalize(z, dim=1, eps): y = z / max(||z||, eps); norm [rows] saved. */
 int molclr_l2norm_fwd(const float* z, float* y, float* norm, int64_t rows, int64_t dim,

@@ -112,6 +112,8 @@ SIGNATURES = {
     "molclr_gine_aggregate_fwd_bf16": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
     "molclr_gine_aggregate_bwd_bf16": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int,
                                                _P, c_size_t, _P]),
+    "molclr_segment_max_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_segment_max_bwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_segment_pool_fwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
     "molclr_segment_pool_bwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_gemm_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P, _I64,

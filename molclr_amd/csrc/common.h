@@ -156,6 +156,7 @@ struct StF32 {
     reinterpret_cast<float4*>(p)[unit] = v;
   }
   __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) { return p[i]; }
+  __device__ __forceinline__ static void st1(T* __restrict__ p, int64_t i, float v) { p[i] = v; }
 };
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t bits16) {
@@ -181,6 +182,9 @@ struct StBF16 {
   }
   __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) {
     return bf16_to_f32(p[i]);
+  }
+  __device__ __forceinline__ static void st1(T* __restrict__ p, int64_t i, float v) {
+    p[i] = (uint16_t)(f32x2_to_bf16x2(v, 0.f) & 0xFFFFu);
   }
 };
 

@@ -509,6 +509,55 @@ __global__ void k_pool_bwd(const float4* __restrict__ dout, const int32_t* __res
   for (int32_t i = beg; i < end; ++i) St::st(dh, (int64_t)i * d4 + c, v);
 }
 
+// global_max_pool (PyG 1.6.3 -> torch_scatter 2.0.6 scatter_max): per graph
+// and column the largest value and the node holding it (the first in node
+// order among equal values, as torch_scatter's CPU loop keeps it: strict >);
+// a graph without nodes pools to 0 with no arg (-1).  The backward routes
+// dout to that node only.
+template <typename St = StF32>
+__global__ void k_pool_max_fwd(const typename St::T* __restrict__ h, const int32_t* __restrict__ ptr,
+                               float4* __restrict__ out, int4* __restrict__ arg, int64_t G, int d4) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= G * d4) return;
+  int64_t g = t / d4;
+  int c = (int)(t - g * d4);
+  int32_t beg = ptr[g], end = ptr[g + 1];
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int a[4] = {-1, -1, -1, -1};
+  for (int32_t i = beg; i < end; ++i) {
+    const float4 v = St::ld(h, (int64_t)i * d4 + c);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (a[j] < 0 || e[j] > m[j]) {
+        m[j] = e[j];
+        a[j] = i;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (a[j] < 0) m[j] = 0.f;
+  out[t] = make_float4(m[0], m[1], m[2], m[3]);
+  arg[t] = make_int4(a[0], a[1], a[2], a[3]);
+}
+
+template <typename St = StF32>
+__global__ void k_pool_max_bwd(const float4* __restrict__ dout, const int4* __restrict__ arg,
+                               typename St::T* __restrict__ dh, int64_t G, int d4) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= G * d4) return;
+  const int c = (int)(t % d4);
+  const float4 v = dout[t];
+  const int4 a = arg[t];
+  const float e[4] = {v.x, v.y, v.z, v.w};
+  const int ai[4] = {a.x, a.y, a.z, a.w};
+  // the other elements of each row stay zero (memset); a node is the arg of
+  // at most one graph, so no two threads write one element
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (ai[j] >= 0) St::st1(dh, (int64_t)ai[j] * (4 * d4) + 4 * c + j, e[j]);
+}
+
 // ---------------------------------------------------------------------------
 // F.normalize (one wave per row)
 // ---------------------------------------------------------------------------
@@ -874,6 +923,55 @@ MOLCLR_API int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* gr
   const int d4 = (int)(D / 4);
   hipLaunchKernelGGL(k_pool_bwd<StBF16>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
                      (const float4*)dout, graph_ptr, dh, G, d4, mode);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+// dtype: MOLCLR_DTYPE_F32 / _BF16 node embeddings h (out and dout stay fp32)
+MOLCLR_API int molclr_segment_max_fwd(const void* h, const int32_t* graph_ptr, float* out,
+                                      int32_t* argmax, int64_t G, int64_t D, int dtype,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_max_fwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_F32 || dtype == MOLCLR_DTYPE_BF16,
+                 "segment_max_fwd: bad dtype %d", dtype);
+  MOLCLR_REQUIRE(G >= 0, "segment_max_fwd: bad graph count");
+  if (G == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(h && graph_ptr && out && argmax, "segment_max_fwd: null pointer");
+  const int d4 = (int)(D / 4);
+  const dim3 g(molclr::ceil_div(G * d4, kT)), b(kT);
+  hipStream_t s = molclr::as_stream(stream);
+  if (dtype == MOLCLR_DTYPE_BF16)
+    hipLaunchKernelGGL(k_pool_max_fwd<StBF16>, g, b, 0, s, static_cast<const uint16_t*>(h),
+                       graph_ptr, (float4*)out, (int4*)argmax, G, d4);
+  else
+    hipLaunchKernelGGL(k_pool_max_fwd<StF32>, g, b, 0, s, static_cast<const float*>(h), graph_ptr,
+                       (float4*)out, (int4*)argmax, G, d4);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_segment_max_bwd(const float* dout, const int32_t* argmax, void* dh,
+                                      int64_t N, int64_t G, int64_t D, int dtype,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_max_bwd: dim must be a multiple of 4");
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_F32 || dtype == MOLCLR_DTYPE_BF16,
+                 "segment_max_bwd: bad dtype %d", dtype);
+  MOLCLR_REQUIRE(N >= 0 && G >= 0, "segment_max_bwd: bad sizes");
+  hipStream_t s = molclr::as_stream(stream);
+  const size_t esz = dtype == MOLCLR_DTYPE_BF16 ? sizeof(uint16_t) : sizeof(float);
+  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * esz, s) != hipSuccess) {
+    molclr::set_error("segment_max_bwd: memset failed");
+    return MOLCLR_ERR_ARG;
+  }
+  if (G == 0) return MOLCLR_OK;
+  const int d4 = (int)(D / 4);
+  const dim3 g(molclr::ceil_div(G * d4, kT)), b(kT);
+  if (dtype == MOLCLR_DTYPE_BF16)
+    hipLaunchKernelGGL(k_pool_max_bwd<StBF16>, g, b, 0, s, (const float4*)dout,
+                       (const int4*)argmax, static_cast<uint16_t*>(dh), G, d4);
+  else
+    hipLaunchKernelGGL(k_pool_max_bwd<StF32>, g, b, 0, s, (const float4*)dout, (const int4*)argmax,
+                       static_cast<float*>(dh), G, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -92,10 +92,8 @@ class GCN(nn.Module):
         for _ in range(num_layer):
             self.batch_norms.append(nn.BatchNorm1d(emb_dim))
 
-        if pool == 'mean' or pool == 'add':
+        if pool in ('mean', 'add', 'max'):
             self.pool = pool
-        elif pool == 'max':
-            raise NotImplementedError("pool='max' is not implemented by molclr_amd (mean, add)")
         else:
             raise ValueError('Not defined pooling!')
 

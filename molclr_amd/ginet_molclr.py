@@ -93,8 +93,6 @@ class GINet(nn.Module):
         # forward time (ginet_molclr.py:83-88); fail at construction instead.
         if pool not in ('mean', 'add', 'max'):
             raise ValueError('Not defined pooling!')
-        if pool == 'max':
-            raise NotImplementedError("pool='max' is not implemented by molclr_amd (mean, add)")
         self.pool = pool
 
         self.feat_lin = nn.Linear(self.emb_dim, self.feat_dim)

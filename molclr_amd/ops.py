@@ -538,6 +538,38 @@ class _SegmentPool(torch.autograd.Function):
         return dh, None, None
 
 
+class _SegmentMax(torch.autograd.Function):
+    """global_max_pool (PyG 1.6.3 -> torch_scatter 2.0.6 scatter_max): the
+    gradient goes to the arg-max node of each (graph, column)."""
+
+    @staticmethod
+    def forward(ctx, h, graph: DeviceGraph):
+        _check(h)
+        h = _c(h)
+        N, D = h.shape
+        G = graph.num_graphs
+        if h.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError(f"segment_max: {h.dtype} node embeddings (fp32 / bf16)")
+        dt = _lib.DTYPE_BF16 if h.dtype == torch.bfloat16 else _lib.DTYPE_F32
+        out = torch.empty(G, D, dtype=torch.float32, device=h.device)
+        arg = torch.empty(G, D, dtype=torch.int32, device=h.device)
+        _lib.call("molclr_segment_max_fwd", h.data_ptr(), graph.graph_ptr.data_ptr(), out.data_ptr(),
+                  arg.data_ptr(), G, D, dt, _stream(h))
+        ctx.save_for_backward(arg)
+        ctx.N, ctx.dtype, ctx.dt = N, h.dtype, dt
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (arg,) = ctx.saved_tensors
+        dout = _c(dout.to(torch.float32))
+        G, D = dout.shape
+        dh = torch.empty(ctx.N, D, dtype=ctx.dtype, device=dout.device)
+        _lib.call("molclr_segment_max_bwd", dout.data_ptr(), arg.data_ptr(), dh.data_ptr(), ctx.N, G,
+                  D, ctx.dt, _stream(dout))
+        return dh, None
+
+
 class _GCNConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, bias, E1, E2, graph: DeviceGraph):
@@ -941,8 +973,11 @@ def batch_norm(z, bn: torch.nn.BatchNorm1d, relu: bool):
 
 
 def segment_pool(h, graph, mode: str):
+    """global_mean_pool / global_add_pool / global_max_pool over graph_ptr."""
+    if mode == "max":
+        return _SegmentMax.apply(h, graph)
     if mode not in POOL_MODES:
-        raise ValueError(f"pool '{mode}' is not supported by molclr_amd (mean, add)")
+        raise ValueError(f"pool '{mode}' is not supported by molclr_amd (mean, add, max)")
     return _SegmentPool.apply(h, graph, POOL_MODES[mode])
 
 

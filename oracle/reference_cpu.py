@@ -82,6 +82,21 @@ def global_add_pool(h: torch.Tensor, batch: torch.Tensor, size: int | None = Non
     return scatter_sum(h, batch, size)
 
 
+def global_max_pool(h: torch.Tensor, batch: torch.Tensor, size: int | None = None):
+    """PyG 1.6.3 global_max_pool = torch_scatter 2.0.6 scatter(reduce='max')
+    (scatter_max): per graph and column the maximum; a graph without nodes
+    pools to 0; the gradient goes to the arg-max node, the first in node order
+    among equal values (torch_scatter's CPU loop keeps a strictly greater
+    value; torch.max(dim) returns the first maximal index and routes its
+    gradient there)."""
+    size = int(batch.max().item()) + 1 if size is None else size
+    rows = []
+    for g in range(size):
+        seg = h[batch == g]
+        rows.append(seg.max(dim=0).values if seg.shape[0] else h.new_zeros(h.shape[1]))
+    return torch.stack(rows)
+
+
 # ---------------------------------------------------------------------------
 # models/ginet_molclr.py
 # ---------------------------------------------------------------------------
@@ -120,7 +135,8 @@ class RefGINet(nn.Module):
         nn.init.xavier_uniform_(self.x_embedding2.weight.data)
         self.gnns = nn.ModuleList([RefGINEConv(emb_dim) for _ in range(num_layer)])
         self.batch_norms = nn.ModuleList([nn.BatchNorm1d(emb_dim) for _ in range(num_layer)])
-        self.pool = {'mean': global_mean_pool, 'add': global_add_pool}[pool]
+        self.pool = {'mean': global_mean_pool, 'add': global_add_pool,
+                     'max': global_max_pool}[pool]                      # ginet_molclr.py:83-88
         self.feat_lin = nn.Linear(self.emb_dim, self.feat_dim)
         self.out_lin = nn.Sequential(nn.Linear(self.feat_dim, self.feat_dim), nn.ReLU(inplace=True),
                                      nn.Linear(self.feat_dim, self.feat_dim // 2))
@@ -189,7 +205,8 @@ class RefGCN(nn.Module):
         nn.init.xavier_uniform_(self.x_embedding2.weight.data)
         self.gnns = nn.ModuleList([RefGCNConv(emb_dim, aggr="add") for _ in range(num_layer)])
         self.batch_norms = nn.ModuleList([nn.BatchNorm1d(emb_dim) for _ in range(num_layer)])
-        self.pool = {'mean': global_mean_pool, 'add': global_add_pool}[pool]
+        self.pool = {'mean': global_mean_pool, 'add': global_add_pool,
+                     'max': global_max_pool}[pool]                      # gcn_molclr.py:121-128
         self.feat_lin = nn.Linear(self.emb_dim, self.feat_dim)
         self.out_lin = nn.Sequential(nn.Linear(self.feat_dim, self.feat_dim), nn.ReLU(inplace=True),
                                      nn.Linear(self.feat_dim, self.feat_dim // 2))

@@ -13,7 +13,7 @@ from molclr_amd.dataset import SyntheticPairBatches
 from oracle import ntxent_math
 from oracle.graph_ref import graph_build
 from oracle.reference_cpu import (RefNTXentLoss, add_self_loops, global_add_pool,
-                                  global_mean_pool, propagate_add)
+                                  global_max_pool, global_mean_pool, propagate_add)
 
 from .conftest import GOLDEN
 
@@ -447,6 +447,31 @@ def test_segment_pool(dev, mode):
     ref.backward(g)
     out.backward(g.to(dev))
     assert rel(hd.grad, h.grad) < TOL
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_segment_max(dev, dtype):
+    """global_max_pool: bit-exact values, gradient to the first arg-max node
+    (ties forced by integer-valued embeddings), empty graphs pool to 0."""
+    from molclr_amd.data import DeviceGraph
+    b = batch(300, 5)
+    N, D = b.x.shape[0], 64
+    torch.manual_seed(5)
+    h = torch.randint(-3, 4, (N, D)).float()  # many ties
+    h[: N // 2] += torch.randn(N // 2, D)      # and some without
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    h = h.to(tdt).float().requires_grad_(True)  # values representable in the storage type
+    G = int(b.num_graphs) + 2                 # two trailing graphs without nodes
+    ref = global_max_pool(h, b.batch, G)
+    g = DeviceGraph(b.edge_index.to(dev), b.edge_attr.to(dev), N, b.batch.to(dev), G)
+    hd = h.detach().to(tdt).to(dev).requires_grad_(True)
+    out = ops.segment_pool(hd, g, "max")
+    assert torch.equal(out.cpu(), ref.detach())
+    gr = torch.randn_like(ref)
+    ref.backward(gr)
+    out.backward(gr.to(dev))
+    expect = h.grad.to(tdt)  # bf16: the routed gradient is stored rounded
+    assert torch.equal(hd.grad.cpu(), expect)
 
 
 def test_l2_normalize(dev):

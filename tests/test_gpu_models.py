@@ -116,6 +116,37 @@ def test_encoder_forward_backward(dev, kind, L, D, B):
         assert rel(dict(mine.named_buffers())[name].float(), buf.float()) < TOL, name
 
 
+@pytest.mark.parametrize("kind,L,D,B", [("gin", 2, 16, 4), ("gcn", 2, 32, 5), ("gin", 3, 128, 16)])
+def test_max_pool_encoder(dev, kind, L, D, B):
+    """pool='max' (global_max_pool, models/ginet_molclr.py:85-86,
+    gcn_molclr.py:125-126) against the fp64 oracle.  The pooled value is
+    continuous in h, so the forward holds the usual 1e-5; the backward routes
+    each (graph, column) gradient to one node, a discontinuous choice, so it is
+    held to 1e-4 norm-wise -- a wrong routing or a wrong node is an O(1)
+    error."""
+    from molclr_amd.gcn_molclr import GCN
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(2)
+    ref = (RefGINet if kind == "gin" else RefGCN)(L, D, 512, pool="max")
+    mine = (GINet if kind == "gin" else GCN)(L, D, 512, pool="max")
+    mine.load_state_dict(ref.state_dict())
+    ref64 = copy.deepcopy(ref).double()
+    mine = mine.to(dev)
+    bi, _ = SyntheticPairBatches(B, seed=5).next()
+    h_6, out_6 = ref64(bi)
+    h_m, out_m = mine(bi.to(dev))
+    assert rel(h_m, h_6) < TOL and rel(out_m, out_6) < TOL
+    torch.manual_seed(3)
+    w1, w2 = torch.randn_like(h_6), torch.randn_like(out_6)
+    ((h_6 * w1).sum() + (out_6 * w2).sum()).backward()
+    ((h_m * w1.float().to(dev)).sum() + (out_m * w2.float().to(dev)).sum()).backward()
+    g64 = dict(ref64.named_parameters())
+    for name, p in mine.named_parameters():
+        if pre_bn_bias(name):
+            continue
+        assert rel(p.grad, g64[name].grad) < 1e-4, name
+
+
 @pytest.mark.parametrize("kind", ["gin", "gcn"])
 def test_training_steps_match_oracle(dev, kind):
     """Three full steps (2 encoder forwards, F.normalize, NT-Xent, backward,

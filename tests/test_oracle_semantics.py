@@ -5,8 +5,8 @@ import numpy as np
 import pytest
 import torch
 
-from oracle.reference_cpu import (RefGCNConv, RefGINEConv, RefGINet, global_mean_pool,
-                                  add_self_loops)
+from oracle.reference_cpu import (RefGCNConv, RefGINEConv, RefGINet, global_max_pool,
+                                  global_mean_pool, add_self_loops)
 from molclr_amd.data import Batch, Data
 
 
@@ -81,6 +81,24 @@ def test_global_mean_pool_known_answer():
     batch = torch.tensor([0, 0, 1, 1, 1, 3])  # graph 2 empty -> 0
     out = global_mean_pool(h, batch).numpy()
     np.testing.assert_allclose(out, [[1, 2], [6, 7], [0, 0], [10, 11]])
+
+
+def test_global_max_pool_known_answer():
+    """torch_scatter 2.0.6 scatter_max semantics: max per graph and column,
+    0 for a graph without nodes, the gradient to the FIRST maximal node."""
+    h = torch.tensor([[1., 5.], [3., 5.], [-2., -1.], [-7., -1.], [4., 0.]], requires_grad=True)
+    batch = torch.tensor([0, 0, 1, 1, 3])  # graph 2 empty
+    out = global_max_pool(h, batch)
+    np.testing.assert_allclose(out.detach().numpy(), [[3, 5], [-2, -1], [0, 0], [4, 0]])
+    out.backward(torch.tensor([[10., 20.], [30., 40.], [50., 60.], [70., 80.]]))
+    # ties (5, 5) and (-1, -1): the first node takes the gradient
+    np.testing.assert_allclose(h.grad.numpy(), [[0, 20], [10, 0], [30, 40], [0, 0], [70, 80]])
+    # without ties it is torch's scatter_reduce amax
+    hr = torch.randn(40, 8)
+    b = torch.sort(torch.randint(0, 6, (40,))).values
+    ref = torch.zeros(6, 8).scatter_reduce(0, b[:, None].expand(-1, 8), hr, "amax",
+                                           include_self=False)
+    np.testing.assert_allclose(global_max_pool(hr, b, 6).numpy(), ref.numpy())
 
 
 def test_ginet_forward_shapes_and_batch_independence():
