@@ -150,8 +150,13 @@ def main():
     else:
         from molclr_amd.gcn_molclr import GCN
         model = GCN(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"]).to(dev)
-    opt = FusedAdam(model.parameters(), 5e-4, weight_decay=1e-5)
+    # parameters in gradient-bucket order: the overlapped all-reduce's buckets
+    # are slices of the flat gradient buffer (DP only)
+    opt = FusedAdam(mdist.bucketed_parameters(model) if world > 1 else model.parameters(), 5e-4,
+                    weight_decay=1e-5)
     mdist.broadcast_params(opt.flat)
+    reducer = (mdist.OverlappedGradReducer(model, opt, torch.distributed.group.WORLD)
+               if world > 1 and not args.two_pass else None)
     group = torch.distributed.group.WORLD if world > 1 else None
     crit = NTXentLoss(dev, B * world, 0.1, True, group=group)
 
@@ -178,6 +183,8 @@ def main():
             g.__dict__.pop("_molclr_graph", None)
             g.__dict__.pop("_molclr_pair_graph", None)
         opt.zero_grad()
+        if reducer is not None:
+            reducer.arm()
         if args.two_pass:
             _, zi = model(xi)
             _, zj = model(xj)
@@ -186,7 +193,9 @@ def main():
             _, z = model.forward_pair(xi, xj)
             loss = crit.forward_pair(ops.l2_normalize(z))
         loss.backward()
-        if world > 1:
+        if reducer is not None:  # bucketed, overlapped with the encoder backward
+            reducer.finish()
+        elif world > 1:
             mdist.allreduce_grads(opt.flat_grad)
         opt.step()
         return loss

@@ -532,6 +532,13 @@ typedef struct molclr_gin_encoder_grads {
   float* edge_embedding2[MOLCLR_MAX_LAYERS];
   float* bn_weight[MOLCLR_MAX_LAYERS];
   float* bn_bias[MOLCLR_MAX_LAYERS];
+  /* Optional (NULL = none): hipEvent_t handles the backward records on its
+   * stream once layer l's parameter gradients (its Linear / GCN weights,
+   * edge tables and BatchNorm affine) are final, and once the atom-embedding
+   * gradients are: a data-parallel caller starts each layer's gradient
+   * all-reduce behind its event while the lower layers' backward runs. */
+  void* layer_done[MOLCLR_MAX_LAYERS];
+  void* embed_done;
 } molclr_gin_encoder_grads;
 
 /* The graph of one batch as molclr_graph_build produced it. */
@@ -604,6 +611,8 @@ typedef struct molclr_gcn_encoder_grads {
   float* edge_embedding2[MOLCLR_MAX_LAYERS];
   float* bn_weight[MOLCLR_MAX_LAYERS];
   float* bn_bias[MOLCLR_MAX_LAYERS];
+  void* layer_done[MOLCLR_MAX_LAYERS]; /* as in molclr_gin_encoder_grads */
+  void* embed_done;
 } molclr_gcn_encoder_grads;
 
 size_t molclr_gcn_encoder_arena_bytes(int num_layer, int64_t num_nodes, int64_t dim);

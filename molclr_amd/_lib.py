@@ -160,7 +160,8 @@ class GinEncoderGrads(ctypes.Structure):
     """struct molclr_gin_encoder_grads."""
     _fields_ = [("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
         (f, _L16) for f in ("mlp0_weight", "mlp0_bias", "mlp2_weight", "mlp2_bias",
-                            "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias")]
+                            "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias")] + [
+        ("layer_done", _L16), ("embed_done", c_void_p)]
 
 
 class GcnEncoder(ctypes.Structure):
@@ -177,7 +178,7 @@ class GcnEncoderGrads(ctypes.Structure):
     """struct molclr_gcn_encoder_grads."""
     _fields_ = [("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
         (f, _L16) for f in ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight",
-                            "bn_bias")]
+                            "bn_bias")] + [("layer_done", _L16), ("embed_done", c_void_p)]
 
 
 class DeviceGraphC(ctypes.Structure):

@@ -110,6 +110,15 @@ int graph_segments(const molclr_device_graph* g, const int64_t* N, SegRows& out)
     if (rc_) return rc_;      \
   } while (0)
 
+// the grads struct's optional "gradients final" events (layer_done / embed_done)
+int record_done(void* ev, molclr_stream_t stream) {
+  if (ev && hipEventRecord(static_cast<hipEvent_t>(ev), molclr::as_stream(stream)) != hipSuccess) {
+    molclr::set_error("encoder_bwd: hipEventRecord failed");
+    return MOLCLR_ERR_ARG;
+  }
+  return MOLCLR_OK;
+}
+
 }  // namespace
 
 MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, int dtype) {
@@ -283,6 +292,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                            g->ecount, (float*)dh, gr->edge_embedding1[l],
                                            gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));
     }
+    MOLCLR_TRY(record_done(gr->layer_done[l], stream));
     dy = dh;
   }
   if (gr->x_embedding1 || gr->x_embedding2) {
@@ -296,6 +306,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       MOLCLR_TRY(molclr_atom_embed_bwd(x, (const float*)dh, gr->x_embedding1, gr->x_embedding2, N,
                                        D, e->n_atom, e->n_chiral, 1, kws, kws_bytes, stream));
   }
+  MOLCLR_TRY(record_done(gr->embed_done, stream));
   return MOLCLR_OK;
 }
 
@@ -460,6 +471,7 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
     MOLCLR_TRY(molclr_gemm_f32_bplanes(dxw, e->weight_planes_t[l], dh, N, D, D, D, D, 0,
                                        MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
                                        stream));
+    MOLCLR_TRY(record_done(gr->layer_done[l], stream));
     dy = dh;
   }
   if (gr->x_embedding1 || gr->x_embedding2) {
@@ -468,5 +480,6 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
     MOLCLR_TRY(molclr_atom_embed_bwd(x, dh, gr->x_embedding1, gr->x_embedding2, N, D, e->n_atom,
                                      e->n_chiral, 1, kws, kws_bytes, stream));
   }
+  MOLCLR_TRY(record_done(gr->embed_done, stream));
   return MOLCLR_OK;
 }

@@ -9,9 +9,15 @@ two exchanges per step, both chosen for a point-to-point xGMI fabric:
    (gather_rows), and one of the per-row logsumexp (gather_lse).  Because the NT-Xent weight matrix
    W_rc = P_rc + P_cr - 2[c = p(r)] is symmetric, each rank then computes the
    exact gradient of its own rows locally: no column-gradient reduce-scatter.
-2. One SUM all-reduce of the flat gradient buffer (FusedAdam.flat_grad,
-   ~9.6 MB fp32 for GIN 5x300) — a single large collective instead of
-   per-parameter buckets, which is what a ring over 7 xGMI links wants.
+2. The SUM all-reduce of the flat gradient buffer (FusedAdam.flat_grad,
+   ~9.6 MB fp32 for GIN 5x300).  OverlappedGradReducer splits it into a few
+   large buckets in the order the backward finishes them -- projection heads,
+   encoder layers L-1 .. 0, atom embeddings (one ~1.9 MB bucket per GIN
+   layer, not per-parameter buckets: a ring over 7 xGMI links wants few,
+   large collectives) -- and starts each on a side stream as soon as the
+   encoder executor records that its gradients are final, so all but the
+   last bucket's reduction hides behind the remaining backward.
+   allreduce_grads is the single blocking collective (two-call steps).
 
 BatchNorm statistics stay per rank and per view (the reference computes
 them per forward call; like DDP without SyncBN), so an N-rank run is the
@@ -113,3 +119,118 @@ def max_over_ranks(value: float, device) -> float:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
     return value
+
+
+# ---------------------------------------------------------------------------
+# Bucketed, overlapped gradient all-reduce
+# ---------------------------------------------------------------------------
+def gradient_buckets(model) -> list[list[torch.nn.Parameter]]:
+    """The model's parameters grouped in the order the backward finalises
+    them: the projection heads (feat_lin, out_lin), then encoder layer
+    L-1 .. 0 (its convolution and BatchNorm), then the atom embeddings."""
+    named = dict(model.named_parameters())
+    L = model.num_layer
+    heads = [p for n, p in named.items() if n.startswith(("feat_lin.", "out_lin."))]
+    layers = [[p for n, p in named.items()
+               if n.startswith((f"gnns.{l}.", f"batch_norms.{l}."))] for l in range(L - 1, -1, -1)]
+    emb = [p for n, p in named.items() if n.startswith(("x_embedding1.", "x_embedding2."))]
+    buckets = [heads, *layers, emb]
+    if sum(len(b) for b in buckets) != len(named):
+        raise ValueError("gradient_buckets: parameters outside the head / layer / embedding groups")
+    return buckets
+
+
+def bucketed_parameters(model) -> list[torch.nn.Parameter]:
+    """Parameter order for FusedAdam that makes every gradient bucket one
+    contiguous slice of its flat gradient buffer (the update rule is
+    elementwise: the order changes nothing else)."""
+    return [p for b in gradient_buckets(model) for p in b]
+
+
+class OverlappedGradReducer:
+    """SUM all-reduce of FusedAdam.flat_grad in gradient_buckets order,
+    overlapped with the backward.
+
+    ``arm()`` before the backward installs it as molclr_amd.ops' gradient
+    hook: when the encoder's backward starts (the heads' gradients are
+    final) the heads bucket is reduced; the encoder executor records one
+    event per layer and one after the atom embeddings (molclr_*_encoder_grads
+    .layer_done / .embed_done), and each layer's bucket is reduced behind its
+    event on a side stream.  ``finish()`` makes the compute stream wait for
+    every bucket before the optimizer step.  One encoder backward per step
+    (the paired-view step); a second one would add to buckets already in
+    flight and is refused."""
+
+    def __init__(self, model, opt, group=None):
+        self.group = group
+        self.flat = opt.flat_grad
+        off = {id(p): (o, (n + 3) // 4 * 4) for p, o, n in opt.views}  # FusedAdam's 4-aligned slots
+        self.slices = []
+        for b in gradient_buckets(model):
+            spans = sorted(off[id(p)] for p in b)
+            for (o0, n0), (o1, _) in zip(spans, spans[1:]):
+                if o1 != o0 + n0:
+                    raise ValueError("OverlappedGradReducer: build FusedAdam over "
+                                     "bucketed_parameters(model)")
+            self.slices.append((spans[0][0], spans[-1][0] + spans[-1][1]))
+        self.num_layer = model.num_layer
+        self.cuda = self.flat.is_cuda
+        self.works, self.calls = [], 0
+        if self.cuda:
+            self.stream = torch.cuda.Stream(device=self.flat.device)
+            # the executor re-records these; a first record creates the handles
+            self.events = [torch.cuda.Event() for _ in range(self.num_layer + 1)]
+            for e in self.events:
+                e.record()
+
+    # -- step protocol --------------------------------------------------------
+    def arm(self):
+        from . import ops
+        self.works, self.calls = [], 0
+        ops.set_grad_hook(self)
+
+    def finish(self):
+        from . import ops
+        ops.set_grad_hook(None)
+        if self.calls == 0:  # no executor backward ran (per-op path): one collective
+            allreduce_grads(self.flat, self.group)
+            return
+        for w in self.works:
+            w.wait()  # the current stream waits for the bucket's collective
+        self.works = []
+
+    def _reduce(self, i, after=None):
+        lo, hi = self.slices[i]
+        view = self.flat[lo:hi]
+        if not self.cuda:
+            dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group)
+            return
+        with torch.cuda.stream(self.stream):
+            if after is not None:
+                self.stream.wait_event(after)
+            self.works.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
+                                              async_op=True))
+
+    # -- hooks called by molclr_amd.ops' encoder backward ----------------------
+    def encoder_backward_begin(self):
+        if self.calls:
+            raise RuntimeError("OverlappedGradReducer: one encoder backward per step (paired views)")
+        self.calls += 1
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._reduce(0, ev)
+        else:
+            self._reduce(0)
+
+    def layer_event_handles(self):
+        """[layer 0 .. L-1, embeddings] hipEvent_t handles for the executor."""
+        if not self.cuda:
+            return None
+        return [e.cuda_event for e in self.events]
+
+    def encoder_backward_enqueued(self):
+        L = self.num_layer
+        for k, l in enumerate(range(L - 1, -1, -1)):
+            self._reduce(1 + k, self.events[l] if self.cuda else None)
+        self._reduce(1 + L, self.events[L] if self.cuda else None)

@@ -117,10 +117,17 @@ class MolCLR(object):
 
     def build_optimizer(self, model):
         from .optim import FusedAdam
-        optimizer = FusedAdam(model.parameters(), self.config['init_lr'],
+        # data parallel: parameters in gradient-bucket order, so each bucket of
+        # the overlapped all-reduce is one slice of the flat gradient buffer
+        params = mdist.bucketed_parameters(model) if self.world > 1 else model.parameters()
+        optimizer = FusedAdam(params, self.config['init_lr'],
                               weight_decay=float(eval(str(self.config['weight_decay']))))
+        self.reducer = None
         if self.world > 1:
             mdist.broadcast_params(optimizer.flat)
+            if getattr(self, "paired", True) and hasattr(model, "forward_pair"):
+                self.reducer = mdist.OverlappedGradReducer(
+                    model, optimizer, torch.distributed.group.WORLD)
         scheduler = CosineAnnealingLR(optimizer, T_max=self.config['epochs'] - self.config['warm_up'],
                                       eta_min=0, last_epoch=-1)
         return optimizer, scheduler
@@ -129,9 +136,14 @@ class MolCLR(object):
         optimizer.zero_grad()
         xis = xis.to(self.device, non_blocking=True)
         xjs = xjs.to(self.device, non_blocking=True)
+        reducer = getattr(self, "reducer", None)
+        if reducer is not None:
+            reducer.arm()
         loss = self._step(model, xis, xjs, n_iter)
         loss.backward()
-        if self.world > 1:
+        if reducer is not None:
+            reducer.finish()
+        elif self.world > 1:
             mdist.allreduce_grads(optimizer.flat_grad)
         optimizer.step()
         return loss

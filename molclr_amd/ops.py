@@ -126,6 +126,32 @@ def set_kernel_timer(timer: KernelTimer | None) -> None:
     _TIMER = timer
 
 
+# Gradient-ready hook of the data-parallel reducer
+# (molclr_amd.distributed.OverlappedGradReducer): told when an encoder
+# backward starts, given per-layer events the executor records, and told when
+# the backward has been enqueued.
+_GRAD_HOOK = None
+
+
+def set_grad_hook(hook) -> None:
+    global _GRAD_HOOK
+    _GRAD_HOOK = hook
+
+
+def _grad_events(grads_struct, L, owned):
+    """Start the hook's heads bucket and fill the executor's done-events."""
+    hook = _GRAD_HOOK
+    if hook is None or not owned:
+        return None
+    hook.encoder_backward_begin()
+    ev = hook.layer_event_handles()
+    if ev is not None:
+        for l in range(L):
+            grads_struct.layer_done[l] = ev[l]
+        grads_struct.embed_done = ev[L]
+    return hook
+
+
 # ---------------------------------------------------------------------------
 # GEMM helpers
 # ---------------------------------------------------------------------------
@@ -818,9 +844,12 @@ class _GINEncoder(torch.autograd.Function):
         ws_bytes = _wsq("molclr_gin_encoder_workspace_bytes", L, N, D, dtype)
         ws = _ws(ws_bytes, dh.device)
         gc = ctx.graph.cstruct()
+        hook = _grad_events(gr, L, owned)
         _lib.call("molclr_gin_encoder_bwd", ctypes.addressof(ctx.enc), ctypes.addressof(gr),
                   ctx.x_idx.data_ptr(), ctypes.addressof(gc), dh.data_ptr(), ctx.arena.data_ptr(),
                   ctx.arena_bytes, ws.data_ptr(), ws_bytes, _stream(dh))
+        if hook is not None:
+            hook.encoder_backward_enqueued()
         if _TIMER is not None:
             for _ in range(L):
                 _TIMER.add("gemm_f32", 4 * 2.0 * N * D * (2 * D))
@@ -906,9 +935,12 @@ class _GCNEncoder(torch.autograd.Function):
         ws_bytes = _wsq("molclr_gcn_encoder_workspace_bytes", L, N, D)
         ws = _ws(ws_bytes, dh.device)
         gc = ctx.graph.cstruct()
+        hook = _grad_events(gr, L, owned)
         _lib.call("molclr_gcn_encoder_bwd", ctypes.addressof(ctx.enc), ctypes.addressof(gr),
                   ctx.x_idx.data_ptr(), ctypes.addressof(gc), dh.data_ptr(), ctx.arena.data_ptr(),
                   ctx.arena_bytes, ws.data_ptr(), ws_bytes, _stream(dh))
+        if hook is not None:
+            hook.encoder_backward_enqueued()
         if _TIMER is not None:
             for _ in range(L):
                 _TIMER.add("gemm_f32", 2 * 2.0 * N * D * D)

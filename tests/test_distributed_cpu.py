@@ -130,3 +130,82 @@ def test_sharded_ntxent_matches_single_process_reference():
     assert reshuffled                                 # a new permutation every epoch
     assert np.linalg.norm(dzi - a.grad.numpy()) <= 1e-5 * np.linalg.norm(a.grad.numpy())
     assert np.linalg.norm(dzj - b.grad.numpy()) <= 1e-5 * np.linalg.norm(b.grad.numpy())
+
+
+class _FlatLayout:
+    """FusedAdam's flat-buffer layout (4-aligned slots in parameter order)
+    without its GPU-only state: what OverlappedGradReducer reads."""
+
+    def __init__(self, params):
+        self.views, off = [], 0
+        for p in params:
+            self.views.append((p, off, p.numel()))
+            off += (p.numel() + 3) // 4 * 4
+        self.flat_grad = torch.zeros(off)
+
+
+def _reducer_worker(rank, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank))
+    from molclr_amd import distributed as mdist
+    from molclr_amd import ops
+    from molclr_amd.ginet_molclr import GINet
+    mdist.init(backend="gloo")
+    torch.manual_seed(0)
+    model = GINet(3, 16, 32)
+    names = {id(p): n for n, p in model.named_parameters()}
+    order = [[names[id(p)] for p in b] for b in mdist.gradient_buckets(model)]
+    layout = _FlatLayout(mdist.bucketed_parameters(model))
+    red = mdist.OverlappedGradReducer(model, layout, dist.group.WORLD)
+    n = layout.flat_grad.numel()
+    base = torch.arange(n, dtype=torch.float32)
+    # the protocol the encoder backward drives (ops._grad_events)
+    layout.flat_grad.copy_(base * (rank + 1))
+    red.arm()
+    assert ops._GRAD_HOOK is red
+    red.encoder_backward_begin()
+    try:
+        red.encoder_backward_begin()  # a second encoder backward in one step
+        second = "accepted"
+    except RuntimeError:
+        second = "refused"
+    red.encoder_backward_enqueued()
+    red.finish()
+    bucketed = layout.flat_grad.clone()
+    # no executor backward in the step: one collective over the whole buffer
+    layout.flat_grad.copy_(base * (rank + 1))
+    red.arm()
+    red.finish()
+    assert ops._GRAD_HOOK is None
+    out_q.put((rank, order, red.slices, n, bucketed.tolist(), layout.flat_grad.tolist(), second))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_overlapped_grad_reducer_buckets_and_sums():
+    """molclr_amd.distributed.OverlappedGradReducer under gloo, world 2: the
+    buckets follow the backward's completion order (heads, layer L-1 .. 0,
+    atom embeddings), tile the flat gradient buffer exactly as contiguous
+    disjoint slices, and the bucketed reduction equals one SUM all-reduce."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(WORLD)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, order, slices, n, bucketed, whole, second = res[0]
+    assert all(x.startswith(("feat_lin.", "out_lin.")) for x in order[0])
+    for k, l in enumerate((2, 1, 0)):
+        assert order[1 + k] and all(x.startswith((f"gnns.{l}.", f"batch_norms.{l}."))
+                                    for x in order[1 + k])
+    assert sorted(order[-1]) == ["x_embedding1.weight", "x_embedding2.weight"]
+    assert slices[0][0] == 0 and slices[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(slices, slices[1:]))  # contiguous, disjoint
+    expect = [3.0 * i for i in range(n)]  # SUM of ranks' (rank + 1) * arange
+    for r in res:
+        assert r[4] == expect and r[5] == expect
+        assert r[6] == "refused"
