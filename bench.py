@@ -76,10 +76,11 @@ def parse():
     p.add_argument("--two-pass", action="store_true",
                    help="run the two views as two encoder calls (the reference's molclr.py:57,60) "
                         "instead of one paired pass with per-view BatchNorm statistics")
-    p.add_argument("--augment", default="host", choices=("host", "device"),
+    p.add_argument("--augment", default="host", choices=("host", "device", "subgraph", "mix"),
                    help="host: pre-built resident batch pairs (default); device: both views "
                         "built inside every step by molclr_mask_views from a resident "
-                        "molecule store")
+                        "molecule store; subgraph / mix: the same with molclr_aug_views "
+                        "(dataset_subgraph.py / dataset_mix.py views)")
     return p.parse_args()
 
 
@@ -161,7 +162,7 @@ def main():
     crit = NTXentLoss(dev, B * world, 0.1, True, group=group)
 
     store = None
-    if args.augment == "device":
+    if args.augment != "host":
         # the un-augmented molecules of NB batches resident in HBM; every step
         # draws B of them and builds both views on the device
         from molclr_amd.augment import DeviceMoleculeStore
@@ -176,7 +177,11 @@ def main():
     def step(i):
         if store is not None:
             k = i % len(id_sets)
-            xi, xj = store.mask_views(id_sets_dev[k], seed=i, host_ids=id_sets[k])
+            if args.augment == "device":
+                xi, xj = store.mask_views(id_sets_dev[k], seed=i, host_ids=id_sets[k])
+            else:
+                xi, xj = store.aug_views(id_sets_dev[k], seed=i, mode=args.augment,
+                                         host_ids=id_sets[k])
         else:
             xi, xj = batches[i % len(batches)]
         for g in (xi, xj):  # rebuild the graph every step: it is part of the work
@@ -324,7 +329,9 @@ def main():
                        "views": ("two encoder calls (molclr.py:57,60)" if args.two_pass else
                                  "one paired encoder pass, per-view BatchNorm statistics"),
                        "augment": ("host: pre-built resident batch pairs" if store is None else
-                                   "device: molclr_mask_views inside the step")},
+                                   "device: molclr_mask_views inside the step"
+                                   if args.augment == "device" else
+                                   f"device: molclr_aug_views ({args.augment}) inside the step")},
             "final_loss": round(final_loss, 5),
             "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
             "roofline": roofline, "roofline_mfma": roofline_mfma,

@@ -155,6 +155,42 @@ int molclr_mask_views(const int64_t* store_x, const int64_t* store_atom_ptr,
                       int32_t* status, void* workspace, size_t workspace_bytes,
                       molclr_stream_t stream);
 
+/* On-device subgraph-removal views (dataset/dataset_subgraph.py:70-177,
+ * mode MOLCLR_AUG_SUBGRAPH) and mixed subgraph + atom/bond masking views
+ * (dataset/dataset_mix.py:46-217, mode MOLCLR_AUG_MIX) + collate, from the
+ * molclr_mask_views store.  Per molecule: the networkx BFS removal
+ * (removeSubgraph: from a random centre, floor(p x atoms-in-bonds) atoms,
+ * p = 0.25 or uniform [0, 0.2) in mix, the frontier in CPython set order)
+ * masks the removed atoms to [118, 0]; bonds survive as G_i.edges keeps them
+ * (mix: both atoms remain; subgraph: additionally (start, end) must be
+ * networkx's orientation); mix then masks max(0, floor(N/4) - removed) more
+ * atoms among the remaining and drops max(0, kept - ceil(3M/4)) surviving
+ * bonds.  Two calls because the edge count is data dependent:
+ *   plan: ptr_out [B+1] (atom offsets), *num_edges_out (device int64) =
+ *         the view's directed-edge count; the plan lives in the workspace;
+ *   write: the Batch fields (as molclr_mask_views) sized by that count.
+ * num_nodes = Σ atoms, num_bonds = Σ bonds of the batch's molecules.  status
+ * bits: 0 molecule id out of range, 1 num_nodes mismatch, 2 edge index out
+ * of its molecule (clamped), 3 the frontier emptied before the quota (the
+ * subgraph module would not terminate; dataset_mix.py:55-56's guard is
+ * applied), 4 a molecule over 256 atoms / 512 bonds (left un-augmented),
+ * 5 a centre atom without bonds (the reference raises). */
+enum { MOLCLR_AUG_SUBGRAPH = 0, MOLCLR_AUG_MIX = 1 };
+size_t molclr_aug_views_workspace_bytes(int64_t batch_size, int64_t num_nodes, int64_t num_bonds);
+int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
+                          const int64_t* store_bond_ptr, int64_t store_mols, int64_t store_edges,
+                          const int64_t* mol_ids, int64_t batch_size, uint64_t seed, int view,
+                          int mode, int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
+                          int64_t* num_edges_out, int32_t* status, void* workspace,
+                          size_t workspace_bytes, molclr_stream_t stream);
+int molclr_aug_views_write(const int64_t* store_x, const int64_t* store_atom_ptr,
+                           const int64_t* store_edge_index, const int64_t* store_edge_attr,
+                           const int64_t* store_bond_ptr, int64_t store_mols, int64_t store_edges,
+                           const int64_t* mol_ids, int64_t batch_size, const int64_t* ptr,
+                           int64_t num_nodes, int64_t num_bonds, int64_t num_edges, int64_t* x_out,
+                           int64_t* edge_index_out, int64_t* edge_attr_out, int64_t* batch_out,
+                           const void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
 /* Atom embedding: h[i] = X1[x[i,0]] + X2[x[i,1]]  (ginet_molclr.py:103).
  * x int64 [N,2]; X1 [n1,D], X2 [n2,D]; h [N,D] f32.  Indices are clamped. */
 int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,

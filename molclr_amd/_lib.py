@@ -106,6 +106,11 @@ SIGNATURES = {
     "molclr_gcn_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
     "molclr_gcn_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
     "molclr_gcn_encoder_bwd": (c_int, [_P, _P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),
+    "molclr_aug_views_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_aug_views_plan": (c_int, [_P, _P, _P, _I64, _I64, _P, _I64, ctypes.c_uint64, c_int,
+                                      c_int, _I64, _I64, _P, _P, _P, _P, c_size_t, _P]),
+    "molclr_aug_views_write": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I64,
+                                       _I64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "molclr_atom_embed_fwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
     "molclr_atom_embed_bwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P,
                                            c_size_t, _P]),
@@ -139,6 +144,7 @@ DTYPE_F32, DTYPE_BF16 = 0, 1
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
 KTIMER_NTXENT = 4
+AUG_SUBGRAPH, AUG_MIX = 0, 1
 
 
 _L16 = c_void_p * 16

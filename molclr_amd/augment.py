@@ -14,6 +14,12 @@ Subsets follow the reference's sizes (max(1, floor(N/4)) atoms, floor(M/4)
 bonds) and are uniform; they are drawn from a counter-based hash of
 (seed, view, molecule id, item) instead of Python's unseeded ``random``, so
 a (seed, batch) pair always gives the same views.
+
+``aug_views(..., mode="subgraph" | "mix")`` builds the other two augmentation
+modules' views the same way (dataset/dataset_subgraph.py,
+dataset/dataset_mix.py; molclr_aug_views_plan / _write): the BFS subgraph
+removal runs on the device, and the only host work is reading the view's edge
+count between the two calls.
 """
 from __future__ import annotations
 
@@ -128,3 +134,62 @@ class DeviceMoleculeStore:
         ``MoleculeDataset.__getitem__`` returns, collated (dataset.py:147)."""
         return (self.mask_view(mol_ids, seed, 0, check, host_ids),
                 self.mask_view(mol_ids, seed, 1, check, host_ids))
+
+    AUG_MODES = {"subgraph": _lib.AUG_SUBGRAPH, "mix": _lib.AUG_MIX}
+
+    def aug_view(self, mol_ids, seed: int, view: int, mode: str = "subgraph",
+                 check: bool = False, host_ids=None) -> Batch:
+        """One collated subgraph-removal (dataset_subgraph.py) or mixed
+        (dataset_mix.py) view of the molecules ``mol_ids``."""
+        if mode not in self.AUG_MODES:
+            raise ValueError(f"augmentation mode {mode!r}: subgraph or mix")
+        on_dev = isinstance(mol_ids, torch.Tensor) and mol_ids.device == self.device
+        if host_ids is None:
+            host_ids = torch.as_tensor(mol_ids).cpu()
+        ids_h = np.asarray(host_ids, dtype=np.int64)
+        if ids_h.size and (ids_h.min() < 0 or ids_h.max() >= self.num_molecules):
+            raise IndexError("molecule id out of range")
+        B = int(ids_h.shape[0])
+        N = int(self.num_atoms[ids_h].sum())
+        Mb = int(self.num_bonds[ids_h].sum())
+        dev = self.device
+        i64 = dict(dtype=torch.int64, device=dev)
+        ids = (mol_ids.to(torch.int64).contiguous() if on_dev
+               else torch.as_tensor(ids_h).to(dev, non_blocking=True))
+        ptr = torch.empty(B + 1, **i64)
+        ne = torch.empty(1, **i64)
+        status = torch.empty(1, dtype=torch.int32, device=dev)
+        ws_bytes = _lib.query("molclr_aug_views_workspace_bytes", B, N, Mb)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        st = _lib.stream_of(dev)
+        E_store = int(self.edge_index.shape[1])
+        _lib.call("molclr_aug_views_plan", self.atom_ptr.data_ptr(), self.edge_index.data_ptr(),
+                  self.bond_ptr.data_ptr(), self.num_molecules, E_store, ids.data_ptr(), B,
+                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(view), self.AUG_MODES[mode], N, Mb,
+                  ptr.data_ptr(), ne.data_ptr(), status.data_ptr(), ws.data_ptr(), ws_bytes, st)
+        E = int(ne.item())  # the data-dependent edge count sizes the outputs
+        x = torch.empty(N, 2, **i64)
+        ei = torch.empty(2, E, **i64)
+        ea = torch.empty(E, 2, **i64)
+        batch = torch.empty(N, **i64)
+        _lib.call("molclr_aug_views_write", self.x.data_ptr(), self.atom_ptr.data_ptr(),
+                  self.edge_index.data_ptr(), self.edge_attr.data_ptr(), self.bond_ptr.data_ptr(),
+                  self.num_molecules, E_store, ids.data_ptr(), B, ptr.data_ptr(), N, Mb, E,
+                  x.data_ptr(), ei.data_ptr(), ea.data_ptr(), batch.data_ptr(), ws.data_ptr(),
+                  ws_bytes, st)
+        if check:
+            sv = int(status.item())
+            if sv & 0b10111:
+                raise ValueError(f"aug_views: invalid store, sizes or molecule (status {sv})")
+        b = Batch(x=x, edge_index=ei, edge_attr=ea, batch=batch)
+        b.ptr = ptr
+        b._num_graphs = B
+        b.status = status
+        return b
+
+    def aug_views(self, mol_ids, seed: int, mode: str = "subgraph", check: bool = False,
+                  host_ids=None) -> tuple[Batch, Batch]:
+        """(Batch_i, Batch_j) of dataset_subgraph.py / dataset_mix.py's
+        __getitem__ (two distinct centres per molecule), collated."""
+        return (self.aug_view(mol_ids, seed, 0, mode, check, host_ids),
+                self.aug_view(mol_ids, seed, 1, mode, check, host_ids))

@@ -182,6 +182,438 @@ __global__ __launch_bounds__(64 * kMolsPerBlock) void k_mask_views(
   if (bad) atomicOr(status, bad);
 }
 
+// ---------------------------------------------------------------------------
+// Subgraph-removal views (dataset/dataset_subgraph.py:70-177) and the mixed
+// subgraph + atom / bond masking views (dataset/dataset_mix.py:46-217).
+//
+// Per molecule the reference builds a networkx graph from the bonds
+// (nx.Graph(edges): nodes in order of first appearance in the bond list,
+// each node's neighbours in bond order; the Graph.copy() inside the removal
+// then lists a node's earlier-in-node-order neighbours first, in node order,
+// and the later ones in bond order), removes a BFS "subgraph" from a
+// random centre (removeSubgraph / remove_subgraph), masks the removed atoms
+// to [118, 0] and keeps the bonds that survive in G_i.edges.  One wave per
+// molecule restates that loop with lane 0 in LDS:
+//   temp = [centre]; while len(removed) < num:
+//     (mix's guard, applied in both modes: stop when temp is empty -- the
+//      subgraph module would loop forever; flagged in status bit 3)
+//     neighbors = [i for n in temp for i in G.neighbors(n) if i not in temp]
+//     remove the temp nodes in order until num are removed
+//     temp = list(set(neighbors))
+// The frontier's order is CPython's set iteration order, which decides which
+// atoms go when `num` runs out inside a frontier, so the set is emulated
+// exactly: open addressing over 8 << k slots, key = hash = the atom index,
+// ten consecutive slots probed from i while i + 9 <= mask, then
+// i = 5 i + 1 + (perturb >>= 5); growth to the next power of two above
+// 4 x used when fill x 5 >= mask x 3, re-inserting in old-slot order; the
+// list is the slot order (CPython 3.x setobject.c; oracle/augment_ref.py
+// uses Python's own set).
+// Bond survival: mix keeps a bond whose two atoms remain; the subgraph module
+// tests only `(start, end) in G_i.edges`, and networkx reports an edge from
+// the endpoint that comes first in node order, so a surviving bond whose end
+// atom appeared in the bond list before its start atom is dropped there too.
+// Random draws (the reference: Python's unseeded random; here splitmix64
+// streams, restated in oracle/augment_ref.py): the two views' centres are the
+// atoms with the smallest / second smallest key of one molecule stream
+// (random.sample(range(N), 2): distinct); mix's percent is 0.2 u with u the
+// top 53 bits of a per-view key; mix's extra atom / bond masks are the
+// k-smallest-key subsets of the remaining atoms / surviving bonds.
+// ---------------------------------------------------------------------------
+constexpr int kAugMaxAtoms = 256;  // per molecule (LDS tables); larger: status bit 4
+constexpr int kAugMaxBonds = 512;
+constexpr int kSetSlots = 2048;    // the emulated set never exceeds this for <= 256 keys
+
+struct AugLds {
+  int16_t adj_off[kAugMaxAtoms + 1];
+  int16_t adj[2 * kAugMaxBonds];
+  int16_t first[kAugMaxAtoms];   // position in nx node order, -1: not in the bond graph
+  uint8_t removed[kAugMaxAtoms];
+  uint8_t in_temp[kAugMaxAtoms];
+  int16_t temp[kAugMaxAtoms];
+  int16_t nbr[2 * kAugMaxBonds];
+  int16_t table[kSetSlots];
+  int16_t fill_cursor[kAugMaxAtoms];
+};
+
+// CPython set(list) of non-negative ints: iteration order into out, returns
+// its length.  `scratch` holds the old keys during a resize (it may be `out`:
+// out is written only at the end).
+__device__ int pyset_order(const int16_t* items, int n_items, int16_t* table, int16_t* out,
+                           int16_t* scratch) {
+  int mask = 7, fill = 0;
+  for (int t = 0; t <= mask; ++t) table[t] = -1;
+  auto insert_clean = [&](int k) {
+    uint32_t i = (uint32_t)k & mask, perturb = (uint32_t)k;
+    while (true) {
+      if (table[i] < 0) {
+        table[i] = (int16_t)k;
+        return;
+      }
+      if (i + 9 <= (uint32_t)mask)
+        for (uint32_t j = i + 1; j <= i + 9; ++j)
+          if (table[j] < 0) {
+            table[j] = (int16_t)k;
+            return;
+          }
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+  };
+  for (int q = 0; q < n_items; ++q) {
+    const int k = items[q];
+    uint32_t i = (uint32_t)k & mask, perturb = (uint32_t)k;
+    bool inserted = false;
+    for (;;) {
+      const uint32_t last = (i + 9 <= (uint32_t)mask) ? i + 9 : i;
+      bool done = false;
+      for (uint32_t j = i; j <= last; ++j) {
+        if (table[j] < 0) {
+          table[j] = (int16_t)k;
+          inserted = done = true;
+          break;
+        }
+        if (table[j] == k) {
+          done = true;
+          break;
+        }
+      }
+      if (done) break;
+      perturb >>= 5;
+      i = (i * 5 + 1 + perturb) & mask;
+    }
+    if (inserted && ++fill * 5 >= mask * 3) {
+      int old = 0;
+      for (int t = 0; t <= mask; ++t)
+        if (table[t] >= 0) scratch[old++] = table[t];
+      int newsize = 8;
+      while (newsize <= fill * 4) newsize <<= 1;
+      mask = newsize - 1;
+      for (int t = 0; t <= mask; ++t) table[t] = -1;
+      for (int t = 0; t < old; ++t) insert_clean(scratch[t]);
+    }
+  }
+  int n = 0;
+  for (int t = 0; t <= mask; ++t)
+    if (table[t] >= 0) out[n++] = table[t];
+  return n;
+}
+
+// pass 1: per batch slot atom and bond offsets (ptr_out, bond_off), sizes
+// checked against the caps
+__global__ void k_aug_offsets(const int64_t* __restrict__ atom_ptr,
+                              const int64_t* __restrict__ bond_ptr,
+                              const int64_t* __restrict__ mol_ids, int64_t B, int64_t G,
+                              int64_t* __restrict__ ptr_out, int64_t* __restrict__ bond_off,
+                              int64_t num_nodes, int32_t* __restrict__ status) {
+  __shared__ int64_t sa[1024], se[1024];
+  __shared__ int64_t carry_a, carry_e;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    carry_a = 0;
+    carry_e = 0;
+    *status = 0;
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int64_t base = 0; base < B; base += 1024) {
+    const int64_t b = base + t;
+    int64_t n = 0, m = 0;
+    if (b < B) {
+      const int64_t id = mol_ids[b];
+      if (id < 0 || id >= G) {
+        bad |= 1;
+      } else {
+        n = atom_ptr[id + 1] - atom_ptr[id];
+        m = bond_ptr[id + 1] - bond_ptr[id];
+        if (n > kAugMaxAtoms || m > kAugMaxBonds) bad |= 16;
+      }
+    }
+    sa[t] = n;
+    se[t] = m;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int64_t va = t >= off ? sa[t - off] : 0;
+      const int64_t ve = t >= off ? se[t - off] : 0;
+      __syncthreads();
+      sa[t] += va;
+      se[t] += ve;
+      __syncthreads();
+    }
+    if (b < B) {
+      ptr_out[b] = carry_a + sa[t] - n;
+      bond_off[b] = carry_e + se[t] - m;
+    }
+    __syncthreads();
+    if (t == 1023) {
+      carry_a += sa[t];
+      carry_e += se[t];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    ptr_out[B] = carry_a;
+    bond_off[B] = carry_e;
+    if (carry_a != num_nodes) bad |= 2;
+  }
+  if (bad) atomicOr(status, bad);
+}
+
+// pass 2: one wave per molecule (lane 0 runs the reference loop in LDS):
+// drop[atom] = masked to [118, 0], keep[bond] = the bond survives, cnt[b] =
+// surviving bonds.  mode 0: dataset_subgraph (25 %), 1: dataset_mix.
+__global__ __launch_bounds__(64) void k_aug_plan(
+    const int64_t* __restrict__ atom_ptr, const int64_t* __restrict__ sei,
+    const int64_t* __restrict__ bond_ptr, int64_t store_edges, const int64_t* __restrict__ mol_ids,
+    int64_t B, int64_t G, uint64_t seed, int view, int mode, const int64_t* __restrict__ ptr,
+    const int64_t* __restrict__ bond_off, uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
+    int64_t* __restrict__ cnt, int32_t* __restrict__ status) {
+  __shared__ AugLds L;
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t id = mol_ids[b];
+  if (id < 0 || id >= G) return;  // flagged by k_aug_offsets
+  const int64_t a0 = atom_ptr[id], n = atom_ptr[id + 1] - a0;
+  const int64_t m0 = bond_ptr[id], M = bond_ptr[id + 1] - m0;
+  const int64_t aoff = ptr[b], boff = bond_off[b];
+  if (n > kAugMaxAtoms || M > kAugMaxBonds) {  // flagged; the molecule passes unchanged
+    for (int64_t i = lane; i < n; i += 64) drop[aoff + i] = 0;
+    for (int64_t m = lane; m < M; m += 64) keep[boff + m] = 1;
+    if (lane == 0) cnt[b] = M;
+    return;
+  }
+  if (lane != 0) return;
+  int bad = 0;
+  // bond endpoints (molecule-local, clamped), nx node order, adjacency in bond order
+  auto ends = [&](int64_t m, int& s, int& e) {
+    int64_t u = sei[2 * (m0 + m)], v = sei[store_edges + 2 * (m0 + m)];
+    if (u < 0 || u >= n || v < 0 || v >= n) {
+      bad |= 4;
+      u = u < 0 ? 0 : (u >= n ? n - 1 : u);
+      v = v < 0 ? 0 : (v >= n ? n - 1 : v);
+    }
+    s = (int)u;
+    e = (int)v;
+  };
+  for (int i = 0; i < n; ++i) {
+    L.first[i] = -1;
+    L.removed[i] = 0;
+    L.in_temp[i] = 0;
+    L.adj_off[i] = 0;
+  }
+  L.adj_off[n] = 0;
+  int nodes = 0;
+  for (int64_t m = 0; m < M; ++m) {
+    int s, e;
+    ends(m, s, e);
+    if (L.first[s] < 0) L.first[s] = (int16_t)nodes++;
+    if (L.first[e] < 0) L.first[e] = (int16_t)nodes++;
+    ++L.adj_off[s + 1];
+    if (e != s) ++L.adj_off[e + 1];
+  }
+  for (int i = 0; i < n; ++i) {
+    L.adj_off[i + 1] += L.adj_off[i];
+    L.fill_cursor[i] = L.adj_off[i];
+  }
+  // neighbours in bond order; a repeated bond adds no second entry (nx.Graph)
+  for (int64_t m = 0; m < M; ++m) {
+    int s, e;
+    ends(m, s, e);
+    bool dup = false;
+    for (int q = L.adj_off[s]; q < L.fill_cursor[s]; ++q) dup |= L.adj[q] == e;
+    if (dup) continue;
+    L.adj[L.fill_cursor[s]++] = (int16_t)e;
+    if (e != s) L.adj[L.fill_cursor[e]++] = (int16_t)s;
+  }
+  // Graph.copy() reorders every neighbour list: the neighbours earlier in node
+  // order first (in node order), then the later ones in bond order
+  for (int w = 0; w < n; ++w) {
+    const int a = L.adj_off[w], d = L.fill_cursor[w] - a;
+    int k = 0;
+    for (int q = 0; q < d; ++q)  // earlier neighbours, insertion-sorted by node order
+      if (L.first[L.adj[a + q]] < L.first[w]) {
+        int p = k++;
+        while (p > 0 && L.first[L.nbr[p - 1]] > L.first[L.adj[a + q]]) {
+          L.nbr[p] = L.nbr[p - 1];
+          --p;
+        }
+        L.nbr[p] = L.adj[a + q];
+      }
+    for (int q = 0; q < d; ++q)
+      if (L.first[L.adj[a + q]] > L.first[w]) L.nbr[k++] = L.adj[a + q];
+    for (int q = 0; q < k; ++q) L.adj[a + q] = L.nbr[q];
+    L.fill_cursor[w] = (int16_t)(a + k);  // a self-loop drops out of the walk
+  }
+  // centres: smallest / second smallest key of the molecule's centre stream
+  int centre = 0;
+  if (n >= 2) {
+    const uint64_t cs = subset_stream(seed, 2, 2, id);
+    int c0 = -1, c1 = -1;
+    uint64_t k0 = 0, k1 = 0;
+    for (int i = 0; i < n; ++i) {
+      const uint64_t k = item_key(cs, i);
+      if (c0 < 0 || k < k0) {
+        c1 = c0;
+        k1 = k0;
+        c0 = i;
+        k0 = k;
+      } else if (c1 < 0 || k < k1) {
+        c1 = i;
+        k1 = k;
+      }
+    }
+    centre = view == 0 ? c0 : c1;
+  }
+  double pct = 0.25;
+  if (mode == 1) {
+    const uint64_t u = splitmix64(subset_stream(seed, view, 3, id));
+    pct = 0.2 * ((double)(u >> 11) * 0x1.0p-53);
+  }
+  const int num = (int)floor((double)nodes * pct);
+  int nrem = 0, nt = 1;
+  L.temp[0] = (int16_t)centre;
+  if (num > 0 && L.first[centre] < 0) bad |= 32;  // the reference raises (centre not in G)
+  while (nrem < num) {
+    if (nt < 1) {  // dataset_mix.py:55-56; dataset_subgraph.py would not terminate
+      bad |= 8;
+      break;
+    }
+    for (int q = 0; q < nt; ++q) L.in_temp[L.temp[q]] = 1;
+    int nn = 0;
+    for (int q = 0; q < nt; ++q) {
+      const int u = L.temp[q];
+      for (int a = L.adj_off[u]; a < L.fill_cursor[u]; ++a) {
+        const int v = L.adj[a];
+        if (!L.removed[v] && !L.in_temp[v]) L.nbr[nn++] = (int16_t)v;
+      }
+    }
+    for (int q = 0; q < nt; ++q) {
+      if (nrem < num) {
+        L.removed[L.temp[q]] = 1;
+        ++nrem;
+      } else {
+        break;
+      }
+    }
+    for (int q = 0; q < nt; ++q) L.in_temp[L.temp[q]] = 0;
+    nt = pyset_order(L.nbr, nn, L.table, L.temp, L.temp);  // temp is free here: scratch, then out
+  }
+  // bonds surviving the removal
+  int64_t kept = 0;
+  for (int64_t m = 0; m < M; ++m) {
+    int s, e;
+    ends(m, s, e);
+    bool k = !L.removed[s] && !L.removed[e];
+    if (mode == 0) k = k && L.first[s] <= L.first[e];  // (start, end) in G_i.edges
+    keep[boff + m] = k ? 1 : 0;
+    kept += k ? 1 : 0;
+  }
+  for (int i = 0; i < n; ++i) drop[aoff + i] = L.removed[i];
+  if (mode == 1) {
+    // extra atom masks among the remaining atoms, extra bond masks among the
+    // surviving bonds (dataset_mix.py:174-181)
+    const int64_t ka = n / 4 - nrem > 0 ? n / 4 - nrem : 0;
+    const int64_t kb0 = kept - (3 * M + 3) / 4;
+    const int64_t kb = kb0 > 0 ? kb0 : 0;
+    const uint64_t as = subset_stream(seed, view, 4, id), bs = subset_stream(seed, view, 5, id);
+    const int64_t nremain = n - nrem;
+    int64_t pos = 0;
+    for (int i = 0; i < n; ++i) {
+      if (L.removed[i]) continue;
+      if (chosen(as, nremain, ka, pos)) drop[aoff + i] = 1;
+      ++pos;
+    }
+    pos = 0;
+    int64_t kept2 = 0;
+    for (int64_t m = 0; m < M; ++m) {
+      if (!keep[boff + m]) continue;
+      if (chosen(bs, kept, kb, pos)) keep[boff + m] = 0;
+      else ++kept2;
+      ++pos;
+    }
+    kept = kept2;
+  }
+  cnt[b] = kept;
+  if (bad) atomicOr(status, bad);
+}
+
+// exclusive scan of the surviving-bond counts into edge offsets (2 per bond)
+__global__ void k_aug_edge_offsets(const int64_t* __restrict__ cnt, int64_t B,
+                                   int64_t* __restrict__ edge_off) {
+  __shared__ int64_t se[1024];
+  __shared__ int64_t carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < B; base += 1024) {
+    const int64_t b = base + t;
+    const int64_t e = b < B ? 2 * cnt[b] : 0;
+    se[t] = e;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const int64_t v = t >= off ? se[t - off] : 0;
+      __syncthreads();
+      se[t] += v;
+      __syncthreads();
+    }
+    if (b < B) edge_off[b] = carry + se[t] - e;
+    __syncthreads();
+    if (t == 1023) carry += se[t];
+    __syncthreads();
+  }
+  if (t == 0) edge_off[B] = carry;
+}
+
+// pass 3: the collated Batch fields of the planned view
+__global__ __launch_bounds__(64 * kMolsPerBlock) void k_aug_write(
+    const int64_t* __restrict__ sx, const int64_t* __restrict__ atom_ptr,
+    const int64_t* __restrict__ sei, const int64_t* __restrict__ sea,
+    const int64_t* __restrict__ bond_ptr, int64_t store_edges, const int64_t* __restrict__ mol_ids,
+    int64_t B, int64_t G, const int64_t* __restrict__ ptr, const int64_t* __restrict__ bond_off,
+    const int64_t* __restrict__ edge_off, const uint8_t* __restrict__ drop,
+    const uint8_t* __restrict__ keep, int64_t* __restrict__ x_out, int64_t* __restrict__ ei_out,
+    int64_t* __restrict__ ea_out, int64_t* __restrict__ batch_out, int64_t num_nodes,
+    int64_t num_edges) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kMolsPerBlock + (threadIdx.x >> 6);
+  if (b >= B) return;  // wave-uniform
+  const int64_t id = mol_ids[b];
+  if (id < 0 || id >= G) return;
+  const int64_t a0 = atom_ptr[id], n = atom_ptr[id + 1] - a0;
+  const int64_t m0 = bond_ptr[id], M = bond_ptr[id + 1] - m0;
+  const int64_t aoff = ptr[b], boff = bond_off[b], eoff = edge_off[b];
+  if (aoff + n > num_nodes || edge_off[b + 1] > num_edges) return;
+  for (int64_t i = lane; i < n; i += 64) {
+    const bool masked = drop[aoff + i] != 0;
+    const int64_t o = aoff + i;
+    const int64_t* src = sx + 2 * (a0 + i);
+    x_out[2 * o] = masked ? 118 : src[0];
+    x_out[2 * o + 1] = masked ? 0 : src[1];
+    batch_out[o] = b;
+  }
+  int64_t kept_before = 0;
+  for (int64_t base = 0; base < M; base += 64) {
+    const int64_t m = base + lane;
+    const bool k = m < M && keep[boff + m];
+    const uint64_t bal = __ballot(k);
+    if (k) {
+      const int64_t p = kept_before + __popcll(bal & ((1ull << lane) - 1ull));
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int64_t se = 2 * (m0 + m) + d;
+        const int64_t oe = eoff + 2 * p + d;
+        int64_t s = sei[se], t = sei[store_edges + se];
+        s = s < 0 ? 0 : (s >= n ? n - 1 : s);
+        t = t < 0 ? 0 : (t >= n ? n - 1 : t);
+        ei_out[oe] = s + aoff;
+        ei_out[num_edges + oe] = t + aoff;
+        ea_out[2 * oe] = sea[2 * se];
+        ea_out[2 * oe + 1] = sea[2 * se + 1];
+      }
+    }
+    kept_before += __popcll(bal);
+  }
+}
+
 }  // namespace
 
 MOLCLR_API size_t molclr_mask_views_workspace_bytes(int64_t batch_size) {
@@ -221,6 +653,103 @@ MOLCLR_API int molclr_mask_views(const int64_t* store_x, const int64_t* store_at
                        store_mols, seed, view, static_cast<const int64_t*>(ptr_out),
                        static_cast<const int64_t*>(edge_off), x_out, edge_index_out,
                        edge_attr_out, batch_out, num_nodes, num_edges, status);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+// ---- subgraph / mix views ----------------------------------------------------
+namespace {
+struct AugWs {
+  int64_t *bond_off, *cnt, *edge_off;
+  uint8_t *drop, *keep;
+};
+AugWs aug_ws(void* w, size_t bytes, int64_t B, int64_t num_nodes, int64_t num_bonds) {
+  molclr::Workspace ws(w, bytes);
+  AugWs a;
+  a.bond_off = ws.take<int64_t>(B + 1);
+  a.cnt = ws.take<int64_t>(B > 0 ? B : 1);
+  a.edge_off = ws.take<int64_t>(B + 1);
+  a.drop = ws.take<uint8_t>(num_nodes > 0 ? num_nodes : 1);
+  a.keep = ws.take<uint8_t>(num_bonds > 0 ? num_bonds : 1);
+  return a;
+}
+}  // namespace
+
+MOLCLR_API size_t molclr_aug_views_workspace_bytes(int64_t batch_size, int64_t num_nodes,
+                                                   int64_t num_bonds) {
+  return (size_t)(3 * batch_size + 3) * sizeof(int64_t) + (size_t)num_nodes + (size_t)num_bonds +
+         6 * 256;
+}
+
+MOLCLR_API int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
+                                     const int64_t* store_bond_ptr, int64_t store_mols,
+                                     int64_t store_edges, const int64_t* mol_ids,
+                                     int64_t batch_size, uint64_t seed, int view, int mode,
+                                     int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
+                                     int64_t* num_edges_out, int32_t* status, void* workspace,
+                                     size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(batch_size >= 0 && store_mols >= 0 && store_edges >= 0 && num_nodes >= 0 &&
+                     num_bonds >= 0,
+                 "aug_views_plan: negative size");
+  MOLCLR_REQUIRE(view == 0 || view == 1, "aug_views_plan: view must be 0 or 1");
+  MOLCLR_REQUIRE(mode == MOLCLR_AUG_SUBGRAPH || mode == MOLCLR_AUG_MIX,
+                 "aug_views_plan: mode %d (0 subgraph, 1 mix)", mode);
+  MOLCLR_REQUIRE(ptr_out && num_edges_out && status, "aug_views_plan: null pointer");
+  MOLCLR_REQUIRE(batch_size == 0 || (store_atom_ptr && store_bond_ptr && mol_ids &&
+                                     (store_edges == 0 || store_edge_index)),
+                 "aug_views_plan: null pointer");
+  MOLCLR_REQUIRE(batch_size <= (1ll << 31), "aug_views_plan: batch too large");
+  MOLCLR_REQUIRE_WS(workspace_bytes,
+                    molclr_aug_views_workspace_bytes(batch_size, num_nodes, num_bonds));
+  hipStream_t s = molclr::as_stream(stream);
+  const AugWs a = aug_ws(workspace, workspace_bytes, batch_size, num_nodes, num_bonds);
+  hipLaunchKernelGGL(k_aug_offsets, dim3(1), dim3(1024), 0, s, store_atom_ptr, store_bond_ptr,
+                     mol_ids, batch_size, store_mols, ptr_out, a.bond_off, num_nodes, status);
+  if (batch_size > 0)
+    hipLaunchKernelGGL(k_aug_plan, dim3((unsigned)batch_size), dim3(64), 0, s, store_atom_ptr,
+                       store_edge_index, store_bond_ptr, store_edges, mol_ids, batch_size,
+                       store_mols, seed, view, mode, static_cast<const int64_t*>(ptr_out),
+                       static_cast<const int64_t*>(a.bond_off), a.drop, a.keep, a.cnt, status);
+  hipLaunchKernelGGL(k_aug_edge_offsets, dim3(1), dim3(1024), 0, s,
+                     static_cast<const int64_t*>(a.cnt), batch_size, a.edge_off);
+  if (hipMemcpyAsync(num_edges_out, a.edge_off + batch_size, sizeof(int64_t),
+                     hipMemcpyDeviceToDevice, s) != hipSuccess) {
+    molclr::set_error("aug_views_plan: copy failed");
+    return MOLCLR_ERR_ARG;
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_aug_views_write(const int64_t* store_x, const int64_t* store_atom_ptr,
+                                      const int64_t* store_edge_index,
+                                      const int64_t* store_edge_attr, const int64_t* store_bond_ptr,
+                                      int64_t store_mols, int64_t store_edges,
+                                      const int64_t* mol_ids, int64_t batch_size,
+                                      const int64_t* ptr, int64_t num_nodes, int64_t num_bonds,
+                                      int64_t num_edges, int64_t* x_out, int64_t* edge_index_out,
+                                      int64_t* edge_attr_out, int64_t* batch_out,
+                                      const void* workspace, size_t workspace_bytes,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(batch_size >= 0 && num_nodes >= 0 && num_edges >= 0, "aug_views_write: bad size");
+  MOLCLR_REQUIRE(num_nodes == 0 || (store_x && x_out && batch_out), "aug_views_write: null pointer");
+  MOLCLR_REQUIRE(num_edges == 0 || (store_edge_index && store_edge_attr && edge_index_out &&
+                                    edge_attr_out),
+                 "aug_views_write: null pointer");
+  MOLCLR_REQUIRE(batch_size == 0 || (store_atom_ptr && store_bond_ptr && mol_ids && ptr),
+                 "aug_views_write: null pointer");
+  MOLCLR_REQUIRE_WS(workspace_bytes,
+                    molclr_aug_views_workspace_bytes(batch_size, num_nodes, num_bonds));
+  if (batch_size == 0) return MOLCLR_OK;
+  const AugWs a = aug_ws(const_cast<void*>(workspace), workspace_bytes, batch_size, num_nodes,
+                         num_bonds);
+  hipLaunchKernelGGL(k_aug_write, dim3((unsigned)molclr::ceil_div(batch_size, kMolsPerBlock)),
+                     dim3(64 * kMolsPerBlock), 0, molclr::as_stream(stream), store_x,
+                     store_atom_ptr, store_edge_index, store_edge_attr, store_bond_ptr, store_edges,
+                     mol_ids, batch_size, store_mols, ptr, static_cast<const int64_t*>(a.bond_off),
+                     static_cast<const int64_t*>(a.edge_off), static_cast<const uint8_t*>(a.drop),
+                     static_cast<const uint8_t*>(a.keep), x_out, edge_index_out, edge_attr_out,
+                     batch_out, num_nodes, num_edges);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -111,3 +111,138 @@ def test_streams_do_not_alias_across_seed_view_kind():
     n, k = 40, 10
     for s in range(32):
         assert not np.array_equal(chosen_items(s, 1, 0, 3, n, k), chosen_items(s ^ 2, 0, 0, 3, n, k))
+
+
+# ---------------------------------------------------------------------------
+# Subgraph-removal / mixed views (dataset_subgraph.py, dataset_mix.py)
+# ---------------------------------------------------------------------------
+def _pyset_emulated(items):
+    """The CPython set-of-small-ints model augment.hip's pyset_order
+    implements (open addressing, 10-slot linear probes while i + 9 <= mask,
+    perturbation i = 5 i + 1 + (perturb >>= 5), growth to the next power of
+    two above 4 x used when fill x 5 >= mask x 3, old-slot-order reinsertion)."""
+    mask, table, fill = 7, [None] * 8, 0
+
+    def insert_clean(k):
+        i, perturb = k & mask, k
+        while True:
+            if table[i] is None:
+                table[i] = k
+                return
+            if i + 9 <= mask:
+                for j in range(i + 1, i + 10):
+                    if table[j] is None:
+                        table[j] = k
+                        return
+            perturb >>= 5
+            i = (i * 5 + 1 + perturb) & mask
+
+    for k in items:
+        i, perturb, inserted = k & mask, k, False
+        while True:
+            last = i + 9 if i + 9 <= mask else i
+            done = False
+            for j in range(i, last + 1):
+                if table[j] is None:
+                    table[j], inserted, done = k, True, True
+                    break
+                if table[j] == k:
+                    done = True
+                    break
+            if done:
+                break
+            perturb >>= 5
+            i = (i * 5 + 1 + perturb) & mask
+        if inserted:
+            fill += 1
+            if fill * 5 >= mask * 3:
+                old = [v for v in table if v is not None]
+                size = 8
+                while size <= fill * 4:
+                    size <<= 1
+                mask, table = size - 1, [None] * size
+                for v in old:
+                    insert_clean(v)
+    return [v for v in table if v is not None]
+
+
+def test_cpython_set_order_model():
+    """The frontier order the kernel emulates is CPython's own list(set(x))."""
+    rng = np.random.default_rng(0)
+    for _ in range(3000):
+        n = int(rng.integers(0, 160))
+        hi = int(rng.choice([8, 40, 256]))
+        items = [int(v) for v in rng.integers(0, hi, size=n)]
+        assert _pyset_emulated(items) == list(set(items)), items
+
+
+def _nx_remove_subgraph(edges, center, percent):
+    """The reference loop run on networkx itself (guarded like
+    dataset_mix.py:55-56)."""
+    import networkx as nx
+    G = nx.Graph(edges).copy()
+    num = int(np.floor(len(G.nodes) * percent))
+    removed, temp = [], [center]
+    while len(removed) < num:
+        if len(temp) < 1:
+            break
+        neighbors = []
+        for n in temp:
+            neighbors.extend([i for i in G.neighbors(n) if i not in temp])
+        for n in temp:
+            if len(removed) < num:
+                G.remove_node(n)
+                removed.append(n)
+            else:
+                break
+        temp = list(set(neighbors))
+    return G, removed
+
+
+def test_subgraph_oracle_matches_networkx():
+    """oracle/augment_ref.py's dict restatement of nx.Graph / neighbours /
+    remove_node / G.edges against networkx 3 on random molecule graphs."""
+    from oracle.augment_ref import bond_graph, graph_edges, remove_subgraph
+    rng = np.random.default_rng(1)
+    for t in range(300):
+        m = random_molecule(rng, "pubchem" if t % 2 else "uniform")
+        M = m.edge_attr.shape[0] // 2
+        bonds = [(int(m.edge_index[0, 2 * b]), int(m.edge_index[1, 2 * b])) for b in range(M)]
+        if t % 3 == 0:  # reversed orientations: networkx reports edges from the earlier node
+            bonds = [(e, s) if (s + e + t) % 2 else (s, e) for s, e in bonds]
+        pct = float(rng.choice([0.25, 0.2 * rng.random(), 0.9]))
+        center = int(rng.integers(0, m.x.shape[0]))
+        G_nx, rem_nx = _nx_remove_subgraph(bonds, center, pct)
+        G_o, rem_o, _ = remove_subgraph(bond_graph(bonds), center, pct)
+        assert rem_o == rem_nx
+        assert graph_edges(G_o) == list(G_nx.edges)
+
+
+def test_aug_views_oracle_properties():
+    """Sizes and invariants of the subgraph / mix views (the reference's
+    counts: floor(p x atoms-in-bonds) removed; mix tops masks up to floor(N/4)
+    atoms and keeps at most ceil(3M/4) bonds)."""
+    from oracle.augment_ref import AUG_MIX, AUG_SUBGRAPH, aug_centres, aug_views
+    rng = np.random.default_rng(2)
+    mols = [random_molecule(rng, "uniform") for _ in range(64)]
+    st = _store(mols)
+    ids = np.arange(64)
+    for mode in (AUG_SUBGRAPH, AUG_MIX):
+        v0, v1 = aug_views(st, ids, 5, 0, mode), aug_views(st, ids, 5, 1, mode)
+        for v in (v0, v1):
+            for g, m in enumerate(mols):
+                n, M = m.x.shape[0], m.edge_attr.shape[0] // 2
+                a0, a1 = v["ptr"][g], v["ptr"][g + 1]
+                masked = int((v["x"][a0:a1, 0] == MASK_ATOM).sum())
+                rem = v["flags"][g]["removed"]
+                if mode == AUG_SUBGRAPH:
+                    assert len(rem) == int(np.floor(n * 0.25))  # connected: all atoms in bonds
+                    assert masked == len(rem)
+                else:
+                    assert masked == max(n // 4, len(rem))
+                    kept = int((v["batch"][v["edge_index"][0]] == g).sum()) // 2
+                    assert kept <= max((3 * M + 3) // 4, 0) or kept == 0
+                assert not v["flags"][g]["guard"]
+        for g, m in enumerate(mols):
+            c0, c1 = aug_centres(5, g, m.x.shape[0])
+            assert c0 != c1

@@ -126,3 +126,74 @@ def test_encoder_on_device_views_matches_host_collate(dev):
         h1, z1 = model(bi)
         h2, z2 = model(ref.to(dev))
     assert torch.equal(h1, h2) and torch.equal(z1, z2)
+
+
+# ---------------------------------------------------------------------------
+# subgraph-removal / mixed views (molclr_aug_views_plan / _write)
+# ---------------------------------------------------------------------------
+def _same_aug(b, ref, allowed_status=0):
+    assert np.array_equal(b.x.cpu().numpy(), ref["x"])
+    assert np.array_equal(b.edge_index.cpu().numpy(), ref["edge_index"])
+    assert np.array_equal(b.edge_attr.cpu().numpy(), ref["edge_attr"])
+    assert np.array_equal(b.batch.cpu().numpy(), ref["batch"])
+    assert np.array_equal(b.ptr.cpu().numpy(), ref["ptr"])
+    assert int(b.status.item()) & ~allowed_status == 0
+
+
+@pytest.mark.parametrize("mode", ["subgraph", "mix"])
+@pytest.mark.parametrize("B,shape,seed", [(512, "uniform", 0), (256, "pubchem", 2**40 + 9)])
+def test_aug_views_match_oracle(dev, mode, B, shape, seed):
+    """Bit-exact Batch fields against oracle/augment_ref.py (networkx's BFS
+    order incl. the CPython set frontier, the G_i.edges survival rule, mix's
+    extra masks)."""
+    from molclr_amd.augment import DeviceMoleculeStore
+    from oracle.augment_ref import AUG_MIX, AUG_SUBGRAPH, aug_views
+    mols = _mols(2 * B, seed=B + 1, shape=shape)
+    store = DeviceMoleculeStore.from_molecules(mols, dev)
+    ids = np.random.default_rng(seed % 997).permutation(2 * B)[:B]
+    host = store.host_store()
+    m = AUG_SUBGRAPH if mode == "subgraph" else AUG_MIX
+    bi, bj = store.aug_views(ids, seed, mode, check=True)
+    _same_aug(bi, aug_views(host, ids, seed, 0, m))
+    _same_aug(bj, aug_views(host, ids, seed, 1, m))
+
+
+def test_aug_views_edge_cases(dev):
+    """One- and two-atom molecules, a disconnected molecule whose centre
+    component is smaller than the quota (the empty-frontier guard, status bit
+    3), an isolated atom, and reversed bond orientations (the subgraph module's
+    (start, end) survival test)."""
+    from molclr_amd.augment import DeviceMoleculeStore
+    from molclr_amd.dataset import Molecule
+    from oracle.augment_ref import AUG_MIX, AUG_SUBGRAPH, aug_views
+
+    def mol(n, bonds):
+        x = np.stack([np.arange(n) % 7, np.zeros(n, np.int64)], 1).astype(np.int64)
+        ei, ea = [], []
+        for k, (s, e) in enumerate(bonds):
+            ei += [(s, e), (e, s)]
+            ea += [(k % 4, 0), (k % 4, 0)]
+        ei = np.asarray(ei, np.int64).T.reshape(2, -1) if ei else np.zeros((2, 0), np.int64)
+        ea = np.asarray(ea, np.int64).reshape(-1, 2)
+        return Molecule(x=x, edge_index=ei, edge_attr=ea)
+
+    rng = np.random.default_rng(3)
+    mols = [mol(1, []), mol(2, [(0, 1)]),
+            mol(12, [(0, 1), (1, 2), (3, 4), (4, 5), (5, 6), (6, 7), (7, 8), (8, 9), (9, 10),
+                     (10, 11)]),                       # components {0,1,2} and {3..11}
+            mol(5, [(1, 2), (2, 3), (3, 4)]),          # atom 0 isolated
+            mol(9, [(4, 3), (3, 5), (0, 5), (5, 6), (2, 6), (7, 2), (8, 7), (1, 8), (0, 4)])]
+    mols += [_mols(1, seed=int(s))[0] for s in rng.integers(0, 1000, 27)]
+    store = DeviceMoleculeStore.from_molecules(mols, dev)
+    host = store.host_store()
+    ids = np.arange(len(mols))
+    for m, name in ((AUG_SUBGRAPH, "subgraph"), (AUG_MIX, "mix")):
+        for seed in range(6):
+            for view in (0, 1):
+                b = store.aug_view(ids, seed, view, name)
+                ref = aug_views(host, ids, seed, view, m)
+                flags = 0
+                for f in ref["flags"]:
+                    flags |= (8 if f["guard"] else 0) | (32 if f["centre_outside"] else 0)
+                _same_aug(b, ref, allowed_status=flags)
+                assert int(b.status.item()) == flags
