@@ -280,9 +280,11 @@ __global__ void k_ecount_weighted_partial(const typename St::T* __restrict__ g,
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = f4zero();
   if (live) {
-    // eight rows' loads in flight per round trip (a block holds ~5 waves per
-    // CU at c2, so the latency is hidden by ILP, not occupancy); the adds stay
-    // in row order
+    // a partition is band x 8 rows (ecount_parts), so a thread's eight rows
+    // of it are ONE round trip with all eight loads in flight; past 1024
+    // partitions (N > 1024 band 8: the c2 paired pass) the cap makes the
+    // partitions longer and the loop takes a second, ragged trip.  The adds
+    // stay in row order
     constexpr int U = 8;
     for (int64_t i0 = beg + r; i0 < end; i0 += U * (int64_t)band) {
       int4 lo[U], hi[U];

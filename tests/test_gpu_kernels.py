@@ -108,7 +108,10 @@ def test_atom_embed(dev, B, D, types):
     assert torch.all(X1d.grad.cpu()[unused] == 0)
 
 
-@pytest.mark.parametrize("B,D", [(64, 128), (512, 300), (16, 512)])
+# (1024, 300) and (1100, 300): N > 1024 edge-table partitions x band x 8 rows
+# (24 rows at D = 300), so the partition count is capped at 1024 and the
+# partitions' rows are ragged (rows_per_part not a multiple of band x 8)
+@pytest.mark.parametrize("B,D", [(64, 128), (512, 300), (16, 512), (1024, 300), (1100, 300)])
 def test_gine_aggregate_matches_reference_order(dev, B, D):
     b = batch(B, 2)
     N = b.x.shape[0]
