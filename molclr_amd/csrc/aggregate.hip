@@ -40,51 +40,183 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
   St::st(h, t, f4add(X1[a * d4 + c], X2[b * d4 + c]));
 }
 
-// Partial per-type column sums of dh.  grid = (P partitions, ceil(D/64)),
-// block = 64 threads (one column each), LDS table [n1+n2][64].
-template <typename St>
-__global__ __launch_bounds__(64) void k_atom_embed_bwd_partial(
-    const int64_t* __restrict__ x, const typename St::T* __restrict__ dh, int64_t N, int64_t D,
-    int64_t n1, int64_t n2, int64_t rows_per_part, double* __restrict__ partial) {
-  // fp32 table within a partition (<= 128 rows), fp64 partials across partitions
-  extern __shared__ __attribute__((aligned(16))) float tab[];  // [(n1+n2)][64]
+// ---------------------------------------------------------------------------
+// Atom-embedding gradient by type-sorted segments.  dX1[a] = Σ_{i: x[i,0]=a}
+// dh[i] and dX2[b] = Σ_{i: x[i,1]=b} dh[i] are segmented column sums over
+// the 2N (node, key) items, key = x[i,0] or n1 + x[i,1].  A stable counting
+// sort groups them (item order within a key = node order); the segments are
+// cut into chunks of kEmbChunk items, each chunk summed in fp32 by one wave
+// (4 columns per lane, whole rows gathered: no LDS read-modify-write chain),
+// and the chunk sums of a key are added in fp64 in chunk order
+// (deterministic; the small tables' gradients are sums of ~10^4-10^6
+// nearly cancelling terms).
+// ---------------------------------------------------------------------------
+constexpr int kEmbBlock = 256;  // items per sort block
+constexpr int kEmbChunk = 128;  // items per fp32 chunk sum
+
+__device__ __forceinline__ int emb_key(const int64_t* __restrict__ x, int64_t item, int64_t N,
+                                       int64_t n1, int64_t n2) {
+  if (item < N) {
+    const int64_t a = x[2 * item];
+    return (int)(a < 0 ? 0 : (a >= n1 ? n1 - 1 : a));
+  }
+  const int64_t b = x[2 * (item - N) + 1];
+  return (int)(n1 + (b < 0 ? 0 : (b >= n2 ? n2 - 1 : b)));
+}
+
+// per sort block: counts of every key
+__global__ __launch_bounds__(kEmbBlock) void k_emb_hist(const int64_t* __restrict__ x, int64_t N,
+                                                        int64_t n1, int64_t n2,
+                                                        int32_t* __restrict__ hist) {
+  extern __shared__ int32_t h[];
+  const int nk = (int)(n1 + n2);
+  for (int k = threadIdx.x; k < nk; k += kEmbBlock) h[k] = 0;
+  __syncthreads();
+  const int64_t item = (int64_t)blockIdx.x * kEmbBlock + threadIdx.x;
+  if (item < 2 * N) atomicAdd(&h[emb_key(x, item, N, n1, n2)], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < nk; k += kEmbBlock) hist[(int64_t)k * gridDim.x + blockIdx.x] = h[k];
+}
+
+// one wave per key: exclusive scan of the key's per-block counts (in place,
+// hist[k][blk] -> offset within the key's segment) and the key's total
+__global__ __launch_bounds__(64) void k_emb_keyscan(int32_t* __restrict__ hist, int nblk,
+                                                    int32_t* __restrict__ total) {
+  const int64_t k = blockIdx.x;
   const int lane = threadIdx.x;
-  const int64_t nt = n1 + n2;
-  for (int64_t r = 0; r < nt; ++r) tab[r * 64 + lane] = 0.f;
-  const int64_t c = (int64_t)blockIdx.y * 64 + lane;
-  const bool active = c < D;
-  const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
-  int64_t end = beg + rows_per_part;
-  if (end > N) end = N;
-  int64_t i = beg;
-  for (; i + 4 <= end; i += 4) {
-    float v[4];
-    int64_t a[4], b[4];
+  int32_t* row = hist + k * nblk;
+  int32_t carry = 0;
+  for (int base = 0; base < nblk; base += 64) {
+    const int b = base + lane;
+    const int32_t v = b < nblk ? row[b] : 0;
+    int32_t incl = v;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = x[2 * (i + u)];
-      b[u] = x[2 * (i + u) + 1];
-      v[u] = active ? St::ld1(dh, (i + u) * D + c) : 0.f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
     }
+    if (b < nblk) row[b] = carry + incl - v;
+    carry += __shfl(incl, 63, 64);
+  }
+  if (lane == 0) total[k] = carry;
+}
+
+// one block: key starts, each key's first chunk, and the chunk table
+// (chunk c: items [cbeg[c], cend[c]) of one key); nchunks[0] = count
+__global__ __launch_bounds__(1024) void k_emb_plan(const int32_t* __restrict__ total, int nk,
+                                                   int32_t* __restrict__ kstart,
+                                                   int32_t* __restrict__ cbeg,
+                                                   int32_t* __restrict__ cend,
+                                                   int32_t* __restrict__ kchunk0,
+                                                   int32_t* __restrict__ nchunks, int max_chunks) {
+  __shared__ int32_t tot[1024], ks[1025], kc[1025];
+  const int t = threadIdx.x;
+  tot[t] = t < nk ? total[t] : 0;
+  __syncthreads();
+  if (t == 0) {
+    int32_t run = 0, ch = 0;
+    for (int k = 0; k < nk; ++k) {
+      ks[k] = run;
+      kc[k] = ch;
+      run += tot[k];
+      ch += (tot[k] + kEmbChunk - 1) / kEmbChunk;
+    }
+    ks[nk] = run;
+    kc[nk] = ch;
+    *nchunks = ch;
+  }
+  __syncthreads();
+  for (int k = t; k <= nk; k += 1024) {
+    kstart[k] = ks[k];
+    kchunk0[k] = kc[k];
+  }
+  const int nch = kc[nk];
+  for (int c = t; c < max_chunks; c += 1024) {
+    if (c >= nch) break;
+    int lo = 0, hi = nk - 1;  // the key whose chunk range holds c
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (kc[mid] <= c) lo = mid;
+      else hi = mid - 1;
+    }
+    const int32_t q = (c - kc[lo]) * kEmbChunk;
+    cbeg[c] = ks[lo] + q;
+    cend[c] = ks[lo] + (q + kEmbChunk < tot[lo] ? q + kEmbChunk : tot[lo]);
+  }
+}
+
+// stable scatter: item -> its slot in key order (rank among the block's
+// earlier items of the same key)
+__global__ __launch_bounds__(kEmbBlock) void k_emb_scatter(const int64_t* __restrict__ x,
+                                                           int64_t N, int64_t n1, int64_t n2,
+                                                           const int32_t* __restrict__ off,
+                                                           const int32_t* __restrict__ kstart,
+                                                           int32_t* __restrict__ perm) {
+  __shared__ int32_t keys[kEmbBlock];
+  const int nk = (int)(n1 + n2);
+  const int64_t item = (int64_t)blockIdx.x * kEmbBlock + threadIdx.x;
+  const bool live = item < 2 * N;
+  const int k = live ? emb_key(x, item, N, n1, n2) : -1;
+  keys[threadIdx.x] = k;
+  __syncthreads();
+  if (!live) return;
+  int rank = 0;
+  for (int j = 0; j < (int)threadIdx.x; ++j) rank += keys[j] == k;
+  (void)nk;
+  perm[kstart[k] + off[(int64_t)k * gridDim.x + blockIdx.x] + rank] =
+      (int32_t)(item < N ? item : item - N);
+}
+
+// one wave per (chunk, 256-column block): fp32 sum of the chunk's rows
+template <typename St>
+__global__ __launch_bounds__(64) void k_emb_chunk_sum(const typename St::T* __restrict__ dh,
+                                                      const int32_t* __restrict__ perm,
+                                                      const int32_t* __restrict__ cbeg,
+                                                      const int32_t* __restrict__ cend,
+                                                      const int32_t* __restrict__ nchunks,
+                                                      int64_t d4, double* __restrict__ csum) {
+  const int64_t ch = blockIdx.x;
+  if (ch >= *nchunks) return;  // the grid is sized for the most chunks possible
+  const int64_t c = (int64_t)blockIdx.y * 64 + threadIdx.x;  // float4 column
+  if (c >= d4) return;
+  const int32_t beg = cbeg[ch], end = cend[ch];
+  float4 acc = f4zero();
+  int32_t i = beg;
+  for (; i + 4 <= end; i += 4) {  // four rows in flight; adds in item order
+    float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      int64_t aa = a[u] < 0 ? 0 : (a[u] >= n1 ? n1 - 1 : a[u]);
-      int64_t bb = b[u] < 0 ? 0 : (b[u] >= n2 ? n2 - 1 : b[u]);
-      tab[aa * 64 + lane] += v[u];
-      tab[(n1 + bb) * 64 + lane] += v[u];
-    }
+    for (int u = 0; u < 4; ++u) v[u] = St::ld(dh, (int64_t)perm[i + u] * d4 + c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = f4add(acc, v[u]);
   }
-  for (; i < end; ++i) {
-    int64_t aa = x[2 * i], bb = x[2 * i + 1];
-    aa = aa < 0 ? 0 : (aa >= n1 ? n1 - 1 : aa);
-    bb = bb < 0 ? 0 : (bb >= n2 ? n2 - 1 : bb);
-    float v = active ? St::ld1(dh, i * D + c) : 0.f;
-    tab[aa * 64 + lane] += v;
-    tab[(n1 + bb) * 64 + lane] += v;
+  for (; i < end; ++i) acc = f4add(acc, St::ld(dh, (int64_t)perm[i] * d4 + c));
+  double* o = csum + ch * 4 * d4 + 4 * c;
+  o[0] = acc.x;
+  o[1] = acc.y;
+  o[2] = acc.z;
+  o[3] = acc.w;
+}
+
+// dX[key][col] (+)= Σ over the key's chunks (in order) in fp64, one thread per element
+__global__ void k_emb_finish(const double* __restrict__ csum, const int32_t* __restrict__ kchunk0,
+                             int64_t n1, int64_t n2, int64_t D, float* __restrict__ dX1,
+                             float* __restrict__ dX2, int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (n1 + n2) * D) return;
+  const int64_t k = t / D, col = t - k * D;
+  double acc = 0.0;
+  int32_t ch = kchunk0[k];
+  const int32_t ce = kchunk0[k + 1];
+  for (; ch + 8 <= ce; ch += 8) {  // eight loads in flight, adds in chunk order
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = csum[(int64_t)(ch + u) * D + col];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
   }
-  if (!active) return;
-  double* out = partial + (int64_t)blockIdx.x * nt * D;
-  for (int64_t r = 0; r < nt; ++r) out[r * D + c] = tab[r * 64 + lane];
+  for (; ch < ce; ++ch) acc += csum[(int64_t)ch * D + col];
+  float* o = k < n1 ? dX1 + k * D + col : dX2 + (k - n1) * D + col;
+  *o = accumulate ? *o + (float)acc : (float)acc;
 }
 
 // out[r][c] = Σ_p partial[p][r][c], rows [0,n1) -> dX1, [n1,n1+n2) -> dX2.
@@ -531,12 +663,6 @@ __global__ __launch_bounds__(kT) void k_transpose_gather_b8(const uint16_t* __re
   st8(dx, t, f8add(acc, ld8(g, t)));
 }
 
-int64_t atom_parts(int64_t N) {
-  int64_t P = molclr::ceil_div(N, 128);
-  if (P > 128) P = 128;
-  if (P < 1) P = 1;
-  return P;
-}
 int64_t ecount_parts(int64_t N, int band) {
   int64_t P = molclr::ceil_div(N, (int64_t)band * 8);
   if (P > 1024) P = 1024;
@@ -568,29 +694,85 @@ MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const fl
   return MOLCLR_OK;
 }
 
+namespace {
+struct EmbWs {
+  int32_t *hist, *total, *kstart, *cbeg, *cend, *kchunk0, *nchunks, *perm;
+  double* csum;
+  int64_t nblk, max_chunks;
+};
+EmbWs emb_ws(void* w, size_t bytes, int64_t N, int64_t D, int64_t n1, int64_t n2) {
+  molclr::Workspace ws(w, bytes);
+  EmbWs e;
+  const int64_t nk = n1 + n2;
+  e.nblk = molclr::ceil_div(2 * N > 0 ? 2 * N : 1, (int64_t)kEmbBlock);
+  e.max_chunks = molclr::ceil_div(2 * N, (int64_t)kEmbChunk) + nk;  // every key may end ragged
+  e.hist = ws.take<int32_t>(e.nblk * nk);
+  e.total = ws.take<int32_t>(nk);
+  e.kstart = ws.take<int32_t>(nk + 1);
+  e.kchunk0 = ws.take<int32_t>(nk + 1);
+  e.cbeg = ws.take<int32_t>(e.max_chunks);
+  e.cend = ws.take<int32_t>(e.max_chunks);
+  e.nchunks = ws.take<int32_t>(1);
+  e.perm = ws.take<int32_t>(2 * N > 0 ? 2 * N : 1);
+  e.csum = ws.take<double>(e.max_chunks * D);
+  return e;
+}
+
+template <typename St>
+int emb_bwd(const int64_t* x, const typename St::T* dh, float* dX1, float* dX2, int64_t N,
+            int64_t D, int64_t n1, int64_t n2, int accumulate, void* workspace,
+            size_t workspace_bytes, hipStream_t s) {
+  const int64_t nk = n1 + n2;
+  const EmbWs e = emb_ws(workspace, workspace_bytes, N, D, n1, n2);
+  const int64_t d4 = D / 4;
+  if (N > 0) {
+    hipLaunchKernelGGL(k_emb_hist, dim3((unsigned)e.nblk), dim3(kEmbBlock), nk * sizeof(int32_t), s,
+                       x, N, n1, n2, e.hist);
+  } else {
+    (void)hipMemsetAsync(e.hist, 0, (size_t)e.nblk * nk * sizeof(int32_t), s);
+  }
+  hipLaunchKernelGGL(k_emb_keyscan, dim3((unsigned)nk), dim3(64), 0, s, e.hist, (int)e.nblk,
+                     e.total);
+  hipLaunchKernelGGL(k_emb_plan, dim3(1), dim3(1024), 0, s, static_cast<const int32_t*>(e.total),
+                     (int)nk, e.kstart, e.cbeg, e.cend, e.kchunk0, e.nchunks, (int)e.max_chunks);
+  if (N > 0) {
+    hipLaunchKernelGGL(k_emb_scatter, dim3((unsigned)e.nblk), dim3(kEmbBlock), 0, s, x, N, n1, n2,
+                       static_cast<const int32_t*>(e.hist), static_cast<const int32_t*>(e.kstart),
+                       e.perm);
+    hipLaunchKernelGGL(k_emb_chunk_sum<St>, dim3((unsigned)e.max_chunks,
+                                                 (unsigned)molclr::ceil_div(d4, 64)),
+                       dim3(64), 0, s, dh, static_cast<const int32_t*>(e.perm),
+                       static_cast<const int32_t*>(e.cbeg), static_cast<const int32_t*>(e.cend),
+                       static_cast<const int32_t*>(e.nchunks), d4, e.csum);
+  }
+  hipLaunchKernelGGL(k_emb_finish, dim3((unsigned)molclr::ceil_div(nk * D, 256)), dim3(256), 0, s,
+                     static_cast<const double*>(e.csum), static_cast<const int32_t*>(e.kchunk0), n1,
+                     n2, D, dX1, dX2, accumulate);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+}  // namespace
+
 MOLCLR_API size_t molclr_atom_embed_bwd_workspace_bytes(int64_t N, int64_t D, int64_t n1,
                                                         int64_t n2) {
-  return (size_t)atom_parts(N) * (n1 + n2) * D * sizeof(double) + 256;
+  const int64_t nk = n1 + n2;
+  const int64_t nblk = molclr::ceil_div(2 * N > 0 ? 2 * N : 1, (int64_t)kEmbBlock);
+  const int64_t max_chunks = molclr::ceil_div(2 * N, (int64_t)kEmbChunk) + nk;
+  return (size_t)(nblk * nk + nk + 2 * (nk + 1) + 2 * max_chunks + 1 + 2 * N) * sizeof(int32_t) +
+         (size_t)max_chunks * D * sizeof(double) + 10 * 256;
 }
 
 MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* dX1, float* dX2,
                                      int64_t N, int64_t D, int64_t n1, int64_t n2, int accumulate,
                                      void* workspace, size_t workspace_bytes,
                                      molclr_stream_t stream) {
-  MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd: bad sizes");
-  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd: tables too large");
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0 && n1 > 0 && n2 > 0 && N >= 0,
+                 "atom_embed_bwd: bad sizes (dim a multiple of 4)");
+  MOLCLR_REQUIRE(n1 + n2 <= 1024, "atom_embed_bwd: tables too large");
+  MOLCLR_REQUIRE(2 * N < (1ll << 31), "atom_embed_bwd: too many nodes");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
-  hipStream_t s = molclr::as_stream(stream);
-  int64_t P = atom_parts(N);
-  int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
-  double* partial = (double*)workspace;
-  size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
-  hipLaunchKernelGGL(k_atom_embed_bwd_partial<StF32>, dim3(P, molclr::ceil_div(D, 64)), dim3(64),
-                     lds, s, x, dh, N, D, n1, n2, rpp, partial);
-  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 16)), dim3(1024),
-                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
+  return emb_bwd<StF32>(x, dh, dX1, dX2, N, D, n1, n2, accumulate, workspace, workspace_bytes,
+                        molclr::as_stream(stream));
 }
 
 MOLCLR_API int molclr_edge_tables_combine(int layers, const float* const* E1s,
@@ -764,20 +946,13 @@ MOLCLR_API int molclr_atom_embed_bwd_bf16(const int64_t* x, const uint16_t* dh, 
                                           float* dX2, int64_t N, int64_t D, int64_t n1, int64_t n2,
                                           int accumulate, void* workspace, size_t workspace_bytes,
                                           molclr_stream_t stream) {
-  MOLCLR_REQUIRE(D > 0 && n1 > 0 && n2 > 0, "atom_embed_bwd_bf16: bad sizes");
-  MOLCLR_REQUIRE((n1 + n2) * 64 * sizeof(float) <= 65536, "atom_embed_bwd_bf16: tables too large");
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0 && n1 > 0 && n2 > 0 && N >= 0,
+                 "atom_embed_bwd_bf16: bad sizes (dim a multiple of 4)");
+  MOLCLR_REQUIRE(n1 + n2 <= 1024, "atom_embed_bwd_bf16: tables too large");
+  MOLCLR_REQUIRE(2 * N < (1ll << 31), "atom_embed_bwd_bf16: too many nodes");
   MOLCLR_REQUIRE_WS(workspace_bytes, molclr_atom_embed_bwd_workspace_bytes(N, D, n1, n2));
-  hipStream_t s = molclr::as_stream(stream);
-  const int64_t P = atom_parts(N);
-  const int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
-  double* partial = (double*)workspace;
-  const size_t lds = (size_t)(n1 + n2) * 64 * sizeof(float);
-  hipLaunchKernelGGL(k_atom_embed_bwd_partial<StBF16>, dim3(P, molclr::ceil_div(D, 64)), dim3(64),
-                     lds, s, x, dh, N, D, n1, n2, rpp, partial);
-  hipLaunchKernelGGL(k_reduce_partials_split, dim3(molclr::ceil_div((n1 + n2) * D, 16)), dim3(1024),
-                     0, s, partial, P, n1 + n2, D, n1, dX1, dX2, accumulate);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
+  return emb_bwd<StBF16>(x, dh, dX1, dX2, N, D, n1, n2, accumulate, workspace, workspace_bytes,
+                         molclr::as_stream(stream));
 }
 
 MOLCLR_API int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* rowptr,
