@@ -21,6 +21,9 @@ for s in $steps; do
     pmc)     export TMPDIR=/tmp; rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
              run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    pmc5)    export TMPDIR=/tmp; rm -rf gpurun_out/pmc5_fetch gpurun_out/pmc5_write
+             run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc5_fetch -o run --output-format csv -- python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc
+             run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_gine_agg_fwd -d gpurun_out/pmc5_write -o run --output-format csv -- python bench.py --config c5 --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     gemm)    run gemm 300 python tools/gemm_bench.py 30556; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     ntx)     run ntx 300 python tools/ntxent_scale.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     ntxprof) export TMPDIR=/tmp; rm -rf gpurun_out/ntxprof
