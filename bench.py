@@ -1,6 +1,7 @@
 """Contrastive pre-training throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--no-cpu-baseline]
+                    [--augment host|device|subgraph|mix]
 
 A step is the reference's hot-loop iteration (molclr.py:108-128): two
 encoder forwards of augmented views, F.normalize, NT-Xent, backward, Adam —
@@ -10,7 +11,10 @@ before the timed region (SURVEY.md §8d generator; rank r uses seed r*10^6),
 rotated every step so repeated steps do not re-read one batch.
 
 Workloads: c2 = GIN 5x300, feat 512, batch 512 per GPU, fp32 (default; the
-config the metric is quoted on); c3 = GCN 5x300.  N > 1 runs under torchrun,
+config the metric is quoted on); c3 = GCN 5x300; c5 = GIN 5x512, bf16
+storage and MFMA with fp32 accumulation, batch 1024 per GPU, PubChem-shaped
+graphs.  Both views run through one paired encoder pass with per-view
+BatchNorm statistics (the reference's two calls).  N > 1 runs under torchrun,
 one rank per GPU over RCCL: the NT-Xent batch is global (512 N), weak scaling.
 
 The JSON line adds:
@@ -19,8 +23,11 @@ The JSON line adds:
                   timed region, against 8.0 TB/s.  Durations are the
                   dispatch-recorded events of hipExtLaunchKernelGGL
                   (molclr_ktimer_*), i.e. the kernel's own execution window.
-  roofline_mfma — all molclr_gemm_f32 kernels (GEMM + split-K reduce) in the
-                  timed region, against 157.3 TF/s (fp32 dense MFMA peak).
+  roofline_mfma — all encoder/head GEMM kernels (GEMM + split-K reduce), timed
+                  over extra steps after the timed region, against 157.3 TF/s
+                  (fp32 dense MFMA peak; fp32 configs, which run split-bf16
+                  "x6" kernels, also report the fraction of their own ceiling
+                  2.5 PF / 6) or 2.5 PF/s (bf16, c5).
   roofline_ntxent — every NT-Xent kernel (forward: S = R R^T as a split-bf16
                   GEMM + the row logsumexp; backward: the weights W from the
                   kept S and dR = W R), work = the two products' flops, against
@@ -285,6 +292,9 @@ def main():
                              "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
                              "traffic": None, "launches": gm["launches"],
                              "ms_per_step": round(gm["ms"] / args.mfma_steps, 3),
+                             **({} if precision == "bf16" else {
+                                 "frac_of_split_bf16_ceiling":
+                                     round(tfs / (BF16_MFMA_PEAK_TFS / 6), 4)}),
                              "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                        f"after the timed region"}
         nx = s.get("ntxent")
