@@ -705,8 +705,10 @@ int molclr_gemm_bf16(const uint16_t* A, const uint16_t* planes, uint16_t* C, int
  * automatic, as molclr_gemm_bf16): output tiles 0 = 128 x 128, 1 = 128 x 256,
  * 2 = 128 x 512, 3 = 64 x 512, 4 = 128 x 256 (8 waves), 5 = 128 x 128 (shallow
  * A prefetch), 6 = 256 x 256 with LDS-DMA staging (K % 64 == 0), 7 = 256 x 256
- * with a four-stage LDS-DMA ring (K % 32 == 0); 6 and 7 fall back to 2 for
- * other K.  Every shape gives the same result bits (those of hipBLASLt's bf16
+ * with a four-stage LDS-DMA ring (K % 32 == 0), 8 = 6 as a persistent kernel
+ * (one block per CU, epilogue overlapped with the next tile's staging; K % 64
+ * == 0); 6, 7 and 8 fall back to 2 for other K.  Every shape gives the same
+ * result bits (those of hipBLASLt's bf16
  * GEMM on the epilogue-free products). */
 int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M,
                           int64_t N, int64_t K, int64_t lda, int64_t ldc, int epilogue,

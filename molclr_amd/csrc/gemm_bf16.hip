@@ -399,6 +399,196 @@ __global__ __launch_bounds__(512) void k_gemm_tb(
 }
 
 // ---------------------------------------------------------------------------
+// k_gemm_tp: k_gemm_tb as a persistent kernel.  One block per CU walks its
+// share of the output tiles; the first K step of the NEXT tile is DMA-staged
+// during the current tile's last step, and the epilogue (a separate 32 KB LDS
+// region, 160 KB in all) runs while that DMA lands, so a tile's output
+// stores and ReLU-mask / bias loads overlap the next tile's staging instead
+// of idling the CU between blocks.  The mask operand is fetched before the
+// last K step's MFMAs (its latency hides behind them).
+// Tiles: XCD x's blocks own a contiguous range of logical tiles (row slab
+// major), in proportion to their number; block p of the XCD takes every P-th.
+// Results are identical to k_gemm_tb (same fragments, same MFMA order).
+// ---------------------------------------------------------------------------
+template <int EPI, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemm_tp(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bp, uint16_t* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const uint16_t* __restrict__ aux, int64_t ldaux) {
+  constexpr int BM = 256, BN = 256, KT = 64;
+  constexpr int SI = BM * KT * 2;       // bytes per operand image per stage (32 KB)
+  constexpr int WMW = NW == 8 ? 4 : 2;  // waves along M (8 waves: 4 x 2, 4 waves: 2 x 2)
+  constexpr int TI = BM / 32 / WMW, TJ = BN / 32 / (NW / WMW);  // a wave's 32 x 32 blocks
+  constexpr int PQ = 32 / NW;           // 1 KB DMA pieces per wave and operand
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * SI + NW * 4096];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntiles = (int)((M + BM - 1) / BM) * ntn;
+  const int G = gridDim.x, x = blockIdx.x & 7, pos = blockIdx.x >> 3;
+  const int q8 = G >> 3, r8 = G & 7;
+  const int P = q8 + (x < r8 ? 1 : 0);                                  // blocks on XCD x
+  const int base = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;  // their first rank
+  const int hi = (int)((int64_t)(base + P) * ntiles / G);
+  int t = (int)((int64_t)base * ntiles / G) + pos;
+  if (t >= hi) return;
+
+  auto tile_src = [&](int tt, const uint16_t* (&as)[PQ], const uint16_t* (&bs)[PQ]) {
+    const int64_t m0 = (int64_t)(tt / ntn) * BM, n0 = (int64_t)(tt % ntn) * BN;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      const int r = 8 * (PQ * wave + q) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int64_t gm = m0 + r < M ? m0 + r : M - 1;
+      const int64_t gn = n0 + r < npad ? n0 + r : npad - 1;
+      as[q] = A + gm * lda + 8 * c;
+      bs[q] = Bp + gn * kp + 8 * c;
+    }
+  };
+  const int nt = (int)(K / KT);
+  auto stage = [&](int buf, const uint16_t* const (&as)[PQ], const uint16_t* const (&bs)[PQ], int s) {
+    const int64_t k0 = (int64_t)s * KT;
+    uint8_t* ia = lds + buf * 2 * SI + wave * (PQ * 1024);
+    uint8_t* ib = ia + SI;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q) {
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(as[q] + k0), (lds_as_ptr)(ia + 1024 * q), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(bs[q] + k0), (lds_as_ptr)(ib + 1024 * q), 16, 0, 0);
+    }
+  };
+
+  const int ra = 32 * TI * wm + li, rb = 32 * TJ * wn + li;  // this lane's fragment rows
+  f32x16 acc[TI][TJ];
+  auto compute = [&](int buf) {
+    const uint8_t* ia = lds + buf * 2 * SI;
+    const uint8_t* ib = ia + SI;
+    bf16x8 fa[2][TI], fb[2][TJ];
+    auto read = [&](int q, bf16x8(&a)[TI], bf16x8(&b)[TJ]) {
+      const int c = 2 * q + lh;
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+        a[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ia + t128(ra + 32 * i, c)));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        b[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ib + t128(rb + 32 * j, c)));
+    };
+    read(0, fa[0], fb[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 3) read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
+                                                               0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // this lane's epilogue pieces of a 32 x 32 block: rows (lane >> 3) + 8 it,
+  // columns 4 (lane & 7) .. +3
+  const int erow = lane >> 3, ec4 = lane & 7;
+  uint2 am[2][TJ][4];  // ReLU-mask operand of one row of blocks, one row ahead
+  auto fetch_mask = [&](int64_t m0, int64_t n0, int i, uint2(&dst)[TJ][4]) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        int64_t m = m0 + 32 * TI * wm + 32 * i + erow + 8 * it;
+        int64_t n = n0 + 32 * TJ * wn + 32 * j + 4 * ec4;
+        m = m < M ? m : M - 1;
+        n = n + 4 <= N ? n : 0;  // partial / outside pieces re-read below or skipped
+        dst[j][it] = *reinterpret_cast<const uint2*>(aux + m * ldaux + n);
+      }
+  };
+
+  float* tw = reinterpret_cast<float*>(lds + 4 * SI) + wave * 32 * 32;
+  const uint16_t* asrc[PQ];
+  const uint16_t* bsrc[PQ];
+  tile_src(t, asrc, bsrc);
+  stage(0, asrc, bsrc, 0);
+  __syncthreads();
+  int buf = 0;
+  for (;;) {
+    const int64_t m0 = (int64_t)(t / ntn) * BM, n0 = (int64_t)(t % ntn) * BN;
+    const int tn = t + P;
+    const bool more = tn < hi;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    for (int s = 0; s < nt; ++s) {
+      if (s + 1 < nt) {
+        stage(buf ^ 1, asrc, bsrc, s + 1);
+      } else if (more) {
+        const uint16_t* an[PQ];
+        const uint16_t* bn[PQ];
+        tile_src(tn, an, bn);
+        stage(buf ^ 1, an, bn, 0);
+      }
+      compute(buf);
+      __syncthreads();  // step s + 1 (or the next tile's step 0) has landed; buf is free
+      buf ^= 1;
+    }
+
+    if (EPI == MOLCLR_EPI_RELU_MASK) fetch_mask(m0, n0, 0, am[0]);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      if (EPI == MOLCLR_EPI_RELU_MASK && i + 1 < TI) fetch_mask(m0, n0, i + 1, am[(i + 1) & 1]);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t mb = m0 + 32 * TI * wm + 32 * i, nb = n0 + 32 * TJ * wn + 32 * j;
+        if (nb >= N) continue;  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tw[acc_row(r, lh) * 32 + li] = acc[i][j][r];
+        wave_lds_sync();
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int row = erow + 8 * it;
+          const int64_t m = mb + row, n = nb + 4 * ec4;
+          if (m >= M || n >= N) continue;
+          float4 v = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * ec4);
+          if (n + 4 <= N) {
+            if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+              v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+              if (EPI == MOLCLR_EPI_BIAS_RELU)
+                v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            }
+            if (EPI == MOLCLR_EPI_RELU_MASK) {
+              const float4 xm = bf16x4_to_f4(am[i & 1][j][it]);
+              v = make_float4(xm.x > 0.f ? v.x : 0.f, xm.y > 0.f ? v.y : 0.f, xm.z > 0.f ? v.z : 0.f,
+                              xm.w > 0.f ? v.w : 0.f);
+            }
+            *reinterpret_cast<uint2*>(C + m * ldc + n) = f4_to_bf16x4(v);
+          } else {
+            const float e[4] = {v.x, v.y, v.z, v.w};
+            for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+              float xv = e[jj];
+              if (EPI == MOLCLR_EPI_BIAS) xv = xv + bias[n + jj];
+              if (EPI == MOLCLR_EPI_BIAS_RELU) xv = fmaxf(xv + bias[n + jj], 0.f);
+              if (EPI == MOLCLR_EPI_RELU_MASK) xv = bf16_to_f32(aux[m * ldaux + n + jj]) > 0.f ? xv : 0.f;
+              C[m * ldc + n + jj] = (uint16_t)(f32x2_to_bf16x2(xv, 0.f) & 0xFFFFu);
+            }
+          }
+        }
+        wave_lds_sync();
+      }
+    }
+    if (!more) break;
+    t = tn;
+    tile_src(t, asrc, bsrc);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_gemm_tc: k_gemm_tb's tile and wave layout with 32-deep K steps in a ring
 // of four LDS stages (32 KB each: [256 rows][64 B] per operand, the xoff
 // swizzle applied on the DMA source address and on the read).  Three steps
@@ -822,6 +1012,43 @@ int launch_tb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
 #undef MOLCLR_TB
 }
 
+// one persistent k_gemm_tp block per CU (160 KB of LDS: one block fits)
+int cu_count() {
+  static int cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+template <int NW>
+int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,
+              int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc, const float* bias,
+              const uint16_t* aux, int64_t ldaux, hipStream_t s) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  MOLCLR_REQUIRE(tiles < (1ll << 31) / 256, "gemm_bf16: too many tiles");
+  const int64_t cus = cu_count();
+  const dim3 g((unsigned)(tiles < cus ? tiles : cus)), b(64 * NW);
+#define MOLCLR_TP(EPV)                                                                          \
+  molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<EPV, NW>, g, b, 0, s, A, Bp, C, M, N, K, lda, kp, \
+                       npad, ldc, bias, aux, ldaux)
+  switch (epi) {
+    case MOLCLR_EPI_NONE: MOLCLR_TP(MOLCLR_EPI_NONE); return MOLCLR_OK;
+    case MOLCLR_EPI_BIAS: MOLCLR_TP(MOLCLR_EPI_BIAS); return MOLCLR_OK;
+    case MOLCLR_EPI_BIAS_RELU: MOLCLR_TP(MOLCLR_EPI_BIAS_RELU); return MOLCLR_OK;
+    case MOLCLR_EPI_RELU_MASK: MOLCLR_TP(MOLCLR_EPI_RELU_MASK); return MOLCLR_OK;
+    default:
+      molclr::set_error("gemm_bf16: bad epilogue %d", epi);
+      return MOLCLR_ERR_ARG;
+  }
+#undef MOLCLR_TP
+}
+
 template <int WM, int WN, int TN, int D>
 int launch_qb_m(bool mask, int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M,
                 int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
@@ -837,14 +1064,19 @@ int launch_qb_m(bool mask, int epi, const uint16_t* A, const uint16_t* Bp, uint1
 // 2 = 128 x 512 (8 waves, 2), 3 = 64 x 512 (8 waves, 4), 4 = 128 x 256 (8
 // waves, 4), 5 = 128 x 128 (4 waves, 2); 6 = k_gemm_tb (256 x 256, LDS-DMA
 // staging of both operands; K % 64 == 0, else 2), 7 = k_gemm_tc (256 x 256,
-// four-stage LDS-DMA ring; K % 32 == 0, else 2)
-constexpr int kQbImpls = 8;
+// four-stage LDS-DMA ring; K % 32 == 0, else 2), 8 = k_gemm_tp (k_gemm_tb
+// persistent, epilogue overlapped with the next tile's staging; K % 64 == 0,
+// else 2), 9 = k_gemm_tp with 4 waves of 128 x 128 (fewer LDS fragment reads
+// per MFMA; K % 64 == 0, else 2)
+constexpr int kQbImpls = 10;
 // measured at the c5 shapes (55k rows, tools/gemm_bf16_bench.py); k_gemm_qb:
 // 128 x 512 for N <= 512, 128 x 128 above
-// k_gemm_tb whenever K % 64 == 0 (10-15 % faster than the best k_gemm_qb
-// shape on all four c5 products), k_gemm_tc for K % 32 == 0
+// the persistent k_gemm_tp whenever K % 64 == 0 (k_gemm_tb was 10-15 %
+// faster than the best k_gemm_qb shape on all four c5 products; k_gemm_tp is
+// 2-5 % faster than k_gemm_tb on the plain products and ~20 % on the ReLU-mask
+// one; its 4-wave 128 x 128 form, 9, is 10-25 % slower), k_gemm_tc for K % 32 == 0
 int qb_default(int64_t N, int64_t K) {
-  if (K % 64 == 0) return 6;
+  if (K % 64 == 0) return 8;
   if (K % 32 == 0) return 7;
   return N > 512 ? 5 : 2;
 }
@@ -923,8 +1155,14 @@ MOLCLR_API int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, 
 #define MOLCLR_QBM(WMV, WNV, TNV, DV)                                                            \
   launch_qb_m<WMV, WNV, TNV, DV>(mask, epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, \
                                  aux, ldaux, s)
-  const int vv = ((v == 6 && K % 64 != 0) || (v == 7 && K % 32 != 0)) ? 2 : v;
+  const int vv = (((v == 6 || v == 8 || v == 9) && K % 64 != 0) || (v == 7 && K % 32 != 0)) ? 2 : v;
   switch (vv) {
+    case 9:
+      rc = launch_tp<4>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, s);
+      break;
+    case 8:
+      rc = launch_tp<8>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, s);
+      break;
     case 6:
       rc = launch_tb<false>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, s);
       break;

@@ -48,7 +48,10 @@ def bf(t):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (1000, 512, 1024), (333, 256, 64),
-                                   (4096, 1024, 512), (37, 96, 40), (500, 512, 1000)])
+                                   (4096, 1024, 512), (37, 96, 40), (500, 512, 1000),
+                                   # > 256 tiles: persistent blocks (impl 8) walk several,
+                                   # with partial row / column tiles among them
+                                   (20000, 1024, 512), (17001, 1000, 128)])
 def test_gemm_bf16(dev, M, N, K):
     from molclr_amd._lib import EPI_BIAS, EPI_BIAS_RELU, EPI_NONE, EPI_RELU_MASK
     lib = _lib.load()
@@ -78,7 +81,7 @@ def test_gemm_bf16(dev, M, N, K):
     # element, in the same k order)
     for epi in (EPI_BIAS_RELU, EPI_RELU_MASK):
         outs = []
-        for impl in (-1, 0, 1, 2, 3, 4, 5, 6, 7):
+        for impl in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
             C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
             assert lib.molclr_gemm_bf16_impl(Ad.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N,
                                              K, K, N, epi, bd.data_ptr(), auxd.data_ptr(), N, None,

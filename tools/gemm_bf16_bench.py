@@ -4,6 +4,7 @@ molclr_gemm_bf16_impl / molclr_linear_wgrad_bf16_impl tile shapes vs torch.matmu
 
     python tools/gemm_bf16_bench.py [rows]
 """
+import os
 import sys
 from pathlib import Path
 
@@ -61,7 +62,7 @@ def main():
     for name, A, P, C, N, K, epi, bias, aux, ref in cases:
         fl = 2.0 * M * N * K
         res = []
-        for v in (-1, 2, 5, 6, 7):
+        for v in (int(a) for a in os.environ.get("IMPLS", "6,8,9").split(",")):
             t = timeit(lambda: lib.molclr_gemm_bf16_impl(A.data_ptr(), P.data_ptr(), C.data_ptr(), M,
                                                          N, K, K, N, epi, _lib.ptr(bias),
                                                          _lib.ptr(aux), N if aux is not None else 0,
