@@ -723,9 +723,10 @@ int molclr_linear_wgrad_bf16(const uint16_t* dy, const uint16_t* x, float* dW, f
                              int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
                              int64_t ld_x, int accumulate, void* workspace,
                              size_t workspace_bytes, molclr_stream_t stream);
-/* The same with the tile shape chosen per call (-1 = automatic): 0 = 128 x 128,
- * 1 = 256 x 256, 2 = 128 x 256 output tiles; each has its own split-K plan
- * (the workspace query covers all). */
+/* The same with the kernel chosen per call (-1 = automatic): 0 = 128 x 128,
+ * 1 = 256 x 256, 2 = 128 x 256 output tiles with register staging, 3 = 256 x
+ * 256 with both operands LDS-DMA staged (64-row K steps); each has its own
+ * split-K plan (the workspace query covers all). */
 int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t* x, float* dW, float* db,
                                   int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy,
                                   int64_t ld_x, int accumulate, void* workspace,

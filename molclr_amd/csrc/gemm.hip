@@ -1226,15 +1226,16 @@ __global__ void k_bplanes_make_batch(PlanesJobs jobs) {
 }
 
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
-// (and colsum[m] = Σ_z cs_partial[z][m] for t < M when cs_partial is given)
+// (and colsum[m] = Σ_{z < cs_splits} cs_partial[z][m] for t < M when cs_partial is given)
 template <int EPI>
 __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, int64_t M, int64_t N,
                                 float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
                                 const float* __restrict__ aux, int64_t ldaux, int accumulate,
-                                const float* __restrict__ cs_partial, float* __restrict__ colsum) {
+                                const float* __restrict__ cs_partial, int cs_splits,
+                                float* __restrict__ colsum) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  // Σ_z p[z * stride] in split order, sixteen partials in flight per round trip
-  auto ordered_sum = [splits](const float* __restrict__ p, int64_t stride) {
+  // Σ_z p[z * stride] for z < splits in order, sixteen partials in flight per round trip
+  auto ordered_sum = [](const float* __restrict__ p, int64_t stride, int splits) {
     float v = 0.f;
     int z = 0;
     for (; z + 16 <= splits; z += 16) {
@@ -1253,12 +1254,12 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
     return v;
   };
   if (cs_partial && t < M) {
-    const float c = ordered_sum(cs_partial + t, M);
+    const float c = ordered_sum(cs_partial + t, M, cs_splits);
     colsum[t] = accumulate ? colsum[t] + c : c;
   }
   if (t >= M * N) return;
   int64_t m = t / N, n = t - m * N;
-  float v = ordered_sum(partial + t, M * N);
+  float v = ordered_sum(partial + t, M * N, splits);
   if (EPI == MOLCLR_EPI_BIAS) v = v + bias[n];
   if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v + bias[n], 0.f);
   if (EPI == MOLCLR_EPI_RELU_MASK) v = aux[m * ldaux + n] > 0.f ? v : 0.f;
@@ -1554,7 +1555,7 @@ int run_w6(const float* A, const float* B, float* C, float* colsum, int64_t M, i
   molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>,
                        dim3((unsigned)molclr::ceil_div(M * N, 256)), dim3(256), 0, s,
                        static_cast<const float*>(part), p.splits, M, N, C, ldc, no_f, no_f,
-                       (int64_t)0, accumulate, static_cast<const float*>(cs_part), colsum);
+                       (int64_t)0, accumulate, static_cast<const float*>(cs_part), p.splits, colsum);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -1605,19 +1606,19 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
       switch (epilogue) {
         case MOLCLR_EPI_NONE:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>, g, dim3(256), 0, s,
-                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, sp, a.colsum);
           break;
         case MOLCLR_EPI_BIAS:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS>, g, dim3(256), 0, s,
-                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
+                               partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, sp, a.colsum);
           break;
         case MOLCLR_EPI_BIAS_RELU:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_BIAS_RELU>, g, dim3(256), 0,
-                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, sp, a.colsum);
           break;
         default:
           molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_RELU_MASK>, g, dim3(256), 0,
-                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, a.colsum);
+                               s, partial, sp, M, N, C, ldc, bias, aux, ldaux, accumulate, cs_partial, sp, a.colsum);
       }
     }
   }
@@ -1633,12 +1634,12 @@ int run_gemm(const Args& a0, int impl, bool bp, int a_kmajor, int b_kmajor, int 
 
 void molclr_splitk_reduce_none(const float* partial, int splits, int64_t M, int64_t N, float* C,
                                int64_t ldc, int accumulate, const float* cs_partial,
-                               float* colsum, hipStream_t s) {
+                               int cs_splits, float* colsum, hipStream_t s) {
   const float* no_f = nullptr;
   molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>,
                        dim3((unsigned)molclr::ceil_div(M * N > M ? M * N : M, 256)), dim3(256), 0,
                        s, partial, splits, M, N, C, ldc, no_f, no_f, (int64_t)0, accumulate,
-                       cs_partial, colsum);
+                       cs_partial, cs_splits, colsum);
 }
 
 MOLCLR_API size_t molclr_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K) {

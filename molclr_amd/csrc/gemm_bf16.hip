@@ -966,6 +966,187 @@ __global__ __launch_bounds__(64 * WM) void k_gemm_wb(
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_gemm_tw: the weight gradient part[split][m][n] = Σ_{k in split} A[k][m]
+// B[k][n] on 256 x 256 tiles with both K-major operands DMA-staged
+// (global_load_lds) into [64 k][256] images, two stages, the transposed LDS
+// read (kmfrag) building the MFMA fragments; 8 waves as 4 (M) x 2 (N), each a
+// 64 x 128 sub-tile -- k_gemm_tp's wave layout, with the k pairing of every
+// other bf16 kernel.  One image k-row is 512 B; the kswz XOR of its 16-byte
+// chunks is applied on the DMA source address and again by kmfrag.  A split's
+// last step may run past K: its rows at or past K are zeroed in LDS once the
+// DMA has landed.  CS: the column sums Σ_k A[k][m] (the bias gradient) are
+// taken from the A images, k-rows ≡ tn (mod ntn) by the block of column tile
+// tn, into cs_part[split * ntn + tn][m] (fixed order).
+// ---------------------------------------------------------------------------
+template <bool CS>
+__global__ __launch_bounds__(512) void k_gemm_tw(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, float* __restrict__ part,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int steps_per_split, int splits,
+    float* __restrict__ cs_part) {
+  constexpr int TM = 256, KT = 64;
+  constexpr int SI = KT * TM * 2;  // bytes per operand image per stage (32 KB)
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * SI];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 3, wn = wave >> 2;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + TM - 1) / TM);
+  const int ntiles = (int)((M + TM - 1) / TM) * ntn;
+  const int id = xcd_remap(blockIdx.x, ntiles * splits);  // a K slice's tiles share an XCD
+  const int split = id / ntiles, tile = id - split * ntiles;
+  const int tn = tile % ntn;
+  const int64_t m0 = (int64_t)(tile / ntn) * TM, n0 = (int64_t)tn * TM;
+  const int nk = (int)((K + KT - 1) / KT);
+  const int s_beg = split * steps_per_split;
+  const int ns = (s_beg + steps_per_split < nk ? s_beg + steps_per_split : nk) - s_beg;  // >= 1
+
+  // DMA: wave w fills 1 KB pieces 4w .. 4w+3 (k-rows 2p, 2p+1) of both images;
+  // lane L: k-row 2p + (L >> 5), slot L & 31 holds logical chunk slot ^ kswz
+  const uint16_t* asrc[4];
+  const uint16_t* bsrc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 2 * (4 * wave + q) + (lane >> 5);
+    const int c = (lane & 31) ^ (kswz<TM>(k) >> 3);
+    const int64_t am = m0 + 8 * c < M ? m0 + 8 * c : M - 8;
+    const int64_t bn = n0 + 8 * c < N ? n0 + 8 * c : N - 8;
+    asrc[q] = A + (int64_t)k * lda + am;
+    bsrc[q] = B + (int64_t)k * ldb + bn;
+  }
+  const int kq0 = 2 * 4 * wave + (lane >> 5);  // k-row of piece q: kq0 + 2q
+  auto stage = [&](int buf, int st) {
+    const int64_t k0 = (int64_t)(s_beg + st) * KT;
+    uint8_t* ia = lds + buf * 2 * SI + wave * 4096;
+    uint8_t* ib = ia + SI;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // rows past K re-read row K - 1 (zeroed in LDS before use)
+      const int64_t kk = k0 + kq0 + 2 * q < K ? k0 : K - 1 - (kq0 + 2 * q);
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(asrc[q] + kk * lda), (lds_as_ptr)(ia + 1024 * q), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)(bsrc[q] + kk * ldb), (lds_as_ptr)(ib + 1024 * q), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int buf) {
+    const uint16_t* ia = reinterpret_cast<const uint16_t*>(lds + buf * 2 * SI);
+    const uint16_t* ib = reinterpret_cast<const uint16_t*>(lds + buf * 2 * SI + SI);
+    bf16x8 fa[2][2], fb[2][4];
+    auto read = [&](int q, bf16x8(&a)[2], bf16x8(&b)[4]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = kmfrag<TM>(ia, 64 * wm + 32 * i, q, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = kmfrag<TM>(ib, 128 * wn + 32 * j, q, lane);
+    };
+    read(0, fa[0], fb[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < 3) read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
+                                                               0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // CS: thread t sums logical chunk (t & 31) (8 columns m) over the k-rows
+  // (t >> 5) + 16 j of every step that are ≡ tn (mod ntn)
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto colsum = [&](int buf) {
+    const uint8_t* ia = lds + buf * 2 * SI;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = (tid >> 5) + 16 * j;
+      if (k % ntn != tn) continue;
+      const int slot = (tid & 31) ^ (kswz<TM>(k) >> 3);
+      const u32x4 w = *reinterpret_cast<const u32x4*>(ia + k * (TM * 2) + 16 * slot);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        cs[2 * e] += bf16_to_f32(w[e] & 0xFFFFu);
+        cs[2 * e + 1] += bf16_to_f32(w[e] >> 16);
+      }
+    }
+  };
+
+  stage(0, 0);
+  __syncthreads();
+  int buf = 0;
+  for (int st = 0; st < ns; ++st) {
+    if (st + 1 < ns) stage(buf ^ 1, st + 1);
+    const int64_t k0 = (int64_t)(s_beg + st) * KT;
+    if (k0 + KT > K) {  // block-uniform: the last step of the last split
+      const int kv = (int)(K - k0);
+      uint8_t* ia = lds + buf * 2 * SI;
+      for (int u = tid; u < 2 * KT * 32; u += 512) {  // 16-byte slots of both images
+        const int img = u / (KT * 32), k = (u % (KT * 32)) / 32, sl = u % 32;
+        if (k >= kv) *reinterpret_cast<u32x4*>(ia + img * SI + k * (TM * 2) + 16 * sl) = u32x4{0u, 0u, 0u, 0u};
+      }
+      __syncthreads();
+    }
+    if constexpr (CS) colsum(buf);
+    compute(buf);
+    __syncthreads();  // step st + 1 has landed; buf is free
+    buf ^= 1;
+  }
+
+  if constexpr (CS) {
+    if (cs_part != nullptr) {
+      // fold the 16 k-row groups of each chunk in a fixed order through LDS
+      float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[e * 512 + tid] = cs[e];
+      __syncthreads();
+      if (tid < TM) {
+        const int c = tid >> 3, e = tid & 7;  // column m0 + tid = chunk c, element e
+        float v = 0.f;
+        for (int g = 0; g < 16; ++g) v += red[e * 512 + 32 * g + c];
+        const int64_t m = m0 + tid;
+        if (m < M) cs_part[((int64_t)split * ntn + tn) * M + m] = v;
+      }
+      __syncthreads();
+    }
+  }
+
+  // partial tile, per 32 x 32 block through the wave's own 4 KB of LDS, 16-byte stores
+  float* tw = reinterpret_cast<float*>(lds) + wave * 32 * 32;
+  float* P = part + (int64_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t mb = m0 + 64 * wm + 32 * i, nb = n0 + 128 * wn + 32 * j;
+      if (mb >= M || nb >= N) continue;  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tw[acc_row(r, lh) * 32 + li] = acc[i][j][r];
+      wave_lds_sync();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int idx = it * 64 + lane;
+        const int row = idx >> 3, c4 = idx & 7;
+        const int64_t m = mb + row, n = nb + 4 * c4;
+        if (m < M && n < N)
+          *reinterpret_cast<float4*>(P + m * N + n) =
+              *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
 // --------------------------------------------------------------------------- host side
 template <int WM, int WN, int TN, int D, bool MASK>
 int launch_qb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,
@@ -1097,15 +1278,30 @@ WbPlan wb_plan(int64_t M, int64_t N, int64_t K, int64_t bm, int64_t bn, int64_t 
   p.splits = (int)((nk + p.kps - 1) / p.kps);  // every split has >= 1 step
   return p;
 }
-// k_gemm_wb tile shapes (molclr_linear_wgrad_bf16_impl): 0 = 128 x 128 (4
-// waves), 1 = 256 x 256 (8 waves), 2 = 128 x 256 (4 waves)
-constexpr int kWbImpls = 3;
+// k_gemm_tw: 256 x 256 tiles over 64-row K steps, >= 4 steps per split
+WbPlan tw_plan(int64_t M, int64_t N, int64_t K) {
+  WbPlan p;
+  p.ntiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t nk = (K + 63) / 64;
+  int64_t s = 256 / p.ntiles;
+  if (s > nk / 4) s = nk / 4;
+  if (s < 1) s = 1;
+  p.kps = (int)((nk + s - 1) / s);
+  p.splits = (int)((nk + p.kps - 1) / p.kps);
+  return p;
+}
+// weight-gradient kernels (molclr_linear_wgrad_bf16_impl): k_gemm_wb with
+// 0 = 128 x 128 (4 waves), 1 = 256 x 256 (8 waves), 2 = 128 x 256 (4 waves);
+// 3 = k_gemm_tw (256 x 256, LDS-DMA staging)
+constexpr int kWbImpls = 4;
 WbPlan wb_plan_impl(int impl, int64_t M, int64_t N, int64_t K) {
+  if (impl == 3) return tw_plan(M, N, K);
   if (impl == 1) return wb_plan(M, N, K, 256, 256, 256);
   if (impl == 2) return wb_plan(M, N, K, 128, 256, 256);
   return wb_plan(M, N, K, 128, 128, 512);
 }
-int wb_default(int64_t M, int64_t N) { return M * N >= 512 * 512 ? 1 : 0; }
+// k_gemm_tw for the large c5 products (2-10 % faster than k_gemm_wb's 256 x 256 shape)
+int wb_default(int64_t M, int64_t N) { return M * N >= 512 * 512 ? 3 : 0; }
 
 template <int WM, int TN, bool MASK>
 void launch_wb(const WbPlan& p, bool cs, hipStream_t s, const uint16_t* dy, const uint16_t* x,
@@ -1195,7 +1391,8 @@ MOLCLR_API size_t molclr_linear_wgrad_bf16_workspace_bytes(int64_t rows, int64_t
   size_t need = 0;
   for (int impl = 0; impl < kWbImpls; ++impl) {
     const WbPlan p = wb_plan_impl(impl, n_out, n_in, rows);
-    const size_t b = (size_t)p.splits * (n_out * n_in + n_out) * sizeof(float) + 256;
+    const int64_t cs_rows = impl == 3 ? (n_in + 255) / 256 : 1;  // tw: per column tile
+    const size_t b = (size_t)p.splits * (n_out * n_in + cs_rows * n_out) * sizeof(float) + 256;
     need = b > need ? b : need;
   }
   return need;
@@ -1228,10 +1425,23 @@ MOLCLR_API int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t*
   float* part = static_cast<float*>(workspace);
   float* cs_part = db ? part + (size_t)p.splits * M * N : nullptr;
   const bool mask = K % BK != 0;
+  if (v == 3) {
+    const int ntn = (int)((N + 255) / 256);
+    const dim3 g((unsigned)(p.ntiles * p.splits)), b(512);
+    if (db)
+      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tw<true>, g, b, 0, s, dy, x, part, M, N, K, ld_dy,
+                           ld_x, p.kps, p.splits, cs_part);
+    else
+      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tw<false>, g, b, 0, s, dy, x, part, M, N, K, ld_dy,
+                           ld_x, p.kps, p.splits, cs_part);
+    molclr_splitk_reduce_none(part, p.splits, M, N, dW, N, accumulate, cs_part, p.splits * ntn, db, s);
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   if (v == 1) launch_wb_m<8, 8>(mask, p, db != nullptr, s, dy, x, part, M, N, K, ld_dy, ld_x, cs_part);
   else if (v == 2) launch_wb_m<4, 8>(mask, p, db != nullptr, s, dy, x, part, M, N, K, ld_dy, ld_x, cs_part);
   else launch_wb_m<4, 4>(mask, p, db != nullptr, s, dy, x, part, M, N, K, ld_dy, ld_x, cs_part);
-  molclr_splitk_reduce_none(part, p.splits, M, N, dW, N, accumulate, cs_part, db, s);
+  molclr_splitk_reduce_none(part, p.splits, M, N, dW, N, accumulate, cs_part, p.splits, db, s);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -100,8 +100,8 @@ __device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r 
 }  // namespace molclr
 
 // split-K partial reduction of the fp32 GEMMs (gemm.hip), shared with the bf16
-// weight-gradient GEMM: C (+)= Σ_z partial[z] (fixed order), colsum (+)= Σ_z
-// cs_partial[z] when cs_partial is given.
+// weight-gradient GEMM: C (+)= Σ_{z < splits} partial[z] (fixed order), colsum
+// (+)= Σ_{z < cs_splits} cs_partial[z] when cs_partial is given.
 void molclr_splitk_reduce_none(const float* partial, int splits, int64_t M, int64_t N, float* C,
                                int64_t ldc, int accumulate, const float* cs_partial,
-                               float* colsum, hipStream_t s);
+                               int cs_splits, float* colsum, hipStream_t s);

@@ -93,7 +93,7 @@ def test_gemm_bf16(dev, M, N, K):
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(55000, 1024, 512), (55000, 512, 1024), (777, 64, 128),
-                                             (8, 8, 16), (4096, 512, 256)])
+                                             (8, 8, 16), (4096, 512, 256), (3001, 264, 520)])
 @pytest.mark.parametrize("acc", [0, 1])
 def test_linear_wgrad_bf16(dev, rows, n_out, n_in, acc):
     lib = _lib.load()
@@ -115,7 +115,7 @@ def test_linear_wgrad_bf16(dev, rows, n_out, n_in, acc):
                                         n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_bytes,
                                         None) == 0
     assert rel(dW2, dy.double().t() @ x.double()) < TOL
-    for impl in (0, 1, 2):  # every tile shape and its split-K plan
+    for impl in (0, 1, 2, 3):  # every kernel / tile shape and its split-K plan
         dW3, db3 = W0.clone().to(dev), b0.clone().to(dev)
         assert lib.molclr_linear_wgrad_bf16_impl(dyd.data_ptr(), xd.data_ptr(), dW3.data_ptr(),
                                                  db3.data_ptr(), rows, n_out, n_in, n_out, n_in,

@@ -81,7 +81,7 @@ def main():
         dW = torch.empty(n_out, n_in, device=dev)
         db = torch.empty(n_out, device=dev)
         res = []
-        for v in (0, 1, 2):
+        for v in (1, 3):
             t = timeit(lambda: lib.molclr_linear_wgrad_bf16_impl(
                 dy.data_ptr(), x.data_ptr(), dW.data_ptr(), db.data_ptr(), M, n_out, n_in, n_out,
                 n_in, 0, ws.data_ptr(), ws_bytes, st, v))
