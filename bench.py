@@ -1,6 +1,6 @@
 """Contrastive pre-training throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c5] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c5] [--no-cpu-baseline]
                     [--augment host|device|subgraph|mix]
 
 A step is the reference's hot-loop iteration (molclr.py:108-128): two
@@ -11,7 +11,8 @@ before the timed region (SURVEY.md §8d generator; rank r uses seed r*10^6),
 rotated every step so repeated steps do not re-read one batch.
 
 Workloads: c2 = GIN 5x300, feat 512, batch 512 per GPU, fp32 (default; the
-config the metric is quoted on); c3 = GCN 5x300; c5 = GIN 5x512, bf16
+config the metric is quoted on); c1 = GIN 3x128, batch 64 (the reference's
+CPU-runnable case: its CPU baseline is cheap); c3 = GCN 5x300; c5 = GIN 5x512, bf16
 storage and MFMA with fp32 accumulation, batch 1024 per GPU, PubChem-shaped
 graphs.  Both views run through one paired encoder pass with per-view
 BatchNorm statistics (the reference's two calls).  N > 1 runs under torchrun,
@@ -56,6 +57,9 @@ HBM_PEAK_GBS = 8000.0
 FP32_MFMA_PEAK_TFS = 157.3
 
 CONFIGS = {
+    "c1": dict(model_type="gin", num_layer=3, emb_dim=128, feat_dim=512, batch=64,
+               shape="uniform", desc="c1: GIN 3x128 feat 512, batch 64, 10-50 atom graphs "
+                                     "(the reference's CPU-runnable case)"),
     "c2": dict(model_type="gin", num_layer=5, emb_dim=300, feat_dim=512, batch=512,
                shape="uniform", desc="c2: GIN 5x300 feat 512, batch 512/GPU, 10-50 atom graphs"),
     "c3": dict(model_type="gcn", num_layer=5, emb_dim=300, feat_dim=512, batch=512,
