@@ -44,7 +44,8 @@ def init(backend: str | None = None) -> tuple[int, int, torch.device]:
     """Initialise the default process group when WORLD_SIZE > 1.
 
     Returns (rank, world_size, device); backend defaults to "nccl" (RCCL) on
-    GPUs and "gloo" on CPU.
+    GPUs and "gloo" on CPU (MOLCLR_DIST_BACKEND overrides it: "gloo" lets
+    several ranks share one GPU, as the multi-process GPU test does).
     """
     rank, world, local = env_world()
     if torch.cuda.is_available():
@@ -55,7 +56,8 @@ def init(backend: str | None = None) -> tuple[int, int, torch.device]:
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        be = backend or ("nccl" if device.type == "cuda" else "gloo")
+        be = backend or os.environ.get("MOLCLR_DIST_BACKEND") or (
+            "nccl" if device.type == "cuda" else "gloo")
         kw = dict(backend=be, rank=rank, world_size=world)
         if be == "nccl":
             kw["device_id"] = device
