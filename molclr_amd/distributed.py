@@ -6,7 +6,8 @@ two exchanges per step, both chosen for a point-to-point xGMI fabric:
 1. NT-Xent over the GLOBAL contrastive batch (molclr_amd.ops._NTXent):
    one all-gather of each rank's normalised rows [zj_local; zi_local]
    ([2 B_local, C]) reordered into the reference's [zj_all; zi_all]
-   (gather_rows), and one of the per-row logsumexp (gather_lse).  Because the NT-Xent weight matrix
+   (gather_rows), and one of the per-row logsumexp with the rank's loss
+   share appended (gather_lse_and_sum).  Because the NT-Xent weight matrix
    W_rc = P_rc + P_cr - 2[c = p(r)] is symmetric, each rank then computes the
    exact gradient of its own rows locally: no column-gradient reduce-scatter.
 2. The SUM all-reduce of the flat gradient buffer (FusedAdam.flat_grad,
@@ -93,6 +94,17 @@ def gather_lse(local_lse: torch.Tensor, group=None) -> torch.Tensor:
     g = _all_gather_stack(local_lse, group)            # [W, 2 B_l]
     bl = g.shape[1] // 2
     return torch.cat([g[:, :bl].reshape(-1), g[:, bl:].reshape(-1)], 0)
+
+
+def gather_lse_and_sum(local_lse: torch.Tensor, local_sum: torch.Tensor, group=None):
+    """gather_lse and the SUM of a per-rank scalar (the loss share) in one
+    all-gather: ([2 B] lse in R's row order, Σ_ranks local_sum in rank order
+    -- the same value on every rank)."""
+    n = local_lse.shape[0]
+    g = _all_gather_stack(torch.cat([local_lse, local_sum.reshape(1).to(local_lse.dtype)]), group)
+    bl = n // 2
+    lse = torch.cat([g[:, :bl].reshape(-1), g[:, bl:n].reshape(-1)], 0)
+    return lse, g[:, n].sum()
 
 
 def global_row_index(b_local: int, rank: int, world: int, device) -> torch.Tensor:

@@ -727,9 +727,8 @@ class _NTXent(torch.autograd.Function):
         _lib.call("molclr_sum_f32", loss_rows.data_ptr(), loss.data_ptr(), n, st)
         if group is None:
             lse_cols = lse
-        else:
-            lse_cols = mdist.gather_lse(lse, group)
-            dist.all_reduce(loss, group=group)
+        else:  # one all-gather carries the row lse and the rank's loss share
+            lse_cols, loss = mdist.gather_lse_and_sum(lse, loss, group)
         ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols, sim)
         ctx.meta = (B, C, float(temperature), int(cosine))
         return loss

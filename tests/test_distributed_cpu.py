@@ -71,6 +71,11 @@ def _worker(rank, port, out_q):
     assert np.allclose(lse_cols, ntxent_math.rows_forward(cols, np.arange(2 * B), cols, B, T)[0])
     loss = torch.tensor([loss_rows.sum()])
     dist.all_reduce(loss)
+    # ops._NTXent's form: lse gather and the loss SUM in one all-gather
+    lse2, loss2 = mdist.gather_lse_and_sum(torch.from_numpy(lse),
+                                           torch.tensor(loss_rows.sum(), dtype=torch.float32))
+    assert np.array_equal(lse2.numpy(), lse_cols)
+    assert np.isclose(loss2.item(), loss.item(), rtol=1e-6)
     drh = ntxent_math.rows_backward(rh, gidx, cols, lse_cols, B, T)
     dR = ntxent_math.prep_bwd(drh, rh, nrm, True)
     # data sharding: disjoint, equally sized per-rank shards every epoch
