@@ -218,11 +218,16 @@ __device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb
   n = nn;
 }
 
-// Per segment and column: Chan-merge the segment's partials (kRedLanes
-// strided lanes, four partials in flight, then a fixed-order tree over the
-// lanes), update the running stats (segments in order), write save_mean /
-// save_invstd and the apply coefficients [seg][D].
+// Per segment and column: Chan-merge the segment's partials, update the
+// running stats (segments in order), write save_mean / save_invstd and the
+// apply coefficients [seg][D].  Segments are reduced two at a time side by
+// side: lanes [0, kSegLanes) of a column take segment s0, the others s0 + 1;
+// a lane folds the partials p = lane (mod kSegLanes), four in flight, then
+// each half is combined by a fixed-order tree (a one-segment call reduces
+// its segment exactly as a pair does: every result bit-identical).
 // grid = ceil(D/kRedCols), block = kRedCols * kRedLanes.
+constexpr int kSegLanes = kRedLanes / 2;
+
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
     const float* __restrict__ pmean, const float* __restrict__ pm2, const float* __restrict__ pn,
     Segs sg, int64_t D, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -232,20 +237,22 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
   __shared__ float rn[kRedLanes][kRedCols], rm[kRedLanes][kRedCols], rq[kRedLanes][kRedCols];
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += sg.n;  // num_batches_tracked
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int half = rl / kSegLanes, sl = rl % kSegLanes;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
-  for (int s = 0; s < sg.n; ++s) {
-    const int64_t P = sg.part0[s + 1] - sg.part0[s];
-    const float* sm = pmean + sg.part0[s] * D;
-    const float* sq = pm2 + sg.part0[s] * D;
-    const float* sn = pn + sg.part0[s];
+  for (int s0 = 0; s0 < sg.n; s0 += 2) {
+    const int s = s0 + half;
     float n = 0.f, mean = 0.f, m2 = 0.f;
-    if (c < D) {
-      int64_t p = rl;
-      for (; p + 3 * kRedLanes < P; p += 4 * kRedLanes) {
+    if (s < sg.n && c < D) {
+      const int64_t P = sg.part0[s + 1] - sg.part0[s];
+      const float* sm = pmean + sg.part0[s] * D;
+      const float* sq = pm2 + sg.part0[s] * D;
+      const float* sn = pn + sg.part0[s];
+      int64_t p = sl;
+      for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
         float bn[4], bm[4], bq[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int64_t q = p + u * kRedLanes;
+          const int64_t q = p + u * kSegLanes;
           bn[u] = sn[q];
           bm[u] = sm[q * D + c];
           bq[u] = sq[q * D + c];
@@ -253,16 +260,16 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
 #pragma unroll
         for (int u = 0; u < 4; ++u) chan1(n, mean, m2, bn[u], bm[u], bq[u]);
       }
-      for (; p < P; p += kRedLanes) chan1(n, mean, m2, sn[p], sm[p * D + c], sq[p * D + c]);
+      for (; p < P; p += kSegLanes) chan1(n, mean, m2, sn[p], sm[p * D + c], sq[p * D + c]);
     }
-    __syncthreads();  // the previous segment's tree is done with the arrays
+    __syncthreads();  // the previous pair's trees are done with the arrays
     rn[rl][cl] = n;
     rm[rl][cl] = mean;
     rq[rl][cl] = m2;
     __syncthreads();
 #pragma unroll
-    for (int stride = kRedLanes / 2; stride > 0; stride >>= 1) {
-      if (rl < stride) {
+    for (int stride = kSegLanes / 2; stride > 0; stride >>= 1) {
+      if (sl < stride) {
         chan1(n, mean, m2, rn[rl + stride][cl], rm[rl + stride][cl], rq[rl + stride][cl]);
         rn[rl][cl] = n;
         rm[rl][cl] = mean;
@@ -271,19 +278,24 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
       __syncthreads();
     }
     if (rl == 0 && c < D) {
-      float var = m2 / n;
-      float invstd = 1.0f / sqrtf(var + eps);
-      save_mean[s * D + c] = mean;
-      save_invstd[s * D + c] = invstd;
-      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-      if (running_var) {
-        float unbiased = n > 1.f ? m2 / (n - 1.f) : var;
-        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+      for (int h = 0; h < 2 && s0 + h < sg.n; ++h) {  // segment order
+        const int ss = s0 + h;
+        const float nn = rn[h * kSegLanes][cl], mu = rm[h * kSegLanes][cl];
+        const float q2 = rq[h * kSegLanes][cl];
+        const float var = q2 / nn;
+        const float invstd = 1.0f / sqrtf(var + eps);
+        save_mean[ss * D + c] = mu;
+        save_invstd[ss * D + c] = invstd;
+        if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+        if (running_var) {
+          const float unbiased = nn > 1.f ? q2 / (nn - 1.f) : var;
+          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+        }
+        float sc, sh;
+        bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mu, invstd, sc, sh);
+        scale[ss * D + c] = sc;
+        shift[ss * D + c] = sh;
       }
-      float sc, sh;
-      bn_coeffs(gamma ? gamma[c] : 1.f, beta ? beta[c] : 0.f, mean, invstd, sc, sh);
-      scale[s * D + c] = sc;
-      shift[s * D + c] = sh;
     }
   }
 }
@@ -405,31 +417,63 @@ __global__ void k_bn_bwd_partial(const typename St::T* __restrict__ dy,
 }
 
 // dgamma / dbeta: Σ over segments in segment order (added to the existing
-// value when accumulate); k1 / k2 [seg][D] per segment.
+// value when accumulate); k1 / k2 [seg][D] per segment.  Segment pairs side
+// by side as in k_bn_stats_final.
 __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
     const float* __restrict__ p1, const float* __restrict__ p2, Segs sg, int64_t D,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ k1,
     float* __restrict__ k2, int accumulate) {
   __shared__ float ra[kRedLanes][kRedCols], rb[kRedLanes][kRedCols];
   const int cl = threadIdx.x % kRedCols, rl = threadIdx.x / kRedCols;
+  const int half = rl / kSegLanes, sl = rl % kSegLanes;
   const int64_t c = (int64_t)blockIdx.x * kRedCols + cl;
-  for (int s = 0; s < sg.n; ++s) {
-    const int64_t P = sg.part0[s + 1] - sg.part0[s];
-    float a = 0.f, b = 0.f;
-    if (c < D) {
-      a = lane_fold(p1 + sg.part0[s] * D, P, D, c, rl);
-      b = lane_fold(p2 + sg.part0[s] * D, P, D, c, rl);
+  for (int s0 = 0; s0 < sg.n; s0 += 2) {
+    const int s = s0 + half;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+    if (s < sg.n && c < D) {
+      const int64_t P = sg.part0[s + 1] - sg.part0[s];
+      const float* q1 = p1 + sg.part0[s] * D;
+      const float* q2 = p2 + sg.part0[s] * D;
+      int64_t p = sl;
+      for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
+        a0 += q1[p * D + c];
+        a1 += q1[(p + kSegLanes) * D + c];
+        a2 += q1[(p + 2 * kSegLanes) * D + c];
+        a3 += q1[(p + 3 * kSegLanes) * D + c];
+        b0 += q2[p * D + c];
+        b1 += q2[(p + kSegLanes) * D + c];
+        b2 += q2[(p + 2 * kSegLanes) * D + c];
+        b3 += q2[(p + 3 * kSegLanes) * D + c];
+      }
+      for (; p < P; p += kSegLanes) {
+        a0 += q1[p * D + c];
+        b0 += q2[p * D + c];
+      }
     }
+    float a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
+    __syncthreads();  // the previous pair's trees are done with the arrays
+    ra[rl][cl] = a;
+    rb[rl][cl] = b;
     __syncthreads();
-    a = lane_tree_sum(ra, rl, cl, a);
-    b = lane_tree_sum(rb, rl, cl, b);
+#pragma unroll
+    for (int stride = kSegLanes / 2; stride > 0; stride >>= 1) {
+      if (sl < stride) {
+        ra[rl][cl] = a = a + ra[rl + stride][cl];
+        rb[rl][cl] = b = b + rb[rl + stride][cl];
+      }
+      __syncthreads();
+    }
     if (rl == 0 && c < D) {
-      const float inv_rows = 1.0f / (float)(sg.row0[s + 1] - sg.row0[s]);
-      const bool add = accumulate || s > 0;
-      if (dbeta) dbeta[c] = add ? dbeta[c] + a : a;
-      if (dgamma) dgamma[c] = add ? dgamma[c] + b : b;
-      k1[s * D + c] = a * inv_rows;
-      k2[s * D + c] = b * inv_rows;
+      for (int h = 0; h < 2 && s0 + h < sg.n; ++h) {  // segment order
+        const int ss = s0 + h;
+        const float sa = ra[h * kSegLanes][cl], sb = rb[h * kSegLanes][cl];
+        const float inv_rows = 1.0f / (float)(sg.row0[ss + 1] - sg.row0[ss]);
+        const bool add = accumulate || ss > 0;
+        if (dbeta) dbeta[c] = add ? dbeta[c] + sa : sa;
+        if (dgamma) dgamma[c] = add ? dgamma[c] + sb : sb;
+        k1[ss * D + c] = sa * inv_rows;
+        k2[ss * D + c] = sb * inv_rows;
+      }
     }
   }
 }
