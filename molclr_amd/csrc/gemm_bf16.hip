@@ -477,16 +477,19 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
         b[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(ib + t128(rb + 32 * j, c)));
     };
     read(0, fa[0], fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (q < 3) read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
                                                                0, 0);
+      if (q < 3) {
+        read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+        interleave_mfma_reads<TI * TJ, TI + TJ>();
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1049,16 +1052,19 @@ __global__ __launch_bounds__(512) void k_gemm_tw(
       for (int j = 0; j < 4; ++j) b[j] = kmfrag<TM>(ib, 128 * wn + 32 * j, q, lane);
     };
     read(0, fa[0], fb[0]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (q < 3) read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
                                                                0, 0);
+      if (q < 3) {
+        read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
+        interleave_mfma_reads<8, 12>();  // kmfrag: two transposed reads per fragment
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };

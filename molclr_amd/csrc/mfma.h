@@ -94,6 +94,24 @@ __device__ __forceinline__ bf16x8 kmfrag(const uint16_t* __restrict__ plane, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Scheduling of one group of MFMAs: NM MFMAs with the NEXT group's NR LDS
+// fragment reads threaded between them (one MFMA, then ceil(NR / NM) reads,
+// ...).  The group's first MFMA then waits only for reads issued a whole
+// group earlier, and the new reads' latency hides under the MFMAs -- left
+// to itself the compiler issued every read of two substeps first and waited
+// for all of them (s_waitcnt lgkmcnt(0)) before the first MFMA.
+template <int NM, int NR, int K = 0>
+__device__ __forceinline__ void interleave_mfma_reads() {
+  if constexpr (K < NM) {
+    constexpr int per = (NR + NM - 1) / NM;
+    constexpr int left = NR - K * per;
+    constexpr int n = left < per ? left : per;
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+    if constexpr (n > 0) __builtin_amdgcn_sched_group_barrier(0x100, n, 0);  // then DS reads
+    interleave_mfma_reads<NM, NR, K + 1>();
+  }
+}
+
 // row of register r of a 32x32 MFMA accumulator, lane half lh
 __device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 
