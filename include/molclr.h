@@ -356,6 +356,44 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
                                int64_t ld_x, int accumulate, void* workspace,
                                size_t workspace_bytes, molclr_stream_t stream, int groups);
 
+/* "h3" fp32 GEMMs: three fp16 MFMA products per element pair instead of six
+ * bf16 ones.  Each operand is scaled by a power of two chosen from its
+ * tensor-wide max |x| (scaled max in [2^14, 2^15)) and split into two
+ * round-to-nearest fp16 parts, x 2^s = hi + lo + t with |t| <= 2^-22 |x 2^s|;
+ * hi_a hi_b + hi_a lo_b + lo_a hi_b accumulates in fp32 and is scaled back
+ * exactly.  Same epilogues and shapes as the q6 / w6 kernels they replace
+ * (models/ginet_molclr.py:19-23: the GIN MLP forward, data and weight
+ * gradients).
+ *   A max slot is 64 floats whose max is the tensor's max |x| (producers
+ *     spread their atomic maxima over the entries).
+ *   molclr_absmax_f32: slot <- max |x| over a [rows][cols] (ld) matrix
+ *     (accumulate != 0: folded into the current slot; else the slot is reset
+ *     first).  The max is order-independent, so every producer of the same
+ *     tensor gives the same slot value.
+ *   molclr_hplanes_make_batch: weights as h3 B operands (molclr_bplanes_make_batch
+ *     arguments): [2][Npad][Kp] fp16 planes, then the max |B| slot,
+ *     molclr_hplanes_bytes(N, K) bytes each.
+ *   molclr_gemm_f32_h3: C = epilogue(A B) for a row-major A [M][K] (lda) with
+ *     its max slot `amax` and h3 planes of B; K <= 1024, K and lda multiples
+ *     of 4.  cmax (may be NULL): max |C| of the stored values folded into
+ *     *cmax (atomic max; the caller resets it).
+ *   molclr_linear_wgrad_h3: molclr_linear_wgrad given the max slots of dy
+ *     and x (n_out, n_in, ld_dy, ld_x multiples of 4; same workspace). */
+int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* slot,
+                      int accumulate, molclr_stream_t stream);
+size_t molclr_hplanes_bytes(int64_t N, int64_t K);
+int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N,
+                              const int64_t* K, const int64_t* ldb, const int* b_kmajor,
+                              uint16_t* const* planes, molclr_stream_t stream);
+int molclr_gemm_f32_h3(const float* A, const float* amax, const uint16_t* hplanes, float* C,
+                       int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
+                       int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
+                       float* cmax, molclr_stream_t stream);
+int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
+                           const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
+                           int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
+                           void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);
 int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, int64_t ld,
@@ -554,6 +592,12 @@ typedef struct molclr_gin_encoder {
    * mixed-precision switch (molclr.py:16-24,93-96,121-123).  h_out / dh_out
    * are then bf16. */
   int32_t dtype;
+  /* fp32 storage only: 0 = split-bf16 "x6" GEMMs (the *_planes fields are
+   * molclr_bplanes_make images); 1 = "h3" GEMMs (molclr_gemm_f32_h3 /
+   * molclr_linear_wgrad_h3; the *_planes fields are molclr_hplanes_make_batch
+   * images, 2 dim <= 1024).  The max |x| slots of agg / a1 live in the arena,
+   * those of dz / dz1 in the workspace. */
+  int32_t fp32_gemm;
 } molclr_gin_encoder;
 
 /* Gradient buffers, same shapes as the parameters; NULL = not needed. */

@@ -67,6 +67,13 @@ SIGNATURES = {
                                     _P]),
     "molclr_linear_wgrad_groups": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
                                            c_size_t, _P, c_int]),
+    "molclr_absmax_f32": (c_int, [_P, _I64, _I64, _I64, _P, c_int, _P]),
+    "molclr_hplanes_bytes": (c_size_t, [_I64, _I64]),
+    "molclr_hplanes_make_batch": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P]),
+    "molclr_gemm_f32_h3": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P,
+                                   _I64, _P, _P]),
+    "molclr_linear_wgrad_h3": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
+                                       _P, c_size_t, _P]),
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_colsum_f32": (c_int, [_P, _P, _I64, _I64, _I64, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_workspace_bytes": (c_size_t, [_I64, _I64]),
@@ -159,7 +166,7 @@ class GinEncoder(ctypes.Structure):
                             "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias",
                             "bn_running_mean", "bn_running_var", "bn_num_batches_tracked",
                             "mlp0_planes", "mlp0_planes_t", "mlp2_planes", "mlp2_planes_t")] + [
-        ("dtype", ctypes.c_int32)]
+        ("dtype", ctypes.c_int32), ("fp32_gemm", ctypes.c_int32)]
 
 
 class GinEncoderGrads(ctypes.Structure):

@@ -198,3 +198,24 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// A tensor's max |x| "slot" (molclr_absmax_f32) is kMaxSlotParts floats whose
+// max is the value: producers spread their atomics over the entries (one
+// address would serialise thousands of them), consumers fold all entries.
+constexpr int kMaxSlotParts = 64;
+
+// Folds a lane's max |x| (v >= 0) into a slot: block max through LDS, then one
+// global atomic max on the float's bits (ordered like the values for v >= 0)
+// into entry blockIdx.x % 64.  Every thread of the block must call it (a
+// block barrier inside).
+__device__ __forceinline__ void absmax_publish(float v, float* slot) {
+  __shared__ float red_[16];
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red_[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)((blockDim.x + 63) >> 6); ++w) v = fmaxf(v, red_[w]);
+    atomicMax(reinterpret_cast<unsigned int*>(slot + blockIdx.x % kMaxSlotParts),
+              __float_as_uint(v));
+  }
+}

@@ -22,7 +22,7 @@ namespace {
 struct ArenaLayout {
   size_t agg[MOLCLR_MAX_LAYERS], a1[MOLCLR_MAX_LAYERS], z[MOLCLR_MAX_LAYERS],
       h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS], invstd[MOLCLR_MAX_LAYERS];
-  size_t h0, ec, total;
+  size_t h0, ec, smax, total;
   ArenaLayout(int L, int64_t N, int64_t D, size_t es) {
     size_t used = 0;
     auto off = [&](size_t bytes) {
@@ -40,6 +40,7 @@ struct ArenaLayout {
     }
     h0 = off(N * D * es);
     ec = off((size_t)L * MOLCLR_NUM_ECOMB * D * sizeof(float));
+    smax = off((size_t)MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float));  // h3: max |agg_l|, |a1_l|
     total = used;
   }
 };
@@ -126,9 +127,14 @@ MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, in
   return ArenaLayout(L, N, D, elem_bytes(dtype)).total;
 }
 
+// workspace: backward scratch | h3 max slots of dz_l / dz1_l (256 B) | the
+// entry points' workspace
+constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float);
+
 MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
   (void)L;
-  return scratch_bytes(N, D, elem_bytes(dtype)) + 256 + kernels_ws(N, D) + 256;
+  return molclr::align_up(scratch_bytes(N, D, elem_bytes(dtype)), 256) + kSlotBytes +
+         kernels_ws(N, D) + 256;
 }
 
 MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t* x,
@@ -150,8 +156,16 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   char* A = (char*)arena;
   auto F = [&](size_t off) { return (float*)(A + off); };
   auto H = [&](size_t off) { return (uint16_t*)(A + off); };
-  void* kws = (char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256);
+  void* kws = (char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) + kSlotBytes;
   const size_t kws_bytes = kernels_ws(N, D);
+  const bool h3 = !bf && e->fp32_gemm == 1;
+  const bool h3w = !bf && e->fp32_gemm == 2;  // h3 weight gradients only
+  float* fmax = F(lay.smax);  // h3: [l][0] = max |agg_l|, [l][1] = max |a1_l|
+  if ((h3 || h3w) && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+                hipSuccess) {
+    molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
+    return MOLCLR_ERR_ARG;
+  }
 
   void* h = A + lay.h0;
   if (bf)
@@ -184,13 +198,30 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
       float *agg = F(lay.agg[l]), *a1 = F(lay.a1[l]), *z = F(lay.z[l]);
       MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
                                            Ecl, agg, N, D, stream));
-      // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
-      MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
-                                         MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
-                                         kws_bytes, stream));
-      MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
-                                         MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
-                                         kws_bytes, stream));
+      if (h3) {
+        // GINEConv.update in h3 (ops._MLP): max |agg| by a pass, max |a1| from
+        // the first GEMM's epilogue
+        float* sl = fmax + 2 * l * kMaxSlotParts;
+        const uint16_t* p0 = e->mlp0_planes[l];
+        const uint16_t* p2 = e->mlp2_planes[l];
+        MOLCLR_TRY(molclr_absmax_f32(agg, N, D, D, sl, 1, stream));
+        MOLCLR_TRY(molclr_gemm_f32_h3(agg, sl, p0, a1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_BIAS_RELU,
+                                      e->mlp0_bias[l], nullptr, 0, sl + kMaxSlotParts, stream));
+        MOLCLR_TRY(molclr_gemm_f32_h3(a1, sl + kMaxSlotParts, p2, z, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_BIAS,
+                                      e->mlp2_bias[l], nullptr, 0, nullptr, stream));
+      } else {
+        // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
+        MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
+                                           MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
+                                           kws_bytes, stream));
+        MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
+                                           MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
+                                           kws_bytes, stream));
+        if (h3w) {
+          MOLCLR_TRY(molclr_absmax_f32(agg, N, D, D, fmax + 2 * l * kMaxSlotParts, 1, stream));
+          MOLCLR_TRY(molclr_absmax_f32(a1, N, 2 * D, 2 * D, fmax + (2 * l + 1) * kMaxSlotParts, 1, stream));
+        }
+      }
       MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
                                           e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
                                           F(lay.mean[l]), F(lay.invstd[l]), seg.n, seg.rows, D,
@@ -228,9 +259,19 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   void* dz = S + (size_t)N * D * es;         // w.r.t. the BatchNorm input z
   void* dagg = S + 2 * (size_t)N * D * es;   // w.r.t. the aggregation output
   void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
-  void* kws = S + molclr::align_up(scratch_bytes(N, D, es), 256);
+  float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
+  void* kws = (char*)bmax + kSlotBytes;
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
+  const bool h3 = !bf && e->fp32_gemm == 1;
+  const bool h3w = !bf && e->fp32_gemm == 2;
+  const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
+  // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
+  if ((h3 || h3w) && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+                hipSuccess) {
+    molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
+    return MOLCLR_ERR_ARG;
+  }
 
   const void* dy = dh_out;
   for (int l = L - 1; l >= 0; --l) {
@@ -265,6 +306,50 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                                 g->nbr_t, g->ecount, (uint16_t*)dh,
                                                 gr->edge_embedding1[l], gr->edge_embedding2[l], N,
                                                 D, 1, kws, kws_bytes, stream));
+    } else if (h3) {
+      // ops._MLP's h3 backward: dW2 (+db2), dz1 (ReLU mask of a1; max |dz1|
+      // from the epilogue), dW1 (+db1), dagg
+      const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
+      float* sl = bmax + 2 * l * kMaxSlotParts;
+      const float* fl = fmax + 2 * l * kMaxSlotParts;
+      MOLCLR_REQUIRE(gr->mlp2_weight[l] && gr->mlp2_bias[l] && gr->mlp0_weight[l] &&
+                         gr->mlp0_bias[l],
+                     "gin_encoder_bwd: h3 needs every MLP gradient");
+      MOLCLR_TRY(molclr_absmax_f32(fz, N, D, D, sl, 1, stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l], gr->mlp2_bias[l],
+                                        N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_h3(fz, sl, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
+                                    2 * D, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D, sl + kMaxSlotParts,
+                                    stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl, gr->mlp0_weight[l],
+                                        gr->mlp0_bias[l], N, 2 * D, D, 2 * D, D, 1, kws, kws_bytes,
+                                        stream));
+      MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, sl + kMaxSlotParts, e->mlp0_planes_t[l], (float*)dagg,
+                                    N, D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE, nullptr, nullptr, 0,
+                                    nullptr, stream));
+      MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
+                                           g->ecount, (float*)dh, gr->edge_embedding1[l],
+                                           gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));
+    } else if (h3w) {
+      const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
+      float* sl = bmax + 2 * l * kMaxSlotParts;
+      const float* fl = fmax + 2 * l * kMaxSlotParts;
+      MOLCLR_TRY(molclr_absmax_f32(fz, N, D, D, sl, 1, stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l], gr->mlp2_bias[l],
+                                        N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(fz, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
+                                         2 * D, 0, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D, kws,
+                                         kws_bytes, stream));
+      MOLCLR_TRY(molclr_absmax_f32((const float*)dz1, N, 2 * D, 2 * D, sl + kMaxSlotParts, 1, stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl, gr->mlp0_weight[l],
+                                        gr->mlp0_bias[l], N, 2 * D, D, 2 * D, D, 1, kws, kws_bytes,
+                                        stream));
+      MOLCLR_TRY(molclr_gemm_f32_bplanes((const float*)dz1, e->mlp0_planes_t[l], (float*)dagg, N,
+                                         D, 2 * D, 2 * D, D, 0, MOLCLR_EPI_NONE, nullptr, nullptr,
+                                         0, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
+                                           g->ecount, (float*)dh, gr->edge_embedding1[l],
+                                           gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));
     } else {
       const float *fz = (const float*)dz, *fa1 = (const float*)a1;
       // second Linear (ops.linear_bwd order: dW with db, dx with the ReLU mask of a1)

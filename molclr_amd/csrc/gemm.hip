@@ -336,7 +336,7 @@ struct PStageK {
 // 4 x 4 blocks transposed in registers into the [row][k] image, spent 60 % of
 // its LDS cycles in bank conflicts: rows 4 apart share banks.)
 // Needs ROWS == 64, rows % 4 == 0 and ld % 4 == 0.
-template <int ROWS, int T>
+template <int ROWS, int T, bool H3 = false>
 struct PStageM {
   static_assert(ROWS == 64 || ROWS == 128 || ROWS == 160,
                 "K-major staging is laid out for 64/128/160-row tiles");
@@ -380,18 +380,26 @@ struct PStageM {
       cs[j] = f4add(cs[j], r[j]);
     }
   }
-  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t) const {
+  // H3: two fp16 planes of the values scaled by 2^sh; else three bf16 planes
+  __device__ __forceinline__ void store(uint16_t* __restrict__ img, int t, int sh = 0) const {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = t + j * T;
       if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
       const int rb = u % (ROWS / 4), k = u / (ROWS / 4);
-      uint2 hi, mid, lo;
-      split4(r[j], hi, mid, lo);
       const int o = k * ROWS + ((4 * rb) ^ kswz<ROWS>(k));
-      *reinterpret_cast<uint2*>(img + o) = hi;
-      *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
-      *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
+      if constexpr (H3) {
+        uint2 hi, lo;
+        hsplit4(r[j], sh, hi, lo);
+        *reinterpret_cast<uint2*>(img + o) = hi;
+        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = lo;
+      } else {
+        uint2 hi, mid, lo;
+        split4(r[j], hi, mid, lo);
+        *reinterpret_cast<uint2*>(img + o) = hi;
+        *reinterpret_cast<uint2*>(img + ROWS * XK + o) = mid;
+        *reinterpret_cast<uint2*>(img + 2 * ROWS * XK + o) = lo;
+      }
     }
   }
 };
@@ -730,9 +738,9 @@ constexpr int64_t kQ6MaxK = 1024;  // longer chains of one fp32 sum: see above
 
 // pre-split planes [3][npad][kp] -> LDS image [3][BN][XK]; unit = (plane, row,
 // 16-byte chunk), rows clamped into the planes (columns >= N are never stored)
-template <int BN, int T>
+template <int BN, int T, int NP = 3>
 struct QStageB {
-  static constexpr int UNITS = 3 * BN * 4;
+  static constexpr int UNITS = NP * BN * 4;
   static constexpr int PER = (UNITS + T - 1) / T;
   u32x4 r[PER];
   int goff[PER];
@@ -775,15 +783,21 @@ struct QStageB {
 // address, so the compiler keeps counted vmcnt waits and the next steps'
 // loads stay in flight across the MFMAs (a conditional load makes it drain
 // every outstanding load at the top of each step).
-template <int TN, int EPI, int KG, bool MASK>
+// H3: the fp16 two-part form (mfma.h "h3"): A scaled by its max slot `amax`
+// and split into 2 parts, the planes are 2 fp16 parts of B scaled by `bmax`,
+// three fp16 MFMAs per product; the sums are scaled back in the epilogue,
+// which also folds max |C| into `cmax` when given (the next product's amax).
+template <int TN, int EPI, int KG, bool MASK, bool H3 = false>
 __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
-    int accumulate) {
+    int accumulate, const float* __restrict__ amax, const float* __restrict__ bmax,
+    float* __restrict__ cmax) {
   constexpr int T = 64 * kQ6Waves;  // threads of one K group
   constexpr int BN = 32 * TN;
-  constexpr int BI = 3 * BN * XK;  // bf16 elements per B image
+  constexpr int NP = H3 ? 2 : 3;    // B planes
+  constexpr int BI = NP * BN * XK;  // 16-bit elements per B image
   static_assert(kQ6Waves * 32 * 32 * (int)sizeof(float) <= 2 * BI * (int)sizeof(uint16_t),
                 "epilogue tiles exceed the LDS images");
   static_assert(KG == 1 || (kQ6Waves * 32 * BN * (int)sizeof(float) <=
@@ -832,6 +846,8 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
+  const int sha = H3 ? h3_shift(amax) : 0;
+  const int shc = H3 ? -(sha + h3_shift(bmax)) : 0;  // epilogue scale-back
   auto compute = [&](const uint16_t* Bs, const float4(&a)[4], int r) {
     float4 am4[4];
 #pragma unroll
@@ -844,6 +860,21 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      if constexpr (H3) {
+        u32x4 h, l;
+        hsplit8(am4[2 * s], am4[2 * s + 1], sha, h, l);
+        const f16x8 ah = __builtin_bit_cast(f16x8, h);
+        const f16x8 al = __builtin_bit_cast(f16x8, l);
+        const int ch = 2 * lh + s;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int row = 32 * b + li;
+          const f16x8 bh = __builtin_bit_cast(f16x8, xfrag(Bs, row, ch));
+          const f16x8 bl = __builtin_bit_cast(f16x8, xfrag(Bs + BN * XK, row, ch));
+          acc[b] = mfma_h3(ah, al, bh, bl, acc[b]);
+        }
+        continue;
+      }
       u32x4 h, m, l;
       split8(am4[2 * s], am4[2 * s + 1], h, m, l);
       const bf16x8 ah = __builtin_bit_cast(bf16x8, h);
@@ -866,7 +897,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     }
   };
 
-  QStageB<BN, T> sb;
+  QStageB<BN, T, NP> sb;
   sb.init(n0, npad, kp, gt);
   uint16_t* buf0 = lds + grp * 2 * BI;
   uint16_t* buf1 = buf0 + BI;
@@ -929,13 +960,16 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
   float* tw = reinterpret_cast<float*>(lds) + wm * 32 * 32;
   const int64_t mw = m0 + 32 * wm;
+  float cm = 0.f;  // max |C| of this lane's stores (H3 with cmax)
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int64_t nb = n0 + 32 * b;
     if (nb >= N) break;  // block-uniform
     if (grp == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+      for (int r = 0; r < 16; ++r)
+        tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] =
+            H3 ? __builtin_ldexpf(acc[b][r], shc) : acc[b][r];
     }
     __syncthreads();
     if (grp == 0) {
@@ -961,6 +995,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
           }
           if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
           *reinterpret_cast<float4*>(o) = v;
+          if (H3) cm = fmaxf(cm, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         } else {
           const float e[4] = {v4.x, v4.y, v4.z, v4.w};
           for (int j = 0; j < 4 && n + j < N; ++j) {
@@ -970,12 +1005,14 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
             if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
             if (accumulate) x += o[j];
             o[j] = x;
+            if (H3) cm = fmaxf(cm, fabsf(x));
           }
         }
       }
     }
     __syncthreads();  // the wave's tile is rewritten by the next block
   }
+  if (H3 && cmax != nullptr) absmax_publish(grp == 0 ? cm : 0.f, cmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -1002,20 +1039,23 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 // ---------------------------------------------------------------------------
 constexpr int kW6BM = 128;
 
-template <int TN, bool CS, int KG>
+// H3: both operands scaled by their max slots and split into two fp16 parts
+// (mfma.h "h3"), three fp16 MFMAs per product, partials scaled back.
+template <int TN, bool CS, int KG, bool H3 = false>
 __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_w6(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ part,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int ktiles_per_split, int splits,
-    float* __restrict__ cs_part) {
+    float* __restrict__ cs_part, const float* __restrict__ amax, const float* __restrict__ bmax) {
   constexpr int T = 256;  // threads of one K group
   constexpr int BM = kW6BM, BN = 32 * TN;
-  constexpr int AI = 3 * BM * XK, BI = 3 * BN * XK;  // bf16 elements per image
+  constexpr int NP = H3 ? 2 : 3;                       // planes per operand
+  constexpr int AI = NP * BM * XK, BI = NP * BN * XK;  // 16-bit elements per image
   static_assert(4 * 32 * 32 * (int)sizeof(float) <= (AI + BI) * (int)sizeof(uint16_t),
                 "epilogue tiles exceed the LDS image");
-  static_assert(KG == 1 || (4 * 32 * BN * (int)sizeof(float) <=
-                            KG * (AI + BI) * (int)sizeof(uint16_t)),
-                "group sums exceed the LDS images");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[KG * (AI + BI)];
+  // the images, or the group sums (4 waves x 32 x BN fp32) when those are larger
+  constexpr int GS = KG > 1 ? 4 * 32 * BN * 2 : 0;
+  constexpr int LDS_ELEMS = KG * (AI + BI) > GS ? KG * (AI + BI) : GS;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_ELEMS];
 
   const int tid = threadIdx.x;
   const int grp = tid / T, gt = tid - grp * T;
@@ -1042,8 +1082,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
-  using SA = PStageM<BM, T>;
-  using SB = PStageM<BN, T>;
+  using SA = PStageM<BM, T, H3>;
+  using SB = PStageM<BN, T, H3>;
+  const int sha = H3 ? h3_shift(amax) : 0, shb = H3 ? h3_shift(bmax) : 0;
   SA sa;
   SB sb;
   sa.init(A, lda, m0, M, gt);
@@ -1060,6 +1101,17 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
   auto compute = [&]() {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if constexpr (H3) {
+        const f16x8 ah = __builtin_bit_cast(f16x8, kmfrag<BM>(As, 32 * wave, ks, lane));
+        const f16x8 al = __builtin_bit_cast(f16x8, kmfrag<BM>(As + BM * XK, 32 * wave, ks, lane));
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const f16x8 bh = __builtin_bit_cast(f16x8, kmfrag<BN>(Bs, 32 * b, ks, lane));
+          const f16x8 bl = __builtin_bit_cast(f16x8, kmfrag<BN>(Bs + BN * XK, 32 * b, ks, lane));
+          acc[b] = mfma_h3(ah, al, bh, bl, acc[b]);
+        }
+        continue;
+      }
       const bf16x8 ah = kmfrag<BM>(As, 32 * wave, ks, lane);
       const bf16x8 am = kmfrag<BM>(As + BM * XK, 32 * wave, ks, lane);
       const bf16x8 al = kmfrag<BM>(As + 2 * BM * XK, 32 * wave, ks, lane);
@@ -1093,8 +1145,8 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
       const int i = q >> 1;
       if ((q & 1) == 0) {
         if constexpr (CS) sa.colsum_add(cs, gt);
-        sa.store(img, gt);
-        sb.store(img + AI, gt);
+        sa.store(img, gt, sha);
+        sb.store(img + AI, gt, shb);
       } else {
         if (i + 1 < ns) {
           sa.load(kof(i + 1), K, gt);
@@ -1163,7 +1215,9 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
     if (nb >= N) break;  // block-uniform
     if (grp == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] = acc[b][r];
+      for (int r = 0; r < 16; ++r)
+        tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] =
+            H3 ? __builtin_ldexpf(acc[b][r], -(sha + shb)) : acc[b][r];
     }
     __syncthreads();
     if (grp == 0) {
@@ -1223,6 +1277,77 @@ __global__ void k_bplanes_make_batch(PlanesJobs jobs) {
   jb.planes[t] = (uint16_t)(h & 0xFFFFu);
   jb.planes[ps + t] = (uint16_t)(m & 0xFFFFu);
   jb.planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
+}
+
+// h3 planes: [2][Npad][Kp] fp16 (hi, lo of B(k, n) 2^sh), zero beyond (N, K),
+// then the max |B| slot (kMaxSlotParts floats), which sets sh.  The max kernel
+// gives each job one block per slot entry, each storing its partial (plain
+// stores: no zeroing, no atomics).
+constexpr int kHMaxParts = kMaxSlotParts;
+__global__ __launch_bounds__(256) void k_hplanes_max_batch(PlanesJobs jobs) {
+  const PlanesJob& jb = jobs.j[blockIdx.y];
+  // B stored [rows][cols]: rows = N (kmajor 0) or K (kmajor 1)
+  const int64_t rows = jb.kmajor ? jb.K : jb.N, cols = jb.kmajor ? jb.N : jb.K;
+  float m = 0.f;
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
+    for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) m = fmaxf(m, fabsf(jb.B[r * jb.ldb + c]));
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x] =
+        fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+// one thread per (n, 8 k) of the padded grid: two 16-byte plane stores
+__global__ __launch_bounds__(256) void k_hplanes_make_batch(PlanesJobs jobs) {
+  const PlanesJob& jb = jobs.j[blockIdx.y];
+  const int64_t ps = jb.npad * jb.kp;
+  const int sh = h3_shift(reinterpret_cast<const float*>(jb.planes + 2 * ps));
+  const int kc = (int)(jb.kp >> 3);  // 8-k chunks per row
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= jb.npad * kc) return;
+  const int64_t n = t / kc;
+  const int64_t k0 = 8 * (t - n * kc);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t k = k0 + j;
+    v[j] = (n < jb.N && k < jb.K) ? (jb.kmajor ? jb.B[k * jb.ldb + n] : jb.B[n * jb.ldb + k]) : 0.f;
+  }
+  u32x4 h, l;
+  hsplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), sh, h, l);
+  *reinterpret_cast<u32x4*>(jb.planes + n * jb.kp + k0) = h;
+  *reinterpret_cast<u32x4*>(jb.planes + ps + n * jb.kp + k0) = l;
+}
+
+// max |x| over a [rows][cols] (ld) fp32 matrix, folded into *slot.  A dense
+// matrix (ld == cols) is one flat range, float4 when aligned; else one block
+// row at a time.  No 64-bit division per element.
+__global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int64_t rows,
+                                                int64_t cols, int64_t ld, float* __restrict__ slot) {
+  float m = 0.f;
+  if (ld == cols) {
+    const int64_t n = rows * cols;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+      const float4* x4 = reinterpret_cast<const float4*>(x);
+      const int64_t n4 = n >> 2;
+      for (; t < n4; t += stride) {
+        const float4 v = x4[t];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+      for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        m = fmaxf(m, fabsf(x[i]));
+    } else {
+      for (; t < n; t += stride) m = fmaxf(m, fabsf(x[t]));
+    }
+  } else {
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
+      for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) m = fmaxf(m, fabsf(x[r * ld + c]));
+  }
+  absmax_publish(m, slot);
 }
 
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
@@ -1313,6 +1438,9 @@ struct Args {
   const uint16_t* Bp = nullptr;  // pre-split planes (molclr_gemm_f32_bplanes)
   int64_t bps = 0;               // their plane stride
   float* colsum = nullptr;       // Σ_k A(m, k) out (molclr_linear_wgrad; K-major A, p6)
+  const float* amax = nullptr;   // h3: max |A| / max |B| slots, max |C| out (may be null)
+  const float* bmax = nullptr;
+  float* cmax = nullptr;
 };
 
 template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1, bool CS = false>
@@ -1433,14 +1561,14 @@ int q6_groups(int64_t M, int64_t N, int64_t K) {
   return (q6_blocks(M, N) < 384 && (K + BK - 1) / BK >= 8) ? 2 : 1;
 }
 
-template <int TN, int EPI, int KG, bool MASK>
+template <int TN, int EPI, int KG, bool MASK, bool H3>
 void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK>),
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK, H3>),
                        dim3((unsigned)q6_blocks(a.M, a.N)), dim3(KG * 64 * kQ6Waves), 0, s, a.A,
                        a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux,
-                       a.accumulate);
+                       a.accumulate, a.amax, a.bmax, a.cmax);
 }
-template <int TN, int EPI>
+template <int TN, int EPI, bool H3>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
   const int64_t nsteps = (a.K + BK - 1) / BK;
   const int kg = q6_groups(a.M, a.N, a.K);
@@ -1448,31 +1576,38 @@ void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
   // the end for some K groups
   const bool mask = a.K % BK != 0 || nsteps % kg != 0;
   if (kg == 2) {
-    if (mask) launch_q6_t<TN, EPI, 2, true>(a, npad, s);
-    else launch_q6_t<TN, EPI, 2, false>(a, npad, s);
+    if (mask) launch_q6_t<TN, EPI, 2, true, H3>(a, npad, s);
+    else launch_q6_t<TN, EPI, 2, false, H3>(a, npad, s);
   } else {
-    if (mask) launch_q6_t<TN, EPI, 1, true>(a, npad, s);
-    else launch_q6_t<TN, EPI, 1, false>(a, npad, s);
+    if (mask) launch_q6_t<TN, EPI, 1, true, H3>(a, npad, s);
+    else launch_q6_t<TN, EPI, 1, false, H3>(a, npad, s);
   }
 }
 
-template <int TN>
+template <int TN, bool H3>
 int dispatch_q6(int epi, const Args& a, int64_t npad, hipStream_t s) {
   switch (epi) {
-    case MOLCLR_EPI_NONE: launch_q6<TN, MOLCLR_EPI_NONE>(a, npad, s); return 0;
-    case MOLCLR_EPI_BIAS: launch_q6<TN, MOLCLR_EPI_BIAS>(a, npad, s); return 0;
-    case MOLCLR_EPI_BIAS_RELU: launch_q6<TN, MOLCLR_EPI_BIAS_RELU>(a, npad, s); return 0;
-    case MOLCLR_EPI_RELU_MASK: launch_q6<TN, MOLCLR_EPI_RELU_MASK>(a, npad, s); return 0;
+    case MOLCLR_EPI_NONE: launch_q6<TN, MOLCLR_EPI_NONE, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS: launch_q6<TN, MOLCLR_EPI_BIAS, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS_RELU: launch_q6<TN, MOLCLR_EPI_BIAS_RELU, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_RELU_MASK: launch_q6<TN, MOLCLR_EPI_RELU_MASK, H3>(a, npad, s); return 0;
     default: return -1;
   }
 }
 
-// a.ldb = kp (the planes' row pitch), a.Bp = the planes
-int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s) {
+// a.ldb = kp (the planes' row pitch), a.Bp = the planes; h3: fp16 two-part
+// planes and a.amax / a.bmax set
+int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, bool h3 = false) {
   const int tn = wide_tn(a.N);
-  const int rc = tn == 5 ? dispatch_q6<5>(epi, a, npad, s)
-                 : tn == 4 ? dispatch_q6<4>(epi, a, npad, s)
-                           : dispatch_q6<2>(epi, a, npad, s);
+  int rc;
+  if (h3)
+    rc = tn == 5 ? dispatch_q6<5, true>(epi, a, npad, s)
+         : tn == 4 ? dispatch_q6<4, true>(epi, a, npad, s)
+                   : dispatch_q6<2, true>(epi, a, npad, s);
+  else
+    rc = tn == 5 ? dispatch_q6<5, false>(epi, a, npad, s)
+         : tn == 4 ? dispatch_q6<4, false>(epi, a, npad, s)
+                   : dispatch_q6<2, false>(epi, a, npad, s);
   if (rc) {
     molclr::set_error("gemm_f32_bplanes: no q6 kernel for epilogue %d", epi);
     return MOLCLR_ERR_UNSUPPORTED;
@@ -1521,36 +1656,46 @@ size_t w6_ws_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
   return need;
 }
 
-template <int TN, int KG>
+template <int TN, int KG, bool H3>
 void launch_w6_kg(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
-                  int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part) {
+                  int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part,
+                  const float* amax, const float* bmax) {
   const dim3 grid((unsigned)(p.ntiles * p.splits));
   if (cs_part)
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true, KG>), grid, dim3(256 * KG), 0, s,
-                         A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true, KG, H3>), grid, dim3(256 * KG), 0,
+                         s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part, amax, bmax);
   else
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false, KG>), grid, dim3(256 * KG), 0,
-                         s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part);
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false, KG, H3>), grid, dim3(256 * KG),
+                         0, s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part, amax, bmax);
 }
-template <int TN>
+template <int TN, bool H3>
 void launch_w6(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
-               int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part) {
-  if (p.kg == 2) launch_w6_kg<TN, 2>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
-  else launch_w6_kg<TN, 1>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+               int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part,
+               const float* amax, const float* bmax) {
+  if (p.kg == 2) launch_w6_kg<TN, 2, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  else launch_w6_kg<TN, 1, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
 }
 
 // C (+)= A^T B over K-major A [K][M] (lda) and B [K][N] (ldb); colsum (+)= Σ_k A
 // when non-null.  Partial tiles in the workspace, then the fixed-order reduce.
+// amax / bmax given: the h3 form (both max slots needed).
 int run_w6(const float* A, const float* B, float* C, float* colsum, int64_t M, int64_t N,
            int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int accumulate, void* ws,
-           size_t ws_bytes, hipStream_t s, int kg = 2) {
+           size_t ws_bytes, hipStream_t s, int kg = 2, const float* amax = nullptr,
+           const float* bmax = nullptr) {
   const W6Plan p = w6_plan(M, N, K, kg);
   MOLCLR_REQUIRE_WS(ws_bytes, w6_ws_bytes(M, N, K, colsum != nullptr));
   float* part = static_cast<float*>(ws);
   float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
-  if (p.tn == 5) launch_w6<5>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
-  else if (p.tn == 4) launch_w6<4>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
-  else launch_w6<2>(p, s, A, B, part, M, N, K, lda, ldb, cs_part);
+  if (amax) {
+    if (p.tn == 5) launch_w6<5, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+    else if (p.tn == 4) launch_w6<4, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+    else launch_w6<2, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  } else {
+    if (p.tn == 5) launch_w6<5, false>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+    else if (p.tn == 4) launch_w6<4, false>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+    else launch_w6<2, false>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  }
   const float* no_f = nullptr;
   molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce<MOLCLR_EPI_NONE>,
                        dim3((unsigned)molclr::ceil_div(M * N, 256)), dim3(256), 0, s,
@@ -1808,7 +1953,7 @@ MOLCLR_API size_t molclr_linear_wgrad_workspace_bytes(int64_t rows, int64_t n_ou
   const size_t fused = sp > 1 ? (size_t)sp * (M * N + M) * sizeof(float) + 256 : 0;
   const size_t cs = molclr_colsum_ws(rows, n_out);
   need = fused > need ? fused : need;
-  if (w6_shape_ok(M, N, K)) {
+  if (M % 4 == 0 && N % 4 == 0 && M * N < (1ll << 28)) {  // w6 (and its h3 form at any K)
     const size_t w6 = w6_ws_bytes(M, N, K, true);
     need = w6 > need ? w6 : need;
   }
@@ -1859,4 +2004,113 @@ MOLCLR_API int molclr_linear_wgrad(const float* dy, const float* x, float* dW, f
                                    size_t workspace_bytes, molclr_stream_t stream) {
   return molclr_linear_wgrad_groups(dy, x, dW, db, rows, n_out, n_in, ld_dy, ld_x, accumulate,
                                     workspace, workspace_bytes, stream, 2);
+}
+
+// ---------------------------------------------------------------------------
+// h3 entry points (mfma.h "h3": three fp16 MFMAs per product with per-tensor
+// power-of-two scaling; see include/molclr.h)
+// ---------------------------------------------------------------------------
+MOLCLR_API int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                                 float* slot, int accumulate, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && slot, "absmax_f32: bad arguments");
+  hipStream_t s = molclr::as_stream(stream);
+  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotParts * sizeof(float), s);
+  if (rows > 0 && cols > 0) {
+    MOLCLR_REQUIRE(x, "absmax_f32: null x");
+    int64_t blocks = ld == cols ? molclr::ceil_div(rows * cols, 256 * 16) : rows;
+    blocks = blocks < 1 ? 1 : blocks > 1024 ? 1024 : blocks;
+    hipLaunchKernelGGL(k_absmax, dim3((unsigned)blocks), dim3(256), 0, s, x, rows, cols, ld, slot);
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API size_t molclr_hplanes_bytes(int64_t N, int64_t K) {
+  return (size_t)2 * planes_npad(N) * planes_kp(K) * sizeof(uint16_t) + kHMaxParts * sizeof(float);
+}
+
+MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N,
+                                         const int64_t* K, const int64_t* ldb,
+                                         const int* b_kmajor, uint16_t* const* planes,
+                                         molclr_stream_t stream) {
+  MOLCLR_REQUIRE(count >= 0 && (count == 0 || (B && N && K && ldb && b_kmajor && planes)),
+                 "hplanes_make_batch: null arrays");
+  for (int base = 0; base < count; base += kPlanesBatch) {
+    PlanesJobs jobs{};
+    const int n = count - base < kPlanesBatch ? count - base : kPlanesBatch;
+    int64_t most = 0;
+    for (int i = 0; i < n; ++i) {
+      const int q = base + i;
+      MOLCLR_REQUIRE(N[q] > 0 && K[q] > 0 && B[q] && planes[q],
+                     "hplanes_make_batch: job %d empty or null", q);
+      MOLCLR_REQUIRE(b_kmajor[q] ? ldb[q] >= N[q] : ldb[q] >= K[q],
+                     "hplanes_make_batch: job %d leading dimension too small", q);
+      jobs.j[i] = PlanesJob{B[q], planes[q], N[q], K[q], ldb[q], planes_npad(N[q]), planes_kp(K[q]),
+                            b_kmajor[q]};
+      const int64_t e = jobs.j[i].npad * jobs.j[i].kp;
+      most = e > most ? e : most;
+    }
+    hipStream_t s = molclr::as_stream(stream);
+    hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)n), dim3(256), 0, s, jobs);
+    hipLaunchKernelGGL(k_hplanes_make_batch, dim3((unsigned)molclr::ceil_div(most / 8, 256), (unsigned)n),
+                       dim3(256), 0, s, jobs);
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, const uint16_t* hplanes,
+                                  float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                  int64_t ldc, int epilogue_flags, const float* bias,
+                                  const float* aux, int64_t ldaux, float* cmax,
+                                  molclr_stream_t stream) {
+  const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
+  const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
+  MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_h3: negative size");
+  MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
+                 "gemm_f32_h3: bad epilogue %d", epilogue);
+  MOLCLR_REQUIRE((epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU) || bias,
+                 "gemm_f32_h3: bias epilogue needs bias");
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux, "gemm_f32_h3: relu-mask epilogue needs aux");
+  MOLCLR_REQUIRE(K % 4 == 0 && lda % 4 == 0 && lda >= K && ldc >= N,
+                 "gemm_f32_h3: K and lda multiples of 4, lda >= K, ldc >= N");
+  MOLCLR_REQUIRE(K <= kQ6MaxK, "gemm_f32_h3: K %lld > %lld", (long long)K, (long long)kQ6MaxK);
+  if (M == 0 || N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(K > 0 && A && amax && hplanes && C, "gemm_f32_h3: null operand or K == 0");
+  const int64_t npad = planes_npad(N), kp = planes_kp(K);
+  MOLCLR_REQUIRE(2 * npad * kp < (1ll << 31) && q6_blocks(M, N) < (1ll << 31),
+                 "gemm_f32_h3: too large");
+  Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, 9};
+  a.Bp = hplanes;
+  a.bps = npad * kp;
+  a.amax = amax;
+  a.bmax = reinterpret_cast<const float*>(hplanes + 2 * npad * kp);
+  a.cmax = cmax;
+  return run_q6(a, npad, epilogue, molclr::as_stream(stream), true);
+}
+
+MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
+                                      const float* xmax, float* dW, float* db, int64_t rows,
+                                      int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
+                                      int accumulate, void* workspace, size_t workspace_bytes,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rows >= 0 && n_out > 0 && n_in > 0, "linear_wgrad_h3: bad sizes");
+  MOLCLR_REQUIRE(dy && dymax && x && xmax && dW, "linear_wgrad_h3: null pointer");
+  MOLCLR_REQUIRE(ld_dy >= n_out && ld_x >= n_in, "linear_wgrad_h3: leading dimension too small");
+  MOLCLR_REQUIRE(n_out % 4 == 0 && n_in % 4 == 0 && ld_dy % 4 == 0 && ld_x % 4 == 0 &&
+                     n_out * n_in < (1ll << 28),
+                 "linear_wgrad_h3: sizes and leading dimensions must be multiples of 4");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_linear_wgrad_workspace_bytes(rows, n_out, n_in));
+  hipStream_t s = molclr::as_stream(stream);
+  if (rows == 0) {
+    if (!accumulate) {
+      (void)hipMemsetAsync(dW, 0, (size_t)n_out * n_in * sizeof(float), s);
+      if (db) (void)hipMemsetAsync(db, 0, (size_t)n_out * sizeof(float), s);
+    }
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  MOLCLR_REQUIRE_WS(workspace_bytes, w6_ws_bytes(n_out, n_in, rows, db != nullptr));
+  return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
+                workspace_bytes, s, 2, dymax, xmax);
 }

@@ -64,6 +64,60 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4& hi
   lo = u32x4{l[0], l[1], l[2], l[3]};
 }
 
+// ---------------------------------------------------------------------------
+// "h3": fp32 products from THREE fp16 MFMAs instead of six bf16 ones.
+// An operand is scaled by a power of two 2^sh chosen from its tensor-wide
+// max |x| (so the scaled max lies in [2^14, 2^15), below fp16's 65504) and
+// split into hi = fp16(x 2^sh) and lo = fp16(x 2^sh - hi) (round to nearest,
+// the subtraction is exact): x 2^sh = hi + lo + t with |t| <= 2^-22 |x 2^sh|
+// while lo is an fp16 normal, i.e. for every element within 2^-17 of the
+// tensor's max (smaller ones keep an absolute error below 2^-38 max |x|).
+// hi_a hi_b + hi_a lo_b + lo_a hi_b then reproduces a b to ~3 2^-22, and the
+// fp32 sums are scaled back by 2^-(sh_a + sh_b) (exact).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Scale exponent of a tensor from its max |x| slot (kMaxSlotParts entries,
+// molclr_absmax_f32): 0 for a zero / NaN / infinite max (NaN and inf then
+// propagate as in fp32).  Every lane of the wave must call it.
+__device__ __forceinline__ int h3_shift(const float* __restrict__ slot) {
+  const float m = wave_max(slot[threadIdx.x & (kMaxSlotParts - 1)]);
+  if (!(m > 0.f) || !(m <= 3.402823466e38f)) return 0;
+  return 15 - __builtin_amdgcn_frexp_expf(m);  // m = f 2^e, f in [0.5, 1)
+}
+
+__device__ __forceinline__ void hsplit2(float a, float b, int sh, uint32_t& h, uint32_t& l) {
+  a = __builtin_ldexpf(a, sh);
+  b = __builtin_ldexpf(b, sh);
+  const f16x2 hh = {(_Float16)a, (_Float16)b};
+  const f16x2 ll = {(_Float16)(a - (float)hh[0]), (_Float16)(b - (float)hh[1])};
+  h = __builtin_bit_cast(uint32_t, hh);
+  l = __builtin_bit_cast(uint32_t, ll);
+}
+
+__device__ __forceinline__ void hsplit4(float4 v, int sh, uint2& hi, uint2& lo) {
+  hsplit2(v.x, v.y, sh, hi.x, lo.x);
+  hsplit2(v.z, v.w, sh, hi.y, lo.y);
+}
+
+__device__ __forceinline__ void hsplit8(const float4 a, const float4 b, int sh, u32x4& hi,
+                                        u32x4& lo) {
+  uint32_t h[4], l[4];
+  hsplit2(a.x, a.y, sh, h[0], l[0]);
+  hsplit2(a.z, a.w, sh, h[1], l[1]);
+  hsplit2(b.x, b.y, sh, h[2], l[2]);
+  hsplit2(b.z, b.w, sh, h[3], l[3]);
+  hi = u32x4{h[0], h[1], h[2], h[3]};
+  lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+// the three fp16 products of an (a, b) element pair, small terms first
+__device__ __forceinline__ f32x16 mfma_h3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
+}
+
 // K-major [k][ROWS] image planes (the dY^T / X^T operands of a weight
 // gradient), read with the gfx950 transposed LDS read.  32-element XOR of
 // k-row k: separates the 4 k-rows one transposed read touches (64-row rows

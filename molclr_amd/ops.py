@@ -25,6 +25,7 @@ from __future__ import annotations
 import torch
 
 import ctypes
+import os
 import functools
 import weakref
 
@@ -188,13 +189,19 @@ def bump_param_generation() -> None:
     PARAM_GENERATION[0] += 1
 
 
-def weight_planes(W, N, K, ldb, b_kmajor) -> torch.Tensor:
-    """Split-bf16 planes of B(k, n) stored in W (molclr_gemm_f32's B layout).
+_PLANE_FNS = {"x6": ("molclr_bplanes_bytes", "molclr_bplanes_make_batch"),
+              "h3": ("molclr_hplanes_bytes", "molclr_hplanes_make_batch")}
+
+
+def weight_planes(W, N, K, ldb, b_kmajor, kind: str = "x6") -> torch.Tensor:
+    """B(k, n) stored in W (molclr_gemm_f32's B layout) as a GEMM operand image:
+    kind "x6" = split-bf16 planes (molclr_bplanes_make), "h3" = fp16 two-part
+    planes and their max slot (molclr_hplanes_make_batch).
 
     After an optimizer step every cached image is stale: the first lookup
-    regenerates all live ones in one batched launch (molclr_bplanes_make_batch),
-    not one launch per weight and orientation."""
-    key = (W.data_ptr(), N, K, ldb, int(b_kmajor))
+    regenerates all live ones in one batched launch per kind, not one launch
+    per weight and orientation."""
+    key = (W.data_ptr(), N, K, ldb, int(b_kmajor), kind)
     gen = PARAM_GENERATION[0]
     ent = _PLANES.get(key)
     if ent is not None and ent[1]() is W and ent[0] == (W._version, gen):
@@ -207,37 +214,100 @@ def weight_planes(W, N, K, ldb, b_kmajor) -> torch.Tensor:
     if len(_PLANES) > 512:  # drop entries of dead tensors
         for k in [k for k, e in _PLANES.items() if e[1]() is None]:
             del _PLANES[k]
-    nbytes = _wsq("molclr_bplanes_bytes", N, K)
+    nbytes = _wsq(_PLANE_FNS[kind][0], N, K)
     planes = torch.empty(nbytes // 2, dtype=torch.int16, device=W.device)
-    _lib.call("molclr_bplanes_make", W.data_ptr(), N, K, ldb, int(b_kmajor), planes.data_ptr(),
-              _stream(W))
+    _make_planes(kind, [(W, (N, K, ldb, int(b_kmajor)), planes)])
     _PLANES[key] = ((W._version, gen), weakref.ref(W), (N, K, ldb, int(b_kmajor)), planes)
     return planes
 
 
+def _make_planes(kind, jobs) -> None:
+    n = len(jobs)
+    arr = lambda vals, ct: (ct * n)(*vals)  # noqa: E731
+    _lib.call(_PLANE_FNS[kind][1], n,
+              arr([j[0].data_ptr() for j in jobs], ctypes.c_void_p),
+              arr([j[1][0] for j in jobs], ctypes.c_int64),
+              arr([j[1][1] for j in jobs], ctypes.c_int64),
+              arr([j[1][2] for j in jobs], ctypes.c_int64),
+              arr([j[1][3] for j in jobs], ctypes.c_int),
+              arr([j[2].data_ptr() for j in jobs], ctypes.c_void_p), _stream(jobs[0][2]))
+
+
 def _refresh_planes(gen: int) -> None:
     """Regenerate every live cached image of an older generation, batched."""
-    jobs = []
+    jobs = {}
     for k, (tok, ref, shape, planes) in list(_PLANES.items()):
         W = ref()
         if W is None:
             del _PLANES[k]
             continue
         if tok[1] != gen and W.data_ptr() == k[0]:
-            jobs.append((k, W, shape, planes))
-    if not jobs:
-        return
-    n = len(jobs)
-    arr = lambda vals, ct: (ct * n)(*vals)  # noqa: E731
-    _lib.call("molclr_bplanes_make_batch", n,
-              arr([j[1].data_ptr() for j in jobs], ctypes.c_void_p),
-              arr([j[2][0] for j in jobs], ctypes.c_int64),
-              arr([j[2][1] for j in jobs], ctypes.c_int64),
-              arr([j[2][2] for j in jobs], ctypes.c_int64),
-              arr([j[2][3] for j in jobs], ctypes.c_int),
-              arr([j[3].data_ptr() for j in jobs], ctypes.c_void_p), _stream(jobs[0][3]))
-    for k, W, shape, planes in jobs:
-        _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, planes)
+            jobs.setdefault(k[5], []).append((k, W, shape, planes))
+    for kind, js in jobs.items():
+        _make_planes(kind, [(W, shape, planes) for _, W, shape, planes in js])
+        for k, W, shape, planes in js:
+            _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, planes)
+
+
+# fp32 GEMMs of the GIN MLP (forward, data and weight gradients): "h3" = three
+# fp16 MFMAs per product with per-tensor power-of-two scaling (molclr_gemm_f32_h3,
+# molclr_linear_wgrad_h3), "x6" = six split-bf16 MFMAs.  The encoder executor
+# reads the same switch, so both paths issue identical kernels.
+FP32_GEMM = os.environ.get("MOLCLR_FP32_GEMM", "x6")
+
+
+MAX_SLOT = 64  # floats per max |x| slot (molclr_absmax_f32)
+
+
+def absmax(x, out=None, accumulate=0) -> torch.Tensor:
+    """max |x| of a row-major fp32 matrix into a device max slot (MAX_SLOT
+    floats whose max is the value)."""
+    if out is None:
+        out = torch.empty(MAX_SLOT, dtype=torch.float32, device=x.device)
+    rows, cols = x.shape
+    _lib.call("molclr_absmax_f32", x.data_ptr(), rows, cols, x.stride(0), out.data_ptr(),
+              int(accumulate), _stream(x))
+    return out
+
+
+def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None):
+    """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3; cmax (a
+    zeroed slot) receives max |C|."""
+    _check(A, W)
+    M = A.shape[0]
+    planes = weight_planes(W, N, K, ldb, b_kmajor, "h3")
+    out = torch.empty(M, N, dtype=torch.float32, device=A.device)
+    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), planes.data_ptr(),
+              out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
+              _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax), _stream(A))
+    if _TIMER is not None:
+        _TIMER.add("gemm_f32", 2.0 * M * N * K)
+    return out
+
+
+def linear_wgrad_h3(dy, dymax, x, xmax, W_param, b_param):
+    """dW = dy^T x and db = Σ dy by molclr_linear_wgrad_h3 (into the FusedAdam
+    .grad when it owns them).  Returns (dW, db) as linear_bwd does."""
+    M, K = x.shape
+    N = dy.shape[1]
+    wbuf, wacc, dW = _grad_sink(W_param, (N, K), dy.device)
+    bbuf, bacc, db = _grad_sink(b_param, (N,), dy.device)
+    if wacc != bacc:
+        wbuf, wacc, dW = _grad_sink(None, (N, K), dy.device)
+        bbuf, bacc, db = _grad_sink(None, (N,), dy.device)
+    ws_bytes = _wsq("molclr_linear_wgrad_workspace_bytes", M, N, K)
+    ws = _ws(ws_bytes, dy.device)
+    _lib.call("molclr_linear_wgrad_h3", dy.data_ptr(), dymax.data_ptr(), x.data_ptr(),
+              xmax.data_ptr(), wbuf.data_ptr(), bbuf.data_ptr(), M, N, K, dy.stride(0),
+              x.stride(0), wacc, ws.data_ptr(), ws_bytes, _stream(dy))
+    if _TIMER is not None:
+        _TIMER.add("gemm_f32", 2.0 * M * N * K)
+    return dW, db
+
+
+def h3_ok(rows, D) -> bool:
+    """Shapes the h3 GIN-MLP GEMMs take (else the x6 kernels run)."""
+    return FP32_GEMM in ("h3", "h3w") and D % 4 == 0 and 2 * D <= 1024 and rows > 0
 
 
 def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
@@ -443,8 +513,18 @@ class _MLP(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, b2):
         _check(x, W1, b1, W2, b2)
         x = _c(x)
-        a1 = linear_fwd(x, W1, b1, relu=True)
-        z = linear_fwd(a1, W2, b2, relu=False)
+        M, D = x.shape
+        ctx.h3 = FP32_GEMM == "h3" and h3_ok(M, D) and W1.shape == (2 * D, D) and W2.shape == (D, 2 * D)
+        if ctx.h3:
+            # h3: max |x| by a pass, max |a1| from the first GEMM's epilogue
+            slots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=x.device)
+            absmax(x, slots[0], accumulate=1)
+            a1 = gemm_h3(x, slots[0], W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1, cmax=slots[1])
+            z = gemm_h3(a1, slots[1], W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2)
+            ctx.slots = slots
+        else:
+            a1 = linear_fwd(x, W1, b1, relu=True)
+            z = linear_fwd(a1, W2, b2, relu=False)
         ctx.save_for_backward(x, W1, W2, a1)
         ctx.params = (W1, b1, W2, b2)
         return z
@@ -455,6 +535,19 @@ class _MLP(torch.autograd.Function):
         pW1, pb1, pW2, pb2 = ctx.params
         dz = _c(dz)
         need = ctx.needs_input_grad
+        if ctx.h3 and all(need[1:]):
+            # the executor's h3 order: dW2 (+db2), dz1 (relu mask of a1, max |dz1|
+            # from its epilogue), dW1 (+db1), dx
+            D = x.shape[1]
+            slots = ctx.slots
+            bslots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=dz.device)
+            absmax(dz, bslots[0], accumulate=1)
+            dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
+            dz1 = gemm_h3(dz, bslots[0], W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
+                          cmax=bslots[1])
+            dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
+            dx = gemm_h3(dz1, bslots[1], W1, D, 2 * D, D, 1) if need[0] else None
+            return dx, dW1, db1, dW2, db2
         # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
         dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],
                                    relu_mask_src=a1, W_param=pW2, b_param=pb2)
@@ -776,6 +869,10 @@ class _GINEncoder(torch.autograd.Function):
         enc = _lib.GinEncoder()
         enc.num_layer, enc.training, enc.dim = L, int(training), D
         enc.dtype = dtype
+        # fp32: the GEMM form ops._MLP would use on these shapes (identical kernels)
+        h3 = dtype == _lib.DTYPE_F32 and h3_ok(N, D)
+        kind = "h3" if h3 and FP32_GEMM == "h3" else "x6"
+        enc.fp32_gemm = (1 if FP32_GEMM == "h3" else 2) if h3 else 0
         enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
         enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
@@ -793,10 +890,10 @@ class _GINEncoder(torch.autograd.Function):
             enc.bn_num_batches_tracked[l] = nbt.data_ptr() if training and nbt is not None else None
             twoD = W0.shape[0]
             # the same planes (and cache entries) ops.linear_fwd / linear_bwd use
-            enc.mlp0_planes[l] = weight_planes(W0, twoD, D, D, 0).data_ptr()
-            enc.mlp0_planes_t[l] = weight_planes(W0, D, twoD, D, 1).data_ptr()
-            enc.mlp2_planes[l] = weight_planes(W2, D, twoD, twoD, 0).data_ptr()
-            enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1).data_ptr()
+            enc.mlp0_planes[l] = weight_planes(W0, twoD, D, D, 0, kind).data_ptr()
+            enc.mlp0_planes_t[l] = weight_planes(W0, D, twoD, D, 1, kind).data_ptr()
+            enc.mlp2_planes[l] = weight_planes(W2, D, twoD, twoD, 0, kind).data_ptr()
+            enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1, kind).data_ptr()
         dev = x_idx.device
         arena_bytes = _wsq("molclr_gin_encoder_arena_bytes", L, N, D, dtype)
         arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)
