@@ -373,10 +373,16 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  *   molclr_hplanes_make_batch: weights as h3 B operands (molclr_bplanes_make_batch
  *     arguments): [2][Npad][Kp] fp16 planes, then the max |B| slot,
  *     molclr_hplanes_bytes(N, K) bytes each.
- *   molclr_gemm_f32_h3: C = epilogue(A B) for a row-major A [M][K] (lda) with
- *     its max slot `amax` and h3 planes of B; K <= 1024, K and lda multiples
- *     of 4.  cmax (may be NULL): max |C| of the stored values folded into
- *     *cmax (atomic max; the caller resets it).
+ *   molclr_absmax_rows_f32: rowmax[r] = max_c |x[r][c]| and the slot as
+ *     molclr_absmax_f32.
+ *   molclr_gemm_f32_h3: C = epilogue(A B) for a row-major A [M][K] (lda) and
+ *     h3 planes of B; K <= 1024, K and lda multiples of 4.  a_rowwise == 0:
+ *     `amax` is A's max slot (one scale for A); != 0: `amax` holds A's row
+ *     maxima [M] and every row is scaled by its own (a row of small values,
+ *     e.g. a node with a small gradient, keeps full precision).  cmax /
+ *     crow (each may be NULL): max |C| of the stored values folded into the
+ *     slot cmax / the row maxima crow [M] (atomic max; the caller zeroes
+ *     them).
  *   molclr_linear_wgrad_h3: molclr_linear_wgrad given the max slots of dy
  *     and x (n_out, n_in, ld_dy, ld_x multiples of 4; same workspace). */
 int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* slot,
@@ -385,10 +391,12 @@ size_t molclr_hplanes_bytes(int64_t N, int64_t K);
 int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N,
                               const int64_t* K, const int64_t* ldb, const int* b_kmajor,
                               uint16_t* const* planes, molclr_stream_t stream);
-int molclr_gemm_f32_h3(const float* A, const float* amax, const uint16_t* hplanes, float* C,
-                       int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
+int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                           float* rowmax, float* slot, int accumulate, molclr_stream_t stream);
+int molclr_gemm_f32_h3(const float* A, const float* amax, int a_rowwise, const uint16_t* hplanes,
+                       float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
-                       float* cmax, molclr_stream_t stream);
+                       float* cmax, float* crow, molclr_stream_t stream);
 int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
                            const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
                            int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
@@ -592,11 +600,15 @@ typedef struct molclr_gin_encoder {
    * mixed-precision switch (molclr.py:16-24,93-96,121-123).  h_out / dh_out
    * are then bf16. */
   int32_t dtype;
-  /* fp32 storage only: 0 = split-bf16 "x6" GEMMs (the *_planes fields are
-   * molclr_bplanes_make images); 1 = "h3" GEMMs (molclr_gemm_f32_h3 /
-   * molclr_linear_wgrad_h3; the *_planes fields are molclr_hplanes_make_batch
-   * images, 2 dim <= 1024).  The max |x| slots of agg / a1 live in the arena,
-   * those of dz / dz1 in the workspace. */
+  /* fp32 storage only, which products run in "h3" (molclr_gemm_f32_h3 /
+   * molclr_linear_wgrad_h3, 2 dim <= 1024) instead of split-bf16 "x6":
+   * 0 = none; bit 0 = the backward (weight gradients with per-tensor scales,
+   * data gradients with row-wise scales; mlp*_planes_t are then
+   * molclr_hplanes_make_batch images); bit 1 = the forward products too
+   * (mlp0/2_planes h3 images; measured to move the c1 3-step trajectory by
+   * 2.5e-5 after one Adam step, so not used by default).  The max slots of
+   * agg / a1 live in the arena, those of dz / dz1 and all row maxima in the
+   * workspace. */
   int32_t fp32_gemm;
 } molclr_gin_encoder;
 

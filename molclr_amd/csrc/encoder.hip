@@ -127,14 +127,15 @@ MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, in
   return ArenaLayout(L, N, D, elem_bytes(dtype)).total;
 }
 
-// workspace: backward scratch | h3 max slots of dz_l / dz1_l (256 B) | the
-// entry points' workspace
+// workspace: backward scratch | h3 max slots of dz_l / dz1_l | h3 row maxima
+// of dz and dz1 [2][N] | the entry points' workspace
 constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float);
+size_t rowmax_bytes(int64_t N) { return molclr::align_up((size_t)2 * N * sizeof(float), 256); }
 
 MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
   (void)L;
   return molclr::align_up(scratch_bytes(N, D, elem_bytes(dtype)), 256) + kSlotBytes +
-         kernels_ws(N, D) + 256;
+         rowmax_bytes(N) + kernels_ws(N, D) + 256;
 }
 
 MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t* x,
@@ -156,12 +157,16 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   char* A = (char*)arena;
   auto F = [&](size_t off) { return (float*)(A + off); };
   auto H = [&](size_t off) { return (uint16_t*)(A + off); };
-  void* kws = (char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) + kSlotBytes;
+  // h3: row maxima of agg and a1 (workspace row-maxima region)
+  float* ragg = (float*)((char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) +
+                         kSlotBytes);
+  float* ra1 = ragg + N;
+  void* kws = (char*)ragg + rowmax_bytes(N);
   const size_t kws_bytes = kernels_ws(N, D);
-  const bool h3 = !bf && e->fp32_gemm == 1;
-  const bool h3w = !bf && e->fp32_gemm == 2;  // h3 weight gradients only
+  const bool h3 = !bf && e->fp32_gemm != 0;
+  const bool h3f = h3 && (e->fp32_gemm & 2);  // h3 forward products (not the default)
   float* fmax = F(lay.smax);  // h3: [l][0] = max |agg_l|, [l][1] = max |a1_l|
-  if ((h3 || h3w) && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
     molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
     return MOLCLR_ERR_ARG;
@@ -198,17 +203,23 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
       float *agg = F(lay.agg[l]), *a1 = F(lay.a1[l]), *z = F(lay.z[l]);
       MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
                                            Ecl, agg, N, D, stream));
-      if (h3) {
+      if (h3f) {
         // GINEConv.update in h3 (ops._MLP): max |agg| by a pass, max |a1| from
         // the first GEMM's epilogue
         float* sl = fmax + 2 * l * kMaxSlotParts;
         const uint16_t* p0 = e->mlp0_planes[l];
         const uint16_t* p2 = e->mlp2_planes[l];
-        MOLCLR_TRY(molclr_absmax_f32(agg, N, D, D, sl, 1, stream));
-        MOLCLR_TRY(molclr_gemm_f32_h3(agg, sl, p0, a1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_BIAS_RELU,
-                                      e->mlp0_bias[l], nullptr, 0, sl + kMaxSlotParts, stream));
-        MOLCLR_TRY(molclr_gemm_f32_h3(a1, sl + kMaxSlotParts, p2, z, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_BIAS,
-                                      e->mlp2_bias[l], nullptr, 0, nullptr, stream));
+        MOLCLR_TRY(molclr_absmax_rows_f32(agg, N, D, D, ragg, sl, 1, stream));
+        if (hipMemsetAsync(ra1, 0, (size_t)N * sizeof(float), molclr::as_stream(stream)) !=
+            hipSuccess) {
+          molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
+          return MOLCLR_ERR_ARG;
+        }
+        MOLCLR_TRY(molclr_gemm_f32_h3(agg, ragg, 1, p0, a1, N, 2 * D, D, D, 2 * D,
+                                      MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
+                                      sl + kMaxSlotParts, ra1, stream));
+        MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, 1, p2, z, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_BIAS,
+                                      e->mlp2_bias[l], nullptr, 0, nullptr, nullptr, stream));
       } else {
         // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
         MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
@@ -217,9 +228,10 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
         MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
                                            MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
                                            kws_bytes, stream));
-        if (h3w) {
+        if (h3) {
           MOLCLR_TRY(molclr_absmax_f32(agg, N, D, D, fmax + 2 * l * kMaxSlotParts, 1, stream));
-          MOLCLR_TRY(molclr_absmax_f32(a1, N, 2 * D, 2 * D, fmax + (2 * l + 1) * kMaxSlotParts, 1, stream));
+          MOLCLR_TRY(molclr_absmax_f32(a1, N, 2 * D, 2 * D, fmax + (2 * l + 1) * kMaxSlotParts, 1,
+                                       stream));
         }
       }
       MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
@@ -260,14 +272,16 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   void* dagg = S + 2 * (size_t)N * D * es;   // w.r.t. the aggregation output
   void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
   float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
-  void* kws = (char*)bmax + kSlotBytes;
+  float* rdz = bmax + kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
+  float* rdz1 = rdz + N;
+  void* kws = (char*)rdz + rowmax_bytes(N);
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
-  const bool h3 = !bf && e->fp32_gemm == 1;
-  const bool h3w = !bf && e->fp32_gemm == 2;
+  const bool h3 = !bf && e->fp32_gemm != 0;
+  const bool h3d = h3 && (e->fp32_gemm & 1);  // h3 data-gradient products
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
-  if ((h3 || h3w) && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
     molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
     return MOLCLR_ERR_ARG;
@@ -307,46 +321,46 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                                 gr->edge_embedding1[l], gr->edge_embedding2[l], N,
                                                 D, 1, kws, kws_bytes, stream));
     } else if (h3) {
-      // ops._MLP's h3 backward: dW2 (+db2), dz1 (ReLU mask of a1; max |dz1|
-      // from the epilogue), dW1 (+db1), dagg
+      // ops._MLP's h3 backward: dW2 (+db2), dz1 (ReLU mask of a1; its max and
+      // row maxima from the epilogue), dW1 (+db1), dagg.  The data-gradient
+      // products scale A row by row (gradient rows span many binades).
       const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
       float* sl = bmax + 2 * l * kMaxSlotParts;
       const float* fl = fmax + 2 * l * kMaxSlotParts;
       MOLCLR_REQUIRE(gr->mlp2_weight[l] && gr->mlp2_bias[l] && gr->mlp0_weight[l] &&
                          gr->mlp0_bias[l],
                      "gin_encoder_bwd: h3 needs every MLP gradient");
-      MOLCLR_TRY(molclr_absmax_f32(fz, N, D, D, sl, 1, stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l], gr->mlp2_bias[l],
-                                        N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
-      MOLCLR_TRY(molclr_gemm_f32_h3(fz, sl, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
-                                    2 * D, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D, sl + kMaxSlotParts,
-                                    stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl, gr->mlp0_weight[l],
-                                        gr->mlp0_bias[l], N, 2 * D, D, 2 * D, D, 1, kws, kws_bytes,
+      MOLCLR_TRY(molclr_absmax_rows_f32(fz, N, D, D, rdz, sl, 1, stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l],
+                                        gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
                                         stream));
-      MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, sl + kMaxSlotParts, e->mlp0_planes_t[l], (float*)dagg,
-                                    N, D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE, nullptr, nullptr, 0,
-                                    nullptr, stream));
-      MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
-                                           g->ecount, (float*)dh, gr->edge_embedding1[l],
-                                           gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));
-    } else if (h3w) {
-      const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
-      float* sl = bmax + 2 * l * kMaxSlotParts;
-      const float* fl = fmax + 2 * l * kMaxSlotParts;
-      MOLCLR_TRY(molclr_absmax_f32(fz, N, D, D, sl, 1, stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l], gr->mlp2_bias[l],
-                                        N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
-      MOLCLR_TRY(molclr_gemm_f32_bplanes(fz, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
-                                         2 * D, 0, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D, kws,
-                                         kws_bytes, stream));
-      MOLCLR_TRY(molclr_absmax_f32((const float*)dz1, N, 2 * D, 2 * D, sl + kMaxSlotParts, 1, stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl, gr->mlp0_weight[l],
-                                        gr->mlp0_bias[l], N, 2 * D, D, 2 * D, D, 1, kws, kws_bytes,
-                                        stream));
-      MOLCLR_TRY(molclr_gemm_f32_bplanes((const float*)dz1, e->mlp0_planes_t[l], (float*)dagg, N,
-                                         D, 2 * D, 2 * D, D, 0, MOLCLR_EPI_NONE, nullptr, nullptr,
-                                         0, kws, kws_bytes, stream));
+      if (hipMemsetAsync(rdz1, 0, (size_t)N * sizeof(float), molclr::as_stream(stream)) !=
+          hipSuccess) {
+        molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
+        return MOLCLR_ERR_ARG;
+      }
+      if (h3d) {
+        MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, 1, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
+                                      2 * D, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D,
+                                      sl + kMaxSlotParts, rdz1, stream));
+      } else {
+        MOLCLR_TRY(molclr_gemm_f32_bplanes(fz, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
+                                           2 * D, 0, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D,
+                                           kws, kws_bytes, stream));
+        MOLCLR_TRY(molclr_absmax_f32((const float*)dz1, N, 2 * D, 2 * D, sl + kMaxSlotParts, 1,
+                                     stream));
+      }
+      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl,
+                                        gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D, 2 * D,
+                                        D, 1, kws, kws_bytes, stream));
+      if (h3d)
+        MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, 1, e->mlp0_planes_t[l],
+                                      (float*)dagg, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE,
+                                      nullptr, nullptr, 0, nullptr, nullptr, stream));
+      else
+        MOLCLR_TRY(molclr_gemm_f32_bplanes((const float*)dz1, e->mlp0_planes_t[l], (float*)dagg,
+                                           N, D, 2 * D, 2 * D, D, 0, MOLCLR_EPI_NONE, nullptr,
+                                           nullptr, 0, kws, kws_bytes, stream));
       MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
                                            g->ecount, (float*)dh, gr->edge_embedding1[l],
                                            gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));

@@ -783,17 +783,21 @@ struct QStageB {
 // address, so the compiler keeps counted vmcnt waits and the next steps'
 // loads stay in flight across the MFMAs (a conditional load makes it drain
 // every outstanding load at the top of each step).
-// H3: the fp16 two-part form (mfma.h "h3"): A scaled by its max slot `amax`
-// and split into 2 parts, the planes are 2 fp16 parts of B scaled by `bmax`,
+// H3 != 0: the fp16 two-part form (mfma.h "h3"): the planes are 2 fp16 parts
+// of B scaled by its max slot `bmax`; A is scaled by its max slot `amax`
+// (H3 == 1) or row by row by the row maxima amax[M] (H3 == 2: each lane splits
+// one row of A, so a row of small values -- a node with a small gradient --
+// keeps its precision however large other rows are) and split into 2 parts;
 // three fp16 MFMAs per product; the sums are scaled back in the epilogue,
-// which also folds max |C| into `cmax` when given (the next product's amax).
-template <int TN, int EPI, int KG, bool MASK, bool H3 = false>
+// which also folds max |C| into the slot `cmax` and the row maxima of C into
+// `crow` [M] (atomic maxima; both optional, the caller zeroes them).
+template <int TN, int EPI, int KG, bool MASK, int H3 = 0>
 __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
     int accumulate, const float* __restrict__ amax, const float* __restrict__ bmax,
-    float* __restrict__ cmax) {
+    float* __restrict__ cmax, float* __restrict__ crow) {
   constexpr int T = 64 * kQ6Waves;  // threads of one K group
   constexpr int BN = 32 * TN;
   constexpr int NP = H3 ? 2 : 3;    // B planes
@@ -846,8 +850,9 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
-  const int sha = H3 ? h3_shift(amax) : 0;
-  const int shc = H3 ? -(sha + h3_shift(bmax)) : 0;  // epilogue scale-back
+  // this lane's A shift (its row's with H3 == 2), the planes' shift
+  const int sha = H3 == 1 ? h3_shift(amax) : H3 == 2 ? h3_shift_of(amax[arow_i]) : 0;
+  const int shb = H3 ? h3_shift(bmax) : 0;
   auto compute = [&](const uint16_t* Bs, const float4(&a)[4], int r) {
     float4 am4[4];
 #pragma unroll
@@ -960,16 +965,21 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
   float* tw = reinterpret_cast<float*>(lds) + wm * 32 * 32;
   const int64_t mw = m0 + 32 * wm;
-  float cm = 0.f;  // max |C| of this lane's stores (H3 with cmax)
+  // H3: max |C| of this lane's stores per epilogue row group it (row
+  // 8 it + lane / 8 of the wave's 32): for cmax and crow
+  float rm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int64_t nb = n0 + 32 * b;
     if (nb >= N) break;  // block-uniform
     if (grp == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] =
-            H3 ? __builtin_ldexpf(acc[b][r], shc) : acc[b][r];
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+        // scale back by the row's shift (held by lane `row`) and the planes'
+        const int sr = H3 == 2 ? __shfl(sha, row, 64) : sha;
+        tw[row * 32 + li] = H3 ? __builtin_ldexpf(acc[b][r], -(sr + shb)) : acc[b][r];
+      }
     }
     __syncthreads();
     if (grp == 0) {
@@ -995,7 +1005,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
           }
           if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
           *reinterpret_cast<float4*>(o) = v;
-          if (H3) cm = fmaxf(cm, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          if (H3) rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         } else {
           const float e[4] = {v4.x, v4.y, v4.z, v4.w};
           for (int j = 0; j < 4 && n + j < N; ++j) {
@@ -1005,14 +1015,30 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
             if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
             if (accumulate) x += o[j];
             o[j] = x;
-            if (H3) cm = fmaxf(cm, fabsf(x));
+            if (H3) rm[it] = fmaxf(rm[it], fabsf(x));
           }
         }
       }
     }
     __syncthreads();  // the wave's tile is rewritten by the next block
   }
-  if (H3 && cmax != nullptr) absmax_publish(grp == 0 ? cm : 0.f, cmax);
+  if constexpr (H3 != 0) {
+    if (crow != nullptr && grp == 0) {
+      // the 8 lanes of a row (lane / 8) fold their maxima, then one atomic per row
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        float v = rm[it];
+        v = fmaxf(v, __shfl_xor(v, 1, 64));
+        v = fmaxf(v, __shfl_xor(v, 2, 64));
+        v = fmaxf(v, __shfl_xor(v, 4, 64));
+        const int64_t m = mw + 8 * it + (lane >> 3);
+        if ((lane & 7) == 0 && m < M)
+          atomicMax(reinterpret_cast<unsigned int*>(crow + m), __float_as_uint(v));
+      }
+    }
+    if (cmax != nullptr)
+      absmax_publish(grp == 0 ? fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3])) : 0.f, cmax);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1350,6 +1376,33 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
   absmax_publish(m, slot);
 }
 
+// row maxima rowmax[r] = max_c |x[r][c]| (plain stores) and the matrix max
+// folded into *slot: a wave per row, float4 columns when aligned
+__global__ __launch_bounds__(256) void k_absmax_rows(const float* __restrict__ x, int64_t rows,
+                                                     int64_t cols, int64_t ld,
+                                                     float* __restrict__ rowmax,
+                                                     float* __restrict__ slot) {
+  const int lane = threadIdx.x & 63;
+  const bool v4 = (cols & 3) == 0 && (ld & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  float all = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
+    const float* xr = x + r * ld;
+    float m = 0.f;
+    if (v4) {
+      for (int64_t c = lane; c < (cols >> 2); c += 64) {
+        const float4 v = reinterpret_cast<const float4*>(xr)[c];
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    } else {
+      for (int64_t c = lane; c < cols; c += 64) m = fmaxf(m, fabsf(xr[c]));
+    }
+    m = wave_max(m);
+    if (lane == 0) rowmax[r] = m;
+    all = fmaxf(all, m);
+  }
+  absmax_publish(all, slot);
+}
+
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
 // (and colsum[m] = Σ_{z < cs_splits} cs_partial[z][m] for t < M when cs_partial is given)
 template <int EPI>
@@ -1438,9 +1491,10 @@ struct Args {
   const uint16_t* Bp = nullptr;  // pre-split planes (molclr_gemm_f32_bplanes)
   int64_t bps = 0;               // their plane stride
   float* colsum = nullptr;       // Σ_k A(m, k) out (molclr_linear_wgrad; K-major A, p6)
-  const float* amax = nullptr;   // h3: max |A| / max |B| slots, max |C| out (may be null)
-  const float* bmax = nullptr;
+  const float* amax = nullptr;   // h3: max |A| slot (or row maxima), max |B| slot,
+  const float* bmax = nullptr;   // max |C| slot and row maxima out (may be null)
   float* cmax = nullptr;
+  float* crow = nullptr;
 };
 
 template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1, bool CS = false>
@@ -1561,14 +1615,14 @@ int q6_groups(int64_t M, int64_t N, int64_t K) {
   return (q6_blocks(M, N) < 384 && (K + BK - 1) / BK >= 8) ? 2 : 1;
 }
 
-template <int TN, int EPI, int KG, bool MASK, bool H3>
+template <int TN, int EPI, int KG, bool MASK, int H3>
 void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
   molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK, H3>),
                        dim3((unsigned)q6_blocks(a.M, a.N)), dim3(KG * 64 * kQ6Waves), 0, s, a.A,
                        a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux,
-                       a.accumulate, a.amax, a.bmax, a.cmax);
+                       a.accumulate, a.amax, a.bmax, a.cmax, a.crow);
 }
-template <int TN, int EPI, bool H3>
+template <int TN, int EPI, int H3>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
   const int64_t nsteps = (a.K + BK - 1) / BK;
   const int kg = q6_groups(a.M, a.N, a.K);
@@ -1584,7 +1638,7 @@ void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
   }
 }
 
-template <int TN, bool H3>
+template <int TN, int H3>
 int dispatch_q6(int epi, const Args& a, int64_t npad, hipStream_t s) {
   switch (epi) {
     case MOLCLR_EPI_NONE: launch_q6<TN, MOLCLR_EPI_NONE, H3>(a, npad, s); return 0;
@@ -1595,19 +1649,19 @@ int dispatch_q6(int epi, const Args& a, int64_t npad, hipStream_t s) {
   }
 }
 
-// a.ldb = kp (the planes' row pitch), a.Bp = the planes; h3: fp16 two-part
-// planes and a.amax / a.bmax set
-int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, bool h3 = false) {
+// a.ldb = kp (the planes' row pitch), a.Bp = the planes; h3 1 / 2: fp16
+// two-part planes, a.amax (a slot / row maxima) and a.bmax set
+template <int H3>
+int dispatch_q6_tn(int epi, const Args& a, int64_t npad, hipStream_t s) {
   const int tn = wide_tn(a.N);
-  int rc;
-  if (h3)
-    rc = tn == 5 ? dispatch_q6<5, true>(epi, a, npad, s)
-         : tn == 4 ? dispatch_q6<4, true>(epi, a, npad, s)
-                   : dispatch_q6<2, true>(epi, a, npad, s);
-  else
-    rc = tn == 5 ? dispatch_q6<5, false>(epi, a, npad, s)
-         : tn == 4 ? dispatch_q6<4, false>(epi, a, npad, s)
-                   : dispatch_q6<2, false>(epi, a, npad, s);
+  return tn == 5 ? dispatch_q6<5, H3>(epi, a, npad, s)
+         : tn == 4 ? dispatch_q6<4, H3>(epi, a, npad, s)
+                   : dispatch_q6<2, H3>(epi, a, npad, s);
+}
+int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, int h3 = 0) {
+  const int rc = h3 == 2   ? dispatch_q6_tn<2>(epi, a, npad, s)
+                 : h3 == 1 ? dispatch_q6_tn<1>(epi, a, npad, s)
+                           : dispatch_q6_tn<0>(epi, a, npad, s);
   if (rc) {
     molclr::set_error("gemm_f32_bplanes: no q6 kernel for epilogue %d", epi);
     return MOLCLR_ERR_UNSUPPORTED;
@@ -2025,6 +2079,24 @@ MOLCLR_API int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int
   return MOLCLR_OK;
 }
 
+MOLCLR_API int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                                      float* rowmax, float* slot, int accumulate,
+                                      molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && rowmax && slot,
+                 "absmax_rows_f32: bad arguments");
+  hipStream_t s = molclr::as_stream(stream);
+  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotParts * sizeof(float), s);
+  if (rows > 0) {
+    MOLCLR_REQUIRE(x || cols == 0, "absmax_rows_f32: null x");
+    int64_t blocks = molclr::ceil_div(rows, 4 * 8);
+    blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+    hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, s, x, rows, cols, ld,
+                       rowmax, slot);
+  }
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
 MOLCLR_API size_t molclr_hplanes_bytes(int64_t N, int64_t K) {
   return (size_t)2 * planes_npad(N) * planes_kp(K) * sizeof(uint16_t) + kHMaxParts * sizeof(float);
 }
@@ -2059,11 +2131,11 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
   return MOLCLR_OK;
 }
 
-MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, const uint16_t* hplanes,
-                                  float* C, int64_t M, int64_t N, int64_t K, int64_t lda,
-                                  int64_t ldc, int epilogue_flags, const float* bias,
-                                  const float* aux, int64_t ldaux, float* cmax,
-                                  molclr_stream_t stream) {
+MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_rowwise,
+                                  const uint16_t* hplanes, float* C, int64_t M, int64_t N,
+                                  int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
+                                  const float* bias, const float* aux, int64_t ldaux, float* cmax,
+                                  float* crow, molclr_stream_t stream) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_h3: negative size");
@@ -2086,7 +2158,8 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, const uint1
   a.amax = amax;
   a.bmax = reinterpret_cast<const float*>(hplanes + 2 * npad * kp);
   a.cmax = cmax;
-  return run_q6(a, npad, epilogue, molclr::as_stream(stream), true);
+  a.crow = crow;
+  return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_rowwise ? 2 : 1);
 }
 
 MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,

@@ -77,13 +77,16 @@ __device__ __forceinline__ void split8(const float4 a, const float4 b, u32x4& hi
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-// Scale exponent of a tensor from its max |x| slot (kMaxSlotParts entries,
-// molclr_absmax_f32): 0 for a zero / NaN / infinite max (NaN and inf then
-// propagate as in fp32).  Every lane of the wave must call it.
-__device__ __forceinline__ int h3_shift(const float* __restrict__ slot) {
-  const float m = wave_max(slot[threadIdx.x & (kMaxSlotParts - 1)]);
+// Scale exponent for values of max |x| = m: 0 for a zero / NaN / infinite m
+// (NaN and inf then propagate as in fp32).
+__device__ __forceinline__ int h3_shift_of(float m) {
   if (!(m > 0.f) || !(m <= 3.402823466e38f)) return 0;
   return 15 - __builtin_amdgcn_frexp_expf(m);  // m = f 2^e, f in [0.5, 1)
+}
+// ... of a tensor from its max slot (kMaxSlotParts entries, molclr_absmax_f32).
+// Every lane of the wave must call it.
+__device__ __forceinline__ int h3_shift(const float* __restrict__ slot) {
+  return h3_shift_of(wave_max(slot[threadIdx.x & (kMaxSlotParts - 1)]));
 }
 
 __device__ __forceinline__ void hsplit2(float a, float b, int sh, uint32_t& h, uint32_t& l) {

@@ -249,11 +249,14 @@ def _refresh_planes(gen: int) -> None:
             _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, planes)
 
 
-# fp32 GEMMs of the GIN MLP (forward, data and weight gradients): "h3" = three
-# fp16 MFMAs per product with per-tensor power-of-two scaling (molclr_gemm_f32_h3,
-# molclr_linear_wgrad_h3), "x6" = six split-bf16 MFMAs.  The encoder executor
-# reads the same switch, so both paths issue identical kernels.
-FP32_GEMM = os.environ.get("MOLCLR_FP32_GEMM", "x6")
+# fp32 GEMMs of the GIN MLP backward (data and weight gradients): "h3" = three
+# fp16 MFMAs per product with power-of-two scaling (molclr_gemm_f32_h3 with
+# row-wise scales, molclr_linear_wgrad_h3), "x6" = six split-bf16 MFMAs.
+# H3_FORWARD puts the forward products on h3 too (off: it moved the c1 3-step
+# trajectory test by 2.5e-5).  The encoder executor reads the same switches,
+# so both paths issue identical kernels.
+FP32_GEMM = os.environ.get("MOLCLR_FP32_GEMM", "h3")
+H3_FORWARD = os.environ.get("MOLCLR_H3_FORWARD", "0") == "1"
 
 
 MAX_SLOT = 64  # floats per max |x| slot (molclr_absmax_f32)
@@ -270,16 +273,19 @@ def absmax(x, out=None, accumulate=0) -> torch.Tensor:
     return out
 
 
-def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None):
-    """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3; cmax (a
-    zeroed slot) receives max |C|."""
+def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None,
+            rowwise=False, crow=None):
+    """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3.  amax: A's
+    max slot, or (rowwise) its row maxima [M]; cmax / crow (zeroed) receive
+    max |C| and C's row maxima."""
     _check(A, W)
     M = A.shape[0]
     planes = weight_planes(W, N, K, ldb, b_kmajor, "h3")
     out = torch.empty(M, N, dtype=torch.float32, device=A.device)
-    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), planes.data_ptr(),
+    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), int(rowwise), planes.data_ptr(),
               out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
-              _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax), _stream(A))
+              _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax),
+              _lib.ptr(crow), _stream(A))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -307,7 +313,7 @@ def linear_wgrad_h3(dy, dymax, x, xmax, W_param, b_param):
 
 def h3_ok(rows, D) -> bool:
     """Shapes the h3 GIN-MLP GEMMs take (else the x6 kernels run)."""
-    return FP32_GEMM in ("h3", "h3w") and D % 4 == 0 and 2 * D <= 1024 and rows > 0
+    return FP32_GEMM == "h3" and D % 4 == 0 and 2 * D <= 1024 and rows > 0
 
 
 def gemm_w(A, W, M, N, K, lda, ldb, a_kmajor, b_kmajor, epi=EPI_NONE, bias=None, aux=None,
@@ -514,13 +520,24 @@ class _MLP(torch.autograd.Function):
         _check(x, W1, b1, W2, b2)
         x = _c(x)
         M, D = x.shape
-        ctx.h3 = FP32_GEMM == "h3" and h3_ok(M, D) and W1.shape == (2 * D, D) and W2.shape == (D, 2 * D)
+        ctx.h3 = h3_ok(M, D) and W1.shape == (2 * D, D) and W2.shape == (D, 2 * D)
         if ctx.h3:
-            # h3: max |x| by a pass, max |a1| from the first GEMM's epilogue
+            # the executor's order: max |x| and its row maxima by a pass, then
+            # the products (row-wise h3 when H3_FORWARD, else x6 with max |a1| by
+            # a pass); the max slots serve the h3 weight gradients
             slots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=x.device)
-            absmax(x, slots[0], accumulate=1)
-            a1 = gemm_h3(x, slots[0], W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1, cmax=slots[1])
-            z = gemm_h3(a1, slots[1], W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2)
+            if H3_FORWARD:
+                rows = torch.zeros(2, M, dtype=torch.float32, device=x.device)
+                _lib.call("molclr_absmax_rows_f32", x.data_ptr(), M, D, x.stride(0),
+                          rows[0].data_ptr(), slots[0].data_ptr(), 1, _stream(x))
+                a1 = gemm_h3(x, rows[0], W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1,
+                             cmax=slots[1], rowwise=True, crow=rows[1])
+                z = gemm_h3(a1, rows[1], W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2, rowwise=True)
+            else:
+                a1 = linear_fwd(x, W1, b1, relu=True)
+                z = linear_fwd(a1, W2, b2, relu=False)
+                absmax(x, slots[0], accumulate=1)
+                absmax(a1, slots[1], accumulate=1)
             ctx.slots = slots
         else:
             a1 = linear_fwd(x, W1, b1, relu=True)
@@ -540,13 +557,16 @@ class _MLP(torch.autograd.Function):
             # from its epilogue), dW1 (+db1), dx
             D = x.shape[1]
             slots = ctx.slots
+            M = x.shape[0]
             bslots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=dz.device)
-            absmax(dz, bslots[0], accumulate=1)
+            rows = torch.zeros(2, M, dtype=torch.float32, device=dz.device)  # row maxima
+            _lib.call("molclr_absmax_rows_f32", dz.data_ptr(), M, D, dz.stride(0),
+                      rows[0].data_ptr(), bslots[0].data_ptr(), 1, _stream(dz))
             dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
-            dz1 = gemm_h3(dz, bslots[0], W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
-                          cmax=bslots[1])
+            dz1 = gemm_h3(dz, rows[0], W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
+                          cmax=bslots[1], rowwise=True, crow=rows[1])
             dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
-            dx = gemm_h3(dz1, bslots[1], W1, D, 2 * D, D, 1) if need[0] else None
+            dx = (gemm_h3(dz1, rows[1], W1, D, 2 * D, D, 1, rowwise=True) if need[0] else None)
             return dx, dW1, db1, dW2, db2
         # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
         dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],
@@ -871,8 +891,9 @@ class _GINEncoder(torch.autograd.Function):
         enc.dtype = dtype
         # fp32: the GEMM form ops._MLP would use on these shapes (identical kernels)
         h3 = dtype == _lib.DTYPE_F32 and h3_ok(N, D)
-        kind = "h3" if h3 and FP32_GEMM == "h3" else "x6"
-        enc.fp32_gemm = (1 if FP32_GEMM == "h3" else 2) if h3 else 0
+        kind = "h3" if h3 and H3_FORWARD else "x6"
+        kind_t = "h3" if h3 else "x6"
+        enc.fp32_gemm = (1 | (2 if H3_FORWARD else 0)) if h3 else 0
         enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
         enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
@@ -891,9 +912,9 @@ class _GINEncoder(torch.autograd.Function):
             twoD = W0.shape[0]
             # the same planes (and cache entries) ops.linear_fwd / linear_bwd use
             enc.mlp0_planes[l] = weight_planes(W0, twoD, D, D, 0, kind).data_ptr()
-            enc.mlp0_planes_t[l] = weight_planes(W0, D, twoD, D, 1, kind).data_ptr()
+            enc.mlp0_planes_t[l] = weight_planes(W0, D, twoD, D, 1, kind_t).data_ptr()
             enc.mlp2_planes[l] = weight_planes(W2, D, twoD, twoD, 0, kind).data_ptr()
-            enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1, kind).data_ptr()
+            enc.mlp2_planes_t[l] = weight_planes(W2, twoD, D, twoD, 1, kind_t).data_ptr()
         dev = x_idx.device
         arena_bytes = _wsq("molclr_gin_encoder_arena_bytes", L, N, D, dtype)
         arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)

@@ -708,3 +708,95 @@ def test_batchnorm_segments_equal_separate_calls(dev, rows, D):
     for a, b in ((y, y2), (rm, rm2), (rv, rv2), (nbt, nbt2), (dz, dz2), (dg, dg2), (db, db2)):
         assert torch.equal(a, b)
     assert int(nbt) == S
+
+
+# ---------------------------------------------------------------------------
+# h3 fp32 GEMMs (three fp16 MFMAs, power-of-two scaling): every tile width
+# (N 64 / 128 / 160 wide), one and two in-block K groups, partial K steps,
+# per-tensor and row-wise A scaling, the max / row-max outputs.  Data with
+# rows spanning 12 binades (gradient-like): row-wise scaling keeps every row
+# at fp32-GEMM accuracy.
+H3_SHAPES = [(30556, 600, 300), (30556, 300, 600), (1500, 128, 256), (1500, 256, 128),
+             (777, 64, 36), (300, 100, 20), (5, 12, 8)]
+
+
+def _h3_planes(lib, W, N, K, kmajor, dev):
+    import ctypes
+    nb = lib.molclr_hplanes_bytes(N, K)
+    buf = torch.empty(nb, dtype=torch.uint8, device=dev)
+    i64 = lambda v: (ctypes.c_int64 * 1)(v)  # noqa: E731
+    rc = lib.molclr_hplanes_make_batch(1, (ctypes.c_void_p * 1)(W.data_ptr()), i64(N), i64(K),
+                                       i64(W.shape[1]), (ctypes.c_int * 1)(kmajor),
+                                       (ctypes.c_void_p * 1)(buf.data_ptr()), ops._stream(W))
+    assert rc == 0, lib.molclr_last_error()
+    return buf
+
+
+@pytest.mark.parametrize("M,N,K", H3_SHAPES)
+@pytest.mark.parametrize("rowwise", [0, 1])
+@pytest.mark.parametrize("epi", [0, 2, 3])
+def test_gemm_h3(dev, M, N, K, rowwise, epi):
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    if rowwise:
+        A *= torch.pow(10.0, -12 * torch.rand(M, 1, generator=g, dtype=torch.float64))
+    W = (torch.rand(N, K, generator=g, dtype=torch.float64) * 2 - 1) / K ** 0.5
+    bias = torch.randn(N, generator=g, dtype=torch.float64) * 0.1
+    aux = torch.randn(M, N, generator=g, dtype=torch.float64)
+    ref = A @ W.t()
+    if epi == 2:
+        ref = (ref + bias).clamp_min(0)
+    if epi == 3:
+        ref = ref * (aux > 0)
+    Ad, Wd = A.float().to(dev), W.float().to(dev)
+    planes = _h3_planes(lib, Wd, N, K, 0, dev)
+    rows = torch.zeros(2, M, device=dev)
+    slots = torch.zeros(2, 64, device=dev)
+    rc = lib.molclr_absmax_rows_f32(Ad.data_ptr(), M, K, K, rows[0].data_ptr(),
+                                    slots[0].data_ptr(), 0, ops._stream(Ad))
+    assert rc == 0
+    C = torch.empty(M, N, device=dev)
+    bd, ad = bias.float().to(dev), aux.float().to(dev)
+    rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
+                                rowwise, planes.data_ptr(), C.data_ptr(), M, N, K, K, N, epi,
+                                bd.data_ptr(), ad.data_ptr(), N, slots[1].data_ptr(),
+                                rows[1].data_ptr(), ops._stream(Ad))
+    assert rc == 0, lib.molclr_last_error()
+    torch.cuda.synchronize()
+    # row-wise scaling: every row at fp32 accuracy (per-row relative error)
+    Cc = C.double().cpu()
+    if rowwise:
+        err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))
+        err = err[ref.norm(dim=1) > 0].max().item()
+    else:
+        err = rel(Cc, ref)
+    assert err < 2e-6, err
+    assert rows[0].cpu().equal(Ad.abs().amax(1).cpu())
+    assert slots[1].max().item() == C.abs().max().item()
+    assert rows[1].cpu().equal(C.abs().amax(1).cpu())
+
+
+@pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
+def test_linear_wgrad_h3(dev, rows, n_out, n_in):
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(rows)
+    dy = torch.randn(rows, n_out, generator=g, dtype=torch.float64) * 1e-6
+    x = torch.randn(rows, n_in, generator=g, dtype=torch.float64)
+    dyd, xd = dy.float().to(dev), x.float().to(dev)
+    slots = torch.zeros(2, 64, device=dev)
+    for t, sl in ((dyd, slots[0]), (xd, slots[1])):
+        assert lib.molclr_absmax_f32(t.data_ptr(), t.shape[0], t.shape[1], t.shape[1],
+                                     sl.data_ptr(), 0, ops._stream(t)) == 0
+    ws_b = lib.molclr_linear_wgrad_workspace_bytes(rows, n_out, n_in)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+    dW = torch.zeros(n_out, n_in, device=dev)  # accumulate into zeros
+    db = torch.zeros(n_out, device=dev)
+    rc = lib.molclr_linear_wgrad_h3(dyd.data_ptr(), slots[0].data_ptr(), xd.data_ptr(),
+                                    slots[1].data_ptr(), dW.data_ptr(), db.data_ptr(), rows, n_out,
+                                    n_in, n_out, n_in, 1, ws.data_ptr(), ws_b, ops._stream(dyd))
+    assert rc == 0, lib.molclr_last_error()
+    assert rel(dW, dy.t() @ x) < 2e-6
+    assert rel(db, dy.sum(0)) < 2e-6

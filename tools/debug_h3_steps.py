@@ -53,5 +53,5 @@ def run(mode):
 
 
 if __name__ == "__main__":
-    for m in sys.argv[1:] or ["x6", "h3", "h3w"]:
+    for m in sys.argv[1:] or ["x6", "h3"]:
         run(m)

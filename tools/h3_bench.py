@@ -93,9 +93,9 @@ def main():
             assert rc == 0, lib.molclr_last_error()
 
         def run3():
-            rc = lib.molclr_gemm_f32_h3(A.data_ptr(), smax[id(A)].data_ptr(), p3.data_ptr(),
+            rc = lib.molclr_gemm_f32_h3(A.data_ptr(), smax[id(A)].data_ptr(), 0, p3.data_ptr(),
                                         C3.data_ptr(), Nr, N, K, K, N, epi, bp, ap, ld_aux,
-                                        cmax.data_ptr(), st)
+                                        cmax.data_ptr(), None, st)
             assert rc == 0, lib.molclr_last_error()
         t6, t3 = timeit(run6), timeit(run3)
         r = ref()
