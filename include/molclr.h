@@ -376,13 +376,13 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  *   molclr_absmax_rows_f32: rowmax[r] = max_c |x[r][c]| and the slot as
  *     molclr_absmax_f32.
  *   molclr_gemm_f32_h3: C = epilogue(A B) for a row-major A [M][K] (lda) and
- *     h3 planes of B; K <= 1024, K and lda multiples of 4.  a_rowwise == 0:
- *     `amax` is A's max slot (one scale for A); != 0: `amax` holds A's row
- *     maxima [M] and every row is scaled by its own (a row of small values,
- *     e.g. a node with a small gradient, keeps full precision).  cmax /
- *     crow (each may be NULL): max |C| of the stored values folded into the
- *     slot cmax / the row maxima crow [M] (atomic max; the caller zeroes
- *     them).
+ *     h3 planes of B; K <= 1024, K and lda multiples of 4.  a_row_parts == 0:
+ *     `amax` is A's max slot (one scale for A); P > 0: `amax` holds A's row
+ *     maxima as P partial arrays [P][M] and every row is scaled by its own
+ *     (a row of small values, e.g. a node with a small gradient, keeps full
+ *     precision).  cmax / crow (each may be NULL): max |C| folded into the
+ *     slot cmax (the caller zeroes it) / C's row maxima as
+ *     molclr_gemm_row_parts(N) partial arrays (plain stores).
  *   molclr_linear_wgrad_h3: molclr_linear_wgrad given the max slots of dy
  *     and x (n_out, n_in, ld_dy, ld_x multiples of 4; same workspace). */
 int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* slot,
@@ -391,9 +391,22 @@ size_t molclr_hplanes_bytes(int64_t N, int64_t K);
 int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N,
                               const int64_t* K, const int64_t* ldb, const int* b_kmajor,
                               uint16_t* const* planes, molclr_stream_t stream);
+/* molclr_gemm_f32_bplanes (x6 planes, row-major A, K <= 1024; same kernel and
+ * result as its automatic choice) that also folds max |A| of its A rows into
+ * the slot amax_out and max |C| into the slot cmax (zeroed by the caller),
+ * and writes C's row maxima as molclr_gemm_row_parts(N) partial arrays
+ * crow[p][M] (plain stores; the row max is the max over p): the scales of
+ * the h3 products that consume A or C, with no pass when the q6 kernel runs.
+ * Each output may be NULL. */
+int64_t molclr_gemm_row_parts(int64_t N);
+int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* planes, float* C, int64_t M,
+                                int64_t N, int64_t K, int64_t lda, int64_t ldc,
+                                int epilogue_flags, const float* bias, const float* aux,
+                                int64_t ldaux, float* amax_out, float* cmax, float* crow,
+                                void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
                            float* rowmax, float* slot, int accumulate, molclr_stream_t stream);
-int molclr_gemm_f32_h3(const float* A, const float* amax, int a_rowwise, const uint16_t* hplanes,
+int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const uint16_t* hplanes,
                        float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
                        float* cmax, float* crow, molclr_stream_t stream);
@@ -457,6 +470,17 @@ int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const float* gamma,
                              const int64_t* seg_rows, int64_t dim, int dtype, int relu,
                              int accumulate, void* workspace, size_t workspace_bytes,
                              molclr_stream_t stream);
+
+/* molclr_batchnorm_seg_bwd (fp32; same dz) that also writes the row maxima of
+ * dz, rowmax[r] = max_c |dz[r][c]| (plain stores), and folds max |dz| into the
+ * slot (may be NULL; the caller zeroes it): the scales of the h3 products
+ * that consume dz (molclr_gemm_f32_h3 row-wise, molclr_linear_wgrad_h3). */
+int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, const float* gamma,
+                                 const float* beta, const float* save_mean,
+                                 const float* save_invstd, float* dz, float* dgamma, float* dbeta,
+                                 int nseg, const int64_t* seg_rows, int64_t dim, int relu,
+                                 int accumulate, float* rowmax, float* slot, void* workspace,
+                                 size_t workspace_bytes, molclr_stream_t stream);
 
 /* Segment pooling over graph_ptr (PyG global_mean_pool / global_add_pool):
  * mode 0 = mean (sum / max(count,1)), 1 = add. */

@@ -110,6 +110,13 @@ size_t molclr_batchnorm_ws_bound(int64_t rows, int64_t D);
     }                                                                                 \
   } while (0)
 
+// return a non-zero status of a nested entry-point call
+#define MOLCLR_TRY_RC(expr)   \
+  do {                        \
+    int rc_ = (expr);         \
+    if (rc_) return rc_;      \
+  } while (0)
+
 #define MOLCLR_LAUNCHED()                                                             \
   do {                                                                                \
     hipError_t e_ = hipGetLastError();                                                \

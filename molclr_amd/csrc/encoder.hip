@@ -128,14 +128,18 @@ MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, in
 }
 
 // workspace: backward scratch | h3 max slots of dz_l / dz1_l | h3 row maxima
-// of dz and dz1 [2][N] | the entry points' workspace
+// of agg / dz [N] and of a1 / dz1 [parts][N] | the entry points' workspace
 constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float);
-size_t rowmax_bytes(int64_t N) { return molclr::align_up((size_t)2 * N * sizeof(float), 256); }
+// row maxima of a [N,D] tensor (1 part) and of a [N,2D] GEMM output
+// (molclr_gemm_row_parts(2D) partial arrays)
+size_t rowmax_bytes(int64_t N, int64_t D) {
+  return molclr::align_up((size_t)(1 + molclr_gemm_row_parts(2 * D)) * N * sizeof(float), 256);
+}
 
 MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
   (void)L;
   return molclr::align_up(scratch_bytes(N, D, elem_bytes(dtype)), 256) + kSlotBytes +
-         rowmax_bytes(N) + kernels_ws(N, D) + 256;
+         rowmax_bytes(N, D) + kernels_ws(N, D) + 256;
 }
 
 MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t* x,
@@ -161,7 +165,7 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   float* ragg = (float*)((char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) +
                          kSlotBytes);
   float* ra1 = ragg + N;
-  void* kws = (char*)ragg + rowmax_bytes(N);
+  void* kws = (char*)ragg + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const bool h3 = !bf && e->fp32_gemm != 0;
   const bool h3f = h3 && (e->fp32_gemm & 2);  // h3 forward products (not the default)
@@ -210,29 +214,28 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
         const uint16_t* p0 = e->mlp0_planes[l];
         const uint16_t* p2 = e->mlp2_planes[l];
         MOLCLR_TRY(molclr_absmax_rows_f32(agg, N, D, D, ragg, sl, 1, stream));
-        if (hipMemsetAsync(ra1, 0, (size_t)N * sizeof(float), molclr::as_stream(stream)) !=
-            hipSuccess) {
-          molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
-          return MOLCLR_ERR_ARG;
-        }
         MOLCLR_TRY(molclr_gemm_f32_h3(agg, ragg, 1, p0, a1, N, 2 * D, D, D, 2 * D,
                                       MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
                                       sl + kMaxSlotParts, ra1, stream));
-        MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, 1, p2, z, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_BIAS,
-                                      e->mlp2_bias[l], nullptr, 0, nullptr, nullptr, stream));
+        MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, (int)molclr_gemm_row_parts(2 * D), p2, z, N, D,
+                                      2 * D, 2 * D, D, MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0,
+                                      nullptr, nullptr, stream));
       } else {
-        // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd)
-        MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
-                                           MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
-                                           kws_bytes, stream));
+        // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd);
+        // h3 backward: the first product also yields max |agg| and max |a1|
+        if (h3)
+          MOLCLR_TRY(molclr_gemm_f32_bplanes_max(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
+                                                 MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
+                                                 fmax + 2 * l * kMaxSlotParts,
+                                                 fmax + (2 * l + 1) * kMaxSlotParts, nullptr, kws,
+                                                 kws_bytes, stream));
+        else
+          MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
+                                             MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
+                                             kws_bytes, stream));
         MOLCLR_TRY(molclr_gemm_f32_bplanes(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D, 0,
                                            MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
                                            kws_bytes, stream));
-        if (h3) {
-          MOLCLR_TRY(molclr_absmax_f32(agg, N, D, D, fmax + 2 * l * kMaxSlotParts, 1, stream));
-          MOLCLR_TRY(molclr_absmax_f32(a1, N, 2 * D, 2 * D, fmax + (2 * l + 1) * kMaxSlotParts, 1,
-                                       stream));
-        }
       }
       MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
                                           e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
@@ -274,7 +277,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
   float* rdz = bmax + kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
   float* rdz1 = rdz + N;
-  void* kws = (char*)rdz + rowmax_bytes(N);
+  void* kws = (char*)rdz + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
   const bool h3 = !bf && e->fp32_gemm != 0;
@@ -294,10 +297,18 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     const void* z = A + lay.z[l];
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
-    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
-                                        F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l],
-                                        seg.n, seg.rows, D, dt, last ? 0 : 1, 1, kws, kws_bytes,
-                                        stream));
+    if (h3) {
+      // dz's row maxima and max slot for the h3 products
+      MOLCLR_TRY(molclr_batchnorm_seg_bwd_max(
+          (const float*)dy, (const float*)z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
+          F(lay.invstd[l]), (float*)dz, gr->bn_weight[l], gr->bn_bias[l], seg.n, seg.rows, D,
+          last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotParts, kws, kws_bytes, stream));
+    } else {
+      MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
+                                          F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l],
+                                          seg.n, seg.rows, D, dt, last ? 0 : 1, 1, kws, kws_bytes,
+                                          stream));
+    }
     if (bf) {
       const uint16_t *hz = (const uint16_t*)dz, *ha1 = (const uint16_t*)a1;
       // second Linear: dW2, db2 from dz and a1; dz1 = (dz W2) * (a1 > 0)
@@ -330,15 +341,9 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       MOLCLR_REQUIRE(gr->mlp2_weight[l] && gr->mlp2_bias[l] && gr->mlp0_weight[l] &&
                          gr->mlp0_bias[l],
                      "gin_encoder_bwd: h3 needs every MLP gradient");
-      MOLCLR_TRY(molclr_absmax_rows_f32(fz, N, D, D, rdz, sl, 1, stream));
       MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l],
                                         gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
                                         stream));
-      if (hipMemsetAsync(rdz1, 0, (size_t)N * sizeof(float), molclr::as_stream(stream)) !=
-          hipSuccess) {
-        molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
-        return MOLCLR_ERR_ARG;
-      }
       if (h3d) {
         MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, 1, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
                                       2 * D, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D,
@@ -354,7 +359,8 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                         gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D, 2 * D,
                                         D, 1, kws, kws_bytes, stream));
       if (h3d)
-        MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, 1, e->mlp0_planes_t[l],
+        MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, (int)molclr_gemm_row_parts(2 * D),
+                                      e->mlp0_planes_t[l],
                                       (float*)dagg, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE,
                                       nullptr, nullptr, 0, nullptr, nullptr, stream));
       else

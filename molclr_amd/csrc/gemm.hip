@@ -785,19 +785,24 @@ struct QStageB {
 // every outstanding load at the top of each step).
 // H3 != 0: the fp16 two-part form (mfma.h "h3"): the planes are 2 fp16 parts
 // of B scaled by its max slot `bmax`; A is scaled by its max slot `amax`
-// (H3 == 1) or row by row by the row maxima amax[M] (H3 == 2: each lane splits
-// one row of A, so a row of small values -- a node with a small gradient --
-// keeps its precision however large other rows are) and split into 2 parts;
-// three fp16 MFMAs per product; the sums are scaled back in the epilogue,
-// which also folds max |C| into the slot `cmax` and the row maxima of C into
-// `crow` [M] (atomic maxima; both optional, the caller zeroes them).
+// (H3 == 1) or row by row (H3 == 2) by its row maxima, given as `arow_parts`
+// partial arrays amax[p][M] (each lane splits one row of A, so a row of small
+// values -- a node with a small gradient -- keeps its precision however large
+// other rows are); three fp16 MFMAs per product; the sums are scaled back in
+// the epilogue.  Any mode: the epilogue folds max |C| into the slot `cmax`
+// (atomic maxima, the caller zeroes it) and stores the row maxima of C over
+// this block's columns into crow[column tile][M] (plain stores: the column
+// tiles' partial row maxima), and `amax_out` (zeroed) receives max |A| over
+// the loaded rows -- the scales an h3 consumer of A or C needs, with no pass
+// of their own.  Each is optional.
 template <int TN, int EPI, int KG, bool MASK, int H3 = 0>
 __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
     int accumulate, const float* __restrict__ amax, const float* __restrict__ bmax,
-    float* __restrict__ cmax, float* __restrict__ crow) {
+    float* __restrict__ cmax, float* __restrict__ crow, float* __restrict__ amax_out,
+    int arow_parts) {
   constexpr int T = 64 * kQ6Waves;  // threads of one K group
   constexpr int BN = 32 * TN;
   constexpr int NP = H3 ? 2 : 3;    // B planes
@@ -851,9 +856,21 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
 
   // this lane's A shift (its row's with H3 == 2), the planes' shift
-  const int sha = H3 == 1 ? h3_shift(amax) : H3 == 2 ? h3_shift_of(amax[arow_i]) : 0;
+  int sha = 0;
+  if constexpr (H3 == 1) sha = h3_shift(amax);
+  if constexpr (H3 == 2) {
+    float m = 0.f;
+    for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
+    sha = h3_shift_of(m);
+  }
   const int shb = H3 ? h3_shift(bmax) : 0;
+  float ain = 0.f;  // max |A| of this lane's loads (amax_out)
   auto compute = [&](const uint16_t* Bs, const float4(&a)[4], int r) {
+    if (amax_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ain = fmaxf(ain, fmaxf(fmaxf(fabsf(a[j].x), fabsf(a[j].y)), fmaxf(fabsf(a[j].z), fabsf(a[j].w))));
+    }
     float4 am4[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -965,8 +982,8 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
   float* tw = reinterpret_cast<float*>(lds) + wm * 32 * 32;
   const int64_t mw = m0 + 32 * wm;
-  // H3: max |C| of this lane's stores per epilogue row group it (row
-  // 8 it + lane / 8 of the wave's 32): for cmax and crow
+  // max |C| of this lane's stores per epilogue row group it (row 8 it +
+  // lane / 8 of the wave's 32): for cmax and crow
   float rm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
@@ -1005,7 +1022,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
           }
           if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
           *reinterpret_cast<float4*>(o) = v;
-          if (H3) rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
         } else {
           const float e[4] = {v4.x, v4.y, v4.z, v4.w};
           for (int j = 0; j < 4 && n + j < N; ++j) {
@@ -1015,14 +1032,14 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
             if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
             if (accumulate) x += o[j];
             o[j] = x;
-            if (H3) rm[it] = fmaxf(rm[it], fabsf(x));
+            rm[it] = fmaxf(rm[it], fabsf(x));
           }
         }
       }
     }
     __syncthreads();  // the wave's tile is rewritten by the next block
   }
-  if constexpr (H3 != 0) {
+  {
     if (crow != nullptr && grp == 0) {
       // the 8 lanes of a row (lane / 8) fold their maxima, then one atomic per row
 #pragma unroll
@@ -1032,12 +1049,12 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
         v = fmaxf(v, __shfl_xor(v, 2, 64));
         v = fmaxf(v, __shfl_xor(v, 4, 64));
         const int64_t m = mw + 8 * it + (lane >> 3);
-        if ((lane & 7) == 0 && m < M)
-          atomicMax(reinterpret_cast<unsigned int*>(crow + m), __float_as_uint(v));
+        if ((lane & 7) == 0 && m < M) crow[(n0 / BN) * M + m] = v;
       }
     }
     if (cmax != nullptr)
       absmax_publish(grp == 0 ? fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3])) : 0.f, cmax);
+    if (amax_out != nullptr) absmax_publish(ain, amax_out);
   }
 }
 
@@ -1400,7 +1417,7 @@ __global__ __launch_bounds__(256) void k_absmax_rows(const float* __restrict__ x
     if (lane == 0) rowmax[r] = m;
     all = fmaxf(all, m);
   }
-  absmax_publish(all, slot);
+  if (slot != nullptr) absmax_publish(all, slot);
 }
 
 // C = epilogue(Σ_z partial[z])  (fixed order -> deterministic)
@@ -1495,6 +1512,8 @@ struct Args {
   const float* bmax = nullptr;   // max |C| slot and row maxima out (may be null)
   float* cmax = nullptr;
   float* crow = nullptr;
+  float* amax_out = nullptr;     // q6: max |A| of the loaded rows out (may be null)
+  int arow_parts = 0;            // h3 row-wise: partial row-max arrays in amax
 };
 
 template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1, bool CS = false>
@@ -1604,6 +1623,10 @@ int wide_tn(int64_t N) {
   const int64_t p4 = (N + 127) / 128 * 128, p5 = (N + 159) / 160 * 160;
   return p5 <= p4 ? 5 : 4;
 }
+int64_t q6_col_tiles(int64_t N) {
+  const int64_t bn = 32 * wide_tn(N);
+  return (N + bn - 1) / bn;
+}
 int64_t q6_blocks(int64_t M, int64_t N) {
   const int64_t bn = 32 * wide_tn(N);
   return ((M + kQ6BM - 1) / kQ6BM) * ((N + bn - 1) / bn);
@@ -1620,7 +1643,7 @@ void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
   molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK, H3>),
                        dim3((unsigned)q6_blocks(a.M, a.N)), dim3(KG * 64 * kQ6Waves), 0, s, a.A,
                        a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux,
-                       a.accumulate, a.amax, a.bmax, a.cmax, a.crow);
+                       a.accumulate, a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts);
 }
 template <int TN, int EPI, int H3>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
@@ -1989,6 +2012,65 @@ MOLCLR_API int molclr_gemm_f32_bplanes_tile(const float* A, const uint16_t* plan
                   molclr::as_stream(stream));
 }
 
+MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* planes, float* C,
+                                           int64_t M, int64_t N, int64_t K, int64_t lda,
+                                           int64_t ldc, int epilogue_flags, const float* bias,
+                                           const float* aux, int64_t ldaux, float* amax_out,
+                                           float* cmax, float* crow, void* workspace,
+                                           size_t workspace_bytes, molclr_stream_t stream) {
+  const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
+  const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
+  MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_bplanes_max: negative size");
+  MOLCLR_REQUIRE(epilogue >= MOLCLR_EPI_NONE && epilogue <= MOLCLR_EPI_RELU_MASK,
+                 "gemm_f32_bplanes_max: bad epilogue %d", epilogue);
+  MOLCLR_REQUIRE((epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU) || bias,
+                 "gemm_f32_bplanes_max: bias epilogue needs bias");
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux,
+                 "gemm_f32_bplanes_max: relu-mask epilogue needs aux");
+  MOLCLR_REQUIRE(K % 4 == 0 && lda % 4 == 0 && lda >= K && ldc >= N && K <= kQ6MaxK,
+                 "gemm_f32_bplanes_max: K (<= %lld) and lda multiples of 4, lda >= K, ldc >= N",
+                 (long long)kQ6MaxK);
+  if (M == 0 || N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(K > 0 && A && planes && C, "gemm_f32_bplanes_max: null operand or K == 0");
+  const int64_t npad = planes_npad(N), kp = planes_kp(K);
+  MOLCLR_REQUIRE(3 * npad * kp < (1ll << 31) && q6_blocks(M, N) < (1ll << 31),
+                 "gemm_f32_bplanes_max: too large");
+  hipStream_t s = molclr::as_stream(stream);
+  if (q6_blocks(M, N) < 128) {
+    // molclr_gemm_f32_bplanes' automatic tile is not q6 here: run it (same
+    // kernel, same result as the plain call), then the max passes; crow's
+    // parts all get the full row maxima
+    MOLCLR_TRY_RC(molclr_gemm_f32_bplanes(A, planes, C, M, N, K, lda, ldc, 0, epilogue_flags, bias,
+                                          aux, ldaux, workspace, workspace_bytes, stream));
+    if (amax_out) MOLCLR_TRY_RC(molclr_absmax_f32(A, M, K, lda, amax_out, 1, stream));
+    if (crow || cmax) {
+      float* rows = crow;
+      if (!rows) {  // cmax only
+        MOLCLR_TRY_RC(molclr_absmax_f32(C, M, N, ldc, cmax, 1, stream));
+        return MOLCLR_OK;
+      }
+      int64_t blocks = molclr::ceil_div(M, 32);
+      blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+      hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, s, C, M, N, ldc, rows,
+                         cmax);
+      for (int64_t p = 1; p < q6_col_tiles(N); ++p)
+        (void)hipMemcpyAsync(rows + p * M, rows, (size_t)M * sizeof(float),
+                             hipMemcpyDeviceToDevice, s);
+    }
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  Args a{A, nullptr, C, M, N, K, lda, kp, ldc, bias, aux, ldaux, 0, accumulate, 9};
+  a.Bp = planes;
+  a.bps = npad * kp;
+  a.cmax = cmax;
+  a.crow = crow;
+  a.amax_out = amax_out;
+  return run_q6(a, npad, epilogue, s, 0);
+}
+
+MOLCLR_API int64_t molclr_gemm_row_parts(int64_t N) { return q6_col_tiles(N); }
+
 MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
                                        int64_t N, int64_t K, int64_t lda, int64_t ldc,
                                        int a_kmajor, int epilogue_flags, const float* bias,
@@ -2131,7 +2213,7 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
   return MOLCLR_OK;
 }
 
-MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_rowwise,
+MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts,
                                   const uint16_t* hplanes, float* C, int64_t M, int64_t N,
                                   int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
                                   const float* bias, const float* aux, int64_t ldaux, float* cmax,
@@ -2159,7 +2241,8 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_rowwi
   a.bmax = reinterpret_cast<const float*>(hplanes + 2 * npad * kp);
   a.cmax = cmax;
   a.crow = crow;
-  return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_rowwise ? 2 : 1);
+  a.arow_parts = a_row_parts;
+  return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
 }
 
 MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,

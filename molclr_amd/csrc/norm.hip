@@ -478,15 +478,14 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
   }
 }
 
+// one float4 of dz (k_bn_bwd_apply), stored and returned
 template <typename St>
-__global__ __launch_bounds__(kT) void k_bn_bwd_apply(
+__device__ __forceinline__ float4 bn_bwd_elem(
     const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
     const float4* __restrict__ mean, const float4* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
-    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t total4, int d4,
-    int relu, Segs sg) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total4) return;
+    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t t, int d4, int relu,
+    Segs sg) {
   const int64_t i = t / d4;
   const int c = (int)(t - i * d4);
   const int s = seg_of_row(sg, i);
@@ -506,7 +505,46 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
   o.z = (g.z - a.z - ((x.z - mu.z) * is.z) * b.z) * sc.z;
   o.w = (g.w - a.w - ((x.w - mu.w) * is.w) * b.w) * sc.w;
   St::st(dz, t, o);
+  return o;
 }
+
+template <typename St>
+__global__ __launch_bounds__(kT) void k_bn_bwd_apply(
+    const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
+    const float4* __restrict__ mean, const float4* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
+    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t total4, int d4,
+    int relu, Segs sg) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total4) return;
+  bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu, sg);
+}
+
+// k_bn_bwd_apply with dz's row maxima: a wave per row (a row's float4 columns
+// on its lanes), rowmax[r] = max |dz[r]| by plain store, max |dz| folded into
+// the slot once per block
+template <typename St>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_rows(
+    const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
+    const float4* __restrict__ mean, const float4* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
+    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t rows, int d4,
+    int relu, Segs sg, float* __restrict__ rowmax, float* __restrict__ slot) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float m = 0.f;
+  if (r < rows) {
+    for (int c = lane; c < d4; c += 64) {
+      const float4 o =
+          bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, r * d4 + c, d4, relu, sg);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+    }
+    m = wave_max(m);
+    if (lane == 0) rowmax[r] = m;
+  }
+  if (slot != nullptr) absmax_publish(m, slot);
+}
+
 // ---------------------------------------------------------------------------
 // segment pooling over graph_ptr
 // ---------------------------------------------------------------------------
@@ -789,7 +827,8 @@ template <typename St>
 int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* beta,
            const float* save_mean, const float* save_invstd, void* dzv, float* dgamma,
            float* dbeta, int nseg, const int64_t* seg_rows, int64_t D, int relu, int accumulate,
-           void* workspace, size_t workspace_bytes, hipStream_t s) {
+           void* workspace, size_t workspace_bytes, hipStream_t s, float* rowmax = nullptr,
+           float* slot = nullptr) {
   Segs sg;
   int64_t P = 0, rows = 0;
   if (int rc = make_segs(nseg, seg_rows, D, sg, P, rows)) return rc;
@@ -817,9 +856,15 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes),
                      0, s, p1, p2, sg, D, dgamma, dbeta, k1, k2, accumulate);
   const int64_t total4 = rows * (D / 4);
-  hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy, z,
-                     (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
-                     (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg);
+  if (rowmax)
+    hipLaunchKernelGGL(k_bn_bwd_apply_rows<St>, dim3((unsigned)molclr::ceil_div(rows, 4)),
+                       dim3(256), 0, s, dy, z, (const float4*)save_mean,
+                       (const float4*)save_invstd, gamma, beta, (const float4*)k1,
+                       (const float4*)k2, dz, rows, (int)(D / 4), relu, sg, rowmax, slot);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy,
+                       z, (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
+                       (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -878,6 +923,19 @@ MOLCLR_API int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const flo
   MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_BF16, "batchnorm_seg_bwd: dtype %d", dtype);
   return bn_bwd<StBF16>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
                         seg_rows, D, relu, accumulate, workspace, workspace_bytes, s);
+}
+
+MOLCLR_API int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, const float* gamma,
+                                            const float* beta, const float* save_mean,
+                                            const float* save_invstd, float* dz, float* dgamma,
+                                            float* dbeta, int nseg, const int64_t* seg_rows,
+                                            int64_t D, int relu, int accumulate, float* rowmax,
+                                            float* slot, void* workspace, size_t workspace_bytes,
+                                            molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rowmax, "batchnorm_seg_bwd_max: null rowmax");
+  return bn_bwd<StF32>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
+                       seg_rows, D, relu, accumulate, workspace, workspace_bytes,
+                       molclr::as_stream(stream), rowmax, slot);
 }
 
 MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,

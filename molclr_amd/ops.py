@@ -273,16 +273,22 @@ def absmax(x, out=None, accumulate=0) -> torch.Tensor:
     return out
 
 
+def row_parts(N: int) -> int:
+    """Partial row-max arrays a GEMM with N output columns writes (crow)."""
+    return int(_lib.load().molclr_gemm_row_parts(N))
+
+
 def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None,
-            rowwise=False, crow=None):
+            rowwise=0, crow=None):
     """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3.  amax: A's
-    max slot, or (rowwise) its row maxima [M]; cmax / crow (zeroed) receive
-    max |C| and C's row maxima."""
+    max slot, or (rowwise = P > 0) its row maxima as P partial arrays [P][M];
+    cmax (zeroed) receives max |C|, crow [row_parts(N)][M] C's row maxima."""
     _check(A, W)
     M = A.shape[0]
     planes = weight_planes(W, N, K, ldb, b_kmajor, "h3")
     out = torch.empty(M, N, dtype=torch.float32, device=A.device)
-    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), int(rowwise), planes.data_ptr(),
+    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), int(rowwise),
+              planes.data_ptr(),
               out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
               _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax),
               _lib.ptr(crow), _stream(A))
@@ -527,17 +533,27 @@ class _MLP(torch.autograd.Function):
             # a pass); the max slots serve the h3 weight gradients
             slots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=x.device)
             if H3_FORWARD:
-                rows = torch.zeros(2, M, dtype=torch.float32, device=x.device)
+                P = row_parts(2 * D)
+                rx = torch.empty(M, dtype=torch.float32, device=x.device)
+                ra1 = torch.empty(P, M, dtype=torch.float32, device=x.device)
                 _lib.call("molclr_absmax_rows_f32", x.data_ptr(), M, D, x.stride(0),
-                          rows[0].data_ptr(), slots[0].data_ptr(), 1, _stream(x))
-                a1 = gemm_h3(x, rows[0], W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1,
-                             cmax=slots[1], rowwise=True, crow=rows[1])
-                z = gemm_h3(a1, rows[1], W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2, rowwise=True)
+                          rx.data_ptr(), slots[0].data_ptr(), 1, _stream(x))
+                a1 = gemm_h3(x, rx, W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1,
+                             cmax=slots[1], rowwise=1, crow=ra1)
+                z = gemm_h3(a1, ra1, W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2, rowwise=P)
             else:
-                a1 = linear_fwd(x, W1, b1, relu=True)
+                # the first product (q6, x6 planes) also yields max |x| and max |a1|
+                a1 = torch.empty(M, 2 * D, dtype=torch.float32, device=x.device)
+                ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, 2 * D, D)
+                ws = _ws(ws_bytes, x.device) if ws_bytes else None
+                _lib.call("molclr_gemm_f32_bplanes_max", x.data_ptr(),
+                          weight_planes(W1, 2 * D, D, D, 0).data_ptr(), a1.data_ptr(), M, 2 * D,
+                          D, x.stride(0), a1.stride(0), EPI_BIAS_RELU, b1.data_ptr(), None, 0,
+                          slots[0].data_ptr(), slots[1].data_ptr(), None, _lib.ptr(ws), ws_bytes,
+                          _stream(x))
+                if _TIMER is not None:
+                    _TIMER.add("gemm_f32", 2.0 * M * 2 * D * D)
                 z = linear_fwd(a1, W2, b2, relu=False)
-                absmax(x, slots[0], accumulate=1)
-                absmax(a1, slots[1], accumulate=1)
             ctx.slots = slots
         else:
             a1 = linear_fwd(x, W1, b1, relu=True)
@@ -558,15 +574,17 @@ class _MLP(torch.autograd.Function):
             D = x.shape[1]
             slots = ctx.slots
             M = x.shape[0]
+            P = row_parts(2 * D)
             bslots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=dz.device)
-            rows = torch.zeros(2, M, dtype=torch.float32, device=dz.device)  # row maxima
+            rdz = torch.empty(M, dtype=torch.float32, device=dz.device)      # row maxima of dz
+            rdz1 = torch.empty(P, M, dtype=torch.float32, device=dz.device)  # ... of dz1
             _lib.call("molclr_absmax_rows_f32", dz.data_ptr(), M, D, dz.stride(0),
-                      rows[0].data_ptr(), bslots[0].data_ptr(), 1, _stream(dz))
+                      rdz.data_ptr(), bslots[0].data_ptr(), 1, _stream(dz))
             dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
-            dz1 = gemm_h3(dz, rows[0], W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
-                          cmax=bslots[1], rowwise=True, crow=rows[1])
+            dz1 = gemm_h3(dz, rdz, W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
+                          cmax=bslots[1], rowwise=1, crow=rdz1)
             dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
-            dx = (gemm_h3(dz1, rows[1], W1, D, 2 * D, D, 1, rowwise=True) if need[0] else None)
+            dx = (gemm_h3(dz1, rdz1, W1, D, 2 * D, D, 1, rowwise=P) if need[0] else None)
             return dx, dW1, db1, dW2, db2
         # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
         dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],

@@ -752,7 +752,9 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
         ref = ref * (aux > 0)
     Ad, Wd = A.float().to(dev), W.float().to(dev)
     planes = _h3_planes(lib, Wd, N, K, 0, dev)
+    P = int(lib.molclr_gemm_row_parts(N))
     rows = torch.zeros(2, M, device=dev)
+    crow = torch.zeros(P, M, device=dev)
     slots = torch.zeros(2, 64, device=dev)
     rc = lib.molclr_absmax_rows_f32(Ad.data_ptr(), M, K, K, rows[0].data_ptr(),
                                     slots[0].data_ptr(), 0, ops._stream(Ad))
@@ -762,7 +764,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
                                 rowwise, planes.data_ptr(), C.data_ptr(), M, N, K, K, N, epi,
                                 bd.data_ptr(), ad.data_ptr(), N, slots[1].data_ptr(),
-                                rows[1].data_ptr(), ops._stream(Ad))
+                                crow.data_ptr(), ops._stream(Ad))
     assert rc == 0, lib.molclr_last_error()
     torch.cuda.synchronize()
     # row-wise scaling: every row at fp32 accuracy (per-row relative error)
@@ -775,7 +777,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     assert err < 2e-6, err
     assert rows[0].cpu().equal(Ad.abs().amax(1).cpu())
     assert slots[1].max().item() == C.abs().max().item()
-    assert rows[1].cpu().equal(C.abs().amax(1).cpu())
+    assert crow.amax(0).cpu().equal(C.abs().amax(1).cpu())
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
@@ -800,3 +802,85 @@ def test_linear_wgrad_h3(dev, rows, n_out, n_in):
     assert rc == 0, lib.molclr_last_error()
     assert rel(dW, dy.t() @ x) < 2e-6
     assert rel(db, dy.sum(0)) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(30556, 600, 300, 2), (15000, 256, 128, 2), (1500, 256, 128, 2),
+                                       (333, 64, 36, 0)])
+def test_gemm_bplanes_max(dev, M, N, K, epi):
+    """The GEMM with its max outputs equals molclr_gemm_f32_bplanes' automatic
+    choice bit for bit (q6, or the small-shape fallback), and the slots hold
+    max |A|, max |C| and C's row maxima."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M)
+    A = (torch.randn(M, K, generator=g) * 3).to(dev)
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    ref = ops.gemm_w(A, W, M, N, K, K, K, False, False, epi, bias=b)  # automatic tile
+    planes = ops.weight_planes(W, N, K, K, 0)
+    C = torch.empty(M, N, device=dev)
+    sl = torch.zeros(2, 64, device=dev)
+    rows = torch.zeros(int(lib.molclr_gemm_row_parts(N)), M, device=dev)
+    ws_b = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
+    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    rc = lib.molclr_gemm_f32_bplanes_max(A.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N, K,
+                                         K, N, epi, b.data_ptr(), None, 0, sl[0].data_ptr(),
+                                         sl[1].data_ptr(), rows.data_ptr(), ws.data_ptr(), ws_b,
+                                         ops._stream(A))
+    assert rc == 0, lib.molclr_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(C, ref)
+    assert sl[0].max().item() == A.abs().max().item()
+    assert sl[1].max().item() == C.abs().max().item()
+    assert torch.equal(rows.amax(0), C.abs().amax(1))
+
+
+@pytest.mark.parametrize("rows,D,relu", [((15300, 15256), 300, 1), ((1950, 2001, 40), 128, 0)])
+def test_batchnorm_seg_bwd_max(dev, rows, D, relu):
+    """molclr_batchnorm_seg_bwd_max: dz bit-identical to molclr_batchnorm_seg_bwd,
+    plus dz's row maxima and max slot."""
+    import ctypes
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(D)
+    R = sum(rows)
+    z = (torch.randn(R, D, generator=g) * 2 + 0.5).to(dev)
+    dy = (torch.randn(R, D, generator=g) * 1e-4).to(dev)
+    gamma, beta = torch.rand(D, generator=g).to(dev), torch.randn(D, generator=g).to(dev)
+    nseg = len(rows)
+    sr = (ctypes.c_int64 * nseg)(*rows)
+    ws_b = lib.molclr_batchnorm_seg_workspace_bytes(nseg, sr, D)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
+    mean = torch.empty(nseg, D, device=dev)
+    inv = torch.empty(nseg, D, device=dev)
+    rm, rv = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    y = torch.empty(R, D, device=dev)
+    st = ops._stream(z)
+    assert lib.molclr_batchnorm_seg_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                        rm.data_ptr(), rv.data_ptr(), None, y.data_ptr(),
+                                        mean.data_ptr(), inv.data_ptr(), nseg, sr, D, 0, 0.1,
+                                        1e-5, 1, relu, ws.data_ptr(), ws_b, st) == 0
+    outs = []
+    for fused in (0, 1):
+        dz = torch.empty(R, D, device=dev)
+        dg, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        rmax, slot = torch.zeros(R, device=dev), torch.zeros(64, device=dev)
+        if fused:
+            rc = lib.molclr_batchnorm_seg_bwd_max(dy.data_ptr(), z.data_ptr(), gamma.data_ptr(),
+                                                  beta.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                                  dz.data_ptr(), dg.data_ptr(), db.data_ptr(), nseg,
+                                                  sr, D, relu, 1, rmax.data_ptr(), slot.data_ptr(),
+                                                  ws.data_ptr(), ws_b, st)
+        else:
+            rc = lib.molclr_batchnorm_seg_bwd(dy.data_ptr(), z.data_ptr(), gamma.data_ptr(),
+                                              beta.data_ptr(), mean.data_ptr(), inv.data_ptr(),
+                                              dz.data_ptr(), dg.data_ptr(), db.data_ptr(), nseg, sr,
+                                              D, 0, relu, 1, ws.data_ptr(), ws_b, st)
+        assert rc == 0, lib.molclr_last_error()
+        outs.append((dz, dg, db, rmax, slot))
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b)
+    dz, rmax, slot = outs[1][0], outs[1][3], outs[1][4]
+    assert torch.equal(rmax, dz.abs().amax(1))
+    assert slot.max().item() == dz.abs().max().item()
