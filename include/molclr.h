@@ -364,8 +364,9 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  * exactly.  Same epilogues and shapes as the q6 / w6 kernels they replace
  * (models/ginet_molclr.py:19-23: the GIN MLP forward, data and weight
  * gradients).
- *   A max slot is 64 floats whose max is the tensor's max |x| (producers
- *     spread their atomic maxima over the entries).
+ *   A max slot is 64 entries 128 bytes apart (2048 floats, 8 KB) whose max
+ *     is the tensor's max |x| (producers spread their atomic maxima over the
+ *     entries; atomics on one cache line serialise).
  *   molclr_absmax_f32: slot <- max |x| over a [rows][cols] (ld) matrix
  *     (accumulate != 0: folded into the current slot; else the slot is reset
  *     first).  The max is order-independent, so every producer of the same
@@ -382,7 +383,8 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  *     (a row of small values, e.g. a node with a small gradient, keeps full
  *     precision).  cmax / crow (each may be NULL): max |C| folded into the
  *     slot cmax (the caller zeroes it) / C's row maxima as
- *     molclr_gemm_row_parts(N) partial arrays (plain stores).
+ *     molclr_gemm_row_parts(N) partial arrays (plain stores); amax_out (may
+ *     be NULL, zeroed by the caller): max |A| folded in.
  *   molclr_linear_wgrad_h3: molclr_linear_wgrad given the max slots of dy
  *     and x (n_out, n_in, ld_dy, ld_x multiples of 4; same workspace). */
 int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* slot,
@@ -409,7 +411,7 @@ int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t l
 int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const uint16_t* hplanes,
                        float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
-                       float* cmax, float* crow, molclr_stream_t stream);
+                       float* cmax, float* crow, float* amax_out, molclr_stream_t stream);
 int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
                            const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
                            int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
@@ -472,9 +474,11 @@ int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const float* gamma,
                              molclr_stream_t stream);
 
 /* molclr_batchnorm_seg_bwd (fp32; same dz) that also writes the row maxima of
- * dz, rowmax[r] = max_c |dz[r][c]| (plain stores), and folds max |dz| into the
- * slot (may be NULL; the caller zeroes it): the scales of the h3 products
- * that consume dz (molclr_gemm_f32_h3 row-wise, molclr_linear_wgrad_h3). */
+ * dz as molclr_bn_row_parts(dim) partial arrays rowmax[p][rows] (plain
+ * stores; max |dz[r]| = max over p) and folds max |dz| into the slot (may be
+ * NULL; the caller zeroes it): the scales of the h3 products that consume dz
+ * (molclr_gemm_f32_h3 row-wise, molclr_linear_wgrad_h3). */
+int molclr_bn_row_parts(int64_t dim);
 int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, const float* gamma,
                                  const float* beta, const float* save_mean,
                                  const float* save_invstd, float* dz, float* dgamma, float* dbeta,

@@ -206,10 +206,13 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// A tensor's max |x| "slot" (molclr_absmax_f32) is kMaxSlotParts floats whose
-// max is the value: producers spread their atomics over the entries (one
-// address would serialise thousands of them), consumers fold all entries.
+// A tensor's max |x| "slot" (molclr_absmax_f32) is kMaxSlotParts entries, each
+// on its own 128-byte line, whose max is the value: producers spread their
+// atomics over the entries (atomics on one line serialise: thousands of them
+// on one or two lines cost tens of microseconds), consumers fold all entries.
 constexpr int kMaxSlotParts = 64;
+constexpr int kMaxSlotStride = 32;  // floats: each entry on its own 128-byte line
+constexpr int kMaxSlotFloats = kMaxSlotParts * kMaxSlotStride;
 
 // Folds a lane's max |x| (v >= 0) into a slot: block max through LDS, then one
 // global atomic max on the float's bits (ordered like the values for v >= 0)
@@ -222,7 +225,8 @@ __device__ __forceinline__ void absmax_publish(float v, float* slot) {
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < (int)((blockDim.x + 63) >> 6); ++w) v = fmaxf(v, red_[w]);
-    atomicMax(reinterpret_cast<unsigned int*>(slot + blockIdx.x % kMaxSlotParts),
+    atomicMax(reinterpret_cast<unsigned int*>(slot + (blockIdx.x % kMaxSlotParts) * kMaxSlotStride),
               __float_as_uint(v));
   }
+  __syncthreads();  // red_ is reused by the block's next call
 }

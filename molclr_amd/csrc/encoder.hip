@@ -40,7 +40,7 @@ struct ArenaLayout {
     }
     h0 = off(N * D * es);
     ec = off((size_t)L * MOLCLR_NUM_ECOMB * D * sizeof(float));
-    smax = off((size_t)MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float));  // h3: max |agg_l|, |a1_l|
+    smax = off((size_t)MOLCLR_MAX_LAYERS * 2 * kMaxSlotFloats * sizeof(float));  // h3: max |agg_l|, |a1_l|
     total = used;
   }
 };
@@ -129,11 +129,12 @@ MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, in
 
 // workspace: backward scratch | h3 max slots of dz_l / dz1_l | h3 row maxima
 // of agg / dz [N] and of a1 / dz1 [parts][N] | the entry points' workspace
-constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotParts * sizeof(float);
+constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotFloats * sizeof(float);
 // row maxima of a [N,D] tensor (1 part) and of a [N,2D] GEMM output
 // (molclr_gemm_row_parts(2D) partial arrays)
 size_t rowmax_bytes(int64_t N, int64_t D) {
-  return molclr::align_up((size_t)(1 + molclr_gemm_row_parts(2 * D)) * N * sizeof(float), 256);
+  return molclr::align_up((size_t)(molclr_bn_row_parts(D) + molclr_gemm_row_parts(2 * D)) * N *
+                              sizeof(float), 256);
 }
 
 MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
@@ -170,7 +171,7 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   const bool h3 = !bf && e->fp32_gemm != 0;
   const bool h3f = h3 && (e->fp32_gemm & 2);  // h3 forward products (not the default)
   float* fmax = F(lay.smax);  // h3: [l][0] = max |agg_l|, [l][1] = max |a1_l|
-  if (h3 && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
     molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
     return MOLCLR_ERR_ARG;
@@ -210,24 +211,24 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
       if (h3f) {
         // GINEConv.update in h3 (ops._MLP): max |agg| by a pass, max |a1| from
         // the first GEMM's epilogue
-        float* sl = fmax + 2 * l * kMaxSlotParts;
+        float* sl = fmax + 2 * l * kMaxSlotFloats;
         const uint16_t* p0 = e->mlp0_planes[l];
         const uint16_t* p2 = e->mlp2_planes[l];
         MOLCLR_TRY(molclr_absmax_rows_f32(agg, N, D, D, ragg, sl, 1, stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(agg, ragg, 1, p0, a1, N, 2 * D, D, D, 2 * D,
                                       MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
-                                      sl + kMaxSlotParts, ra1, stream));
+                                      sl + kMaxSlotFloats, ra1, nullptr, stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, (int)molclr_gemm_row_parts(2 * D), p2, z, N, D,
                                       2 * D, 2 * D, D, MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0,
-                                      nullptr, nullptr, stream));
+                                      nullptr, nullptr, nullptr, stream));
       } else {
         // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd);
         // h3 backward: the first product also yields max |agg| and max |a1|
         if (h3)
           MOLCLR_TRY(molclr_gemm_f32_bplanes_max(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
                                                  MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
-                                                 fmax + 2 * l * kMaxSlotParts,
-                                                 fmax + (2 * l + 1) * kMaxSlotParts, nullptr, kws,
+                                                 fmax + 2 * l * kMaxSlotFloats,
+                                                 fmax + (2 * l + 1) * kMaxSlotFloats, nullptr, kws,
                                                  kws_bytes, stream));
         else
           MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
@@ -276,15 +277,14 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
   float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
   float* rdz = bmax + kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
-  float* rdz1 = rdz + N;
+  float* rdz1 = rdz + (size_t)molclr_bn_row_parts(D) * N;  // after dz's row-max parts
   void* kws = (char*)rdz + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
   const bool h3 = !bf && e->fp32_gemm != 0;
-  const bool h3d = h3 && (e->fp32_gemm & 1);  // h3 data-gradient products
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
-  if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotParts * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
     molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
     return MOLCLR_ERR_ARG;
@@ -302,7 +302,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       MOLCLR_TRY(molclr_batchnorm_seg_bwd_max(
           (const float*)dy, (const float*)z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
           F(lay.invstd[l]), (float*)dz, gr->bn_weight[l], gr->bn_bias[l], seg.n, seg.rows, D,
-          last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotParts, kws, kws_bytes, stream));
+          last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotFloats, kws, kws_bytes, stream));
     } else {
       MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
                                           F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l],
@@ -332,41 +332,32 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                                 gr->edge_embedding1[l], gr->edge_embedding2[l], N,
                                                 D, 1, kws, kws_bytes, stream));
     } else if (h3) {
-      // ops._MLP's h3 backward: dW2 (+db2), dz1 (ReLU mask of a1; its max and
-      // row maxima from the epilogue), dW1 (+db1), dagg.  The data-gradient
-      // products scale A row by row (gradient rows span many binades).
+      // ops._MLP's h3 backward: dz1 (ReLU mask of a1), dW2 (+db2), dW1 (+db1),
+      // dagg.  The data-gradient products scale A row by row (gradient rows
+      // span many binades): dz's row maxima and max come from the BatchNorm
+      // backward, dz1's from the dz1 product's epilogue.
       const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
-      float* sl = bmax + 2 * l * kMaxSlotParts;
-      const float* fl = fmax + 2 * l * kMaxSlotParts;
+      float* sl = bmax + 2 * l * kMaxSlotFloats;
+      const float* fl = fmax + 2 * l * kMaxSlotFloats;
       MOLCLR_REQUIRE(gr->mlp2_weight[l] && gr->mlp2_bias[l] && gr->mlp0_weight[l] &&
                          gr->mlp0_bias[l],
                      "gin_encoder_bwd: h3 needs every MLP gradient");
-      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotParts, gr->mlp2_weight[l],
+      // dz1 (its epilogue yields dz1's max and row maxima), then the weight
+      // gradients
+      MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, molclr_bn_row_parts(D), e->mlp2_planes_t[l],
+                                    (float*)dz1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_RELU_MASK,
+                                    nullptr, fa1, 2 * D, sl + kMaxSlotFloats, rdz1, nullptr,
+                                    stream));
+      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
                                         gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
                                         stream));
-      if (h3d) {
-        MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, 1, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
-                                      2 * D, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D,
-                                      sl + kMaxSlotParts, rdz1, stream));
-      } else {
-        MOLCLR_TRY(molclr_gemm_f32_bplanes(fz, e->mlp2_planes_t[l], (float*)dz1, N, 2 * D, D, D,
-                                           2 * D, 0, MOLCLR_EPI_RELU_MASK, nullptr, fa1, 2 * D,
-                                           kws, kws_bytes, stream));
-        MOLCLR_TRY(molclr_absmax_f32((const float*)dz1, N, 2 * D, 2 * D, sl + kMaxSlotParts, 1,
-                                     stream));
-      }
-      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotParts, fagg, fl,
+      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotFloats, fagg, fl,
                                         gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D, 2 * D,
                                         D, 1, kws, kws_bytes, stream));
-      if (h3d)
-        MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, (int)molclr_gemm_row_parts(2 * D),
-                                      e->mlp0_planes_t[l],
-                                      (float*)dagg, N, D, 2 * D, 2 * D, D, MOLCLR_EPI_NONE,
-                                      nullptr, nullptr, 0, nullptr, nullptr, stream));
-      else
-        MOLCLR_TRY(molclr_gemm_f32_bplanes((const float*)dz1, e->mlp0_planes_t[l], (float*)dagg,
-                                           N, D, 2 * D, 2 * D, D, 0, MOLCLR_EPI_NONE, nullptr,
-                                           nullptr, 0, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, (int)molclr_gemm_row_parts(2 * D),
+                                    e->mlp0_planes_t[l], (float*)dagg, N, D, 2 * D, 2 * D, D,
+                                    MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr,
+                                    nullptr, stream));
       MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
                                            g->ecount, (float*)dh, gr->edge_embedding1[l],
                                            gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));

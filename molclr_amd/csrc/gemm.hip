@@ -1339,7 +1339,7 @@ __global__ __launch_bounds__(256) void k_hplanes_max_batch(PlanesJobs jobs) {
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0)
-    reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x] =
+    reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x * kMaxSlotStride] =
         fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 // one thread per (n, 8 k) of the padded grid: two 16-byte plane stores
@@ -2150,7 +2150,7 @@ MOLCLR_API int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int
                                  float* slot, int accumulate, molclr_stream_t stream) {
   MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && slot, "absmax_f32: bad arguments");
   hipStream_t s = molclr::as_stream(stream);
-  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotParts * sizeof(float), s);
+  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotFloats * sizeof(float), s);
   if (rows > 0 && cols > 0) {
     MOLCLR_REQUIRE(x, "absmax_f32: null x");
     int64_t blocks = ld == cols ? molclr::ceil_div(rows * cols, 256 * 16) : rows;
@@ -2167,7 +2167,7 @@ MOLCLR_API int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols
   MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && rowmax && slot,
                  "absmax_rows_f32: bad arguments");
   hipStream_t s = molclr::as_stream(stream);
-  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotParts * sizeof(float), s);
+  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotFloats * sizeof(float), s);
   if (rows > 0) {
     MOLCLR_REQUIRE(x || cols == 0, "absmax_rows_f32: null x");
     int64_t blocks = molclr::ceil_div(rows, 4 * 8);
@@ -2180,7 +2180,7 @@ MOLCLR_API int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols
 }
 
 MOLCLR_API size_t molclr_hplanes_bytes(int64_t N, int64_t K) {
-  return (size_t)2 * planes_npad(N) * planes_kp(K) * sizeof(uint16_t) + kHMaxParts * sizeof(float);
+  return (size_t)2 * planes_npad(N) * planes_kp(K) * sizeof(uint16_t) + kMaxSlotFloats * sizeof(float);
 }
 
 MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N,
@@ -2217,7 +2217,7 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
                                   const uint16_t* hplanes, float* C, int64_t M, int64_t N,
                                   int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
                                   const float* bias, const float* aux, int64_t ldaux, float* cmax,
-                                  float* crow, molclr_stream_t stream) {
+                                  float* crow, float* amax_out, molclr_stream_t stream) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_h3: negative size");
@@ -2241,6 +2241,7 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
   a.bmax = reinterpret_cast<const float*>(hplanes + 2 * npad * kp);
   a.cmax = cmax;
   a.crow = crow;
+  a.amax_out = amax_out;
   a.arow_parts = a_row_parts;
   return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
 }

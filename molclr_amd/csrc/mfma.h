@@ -86,7 +86,7 @@ __device__ __forceinline__ int h3_shift_of(float m) {
 // ... of a tensor from its max slot (kMaxSlotParts entries, molclr_absmax_f32).
 // Every lane of the wave must call it.
 __device__ __forceinline__ int h3_shift(const float* __restrict__ slot) {
-  return h3_shift_of(wave_max(slot[threadIdx.x & (kMaxSlotParts - 1)]));
+  return h3_shift_of(wave_max(slot[(threadIdx.x & (kMaxSlotParts - 1)) * kMaxSlotStride]));
 }
 
 __device__ __forceinline__ void hsplit2(float a, float b, int sh, uint32_t& h, uint32_t& l) {

@@ -514,36 +514,45 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
     const float4* __restrict__ mean, const float4* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
     const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t total4, int d4,
-    int relu, Segs sg) {
+    int relu, Segs sg, float* __restrict__ rowparts, int nparts, float* __restrict__ slot) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (rowparts != nullptr) {  // block-uniform: every thread reaches the reductions
+    // dz's row maxima as plain stores: a row's float4s are contiguous lanes,
+    // spread over at most nparts waves; each wave's piece of a row (a
+    // segment) is reduced by a segmented shuffle and its first lane stores
+    // the piece's max as part (its wave - the row's first wave)
+    const int64_t rows = total4 / d4;
+    float m = 0.f;
+    int row = -1;
+    if (t < total4) {
+      const float4 o = bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu,
+                                       sg);
+      m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+      row = (int)(t / d4);
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float mv = __shfl_down(m, off, 64);
+      const int rv = __shfl_down(row, off, 64);
+      if (lane + off < 64 && rv == row) m = fmaxf(m, mv);
+    }
+    const int rp = __shfl_up(row, 1, 64);
+    if (row >= 0 && (lane == 0 || rp != row)) {
+      const int64_t rs = (int64_t)row * d4;  // the row's first float4
+      const int part = (int)((t >> 6) - (rs >> 6));
+      rowparts[part * rows + row] = m;
+      if (part == 0)  // parts this row does not reach
+        for (int q = (int)(((rs + d4 - 1) >> 6) - (rs >> 6)) + 1; q < nparts; ++q)
+          rowparts[q * rows + row] = 0.f;
+    }
+    if (slot != nullptr) absmax_publish(m, slot);
+    return;
+  }
   if (t >= total4) return;
   bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu, sg);
 }
 
-// k_bn_bwd_apply with dz's row maxima: a wave per row (a row's float4 columns
-// on its lanes), rowmax[r] = max |dz[r]| by plain store, max |dz| folded into
-// the slot once per block
-template <typename St>
-__global__ __launch_bounds__(256) void k_bn_bwd_apply_rows(
-    const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
-    const float4* __restrict__ mean, const float4* __restrict__ invstd,
-    const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
-    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t rows, int d4,
-    int relu, Segs sg, float* __restrict__ rowmax, float* __restrict__ slot) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  float m = 0.f;
-  if (r < rows) {
-    for (int c = lane; c < d4; c += 64) {
-      const float4 o =
-          bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, r * d4 + c, d4, relu, sg);
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
-    }
-    m = wave_max(m);
-    if (lane == 0) rowmax[r] = m;
-  }
-  if (slot != nullptr) absmax_publish(m, slot);
-}
 
 // ---------------------------------------------------------------------------
 // segment pooling over graph_ptr
@@ -823,11 +832,14 @@ int bn_fwd(const void* zv, const float* gamma, const float* beta, float* running
   return MOLCLR_OK;
 }
 
+// waves a row of D / 4 float4s can touch (k_bn_bwd_apply's row parts)
+int bn_row_parts(int64_t D) { return (int)((D / 4 + 62) / 64) + 1; }
+
 template <typename St>
 int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* beta,
            const float* save_mean, const float* save_invstd, void* dzv, float* dgamma,
            float* dbeta, int nseg, const int64_t* seg_rows, int64_t D, int relu, int accumulate,
-           void* workspace, size_t workspace_bytes, hipStream_t s, float* rowmax = nullptr,
+           void* workspace, size_t workspace_bytes, hipStream_t s, float* rowparts = nullptr,
            float* slot = nullptr) {
   Segs sg;
   int64_t P = 0, rows = 0;
@@ -856,15 +868,12 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
   hipLaunchKernelGGL(k_bn_bwd_final, dim3(molclr::ceil_div(D, kRedCols)), dim3(kRedCols * kRedLanes),
                      0, s, p1, p2, sg, D, dgamma, dbeta, k1, k2, accumulate);
   const int64_t total4 = rows * (D / 4);
-  if (rowmax)
-    hipLaunchKernelGGL(k_bn_bwd_apply_rows<St>, dim3((unsigned)molclr::ceil_div(rows, 4)),
-                       dim3(256), 0, s, dy, z, (const float4*)save_mean,
-                       (const float4*)save_invstd, gamma, beta, (const float4*)k1,
-                       (const float4*)k2, dz, rows, (int)(D / 4), relu, sg, rowmax, slot);
-  else
-    hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy,
-                       z, (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
-                       (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg);
+  static_assert(kT % 64 == 0, "row parts follow the waves");
+  MOLCLR_REQUIRE(!rowparts || rows < (1ll << 31), "batchnorm_seg_bwd_max: too many rows");
+  hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy, z,
+                     (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
+                     (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg,
+                     rowparts, bn_row_parts(D), slot);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -924,6 +933,8 @@ MOLCLR_API int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const flo
   return bn_bwd<StBF16>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
                         seg_rows, D, relu, accumulate, workspace, workspace_bytes, s);
 }
+
+MOLCLR_API int molclr_bn_row_parts(int64_t dim) { return bn_row_parts(dim); }
 
 MOLCLR_API int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, const float* gamma,
                                             const float* beta, const float* save_mean,

@@ -259,7 +259,7 @@ FP32_GEMM = os.environ.get("MOLCLR_FP32_GEMM", "h3")
 H3_FORWARD = os.environ.get("MOLCLR_H3_FORWARD", "0") == "1"
 
 
-MAX_SLOT = 64  # floats per max |x| slot (molclr_absmax_f32)
+MAX_SLOT = 64 * 32  # floats per max |x| slot (molclr_absmax_f32: 64 entries, 128 B apart)
 
 
 def absmax(x, out=None, accumulate=0) -> torch.Tensor:
@@ -279,7 +279,7 @@ def row_parts(N: int) -> int:
 
 
 def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None,
-            rowwise=0, crow=None):
+            rowwise=0, crow=None, amax_out=None):
     """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3.  amax: A's
     max slot, or (rowwise = P > 0) its row maxima as P partial arrays [P][M];
     cmax (zeroed) receives max |C|, crow [row_parts(N)][M] C's row maxima."""
@@ -291,7 +291,7 @@ def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, 
               planes.data_ptr(),
               out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
               _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax),
-              _lib.ptr(crow), _stream(A))
+              _lib.ptr(crow), _lib.ptr(amax_out), _stream(A))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -569,8 +569,8 @@ class _MLP(torch.autograd.Function):
         dz = _c(dz)
         need = ctx.needs_input_grad
         if ctx.h3 and all(need[1:]):
-            # the executor's h3 order: dW2 (+db2), dz1 (relu mask of a1, max |dz1|
-            # from its epilogue), dW1 (+db1), dx
+            # the executor's h3 order: dz1 (relu mask of a1; max |dz1| and its row
+            # maxima from its epilogue), dW2 (+db2), dW1 (+db1), dx
             D = x.shape[1]
             slots = ctx.slots
             M = x.shape[0]
@@ -580,9 +580,9 @@ class _MLP(torch.autograd.Function):
             rdz1 = torch.empty(P, M, dtype=torch.float32, device=dz.device)  # ... of dz1
             _lib.call("molclr_absmax_rows_f32", dz.data_ptr(), M, D, dz.stride(0),
                       rdz.data_ptr(), bslots[0].data_ptr(), 1, _stream(dz))
-            dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
             dz1 = gemm_h3(dz, rdz, W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
                           cmax=bslots[1], rowwise=1, crow=rdz1)
+            dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
             dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
             dx = (gemm_h3(dz1, rdz1, W1, D, 2 * D, D, 1, rowwise=P) if need[0] else None)
             return dx, dW1, db1, dW2, db2

@@ -755,7 +755,8 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     P = int(lib.molclr_gemm_row_parts(N))
     rows = torch.zeros(2, M, device=dev)
     crow = torch.zeros(P, M, device=dev)
-    slots = torch.zeros(2, 64, device=dev)
+    slots = torch.zeros(2, 2048, device=dev)
+    aout = torch.zeros(2048, device=dev)
     rc = lib.molclr_absmax_rows_f32(Ad.data_ptr(), M, K, K, rows[0].data_ptr(),
                                     slots[0].data_ptr(), 0, ops._stream(Ad))
     assert rc == 0
@@ -764,7 +765,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
                                 rowwise, planes.data_ptr(), C.data_ptr(), M, N, K, K, N, epi,
                                 bd.data_ptr(), ad.data_ptr(), N, slots[1].data_ptr(),
-                                crow.data_ptr(), ops._stream(Ad))
+                                crow.data_ptr(), aout.data_ptr(), ops._stream(Ad))
     assert rc == 0, lib.molclr_last_error()
     torch.cuda.synchronize()
     # row-wise scaling: every row at fp32 accuracy (per-row relative error)
@@ -778,6 +779,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     assert rows[0].cpu().equal(Ad.abs().amax(1).cpu())
     assert slots[1].max().item() == C.abs().max().item()
     assert crow.amax(0).cpu().equal(C.abs().amax(1).cpu())
+    assert aout.max().item() == Ad.abs().max().item()
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
@@ -788,7 +790,7 @@ def test_linear_wgrad_h3(dev, rows, n_out, n_in):
     dy = torch.randn(rows, n_out, generator=g, dtype=torch.float64) * 1e-6
     x = torch.randn(rows, n_in, generator=g, dtype=torch.float64)
     dyd, xd = dy.float().to(dev), x.float().to(dev)
-    slots = torch.zeros(2, 64, device=dev)
+    slots = torch.zeros(2, 2048, device=dev)
     for t, sl in ((dyd, slots[0]), (xd, slots[1])):
         assert lib.molclr_absmax_f32(t.data_ptr(), t.shape[0], t.shape[1], t.shape[1],
                                      sl.data_ptr(), 0, ops._stream(t)) == 0
@@ -819,7 +821,7 @@ def test_gemm_bplanes_max(dev, M, N, K, epi):
     ref = ops.gemm_w(A, W, M, N, K, K, K, False, False, epi, bias=b)  # automatic tile
     planes = ops.weight_planes(W, N, K, K, 0)
     C = torch.empty(M, N, device=dev)
-    sl = torch.zeros(2, 64, device=dev)
+    sl = torch.zeros(2, 2048, device=dev)
     rows = torch.zeros(int(lib.molclr_gemm_row_parts(N)), M, device=dev)
     ws_b = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
     ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
@@ -864,7 +866,8 @@ def test_batchnorm_seg_bwd_max(dev, rows, D, relu):
     for fused in (0, 1):
         dz = torch.empty(R, D, device=dev)
         dg, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
-        rmax, slot = torch.zeros(R, device=dev), torch.zeros(64, device=dev)
+        rmax = torch.full((lib.molclr_bn_row_parts(D), R), 7.0, device=dev)  # all overwritten
+        slot = torch.zeros(2048, device=dev)
         if fused:
             rc = lib.molclr_batchnorm_seg_bwd_max(dy.data_ptr(), z.data_ptr(), gamma.data_ptr(),
                                                   beta.data_ptr(), mean.data_ptr(), inv.data_ptr(),
@@ -882,5 +885,5 @@ def test_batchnorm_seg_bwd_max(dev, rows, D, relu):
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, b)
     dz, rmax, slot = outs[1][0], outs[1][3], outs[1][4]
-    assert torch.equal(rmax, dz.abs().amax(1))
+    assert torch.equal(rmax.amax(0), dz.abs().amax(1))
     assert slot.max().item() == dz.abs().max().item()

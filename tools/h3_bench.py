@@ -58,7 +58,7 @@ def main():
         return buf
 
     def slot(t):
-        s = torch.empty(64, device=dev)
+        s = torch.empty(2048, device=dev)
         lib.molclr_absmax_f32(t.data_ptr(), t.shape[0], t.shape[1], t.shape[1], s.data_ptr(), 0, st)
         return s
 
@@ -85,7 +85,7 @@ def main():
         bp = bias.data_ptr() if bias is not None else None
         ap = aux.data_ptr() if aux is not None else None
         ld_aux = N if aux is not None else 0
-        cmax = torch.zeros(64, device=dev)
+        cmax = torch.zeros(2048, device=dev)
 
         def run6():
             rc = lib.molclr_gemm_f32_bplanes(A.data_ptr(), p6.data_ptr(), C6.data_ptr(), Nr, N, K, K,
@@ -95,7 +95,7 @@ def main():
         def run3():
             rc = lib.molclr_gemm_f32_h3(A.data_ptr(), smax[id(A)].data_ptr(), 0, p3.data_ptr(),
                                         C3.data_ptr(), Nr, N, K, K, N, epi, bp, ap, ld_aux,
-                                        cmax.data_ptr(), None, st)
+                                        cmax.data_ptr(), None, None, st)
             assert rc == 0, lib.molclr_last_error()
         t6, t3 = timeit(run6), timeit(run3)
         r = ref()
