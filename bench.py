@@ -125,6 +125,23 @@ def cpu_baseline(cfg, batches_cpu, steps):
                       f"torch CPU fp32, {threads} threads, median step"}
 
 
+def split_ceiling(tfs, model_type) -> dict:
+    """fp32 GEMMs: fraction of their own MFMA ceiling.  Forward products run as
+    split-bf16 x6 (six bf16 MFMAs: 2.5 PF / 6); with ops.FP32_GEMM == "h3" the
+    GIN backward products (4 of every layer's 6 equal-size products) run as h3
+    (three fp16 MFMAs: 2.5 PF / 3), so the ceiling is their flop-weighted
+    harmonic mean."""
+    from molclr_amd import ops
+    x6 = BF16_MFMA_PEAK_TFS / 6
+    if model_type == "gin" and ops.FP32_GEMM == "h3":
+        ceil = 1.0 / ((2 / 6) / x6 + (4 / 6) / (BF16_MFMA_PEAK_TFS / 3))
+        form = "x6 forward, h3 backward"
+    else:
+        ceil, form = x6, "x6"
+    return {"split_ceiling_tfs": round(ceil, 1), "split_form": form,
+            "frac_of_split_ceiling": round(tfs / ceil, 4)}
+
+
 def main():
     args = parse()
     import torch
@@ -296,9 +313,8 @@ def main():
                              "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
                              "traffic": None, "launches": gm["launches"],
                              "ms_per_step": round(gm["ms"] / args.mfma_steps, 3),
-                             **({} if precision == "bf16" else {
-                                 "frac_of_split_bf16_ceiling":
-                                     round(tfs / (BF16_MFMA_PEAK_TFS / 6), 4)}),
+                             **({} if precision == "bf16" else
+                                split_ceiling(tfs, cfg["model_type"])),
                              "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                        f"after the timed region"}
         nx = s.get("ntxent")
