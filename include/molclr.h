@@ -384,7 +384,9 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  *     precision).  cmax / crow (each may be NULL): max |C| folded into the
  *     slot cmax (the caller zeroes it) / C's row maxima as
  *     molclr_gemm_row_parts(N) partial arrays (plain stores); amax_out (may
- *     be NULL, zeroed by the caller): max |A| folded in.
+ *     be NULL, zeroed by the caller): max |A| folded in.  A RELU_MASK
+ *     epilogue takes its mask from mask_bits (molclr_gemm_f32_bplanes_max's
+ *     relu_bits of the same [M][N]) when given, else from aux.
  *   molclr_linear_wgrad_h3: molclr_linear_wgrad given the max slots of dy
  *     and x (n_out, n_in, ld_dy, ld_x multiples of 4; same workspace). */
 int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int64_t ld, float* slot,
@@ -399,19 +401,23 @@ int molclr_hplanes_make_batch(int count, const float* const* B, const int64_t* N
  * and writes C's row maxima as molclr_gemm_row_parts(N) partial arrays
  * crow[p][M] (plain stores; the row max is the max over p): the scales of
  * the h3 products that consume A or C, with no pass when the q6 kernel runs.
+ * relu_bits: bit (n % 32) of word [n / 32][m] (ceil(N / 32) x M words) =
+ * (C[m][n] > 0) -- the ReLU mask of a bias+ReLU product in 1/32 of the bytes.
  * Each output may be NULL. */
 int64_t molclr_gemm_row_parts(int64_t N);
 int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* planes, float* C, int64_t M,
                                 int64_t N, int64_t K, int64_t lda, int64_t ldc,
                                 int epilogue_flags, const float* bias, const float* aux,
                                 int64_t ldaux, float* amax_out, float* cmax, float* crow,
-                                void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+                                uint32_t* relu_bits, void* workspace, size_t workspace_bytes,
+                                molclr_stream_t stream);
 int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols, int64_t ld,
                            float* rowmax, float* slot, int accumulate, molclr_stream_t stream);
 int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const uint16_t* hplanes,
                        float* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
-                       float* cmax, float* crow, float* amax_out, molclr_stream_t stream);
+                       const uint32_t* mask_bits, float* cmax, float* crow, float* amax_out,
+                       molclr_stream_t stream);
 int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
                            const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
                            int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,

@@ -76,9 +76,9 @@ SIGNATURES = {
                                              c_int, c_int, _P, _P, _P, c_size_t, _P]),
     "molclr_gemm_row_parts": (_I64, [_I64]),
     "molclr_gemm_f32_bplanes_max": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
-                                            _P, _I64, _P, _P, _P, _P, c_size_t, _P]),
+                                            _P, _I64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "molclr_gemm_f32_h3": (c_int, [_P, _P, c_int, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
-                                   _P, _I64, _P, _P, _P, _P]),
+                                   _P, _I64, _P, _P, _P, _P, _P]),
     "molclr_linear_wgrad_h3": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
                                        _P, c_size_t, _P]),
     "molclr_colsum_f32_workspace_bytes": (c_size_t, [_I64, _I64]),

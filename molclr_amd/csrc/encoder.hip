@@ -22,6 +22,7 @@ namespace {
 struct ArenaLayout {
   size_t agg[MOLCLR_MAX_LAYERS], a1[MOLCLR_MAX_LAYERS], z[MOLCLR_MAX_LAYERS],
       h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS], invstd[MOLCLR_MAX_LAYERS];
+  size_t bits[MOLCLR_MAX_LAYERS];  // h3: ReLU mask of a1_l as bits [ceil(2D / 32)][N]
   size_t h0, ec, smax, total;
   ArenaLayout(int L, int64_t N, int64_t D, size_t es) {
     size_t used = 0;
@@ -37,6 +38,7 @@ struct ArenaLayout {
       h[l] = off(N * D * es);
       mean[l] = off(MOLCLR_MAX_SEGMENTS * D * sizeof(float));  // [segment][D]
       invstd[l] = off(MOLCLR_MAX_SEGMENTS * D * sizeof(float));
+      bits[l] = off((size_t)N * ((2 * D + 31) / 32) * sizeof(uint32_t));
     }
     h0 = off(N * D * es);
     ec = off((size_t)L * MOLCLR_NUM_ECOMB * D * sizeof(float));
@@ -216,10 +218,11 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
         const uint16_t* p2 = e->mlp2_planes[l];
         MOLCLR_TRY(molclr_absmax_rows_f32(agg, N, D, D, ragg, sl, 1, stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(agg, ragg, 1, p0, a1, N, 2 * D, D, D, 2 * D,
-                                      MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
+                                      MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, nullptr,
                                       sl + kMaxSlotFloats, ra1, nullptr, stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, (int)molclr_gemm_row_parts(2 * D), p2, z, N, D,
                                       2 * D, 2 * D, D, MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0,
+                                      nullptr,
                                       nullptr, nullptr, nullptr, stream));
       } else {
         // GINEConv.update: Linear(D,2D) + ReLU, Linear(2D,D)  (ops.linear_fwd);
@@ -228,8 +231,9 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
           MOLCLR_TRY(molclr_gemm_f32_bplanes_max(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
                                                  MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0,
                                                  fmax + 2 * l * kMaxSlotFloats,
-                                                 fmax + (2 * l + 1) * kMaxSlotFloats, nullptr, kws,
-                                                 kws_bytes, stream));
+                                                 fmax + (2 * l + 1) * kMaxSlotFloats, nullptr,
+                                                 (uint32_t*)(A + lay.bits[l]), kws, kws_bytes,
+                                                 stream));
         else
           MOLCLR_TRY(molclr_gemm_f32_bplanes(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D, 0,
                                              MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, kws,
@@ -282,6 +286,9 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
   const bool h3 = !bf && e->fp32_gemm != 0;
+  // the forward wrote a1's ReLU bits unless its products ran in h3 (then the
+  // mask is read from a1 itself)
+  const bool fwd_h3 = h3 && (e->fp32_gemm & 2);
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
   if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
@@ -346,8 +353,8 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       // gradients
       MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, molclr_bn_row_parts(D), e->mlp2_planes_t[l],
                                     (float*)dz1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_RELU_MASK,
-                                    nullptr, fa1, 2 * D, sl + kMaxSlotFloats, rdz1, nullptr,
-                                    stream));
+                                    nullptr, fa1, 2 * D, fwd_h3 ? nullptr : (const uint32_t*)(A + lay.bits[l]),
+                                    sl + kMaxSlotFloats, rdz1, nullptr, stream));
       MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
                                         gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
                                         stream));
@@ -357,7 +364,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, (int)molclr_gemm_row_parts(2 * D),
                                     e->mlp0_planes_t[l], (float*)dagg, N, D, 2 * D, 2 * D, D,
                                     MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr,
-                                    nullptr, stream));
+                                    nullptr, nullptr, stream));
       MOLCLR_TRY(molclr_gine_aggregate_bwd((const float*)dagg, g->rowptr_t, g->col_t, g->nbr_t,
                                            g->ecount, (float*)dh, gr->edge_embedding1[l],
                                            gr->edge_embedding2[l], N, D, 1, kws, kws_bytes, stream));

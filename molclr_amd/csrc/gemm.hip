@@ -794,7 +794,11 @@ struct QStageB {
 // this block's columns into crow[column tile][M] (plain stores: the column
 // tiles' partial row maxima), and `amax_out` (zeroed) receives max |A| over
 // the loaded rows -- the scales an h3 consumer of A or C needs, with no pass
-// of their own.  Each is optional.
+// of their own.  Each is optional.  ReLU as bits: `bits_out` (optional)
+// receives bit (n % 32) of word [n / 32][m] (column-block major, bits_ld =
+// M: a wave's 8 rows of one block are 32 contiguous bytes) = C > 0 after the
+// epilogue; a RELU_MASK epilogue given `bits_in` takes its mask from such bits
+// instead of reading aux (32x fewer bytes than the fp32 a1).
 template <int TN, int EPI, int KG, bool MASK, int H3 = 0>
 __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_q6(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
@@ -802,7 +806,8 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
     int accumulate, const float* __restrict__ amax, const float* __restrict__ bmax,
     float* __restrict__ cmax, float* __restrict__ crow, float* __restrict__ amax_out,
-    int arow_parts) {
+    int arow_parts, uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in,
+    int64_t bits_ld) {
   constexpr int T = 64 * kQ6Waves;  // threads of one K group
   constexpr int BN = 32 * TN;
   constexpr int NP = H3 ? 2 : 3;    // B planes
@@ -976,7 +981,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   // its own 4 KB of LDS so that rows leave as 16-byte pieces (8 rows x 128 B
   // per store instruction).
   const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
-                   (EPI != MOLCLR_EPI_RELU_MASK ||
+                   (EPI != MOLCLR_EPI_RELU_MASK || bits_in != nullptr ||
                     (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
                    ((EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
@@ -1005,35 +1010,58 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
         const int idx = it * 64 + lane;
         const int row = idx >> 3, c4 = idx & 7;
         const int64_t m = mw + row, n = nb + 4 * c4;
-        if (m >= M || n >= N) continue;
-        const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
-        float* o = C + m * ldc + n;
-        if (vec && n + 4 <= N) {
-          float4 v = v4;
-          if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
-            v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
-            if (EPI == MOLCLR_EPI_BIAS_RELU)
-              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+        uint32_t pos = 0;  // bits of C > 0 for this lane's 4 columns (bits_out)
+        if (m < M && n < N) {
+          const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+          float* o = C + m * ldc + n;
+          // the mask nibble of this lane's columns (RELU_MASK with bits_in)
+          uint32_t mk = 15u;
+          if (EPI == MOLCLR_EPI_RELU_MASK && bits_in != nullptr)
+            mk = (bits_in[(nb >> 5) * bits_ld + m] >> (4 * c4)) & 15u;
+          if (vec && n + 4 <= N) {
+            float4 v = v4;
+            if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
+              v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+              if (EPI == MOLCLR_EPI_BIAS_RELU)
+                v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            }
+            if (EPI == MOLCLR_EPI_RELU_MASK) {
+              if (bits_in != nullptr) {
+                v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                                mk & 8u ? v.w : 0.f);
+              } else {
+                const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+                v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f,
+                                x.z > 0.f ? v.z : 0.f, x.w > 0.f ? v.w : 0.f);
+              }
+            }
+            if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+            *reinterpret_cast<float4*>(o) = v;
+            rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            pos = (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+                  (v.w > 0.f ? 8u : 0u);
+          } else {
+            const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+            for (int j = 0; j < 4 && n + j < N; ++j) {
+              float x = e[j];
+              if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+              if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+              if (EPI == MOLCLR_EPI_RELU_MASK)
+                x = (bits_in != nullptr ? ((mk >> j) & 1u) != 0u : aux[m * ldaux + n + j] > 0.f)
+                        ? x : 0.f;
+              if (accumulate) x += o[j];
+              o[j] = x;
+              rm[it] = fmaxf(rm[it], fabsf(x));
+              pos |= (x > 0.f ? 1u : 0u) << j;
+            }
           }
-          if (EPI == MOLCLR_EPI_RELU_MASK) {
-            const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
-            v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f, x.z > 0.f ? v.z : 0.f,
-                            x.w > 0.f ? v.w : 0.f);
-          }
-          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
-          *reinterpret_cast<float4*>(o) = v;
-          rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-        } else {
-          const float e[4] = {v4.x, v4.y, v4.z, v4.w};
-          for (int j = 0; j < 4 && n + j < N; ++j) {
-            float x = e[j];
-            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
-            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
-            if (EPI == MOLCLR_EPI_RELU_MASK) x = aux[m * ldaux + n + j] > 0.f ? x : 0.f;
-            if (accumulate) x += o[j];
-            o[j] = x;
-            rm[it] = fmaxf(rm[it], fabsf(x));
-          }
+        }
+        if (bits_out != nullptr) {  // the 8 lanes of a row OR their nibbles into one word
+          uint32_t w = pos << (4 * c4);
+          w |= __shfl_xor(w, 1, 64);
+          w |= __shfl_xor(w, 2, 64);
+          w |= __shfl_xor(w, 4, 64);
+          if (c4 == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = w;
         }
       }
     }
@@ -1393,6 +1421,18 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
   absmax_publish(m, slot);
 }
 
+// bits[w][m] bit j = (C[m][32 w + j] > 0): thread per word
+__global__ __launch_bounds__(256) void k_relu_bits(const float* __restrict__ C, int64_t M,
+                                                   int64_t N, int64_t ldc,
+                                                   uint32_t* __restrict__ bits, int64_t words) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= M * words) return;
+  const int64_t w = t / M, m = t - w * M;
+  uint32_t b = 0;
+  for (int j = 0; j < 32 && 32 * w + j < N; ++j) b |= (C[m * ldc + 32 * w + j] > 0.f ? 1u : 0u) << j;
+  bits[t] = b;
+}
+
 // row maxima rowmax[r] = max_c |x[r][c]| (plain stores) and the matrix max
 // folded into *slot: a wave per row, float4 columns when aligned
 __global__ __launch_bounds__(256) void k_absmax_rows(const float* __restrict__ x, int64_t rows,
@@ -1514,6 +1554,9 @@ struct Args {
   float* crow = nullptr;
   float* amax_out = nullptr;     // q6: max |A| of the loaded rows out (may be null)
   int arow_parts = 0;            // h3 row-wise: partial row-max arrays in amax
+  uint32_t* bits_out = nullptr;  // q6: C > 0 as bits out / RELU_MASK bits in
+  const uint32_t* bits_in = nullptr;
+  int64_t bits_ld = 0;           // words per row of both
 };
 
 template <int TM, int AMODE, int BMODE, int EPI, bool SPLIT, int TN = 1, bool CS = false>
@@ -1643,7 +1686,8 @@ void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
   molclr::launch_timed(molclr::kTimeGemm, (k_gemm_q6<TN, EPI, KG, MASK, H3>),
                        dim3((unsigned)q6_blocks(a.M, a.N)), dim3(KG * 64 * kQ6Waves), 0, s, a.A,
                        a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux,
-                       a.accumulate, a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts);
+                       a.accumulate, a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts,
+                       a.bits_out, a.bits_in, a.bits_ld);
 }
 template <int TN, int EPI, int H3>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
@@ -2016,8 +2060,9 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
                                            int64_t M, int64_t N, int64_t K, int64_t lda,
                                            int64_t ldc, int epilogue_flags, const float* bias,
                                            const float* aux, int64_t ldaux, float* amax_out,
-                                           float* cmax, float* crow, void* workspace,
-                                           size_t workspace_bytes, molclr_stream_t stream) {
+                                           float* cmax, float* crow, uint32_t* relu_bits,
+                                           void* workspace, size_t workspace_bytes,
+                                           molclr_stream_t stream) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_bplanes_max: negative size");
@@ -2043,6 +2088,11 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
     MOLCLR_TRY_RC(molclr_gemm_f32_bplanes(A, planes, C, M, N, K, lda, ldc, 0, epilogue_flags, bias,
                                           aux, ldaux, workspace, workspace_bytes, stream));
     if (amax_out) MOLCLR_TRY_RC(molclr_absmax_f32(A, M, K, lda, amax_out, 1, stream));
+    if (relu_bits) {
+      const int64_t words = (N + 31) / 32;
+      hipLaunchKernelGGL(k_relu_bits, dim3((unsigned)molclr::ceil_div(M * words, 256)), dim3(256),
+                         0, s, C, M, N, ldc, relu_bits, words);
+    }
     if (crow || cmax) {
       float* rows = crow;
       if (!rows) {  // cmax only
@@ -2066,6 +2116,8 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
   a.cmax = cmax;
   a.crow = crow;
   a.amax_out = amax_out;
+  a.bits_out = relu_bits;
+  a.bits_ld = M;
   return run_q6(a, npad, epilogue, s, 0);
 }
 
@@ -2216,8 +2268,9 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
 MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts,
                                   const uint16_t* hplanes, float* C, int64_t M, int64_t N,
                                   int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
-                                  const float* bias, const float* aux, int64_t ldaux, float* cmax,
-                                  float* crow, float* amax_out, molclr_stream_t stream) {
+                                  const float* bias, const float* aux, int64_t ldaux,
+                                  const uint32_t* mask_bits, float* cmax, float* crow,
+                                  float* amax_out, molclr_stream_t stream) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_h3: negative size");
@@ -2225,7 +2278,8 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
                  "gemm_f32_h3: bad epilogue %d", epilogue);
   MOLCLR_REQUIRE((epilogue != MOLCLR_EPI_BIAS && epilogue != MOLCLR_EPI_BIAS_RELU) || bias,
                  "gemm_f32_h3: bias epilogue needs bias");
-  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux, "gemm_f32_h3: relu-mask epilogue needs aux");
+  MOLCLR_REQUIRE(epilogue != MOLCLR_EPI_RELU_MASK || aux || mask_bits,
+                 "gemm_f32_h3: relu-mask epilogue needs aux or mask bits");
   MOLCLR_REQUIRE(K % 4 == 0 && lda % 4 == 0 && lda >= K && ldc >= N,
                  "gemm_f32_h3: K and lda multiples of 4, lda >= K, ldc >= N");
   MOLCLR_REQUIRE(K <= kQ6MaxK, "gemm_f32_h3: K %lld > %lld", (long long)K, (long long)kQ6MaxK);
@@ -2243,6 +2297,8 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
   a.crow = crow;
   a.amax_out = amax_out;
   a.arow_parts = a_row_parts;
+  a.bits_in = epilogue == MOLCLR_EPI_RELU_MASK ? mask_bits : nullptr;
+  a.bits_ld = M;
   return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
 }
 

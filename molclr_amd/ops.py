@@ -279,7 +279,7 @@ def row_parts(N: int) -> int:
 
 
 def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None,
-            rowwise=0, crow=None, amax_out=None):
+            rowwise=0, crow=None, amax_out=None, mask_bits=None):
     """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3.  amax: A's
     max slot, or (rowwise = P > 0) its row maxima as P partial arrays [P][M];
     cmax (zeroed) receives max |C|, crow [row_parts(N)][M] C's row maxima."""
@@ -290,8 +290,8 @@ def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, 
     _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), int(rowwise),
               planes.data_ptr(),
               out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
-              _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(cmax),
-              _lib.ptr(crow), _lib.ptr(amax_out), _stream(A))
+              _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(mask_bits),
+              _lib.ptr(cmax), _lib.ptr(crow), _lib.ptr(amax_out), _stream(A))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -532,6 +532,7 @@ class _MLP(torch.autograd.Function):
             # the products (row-wise h3 when H3_FORWARD, else x6 with max |a1| by
             # a pass); the max slots serve the h3 weight gradients
             slots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=x.device)
+            ctx.bits = None
             if H3_FORWARD:
                 P = row_parts(2 * D)
                 rx = torch.empty(M, dtype=torch.float32, device=x.device)
@@ -543,14 +544,16 @@ class _MLP(torch.autograd.Function):
                 z = gemm_h3(a1, ra1, W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2, rowwise=P)
             else:
                 # the first product (q6, x6 planes) also yields max |x| and max |a1|
+                # and a1's ReLU mask as bits for the dz1 product
                 a1 = torch.empty(M, 2 * D, dtype=torch.float32, device=x.device)
+                ctx.bits = torch.empty((2 * D + 31) // 32, M, dtype=torch.int32, device=x.device)
                 ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, 2 * D, D)
                 ws = _ws(ws_bytes, x.device) if ws_bytes else None
                 _lib.call("molclr_gemm_f32_bplanes_max", x.data_ptr(),
                           weight_planes(W1, 2 * D, D, D, 0).data_ptr(), a1.data_ptr(), M, 2 * D,
                           D, x.stride(0), a1.stride(0), EPI_BIAS_RELU, b1.data_ptr(), None, 0,
-                          slots[0].data_ptr(), slots[1].data_ptr(), None, _lib.ptr(ws), ws_bytes,
-                          _stream(x))
+                          slots[0].data_ptr(), slots[1].data_ptr(), None, ctx.bits.data_ptr(),
+                          _lib.ptr(ws), ws_bytes, _stream(x))
                 if _TIMER is not None:
                     _TIMER.add("gemm_f32", 2.0 * M * 2 * D * D)
                 z = linear_fwd(a1, W2, b2, relu=False)
@@ -581,7 +584,7 @@ class _MLP(torch.autograd.Function):
             _lib.call("molclr_absmax_rows_f32", dz.data_ptr(), M, D, dz.stride(0),
                       rdz.data_ptr(), bslots[0].data_ptr(), 1, _stream(dz))
             dz1 = gemm_h3(dz, rdz, W2, 2 * D, D, 2 * D, 1, EPI_RELU_MASK, aux=a1,
-                          cmax=bslots[1], rowwise=1, crow=rdz1)
+                          cmax=bslots[1], rowwise=1, crow=rdz1, mask_bits=ctx.bits)
             dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
             dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
             dx = (gemm_h3(dz1, rdz1, W1, D, 2 * D, D, 1, rowwise=P) if need[0] else None)

@@ -764,7 +764,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     bd, ad = bias.float().to(dev), aux.float().to(dev)
     rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
                                 rowwise, planes.data_ptr(), C.data_ptr(), M, N, K, K, N, epi,
-                                bd.data_ptr(), ad.data_ptr(), N, slots[1].data_ptr(),
+                                bd.data_ptr(), ad.data_ptr(), N, None, slots[1].data_ptr(),
                                 crow.data_ptr(), aout.data_ptr(), ops._stream(Ad))
     assert rc == 0, lib.molclr_last_error()
     torch.cuda.synchronize()
@@ -780,6 +780,21 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
     assert slots[1].max().item() == C.abs().max().item()
     assert crow.amax(0).cpu().equal(C.abs().amax(1).cpu())
     assert aout.max().item() == Ad.abs().max().item()
+    if epi == 3:  # the mask from bits of (aux > 0) gives the same C bit for bit
+        words = (N + 31) // 32
+        pos = torch.zeros(M, words * 32, dtype=torch.bool, device=dev)
+        pos[:, :N] = ad > 0
+        mb = ((pos.view(M, words, 32).long() << torch.arange(32, device=dev)).sum(-1)
+              .remainder(1 << 32).t().contiguous())
+        mb = torch.where(mb >= (1 << 31), mb - (1 << 32), mb).to(torch.int32)
+        C2 = torch.empty_like(C)
+        rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
+                                    rowwise, planes.data_ptr(), C2.data_ptr(), M, N, K, K, N, epi,
+                                    None, None, 0, mb.data_ptr(), None, None, None,
+                                    ops._stream(Ad))
+        assert rc == 0, lib.molclr_last_error()
+        torch.cuda.synchronize()
+        assert torch.equal(C2, C)
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
@@ -825,16 +840,23 @@ def test_gemm_bplanes_max(dev, M, N, K, epi):
     rows = torch.zeros(int(lib.molclr_gemm_row_parts(N)), M, device=dev)
     ws_b = lib.molclr_gemm_f32_workspace_bytes(M, N, K)
     ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    words = (N + 31) // 32
+    bits = torch.zeros(words, M, dtype=torch.int32, device=dev)
     rc = lib.molclr_gemm_f32_bplanes_max(A.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N, K,
                                          K, N, epi, b.data_ptr(), None, 0, sl[0].data_ptr(),
-                                         sl[1].data_ptr(), rows.data_ptr(), ws.data_ptr(), ws_b,
-                                         ops._stream(A))
+                                         sl[1].data_ptr(), rows.data_ptr(), bits.data_ptr(),
+                                         ws.data_ptr(), ws_b, ops._stream(A))
     assert rc == 0, lib.molclr_last_error()
     torch.cuda.synchronize()
     assert torch.equal(C, ref)
     assert sl[0].max().item() == A.abs().max().item()
     assert sl[1].max().item() == C.abs().max().item()
     assert torch.equal(rows.amax(0), C.abs().amax(1))
+    # the ReLU bits: bit j of word w <-> C[:, 32 w + j] > 0
+    pos = torch.zeros(M, words * 32, dtype=torch.bool, device=dev)
+    pos[:, :N] = C > 0
+    want = (pos.view(M, words, 32).long() << torch.arange(32, device=dev)).sum(-1).t()
+    assert torch.equal(bits.long() & 0xFFFFFFFF, want & 0xFFFFFFFF)
 
 
 @pytest.mark.parametrize("rows,D,relu", [((15300, 15256), 300, 1), ((1950, 2001, 40), 128, 0)])

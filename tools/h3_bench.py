@@ -94,15 +94,27 @@ def main():
 
         def run3():
             rc = lib.molclr_gemm_f32_h3(A.data_ptr(), smax[id(A)].data_ptr(), 0, p3.data_ptr(),
-                                        C3.data_ptr(), Nr, N, K, K, N, epi, bp, ap, ld_aux,
+                                        C3.data_ptr(), Nr, N, K, K, N, epi, bp, ap, ld_aux, None,
                                         cmax.data_ptr(), None, None, st)
             assert rc == 0, lib.molclr_last_error()
-        t6, t3 = timeit(run6), timeit(run3)
+        rws = torch.empty(Nr, device=dev)
+        tmp_slot = torch.zeros(2048, device=dev)
+        lib.molclr_absmax_rows_f32(A.data_ptr(), Nr, K, K, rws.data_ptr(), tmp_slot.data_ptr(), 1, st)
+        C3r = torch.empty(Nr, N, device=dev)
+        crow = torch.empty(lib.molclr_gemm_row_parts(N), Nr, device=dev)
+
+        def run3r():  # row-wise A scales, C's row maxima out (the backward's form)
+            rc = lib.molclr_gemm_f32_h3(A.data_ptr(), rws.data_ptr(), 1, p3.data_ptr(),
+                                        C3r.data_ptr(), Nr, N, K, K, N, epi, bp, ap, ld_aux, None,
+                                        cmax.data_ptr(), crow.data_ptr(), None, st)
+            assert rc == 0, lib.molclr_last_error()
+        t6, t3, t3r = timeit(run6), timeit(run3), timeit(run3r)
         r = ref()
         f32 = (A @ (W.t() if km == 0 else W))
         fl = 2 * Nr * N * K
         print(f"{name:24s} x6 {t6*1e6:6.1f}us ({fl/t6/1e12:5.1f}TF) err {rel(C6, r):.2e} | "
               f"h3 {t3*1e6:6.1f}us ({fl/t3/1e12:5.1f}TF) err {rel(C3, r):.2e} | "
+              f"h3 row-wise {t3r*1e6:6.1f}us err {rel(C3r, r):.2e} | "
               f"torch fp32 matmul err {rel(f32 + (bias if bias is not None else 0), (A.double() @ (W.double().t() if km == 0 else W.double())) + (bias.double() if bias is not None else 0)):.2e}"
               f" | cmax {cmax.max().item():.4e} vs {C3.abs().max().item():.4e}", flush=True)
     wg_cases = [
