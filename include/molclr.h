@@ -418,6 +418,13 @@ int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
                        const uint32_t* mask_bits, float* cmax, float* crow, float* amax_out,
                        molclr_stream_t stream);
+/* molclr_linear_wgrad_h3 with the K groups per block chosen per call (the plain
+ * call is groups = 2), as molclr_linear_wgrad_groups. */
+int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,
+                                  const float* xmax, float* dW, float* db, int64_t rows,
+                                  int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
+                                  int accumulate, void* workspace, size_t workspace_bytes,
+                                  molclr_stream_t stream, int groups);
 int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
                            const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
                            int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,

@@ -2302,11 +2302,13 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
   return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
 }
 
-MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
-                                      const float* xmax, float* dW, float* db, int64_t rows,
-                                      int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
-                                      int accumulate, void* workspace, size_t workspace_bytes,
-                                      molclr_stream_t stream) {
+MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,
+                                             const float* xmax, float* dW, float* db, int64_t rows,
+                                             int64_t n_out, int64_t n_in, int64_t ld_dy,
+                                             int64_t ld_x, int accumulate, void* workspace,
+                                             size_t workspace_bytes, molclr_stream_t stream,
+                                             int groups) {
+  MOLCLR_REQUIRE(groups == 1 || groups == 2, "linear_wgrad_h3: groups must be 1 or 2");
   MOLCLR_REQUIRE(rows >= 0 && n_out > 0 && n_in > 0, "linear_wgrad_h3: bad sizes");
   MOLCLR_REQUIRE(dy && dymax && x && xmax && dW, "linear_wgrad_h3: null pointer");
   MOLCLR_REQUIRE(ld_dy >= n_out && ld_x >= n_in, "linear_wgrad_h3: leading dimension too small");
@@ -2325,5 +2327,14 @@ MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const
   }
   MOLCLR_REQUIRE_WS(workspace_bytes, w6_ws_bytes(n_out, n_in, rows, db != nullptr));
   return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
-                workspace_bytes, s, 2, dymax, xmax);
+                workspace_bytes, s, groups, dymax, xmax);
+}
+
+MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
+                                      const float* xmax, float* dW, float* db, int64_t rows,
+                                      int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
+                                      int accumulate, void* workspace, size_t workspace_bytes,
+                                      molclr_stream_t stream) {
+  return molclr_linear_wgrad_h3_groups(dy, dymax, x, xmax, dW, db, rows, n_out, n_in, ld_dy, ld_x,
+                                       accumulate, workspace, workspace_bytes, stream, 2);
 }

@@ -135,7 +135,14 @@ def main():
                                             smax[id(X)].data_ptr(), dW3.data_ptr(), db3.data_ptr(),
                                             Nr, n_out, n_in, n_out, n_in, 0, ws.data_ptr(), ws_b, st)
             assert rc == 0, lib.molclr_last_error()
-        t6, t3 = timeit(run6), timeit(run3)
+        def run3g1():
+            rc = lib.molclr_linear_wgrad_h3_groups(
+                dy.data_ptr(), smax[id(dy)].data_ptr(), X.data_ptr(), smax[id(X)].data_ptr(),
+                dW3.data_ptr(), db3.data_ptr(), Nr, n_out, n_in, n_out, n_in, 0, ws.data_ptr(),
+                ws_b, st, 1)
+            assert rc == 0, lib.molclr_last_error()
+        t6, t3, t3g1 = timeit(run6), timeit(run3), timeit(run3g1)
+        print(f"   h3 wgrad one K group per block: {t3g1*1e6:6.1f}us")
         r = dy.double().t() @ X.double()
         rb = dy.double().sum(0)
         fl = 2 * Nr * n_out * n_in
