@@ -733,6 +733,11 @@ typedef struct molclr_gcn_encoder {
   int64_t* bn_num_batches_tracked[MOLCLR_MAX_LAYERS];
   const uint16_t* weight_planes[MOLCLR_MAX_LAYERS];
   const uint16_t* weight_planes_t[MOLCLR_MAX_LAYERS];
+  /* 0 = split-bf16 x6 products; 1 = the backward in h3 (as molclr_gin_encoder's
+   * bit 0: the weight gradient with per-tensor scales, dx = dxw W^T with
+   * row-wise scales; weight_planes_t are then molclr_hplanes_make_batch
+   * images, dim <= 1024). */
+  int32_t fp32_gemm;
 } molclr_gcn_encoder;
 
 typedef struct molclr_gcn_encoder_grads {

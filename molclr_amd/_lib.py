@@ -193,7 +193,8 @@ class GcnEncoder(ctypes.Structure):
                 ("eps", c_double), ("x_embedding1", c_void_p), ("x_embedding2", c_void_p)] + [
         (f, _L16) for f in ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight",
                             "bn_bias", "bn_running_mean", "bn_running_var",
-                            "bn_num_batches_tracked", "weight_planes", "weight_planes_t")]
+                            "bn_num_batches_tracked", "weight_planes", "weight_planes_t")] + [
+        ("fp32_gemm", ctypes.c_int32)]
 
 
 class GcnEncoderGrads(ctypes.Structure):

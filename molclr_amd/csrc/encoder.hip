@@ -425,6 +425,7 @@ namespace {
 struct GcnArena {
   size_t z[MOLCLR_MAX_LAYERS], h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS],
       invstd[MOLCLR_MAX_LAYERS];
+  size_t hmax[MOLCLR_MAX_LAYERS];  // h3: max slot of layer l's input (floats, contiguous)
   size_t h0, total;
   GcnArena(int L, int64_t N, int64_t D) {
     size_t used = 0;
@@ -439,6 +440,8 @@ struct GcnArena {
       mean[l] = off(MOLCLR_MAX_SEGMENTS * D);  // [segment][D]
       invstd[l] = off(MOLCLR_MAX_SEGMENTS * D);
     }
+    const size_t slots = off((size_t)L * kMaxSlotFloats);
+    for (int l = 0; l < L; ++l) hmax[l] = slots + (size_t)l * kMaxSlotFloats;
     h0 = off(N * D);
     total = used * sizeof(float);
   }
@@ -449,12 +452,17 @@ size_t gcn_kernels_ws(int64_t N, int64_t D) {
   auto mx = [&](size_t v) { m = v > m ? v : m; };
   mx(molclr_gemm_f32_workspace_bytes(N, D, D));  // x W, dxw W^T
   mx(molclr_gemm_f32_workspace_bytes(D, D, N));  // dW = x^T dxw
+  mx(molclr_linear_wgrad_workspace_bytes(N, D, D));  // its h3 form
   mx(molclr_batchnorm_ws_bound(N, D));
   mx(molclr_gcn_aggregate_bwd_workspace_bytes(N, D));
   mx(molclr_atom_embed_bwd_workspace_bytes(N, D, MOLCLR_NUM_ATOM_TYPE, MOLCLR_NUM_CHIRALITY));
   return m;
 }
 size_t gcn_scratch_floats(int64_t N, int64_t D) { return (size_t)N * D * 3; }
+// h3 backward: dxw's row maxima [N] and max slot, after the scratch
+size_t gcn_h3_bytes(int64_t N) {
+  return molclr::align_up((size_t)N * sizeof(float), 256) + kMaxSlotFloats * sizeof(float);
+}
 
 int check_gcn(const molclr_gcn_encoder* e, const molclr_device_graph* g) {
   MOLCLR_REQUIRE(e && g, "gcn_encoder: null encoder / graph");
@@ -481,7 +489,8 @@ MOLCLR_API size_t molclr_gcn_encoder_arena_bytes(int L, int64_t N, int64_t D) {
 
 MOLCLR_API size_t molclr_gcn_encoder_workspace_bytes(int L, int64_t N, int64_t D) {
   (void)L;
-  return gcn_scratch_floats(N, D) * sizeof(float) + 256 + gcn_kernels_ws(N, D) + 256;
+  return gcn_scratch_floats(N, D) * sizeof(float) + 256 + gcn_h3_bytes(N) + gcn_kernels_ws(N, D) +
+         256;
 }
 
 MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t* x,
@@ -503,6 +512,12 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
   void* kws = (char*)workspace + molclr::align_up(gcn_scratch_floats(N, D) * sizeof(float), 256);
   const size_t kws_bytes = gcn_kernels_ws(N, D);
 
+  const bool h3 = e->fp32_gemm == 1;
+  if (h3 && hipMemsetAsync(A + lay.hmax[0], 0, (size_t)L * kMaxSlotFloats * sizeof(float),
+                           molclr::as_stream(stream)) != hipSuccess) {
+    molclr::set_error("gcn_encoder_fwd: hipMemsetAsync failed");
+    return MOLCLR_ERR_ARG;
+  }
   float* h = A + lay.h0;
   MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, h, N, D, e->n_atom,
                                    e->n_chiral, stream));
@@ -511,7 +526,13 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
     const bool last = l == L - 1;
     float* y = last ? h_out : A + lay.h[l];
     // x W, W [in, out] as a K-major B (ops.gemm_w(x, W, N, D, D, D, D, False, True))
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(h, e->weight_planes[l], xw, N, D, D, D, D, 0,
+    if (h3)  // the same product, also folding max |h| into the layer's slot
+      MOLCLR_TRY(molclr_gemm_f32_bplanes_max(h, e->weight_planes[l], xw, N, D, D, D, D,
+                                             MOLCLR_EPI_NONE, nullptr, nullptr, 0,
+                                             (float*)(A + lay.hmax[l]), nullptr, nullptr, nullptr,
+                                             kws, kws_bytes, stream));
+    else
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(h, e->weight_planes[l], xw, N, D, D, D, D, 0,
                                        MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
                                        stream));
     MOLCLR_TRY(molclr_gcn_aggregate_fwd(xw, g->rowptr, g->col, g->ecode, g->nbr,
@@ -549,8 +570,13 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
   float* dxw = S;
   float* dz = S + N * D;
   float* dh = S + 2 * N * D;
-  void* kws = (char*)workspace + molclr::align_up(gcn_scratch_floats(N, D) * sizeof(float), 256);
+  // h3: dxw's row maxima and max slot
+  float* rdxw = (float*)((char*)workspace +
+                         molclr::align_up(gcn_scratch_floats(N, D) * sizeof(float), 256));
+  float* sdxw = (float*)((char*)rdxw + molclr::align_up((size_t)N * sizeof(float), 256));
+  void* kws = (char*)rdxw + gcn_h3_bytes(N);
   const size_t kws_bytes = gcn_kernels_ws(N, D);
+  const bool h3 = e->fp32_gemm == 1;
 
   const float* dy = dh_out;
   for (int l = L - 1; l >= 0; --l) {
@@ -566,14 +592,26 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
     MOLCLR_TRY(molclr_gcn_aggregate_bwd(dz, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dxw,
                                         gr->edge_embedding1[l], gr->edge_embedding2[l],
                                         gr->bias[l], N, D, 1, kws, kws_bytes, stream));
-    if (gr->weight[l])  // dW [in, out] = x^T dxw
-      MOLCLR_TRY(molclr_gemm_f32(xin, dxw, gr->weight[l], D, D, N, D, D, D, 1, 1,
-                                 MOLCLR_EPI_NONE | MOLCLR_EPI_ACCUMULATE, nullptr, nullptr, 0, kws,
-                                 kws_bytes, stream));
-    // dx = dxw W^T  (ops.gemm_w(dxw, W, N, D, D, D, D, False, False))
-    MOLCLR_TRY(molclr_gemm_f32_bplanes(dxw, e->weight_planes_t[l], dh, N, D, D, D, D, 0,
-                                       MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
-                                       stream));
+    if (h3) {
+      // ops._GCNConv's h3 backward: dxw's row maxima / max, dW = x^T dxw
+      // (per-tensor scales), dx = dxw W^T (row-wise)
+      MOLCLR_TRY(molclr_absmax_rows_f32(dxw, N, D, D, rdxw, sdxw, 0, stream));
+      if (gr->weight[l])
+        MOLCLR_TRY(molclr_linear_wgrad_h3(xin, A + lay.hmax[l], dxw, sdxw, gr->weight[l], nullptr,
+                                          N, D, D, D, D, 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(molclr_gemm_f32_h3(dxw, rdxw, 1, e->weight_planes_t[l], dh, N, D, D, D, D,
+                                    MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr,
+                                    nullptr, nullptr, stream));
+    } else {
+      if (gr->weight[l])  // dW [in, out] = x^T dxw
+        MOLCLR_TRY(molclr_gemm_f32(xin, dxw, gr->weight[l], D, D, N, D, D, D, 1, 1,
+                                   MOLCLR_EPI_NONE | MOLCLR_EPI_ACCUMULATE, nullptr, nullptr, 0,
+                                   kws, kws_bytes, stream));
+      // dx = dxw W^T  (ops.gemm_w(dxw, W, N, D, D, D, D, False, False))
+      MOLCLR_TRY(molclr_gemm_f32_bplanes(dxw, e->weight_planes_t[l], dh, N, D, D, D, D, 0,
+                                         MOLCLR_EPI_NONE, nullptr, nullptr, 0, kws, kws_bytes,
+                                         stream));
+    }
     MOLCLR_TRY(record_done(gr->layer_done[l], stream));
     dy = dh;
   }

@@ -317,6 +317,11 @@ def linear_wgrad_h3(dy, dymax, x, xmax, W_param, b_param):
     return dW, db
 
 
+def gcn_h3_ok(rows, D) -> bool:
+    """Shapes GCNConv's h3 backward takes (else x6)."""
+    return FP32_GEMM == "h3" and D % 4 == 0 and D <= 1024 and rows > 0
+
+
 def h3_ok(rows, D) -> bool:
     """Shapes the h3 GIN-MLP GEMMs take (else the x6 kernels run)."""
     return FP32_GEMM == "h3" and D % 4 == 0 and 2 * D <= 1024 and rows > 0
@@ -738,7 +743,18 @@ class _GCNConv(torch.autograd.Function):
         N, Din = x.shape
         Dout = W.shape[1]
         # xW with W stored [in, out] (gcn_molclr.py:45,76): B K-major, ldb = Dout
-        xw = gemm_w(x, W, N, Dout, Din, Din, Dout, False, True)
+        ctx.h3 = Din == Dout and gcn_h3_ok(N, Din)
+        if ctx.h3:  # the same product, also folding max |x| (the h3 weight gradient's scale)
+            ctx.xmax = torch.zeros(MAX_SLOT, dtype=torch.float32, device=x.device)
+            xw = torch.empty(N, Dout, dtype=torch.float32, device=x.device)
+            ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", N, Dout, Din)
+            ws = _ws(ws_bytes, x.device) if ws_bytes else None
+            _lib.call("molclr_gemm_f32_bplanes_max", x.data_ptr(),
+                      weight_planes(W, Dout, Din, Dout, 1).data_ptr(), xw.data_ptr(), N, Dout,
+                      Din, x.stride(0), xw.stride(0), EPI_NONE, None, None, 0,
+                      ctx.xmax.data_ptr(), None, None, None, _lib.ptr(ws), ws_bytes, _stream(x))
+        else:
+            xw = gemm_w(x, W, N, Dout, Din, Din, Dout, False, True)
         out = torch.empty(N, Dout, dtype=torch.float32, device=x.device)
         _lib.call("molclr_gcn_aggregate_fwd", xw.data_ptr(), graph.rowptr.data_ptr(),
                   graph.col.data_ptr(), graph.ecode.data_ptr(), graph.nbr.data_ptr(),
@@ -774,6 +790,23 @@ class _GCNConv(torch.autograd.Function):
                   N, Dout, acc, ws.data_ptr(), ws_bytes, _stream(g))
         db, dE1, dE2 = sinks["b"][2], sinks["e1"][2], sinks["e2"][2]
         dx = dW = None
+        if ctx.h3:
+            # the executor's h3 order: dxw's row maxima / max, dW (per-tensor
+            # scales), dx = dxw W^T (row-wise scales)
+            rows = torch.empty(N, dtype=torch.float32, device=g.device)
+            dmax = torch.empty(MAX_SLOT, dtype=torch.float32, device=g.device)
+            _lib.call("molclr_absmax_rows_f32", dxw.data_ptr(), N, Dout, dxw.stride(0),
+                      rows.data_ptr(), dmax.data_ptr(), 0, _stream(g))
+            if need[1]:
+                buf, a, dW = _grad_sink(pW, (Din, Dout), g.device)
+                wsb = _wsq("molclr_linear_wgrad_workspace_bytes", N, Din, Dout)
+                wsw = _ws(wsb, g.device)
+                _lib.call("molclr_linear_wgrad_h3", x.data_ptr(), ctx.xmax.data_ptr(),
+                          dxw.data_ptr(), dmax.data_ptr(), buf.data_ptr(), None, N, Din, Dout,
+                          x.stride(0), dxw.stride(0), a, wsw.data_ptr(), wsb, _stream(g))
+            if need[0]:
+                dx = gemm_h3(dxw, rows, W, Din, Dout, Dout, 0, rowwise=1)
+            return dx, dW, db, dE1, dE2, None
         if need[1]:
             # dW[Din,Dout] = x^T dxw
             buf, a, dW = _grad_sink(pW, (Din, Dout), g.device)
@@ -1017,6 +1050,8 @@ class _GCNEncoder(torch.autograd.Function):
         enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
         enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
+        h3 = gcn_h3_ok(N, D)  # the form _GCNConv uses on these shapes
+        enc.fp32_gemm = int(h3)
         for l in range(L):
             W, b, E1, E2, g, bb = params[2 + GCN_PARAMS_PER_LAYER * l:
                                          2 + GCN_PARAMS_PER_LAYER * (l + 1)]
@@ -1030,7 +1065,7 @@ class _GCNEncoder(torch.autograd.Function):
             enc.bn_num_batches_tracked[l] = nbt.data_ptr() if training and nbt is not None else None
             # the planes (and cache entries) _GCNConv's gemm_w calls use
             enc.weight_planes[l] = weight_planes(W, D, D, D, 1).data_ptr()
-            enc.weight_planes_t[l] = weight_planes(W, D, D, D, 0).data_ptr()
+            enc.weight_planes_t[l] = weight_planes(W, D, D, D, 0, "h3" if h3 else "x6").data_ptr()
         dev = x_idx.device
         arena_bytes = _wsq("molclr_gcn_encoder_arena_bytes", L, N, D)
         arena = torch.empty(max(arena_bytes // 4, 1), dtype=torch.float32, device=dev)
