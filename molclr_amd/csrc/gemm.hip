@@ -1056,12 +1056,23 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
             }
           }
         }
-        if (bits_out != nullptr) {  // the 8 lanes of a row OR their nibbles into one word
-          uint32_t w = pos << (4 * c4);
-          w |= __shfl_xor(w, 1, 64);
-          w |= __shfl_xor(w, 2, 64);
-          w |= __shfl_xor(w, 4, 64);
-          if (c4 == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = w;
+        if (bits_out != nullptr) {
+          // one ballot per column slot j (bit 8 row + c4 of the wave); a row's
+          // word interleaves the 8 bits of its lanes: bit 4 c4 + j
+          const uint64_t bj[4] = {__ballot((pos & 1u) != 0u), __ballot((pos & 2u) != 0u),
+                                  __ballot((pos & 4u) != 0u), __ballot((pos & 8u) != 0u)};
+          if (c4 == 0 && m < M) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              uint32_t x = (uint32_t)(bj[j] >> (8 * (lane >> 3))) & 0xFFu;  // bit c -> bit 4 c
+              x = (x | (x << 12)) & 0x000F000Fu;
+              x = (x | (x << 6)) & 0x03030303u;
+              x = (x | (x << 3)) & 0x11111111u;
+              w |= x << j;
+            }
+            bits_out[(nb >> 5) * bits_ld + m] = w;
+          }
         }
       }
     }
