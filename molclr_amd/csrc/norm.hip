@@ -57,7 +57,7 @@ __global__ void k_colsum_partial(const float4* __restrict__ X, int64_t rows, int
 // kRedLanes), four loads in flight per step, then the lanes are combined by
 // a fixed-order tree through LDS (deterministic, no long serial chain: the
 // previous 16-lane form spent 8-19 us waiting on one dependent load at a time).
-constexpr int kRedCols = 16, kRedLanes = 64;
+constexpr int kRedCols = 4, kRedLanes = 256;
 
 // sum-tree over the lanes of red[kRedLanes][kRedCols]; lane 0 ends with the total
 template <typename T>
