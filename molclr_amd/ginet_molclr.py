@@ -109,9 +109,9 @@ class GINet(nn.Module):
     use_executor = True
 
     def _executor_ok(self) -> bool:
-        if not self.use_executor or self.num_layer > 16 or self.emb_dim % 4:
-            return False
-        if self.precision == 'bf16' and self.emb_dim % 8:
+        # any emb_dim: the executor runs on the width padded to the kernels'
+        # multiple (_dim_pad) with zero columns
+        if not self.use_executor or self.num_layer > 16:
             return False
         if self.drop_ratio > 0 and self.training:
             return False
@@ -120,21 +120,54 @@ class GINet(nn.Module):
                    and bn.training == bn0.training and bn.momentum == bn0.momentum
                    and bn.eps == bn0.eps for bn in self.batch_norms)
 
+    def _dim_pad(self) -> int:
+        """Zero columns that bring emb_dim to the kernels' multiple (4 fp32, 8 bf16)."""
+        return (-self.emb_dim) % (8 if self.precision == 'bf16' else 4)
+
     def _encoder_params(self):
         params = [self.x_embedding1.weight, self.x_embedding2.weight]
         for g, bn in zip(self.gnns, self.batch_norms):
             params += [g.mlp[0].weight, g.mlp[0].bias, g.mlp[2].weight, g.mlp[2].bias,
                        g.edge_embedding1.weight, g.edge_embedding2.weight, bn.weight, bn.bias]
-        return params
+        p = self._dim_pad()
+        if not p:
+            return params
+        # emb_dim D -> D + p (hidden 2D -> 2D + 2p) with zero rows / columns
+        # (F.pad: the gradients of the real entries flow back, the pads' drop).
+        # A zero column stays zero through every layer: embeddings and edge
+        # tables add 0, the Linear weights' zero rows / columns keep it out of
+        # the real columns, and BatchNorm with gamma = beta = 0 maps it to 0.
+        out = [F.pad(params[0], (0, p)), F.pad(params[1], (0, p))]
+        for l in range(self.num_layer):
+            W0, b0, W2, b2, E1, E2, g, b = params[2 + 8 * l: 2 + 8 * (l + 1)]
+            out += [F.pad(W0, (0, p, 0, 2 * p)), F.pad(b0, (0, 2 * p)),
+                    F.pad(W2, (0, 2 * p, 0, p)), F.pad(b2, (0, p)),
+                    F.pad(E1, (0, p)), F.pad(E2, (0, p)), F.pad(g, (0, p)), F.pad(b, (0, p))]
+        return out
+
+    def _run_encoder(self, x, graph):
+        """ops.gin_encoder on the (padded) width; returns h [N, emb_dim + pad]."""
+        p = self._dim_pad()
+        bns = list(self.batch_norms)
+        if p:  # running statistics on the padded width, copied back after the call
+            bns = [_PaddedBatchNorm(bn, p) for bn in bns]
+        h = ops.gin_encoder(x, graph, bns, self._encoder_params(), self.precision)
+        if p:
+            for pb in bns:
+                pb.copy_back()
+        return h
 
     def encode(self, data, graph: DeviceGraph | None = None):
         """Node embeddings after the last layer (ginet_molclr.py:103-111)."""
         graph = graph or device_graph(data)
         if self._executor_ok():
-            return ops.gin_encoder(data.x, graph, list(self.batch_norms),
-                                   self._encoder_params(), self.precision), graph
+            h = self._run_encoder(data.x, graph)
+            return (h[:, :self.emb_dim] if self._dim_pad() else h), graph
         if self.precision != 'fp32':
             raise NotImplementedError("bf16 runs through the encoder executor only "
+                                      "(dropout 0, tracked BatchNorm statistics)")
+        if self._dim_pad():
+            raise NotImplementedError("emb_dim %% 4 != 0 runs through the encoder executor only "
                                       "(dropout 0, tracked BatchNorm statistics)")
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         # per-edge embeddings E1[bt] + E2[bd] of every layer, tabulated in one launch
@@ -150,12 +183,18 @@ class GINet(nn.Module):
 
     def _readout(self, h, graph):
         h = ops.segment_pool(h, graph, self.pool)
-        h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
+        W = self.feat_lin.weight
+        if h.shape[1] != W.shape[1]:  # padded width: zero weight columns for the pads
+            W = F.pad(W, (0, h.shape[1] - W.shape[1]))
+        h = ops.linear(h, W, self.feat_lin.bias)
         out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
                                   self.out_lin[2].weight, self.out_lin[2].bias)
         return h, out
 
     def forward(self, data):
+        if self._executor_ok():  # keep the padded width into the readout
+            graph = device_graph(data)
+            return self._readout(self._run_encoder(data.x, graph), graph)
         h, graph = self.encode(data)
         return self._readout(h, graph)
 
@@ -173,6 +212,21 @@ class GINet(nn.Module):
             return torch.cat([hi, hj], 0), torch.cat([oi, oj], 0)
         graph = pair_graph(xi, xj)
         x = torch.cat([xi.x, xj.x], 0)
-        h = ops.gin_encoder(x, graph, list(self.batch_norms), self._encoder_params(),
-                            self.precision)
-        return self._readout(h, graph)
+        return self._readout(self._run_encoder(x, graph), graph)
+
+
+class _PaddedBatchNorm:
+    """A BatchNorm1d's settings and running statistics on the padded width
+    (GINet._run_encoder); copy_back() writes the real columns back."""
+
+    def __init__(self, bn: nn.BatchNorm1d, p: int):
+        self.bn = bn
+        self.training, self.momentum, self.eps = bn.training, bn.momentum, bn.eps
+        self.num_batches_tracked = bn.num_batches_tracked
+        self.running_mean = F.pad(bn.running_mean, (0, p))
+        self.running_var = F.pad(bn.running_var, (0, p), value=1.0)
+
+    def copy_back(self):
+        D = self.bn.running_mean.shape[0]
+        self.bn.running_mean.copy_(self.running_mean[:D])
+        self.bn.running_var.copy_(self.running_var[:D])

@@ -429,3 +429,43 @@ def test_paired_step_trainer_and_eval(dev):
         hi, oi = m(xi)
         hj, oj = m(xj)
     assert rel(op, torch.cat([oi, oj])) < 1e-6 and rel(hp, torch.cat([hi, hj])) < 1e-6
+
+
+@pytest.mark.parametrize("L,D,B,pool", [(2, 30, 6, "mean"), (3, 77, 8, "add"), (2, 13, 5, "max")])
+def test_gin_any_emb_dim(dev, L, D, B, pool):
+    """emb_dim not a multiple of 4 (the reference takes any): the executor runs
+    on the zero-padded width; h / out, every gradient (bar the pre-BatchNorm
+    biases, whose exact gradient is 0) and the BatchNorm running statistics
+    match the fp64 oracle, and the forward pair equals two forwards."""
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(4)
+    ref = RefGINet(L, D, 64, pool=pool)
+    mine = GINet(L, D, 64, pool=pool)
+    mine.load_state_dict(ref.state_dict())
+    ref64 = copy.deepcopy(ref).double()
+    mine = mine.to(dev)
+    assert mine._dim_pad() and mine._executor_ok()
+    bi, bj = SyntheticPairBatches(B, seed=D).next()
+    h_6, out_6 = ref64(bi)
+    h_m, out_m = mine(bi.to(dev))
+    assert h_m.shape == h_6.shape and out_m.shape == out_6.shape
+    assert rel(h_m, h_6) < TOL and rel(out_m, out_6) < TOL
+    torch.manual_seed(3)
+    w1, w2 = torch.randn_like(h_6), torch.randn_like(out_6)
+    ((h_6 * w1).sum() + (out_6 * w2).sum()).backward()
+    ((h_m * w1.float().to(dev)).sum() + (out_m * w2.float().to(dev)).sum()).backward()
+    g64 = dict(ref64.named_parameters())
+    for name, p in mine.named_parameters():
+        assert p.grad is not None and p.grad.shape == p.shape, name
+        if pre_bn_bias(name):
+            continue
+        bound = 1e-4 if pool == "max" else TOL  # max pooling routes discontinuously
+        assert rel(p.grad, g64[name].grad) < bound, name
+    for name, buf in ref64.named_buffers():
+        assert rel(dict(mine.named_buffers())[name].double(), buf) < TOL, name
+    # the paired pass over (bi, bj) equals two separate forwards
+    a, b = copy.deepcopy(mine), copy.deepcopy(mine)
+    hp, op = a.forward_pair(bi.to(dev), bj.to(dev))
+    h1, o1 = b(bi.to(dev))
+    h2, o2 = b(bj.to(dev))
+    assert rel(hp, torch.cat([h1, h2])) < TOL and rel(op, torch.cat([o1, o2])) < TOL
