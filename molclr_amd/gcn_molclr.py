@@ -20,6 +20,7 @@ from torch import nn
 from torch.nn import Parameter
 
 from . import ops
+from .ginet_molclr import _PaddedBatchNorm
 from .data import DeviceGraph, device_graph, pair_graph
 
 num_atom_type = 119  # including the extra mask tokens
@@ -111,7 +112,8 @@ class GCN(nn.Module):
     use_executor = True
 
     def _executor_ok(self) -> bool:
-        if not self.use_executor or self.num_layer > 16 or self.emb_dim % 4:
+        # any emb_dim: the executor runs on the width padded to a multiple of 4
+        if not self.use_executor or self.num_layer > 16:
             return False
         if self.drop_ratio > 0 and self.training:
             return False
@@ -120,18 +122,45 @@ class GCN(nn.Module):
                    and bn.training == bn0.training and bn.momentum == bn0.momentum
                    and bn.eps == bn0.eps for bn in self.batch_norms)
 
+    def _dim_pad(self) -> int:
+        return (-self.emb_dim) % 4
+
     def _encoder_params(self):
         params = [self.x_embedding1.weight, self.x_embedding2.weight]
         for g, bn in zip(self.gnns, self.batch_norms):
             params += [g.weight, g.bias, g.edge_embedding1.weight, g.edge_embedding2.weight,
                        bn.weight, bn.bias]
-        return params
+        p = self._dim_pad()
+        if not p:
+            return params
+        # zero-padded width (GINet._encoder_params); the scalar edge terms reach
+        # the pad columns, and BatchNorm's zero gamma / beta map them back to 0
+        out = [F.pad(params[0], (0, p)), F.pad(params[1], (0, p))]
+        for l in range(self.num_layer):
+            W, b, E1, E2, g, bb = params[2 + 6 * l: 2 + 6 * (l + 1)]
+            out += [F.pad(W, (0, p, 0, p)), F.pad(b, (0, p)), E1, E2, F.pad(g, (0, p)),
+                    F.pad(bb, (0, p))]
+        return out
+
+    def _run_encoder(self, x, graph):
+        p = self._dim_pad()
+        bns = list(self.batch_norms)
+        if p:
+            bns = [_PaddedBatchNorm(bn, p) for bn in bns]
+        h = ops.gcn_encoder(x, graph, bns, self._encoder_params())
+        if p:
+            for pb in bns:
+                pb.copy_back()
+        return h
 
     def encode(self, data, graph: DeviceGraph | None = None):
         graph = graph or device_graph(data)
         if self._executor_ok():
-            return ops.gcn_encoder(data.x, graph, list(self.batch_norms),
-                                   self._encoder_params()), graph
+            h = self._run_encoder(data.x, graph)
+            return (h[:, :self.emb_dim] if self._dim_pad() else h), graph
+        if self._dim_pad():
+            raise NotImplementedError("emb_dim % 4 != 0 runs through the encoder executor only "
+                                      "(dropout 0, tracked BatchNorm statistics)")
         h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
         for layer in range(self.num_layer):
             h = self.gnns[layer].conv(h, graph)
@@ -143,12 +172,18 @@ class GCN(nn.Module):
 
     def _readout(self, h, graph):
         h = ops.segment_pool(h, graph, self.pool)
-        h = ops.linear(h, self.feat_lin.weight, self.feat_lin.bias)
+        W = self.feat_lin.weight
+        if h.shape[1] != W.shape[1]:  # padded width: zero weight columns for the pads
+            W = F.pad(W, (0, h.shape[1] - W.shape[1]))
+        h = ops.linear(h, W, self.feat_lin.bias)
         out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
                                   self.out_lin[2].weight, self.out_lin[2].bias)
         return h, out
 
     def forward(self, data):
+        if self._executor_ok():  # keep the padded width into the readout
+            graph = device_graph(data)
+            return self._readout(self._run_encoder(data.x, graph), graph)
         h, graph = self.encode(data)
         return self._readout(h, graph)
 
@@ -161,5 +196,4 @@ class GCN(nn.Module):
             return torch.cat([hi, hj], 0), torch.cat([oi, oj], 0)
         graph = pair_graph(xi, xj)
         x = torch.cat([xi.x, xj.x], 0)
-        h = ops.gcn_encoder(x, graph, list(self.batch_norms), self._encoder_params())
-        return self._readout(h, graph)
+        return self._readout(self._run_encoder(x, graph), graph)

@@ -431,16 +431,19 @@ def test_paired_step_trainer_and_eval(dev):
     assert rel(op, torch.cat([oi, oj])) < 1e-6 and rel(hp, torch.cat([hi, hj])) < 1e-6
 
 
-@pytest.mark.parametrize("L,D,B,pool", [(2, 30, 6, "mean"), (3, 77, 8, "add"), (2, 13, 5, "max")])
-def test_gin_any_emb_dim(dev, L, D, B, pool):
+@pytest.mark.parametrize("kind,L,D,B,pool", [("gin", 2, 30, 6, "mean"), ("gin", 3, 77, 8, "add"),
+                                             ("gin", 2, 13, 5, "max"), ("gcn", 2, 30, 6, "mean"),
+                                             ("gcn", 3, 45, 5, "add")])
+def test_any_emb_dim(dev, kind, L, D, B, pool):
     """emb_dim not a multiple of 4 (the reference takes any): the executor runs
     on the zero-padded width; h / out, every gradient (bar the pre-BatchNorm
     biases, whose exact gradient is 0) and the BatchNorm running statistics
     match the fp64 oracle, and the forward pair equals two forwards."""
+    from molclr_amd.gcn_molclr import GCN
     from molclr_amd.ginet_molclr import GINet
     torch.manual_seed(4)
-    ref = RefGINet(L, D, 64, pool=pool)
-    mine = GINet(L, D, 64, pool=pool)
+    ref = (RefGINet if kind == "gin" else RefGCN)(L, D, 64, pool=pool)
+    mine = (GINet if kind == "gin" else GCN)(L, D, 64, pool=pool)
     mine.load_state_dict(ref.state_dict())
     ref64 = copy.deepcopy(ref).double()
     mine = mine.to(dev)
