@@ -65,6 +65,9 @@ enum {
 #define MOLCLR_NBR_SLOTS 4           /* in-edges held in a node's neighbour slots */
 #define MOLCLR_NBR_OVERFLOW 7        /* degree field: > MOLCLR_NBR_SLOTS, use the CSR */
 #define MOLCLR_NBR_MAX_NODES (1 << 24)
+/* bit of a graph's status word (molclr_graph_build) that the atom embedding
+ * sets when an atom type or chirality index lies outside its table */
+#define MOLCLR_STATUS_ATOM_RANGE 8
 
 /* ecode (bond_type | bond_dir << 3) -> combined edge-table row */
 #define MOLCLR_ECOMB(ecode) ((int)((ecode) & 7u) * 3 + (int)((ecode) >> 3))
@@ -99,7 +102,9 @@ const char* molclr_last_error(void);
  *   graph_ptr [G+1] i32 : node range of every graph.
  *   status [1] i32 : bit 0 edge index out of range, bit 1 edge attr out of
  *       range, bit 2 batch not ascending / out of range.  Offending entries
- *       are clamped so no later kernel reads out of bounds.
+ *       are clamped so no later kernel reads out of bounds.  The encoders'
+ *       atom embedding adds bit 3 (MOLCLR_STATUS_ATOM_RANGE) when handed the
+ *       word.
  * ------------------------------------------------------------------------ */
 size_t molclr_graph_build_workspace_bytes(int64_t num_nodes, int64_t num_edges);
 int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
@@ -192,10 +197,13 @@ int molclr_aug_views_write(const int64_t* store_x, const int64_t* store_atom_ptr
                            const void* workspace, size_t workspace_bytes, molclr_stream_t stream);
 
 /* Atom embedding: h[i] = X1[x[i,0]] + X2[x[i,1]]  (ginet_molclr.py:103).
- * x int64 [N,2]; X1 [n1,D], X2 [n2,D]; h [N,D] f32.  Indices are clamped. */
+ * x int64 [N,2]; X1 [n1,D], X2 [n2,D]; h [N,D] f32.  A node whose atom type
+ * or chirality lies outside [0,n1) / [0,n2) -- where the reference's
+ * nn.Embedding raises -- gets a NaN row and sets MOLCLR_STATUS_ATOM_RANGE in
+ * *status (nullable: e.g. the batch's graph status word). */
 int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
                           float* h, int64_t num_nodes, int64_t dim, int64_t n1,
-                          int64_t n2, molclr_stream_t stream);
+                          int64_t n2, int32_t* status, molclr_stream_t stream);
 /* dX1 [n1,D], dX2 [n2,D] = Σ over nodes of each type of dh (deterministic, fp64
  * accumulation).  accumulate != 0 adds into dX1/dX2 (fused gradient
  * accumulation into a parameter's .grad); the same flag on the other
@@ -651,6 +659,8 @@ typedef struct molclr_gin_encoder {
    * agg / a1 live in the arena, those of dz / dz1 and all row maxima in the
    * workspace. */
   int32_t fp32_gemm;
+  /* nullable: receives MOLCLR_STATUS_ATOM_RANGE (molclr_atom_embed_fwd) */
+  int32_t* status;
 } molclr_gin_encoder;
 
 /* Gradient buffers, same shapes as the parameters; NULL = not needed. */
@@ -738,6 +748,7 @@ typedef struct molclr_gcn_encoder {
    * row-wise scales; weight_planes_t are then molclr_hplanes_make_batch
    * images, dim <= 1024). */
   int32_t fp32_gemm;
+  int32_t* status; /* nullable: MOLCLR_STATUS_ATOM_RANGE, as molclr_gin_encoder */
 } molclr_gcn_encoder;
 
 typedef struct molclr_gcn_encoder_grads {
@@ -772,7 +783,7 @@ int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* enc, const molclr_gcn_encod
  * ------------------------------------------------------------------------ */
 int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, const float* X2, uint16_t* h,
                                int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,
-                               molclr_stream_t stream);
+                               int32_t* status, molclr_stream_t stream);
 /* workspace: molclr_atom_embed_bwd_workspace_bytes */
 int molclr_atom_embed_bwd_bf16(const int64_t* x, const uint16_t* dh, float* dX1, float* dX2,
                                int64_t num_nodes, int64_t dim, int64_t n1, int64_t n2,

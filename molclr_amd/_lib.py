@@ -35,7 +35,7 @@ SIGNATURES = {
     "molclr_mask_views_workspace_bytes": (c_size_t, [_I64]),
     "molclr_mask_views": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, c_uint64, c_int, _P, _P,
                                   _P, _P, _P, _I64, _I64, _P, _P, c_size_t, _P]),
-    "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "molclr_atom_embed_fwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P]),
     "molclr_atom_embed_bwd_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64]),
     "molclr_atom_embed_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P, c_size_t,
                                       _P]),
@@ -127,7 +127,7 @@ SIGNATURES = {
                                       c_int, _I64, _I64, _P, _P, _P, _P, c_size_t, _P]),
     "molclr_aug_views_write": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I64,
                                        _I64, _P, _P, _P, _P, _P, c_size_t, _P]),
-    "molclr_atom_embed_fwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P]),
+    "molclr_atom_embed_fwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P]),
     "molclr_atom_embed_bwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, c_int, _P,
                                            c_size_t, _P]),
     "molclr_gine_aggregate_fwd_bf16": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
@@ -157,6 +157,7 @@ NUM_ECOMB = 15  # combined edge-table rows (bond type * 3 + bond dir)
 MAX_LAYERS = 16
 MAX_SEGMENTS = 8
 DTYPE_F32, DTYPE_BF16 = 0, 1
+STATUS_ATOM_RANGE = 8  # MOLCLR_STATUS_ATOM_RANGE
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
 KTIMER_NTXENT = 4
@@ -175,7 +176,7 @@ class GinEncoder(ctypes.Structure):
                             "edge_embedding1", "edge_embedding2", "bn_weight", "bn_bias",
                             "bn_running_mean", "bn_running_var", "bn_num_batches_tracked",
                             "mlp0_planes", "mlp0_planes_t", "mlp2_planes", "mlp2_planes_t")] + [
-        ("dtype", ctypes.c_int32), ("fp32_gemm", ctypes.c_int32)]
+        ("dtype", ctypes.c_int32), ("fp32_gemm", ctypes.c_int32), ("status", c_void_p)]
 
 
 class GinEncoderGrads(ctypes.Structure):
@@ -194,7 +195,7 @@ class GcnEncoder(ctypes.Structure):
         (f, _L16) for f in ("weight", "bias", "edge_embedding1", "edge_embedding2", "bn_weight",
                             "bn_bias", "bn_running_mean", "bn_running_var",
                             "bn_num_batches_tracked", "weight_planes", "weight_planes_t")] + [
-        ("fp32_gemm", ctypes.c_int32)]
+        ("fp32_gemm", ctypes.c_int32), ("status", c_void_p)]
 
 
 class GcnEncoderGrads(ctypes.Structure):

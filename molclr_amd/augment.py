@@ -136,6 +136,12 @@ class DeviceMoleculeStore:
                 self.mask_view(mol_ids, seed, 1, check, host_ids))
 
     AUG_MODES = {"subgraph": _lib.AUG_SUBGRAPH, "mix": _lib.AUG_MIX}
+    AUG_MAX_ATOMS, AUG_MAX_BONDS = 256, 512   # augment.hip kAugMaxAtoms / kAugMaxBonds
+
+    def aug_capable(self) -> np.ndarray:
+        """Per molecule: small enough for the subgraph / mix kernels (larger
+        molecules come back unaugmented with status bit 4)."""
+        return (self.num_atoms <= self.AUG_MAX_ATOMS) & (self.num_bonds <= self.AUG_MAX_BONDS)
 
     def aug_view(self, mol_ids, seed: int, view: int, mode: str = "subgraph",
                  check: bool = False, host_ids=None) -> Batch:

@@ -26,17 +26,25 @@ constexpr int kT = 256;
 // ---------------------------------------------------------------------------
 // atom embedding
 // ---------------------------------------------------------------------------
+// An atom type or chirality outside the tables (the reference's
+// nn.Embedding raises an IndexError on it) makes the row NaN and sets bit 3 of
+// *status (MOLCLR_STATUS_ATOM_RANGE) instead of being clamped to a valid row.
 template <typename St>
 __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __restrict__ X1,
                                  const float4* __restrict__ X2, typename St::T* __restrict__ h,
-                                 int64_t N, int d4, int64_t n1, int64_t n2) {
+                                 int64_t N, int d4, int64_t n1, int64_t n2,
+                                 int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
-  int64_t a = x[2 * i], b = x[2 * i + 1];
-  a = a < 0 ? 0 : (a >= n1 ? n1 - 1 : a);
-  b = b < 0 ? 0 : (b >= n2 ? n2 - 1 : b);
+  const int64_t a = x[2 * i], b = x[2 * i + 1];
+  if (a < 0 || a >= n1 || b < 0 || b >= n2) {
+    const float q = __builtin_nanf("");
+    St::st(h, t, make_float4(q, q, q, q));
+    if (c == 0 && status != nullptr) atomicOr(status, MOLCLR_STATUS_ATOM_RANGE);
+    return;
+  }
   St::st(h, t, f4add(X1[a * d4 + c], X2[b * d4 + c]));
 }
 
@@ -54,6 +62,8 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
 constexpr int kEmbBlock = 256;  // items per sort block
 constexpr int kEmbChunk = 128;  // items per fp32 chunk sum
 
+// Out-of-range indices were reported by the forward (NaN rows, status bit 3);
+// they are clamped here only to keep the sort's keys in bounds.
 __device__ __forceinline__ int emb_key(const int64_t* __restrict__ x, int64_t item, int64_t N,
                                        int64_t n1, int64_t n2) {
   if (item < N) {
@@ -680,7 +690,7 @@ size_t molclr_colsum_ws(int64_t rows, int64_t cols);
 
 MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const float* X2,
                                      float* h, int64_t N, int64_t D, int64_t n1, int64_t n2,
-                                     molclr_stream_t stream) {
+                                     int32_t* status, molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "atom_embed_fwd: dim %lld must be a positive multiple of 4",
                  (long long)D);
   MOLCLR_REQUIRE(n1 > 0 && n2 > 0, "atom_embed_fwd: empty table");
@@ -689,7 +699,7 @@ MOLCLR_API int molclr_atom_embed_fwd(const int64_t* x, const float* X1, const fl
   int d4 = (int)(D / 4);
   hipLaunchKernelGGL(k_atom_embed_fwd<StF32>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
                      molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N, d4,
-                     n1, n2);
+                     n1, n2, status);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -929,7 +939,7 @@ MOLCLR_API int molclr_gcn_aggregate_bwd(const float* g, const int32_t* rowptr_t,
 // ---------------------------------------------------------------------------
 MOLCLR_API int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, const float* X2,
                                           uint16_t* h, int64_t N, int64_t D, int64_t n1,
-                                          int64_t n2, molclr_stream_t stream) {
+                                          int64_t n2, int32_t* status, molclr_stream_t stream) {
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "atom_embed_fwd_bf16: dim must be a multiple of 4");
   MOLCLR_REQUIRE(n1 > 0 && n2 > 0, "atom_embed_fwd_bf16: empty table");
   if (N == 0) return MOLCLR_OK;
@@ -937,7 +947,7 @@ MOLCLR_API int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, con
   const int d4 = (int)(D / 4);
   hipLaunchKernelGGL(k_atom_embed_fwd<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
                      molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N, d4,
-                     n1, n2);
+                     n1, n2, status);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -182,10 +182,10 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   void* h = A + lay.h0;
   if (bf)
     MOLCLR_TRY(molclr_atom_embed_fwd_bf16(x, e->x_embedding1, e->x_embedding2, (uint16_t*)h, N, D,
-                                          e->n_atom, e->n_chiral, stream));
+                                          e->n_atom, e->n_chiral, e->status, stream));
   else
     MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, (float*)h, N, D,
-                                     e->n_atom, e->n_chiral, stream));
+                                     e->n_atom, e->n_chiral, e->status, stream));
   float* Ec = F(lay.ec);
   MOLCLR_TRY(molclr_edge_tables_combine(L, e->edge_embedding1, e->edge_embedding2, Ec, D, stream));
   for (int l = 0; l < L; ++l) {
@@ -520,7 +520,7 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
   }
   float* h = A + lay.h0;
   MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, h, N, D, e->n_atom,
-                                   e->n_chiral, stream));
+                                   e->n_chiral, e->status, stream));
   for (int l = 0; l < L; ++l) {
     float* z = A + lay.z[l];
     const bool last = l == L - 1;

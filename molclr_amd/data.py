@@ -199,6 +199,9 @@ class DeviceGraph:
                 what.append("edge_attr out of range")
             if st & 4:
                 what.append("batch not ascending / out of range")
+            if st & _lib.STATUS_ATOM_RANGE:
+                what.append("atom type / chirality outside the model's embedding tables "
+                            "(the reference's nn.Embedding raises IndexError)")
             raise ValueError("invalid graph batch: " + ", ".join(what))
 
 

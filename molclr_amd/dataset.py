@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from .data import Batch, Data, collate_pairs
+from .shards import read_smiles  # noqa: F401  (dataset/dataset.py:46-53)
 
 MASK_ATOM = 118  # len(ATOM_LIST), dataset/dataset.py:123
 
@@ -223,18 +224,91 @@ class ShardedSubsetSampler(torch.utils.data.Sampler):
         return len(self.indices) // self.world
 
 
+def view_seed(seed: int, rank: int, epoch: int, batch: int) -> int:
+    """The 64-bit key the device augmentation draws a batch's subsets from:
+    distinct for every (seed, rank, epoch, batch), so a molecule gets new
+    views every epoch and the same ones on a rerun."""
+    z = 0
+    for v in (seed, rank, epoch, batch):
+        z = (z ^ (int(v) & _M64)) * 0x9E3779B97F4A7C15 & _M64
+        z ^= z >> 29
+    return z
+
+
+_M64 = (1 << 64) - 1
+AUG_MODES = ("node", "subgraph", "mix")
+
+
+class DeviceViewLoader:
+    """The DataLoader of the device path: every batch is ``batch_size``
+    molecule ids from ``sampler`` (drop_last, dataset/dataset.py:179-183) and
+    both views are built on the GPU from the resident
+    :class:`~molclr_amd.augment.DeviceMoleculeStore` -- node masking
+    (dataset.py:111-147), subgraph removal (dataset_subgraph.py:96-177) or
+    both (dataset_mix.py:86-217), collated into the Batch fields.  Yields the
+    (Batch_i, Batch_j) pairs ``MolCLR.train`` iterates over
+    (molclr.py:108), already on the device."""
+
+    def __init__(self, store, sampler, batch_size: int, aug: str = "node", seed: int = 0,
+                 rank: int = 0):
+        if aug not in AUG_MODES:
+            raise ValueError(f"aug {aug!r}: one of {AUG_MODES}")
+        self.store, self.sampler = store, sampler
+        self.batch_size, self.aug, self.seed, self.rank = int(batch_size), aug, seed, rank
+        self.epoch = 0
+
+    def __len__(self):
+        return len(self.sampler) // self.batch_size
+
+    def __iter__(self):
+        ids = np.fromiter(iter(self.sampler), dtype=np.int64)
+        epoch = self.epoch
+        self.epoch += 1
+        bs = self.batch_size
+        for b in range(ids.shape[0] // bs):
+            host = ids[b * bs:(b + 1) * bs]
+            key = view_seed(self.seed, self.rank, epoch, b)
+            self.last = (host, key)   # the batch's molecule ids and subset key
+            if self.aug == "node":
+                yield self.store.mask_views(host, key, host_ids=host)
+            else:
+                yield self.store.aug_views(host, key, mode=self.aug, host_ids=host)
+
+
 class MoleculeDatasetWrapper:
-    """dataset/dataset.py:153-185: shuffled train/valid split, DataLoaders with
-    ``drop_last=True`` (NT-Xent needs full batches).  ``data_path`` is read as
-    ``synthetic:<num_molecules>`` (SMILES featurisation needs RDKit, absent) or
-    a binary graph shard (molclr_amd.shards).
+    """dataset/dataset.py:153-185 (and the subgraph / mix modules' copies):
+    a shuffled train / valid split and loaders of full batches (drop_last:
+    NT-Xent needs them).
+
+    ``data_path`` is what config.yaml names (config.yaml:27):
+
+    * a SMILES text file, read as ``read_smiles`` does (dataset.py:46-53: the
+      last comma-separated field of every line), featurised once into a
+      cached binary shard next to it (molclr_amd.shards; with explicit
+      hydrogens for ``aug: mix``, whose module calls ``Chem.AddHs``,
+      dataset_mix.py:87-88);
+    * a binary graph shard (molclr_amd.shards);
+    * ``synthetic:<num_molecules>`` (SURVEY §8d generator).
+
+    ``aug`` picks the augmentation (molclr.py:184-191).  ``views='device'``
+    (default) keeps the molecules resident in HBM and builds both views of
+    every batch on the GPU (:class:`DeviceViewLoader`); ``views='host'`` is
+    the reference's DataLoader of host-built node-mask views
+    (``aug: node`` only).
 
     Data parallel: with ``torch.distributed`` initialised (or ``rank`` /
     ``world`` given), each rank draws a disjoint, equally sized shard of the
     train and valid index sets every epoch (ShardedSubsetSampler)."""
 
     def __init__(self, batch_size, num_workers, valid_size, data_path, seed: int = 0,
-                 shape: str = "uniform", rank: int | None = None, world: int | None = None):
+                 shape: str = "uniform", rank: int | None = None, world: int | None = None,
+                 aug: str = "node", views: str = "device"):
+        if aug not in AUG_MODES:
+            raise ValueError("Not defined molecule augmentation!")
+        if views not in ("device", "host"):
+            raise ValueError(f"views {views!r}: 'device' or 'host'")
+        if views == "host" and aug != "node":
+            raise ValueError(f"aug {aug!r} views are built on the device only (views='device')")
         self.batch_size = batch_size
         self.num_workers = num_workers
         self.valid_size = valid_size
@@ -242,6 +316,7 @@ class MoleculeDatasetWrapper:
         self.seed = seed
         self.shape = shape
         self.rank, self.world = rank, world
+        self.aug, self.views = aug, views
 
     def _rank_world(self) -> tuple[int, int]:
         if self.rank is not None and self.world is not None:
@@ -252,31 +327,69 @@ class MoleculeDatasetWrapper:
         return 0, 1
 
     def _num_molecules(self) -> int:
+        return int(str(self.data_path).split(":", 1)[1])
+
+    def shard_path(self):
+        """The binary shard behind ``data_path`` (featurising a SMILES file
+        once), or None for synthetic data."""
+        from .shards import cached_smiles_shard, is_shard
         p = str(self.data_path)
         if p.startswith("synthetic:"):
-            return int(p.split(":", 1)[1])
-        raise NotImplementedError(
-            f"data_path {p!r}: SMILES featurisation needs RDKit, which is not available; "
-            "use 'synthetic:<num_molecules>' or a binary graph shard")
+            return None
+        if is_shard(p):
+            return p
+        return cached_smiles_shard(p, add_hs=(self.aug == "mix"))
 
     def get_data_loaders(self):
         rank, _ = self._rank_world()
-        p = str(self.data_path)
-        if p.startswith("synthetic:"):
+        shard = self.shard_path()
+        if self.views == "device":
+            store = self.device_store(shard)
+            return self.get_train_validation_data_loaders(store, len_=store.num_molecules)
+        if shard is None:
             train_dataset = MoleculeDataset(self._num_molecules(), self.seed, self.shape, rank=rank)
         else:
             from .shards import ShardMoleculeDataset
-            train_dataset = ShardMoleculeDataset(p, seed=self.seed, rank=rank)
+            train_dataset = ShardMoleculeDataset(shard, seed=self.seed, rank=rank)
         return self.get_train_validation_data_loaders(train_dataset)
 
-    def get_train_validation_data_loaders(self, train_dataset):
+    def device_store(self, shard=None):
+        """The whole dataset resident on the current GPU (every rank holds it:
+        10 M PubChem molecules take ~28 GB of the 288 GB)."""
+        from .augment import DeviceMoleculeStore
+        if not torch.cuda.is_available():
+            raise RuntimeError("device views need a GPU (views='host' for the CPU DataLoader)")
+        dev = torch.device("cuda", torch.cuda.current_device())
+        if shard is None:
+            rng = np.random.default_rng(self.seed)
+            mols = [random_molecule(rng, self.shape) for _ in range(self._num_molecules())]
+            return DeviceMoleculeStore.from_molecules(mols, dev)
+        from .shards import GraphShard
+        return GraphShard(shard).device_store(dev)
+
+    def get_train_validation_data_loaders(self, train_dataset, len_: int | None = None):
         rank, world = self._rank_world()
-        num_train = len(train_dataset)
+        num_train = len(train_dataset) if len_ is None else len_
         indices = np.random.default_rng(self.seed).permutation(num_train).tolist()
+        if self.views == "device" and self.aug != "node":
+            # subgraph / mix views hold a molecule in LDS: larger ones are left out
+            from .augment import DeviceMoleculeStore
+            ok = train_dataset.aug_capable()
+            dropped = int((~ok).sum())
+            if dropped:
+                print(f"{dropped} molecules above {DeviceMoleculeStore.AUG_MAX_ATOMS} atoms / "
+                      f"{DeviceMoleculeStore.AUG_MAX_BONDS} bonds left out of aug={self.aug}")
+                indices = [i for i in indices if ok[i]]
+                num_train = len(indices)
         split = int(np.floor(self.valid_size * num_train))
         train_idx, valid_idx = indices[split:], indices[:split]
         train_sampler = ShardedSubsetSampler(train_idx, rank, world, seed=self.seed + 1)
         valid_sampler = ShardedSubsetSampler(valid_idx, rank, world, seed=self.seed + 2)
+        if self.views == "device":
+            return (DeviceViewLoader(train_dataset, train_sampler, self.batch_size, self.aug,
+                                     self.seed + 1, rank),
+                    DeviceViewLoader(train_dataset, valid_sampler, self.batch_size, self.aug,
+                                     self.seed + 2, rank))
         kw = dict(batch_size=self.batch_size, num_workers=self.num_workers, drop_last=True,
                   collate_fn=collate_pairs)
         train_loader = torch.utils.data.DataLoader(train_dataset, sampler=train_sampler, **kw)

@@ -161,7 +161,8 @@ class GCN(nn.Module):
         if self._dim_pad():
             raise NotImplementedError("emb_dim % 4 != 0 runs through the encoder executor only "
                                       "(dropout 0, tracked BatchNorm statistics)")
-        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
+        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight,
+                           graph.status)
         for layer in range(self.num_layer):
             h = self.gnns[layer].conv(h, graph)
             last = layer == self.num_layer - 1

@@ -169,7 +169,8 @@ class GINet(nn.Module):
         if self._dim_pad():
             raise NotImplementedError("emb_dim %% 4 != 0 runs through the encoder executor only "
                                       "(dropout 0, tracked BatchNorm statistics)")
-        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight)
+        h = ops.atom_embed(data.x, self.x_embedding1.weight, self.x_embedding2.weight,
+                           graph.status)
         # per-edge embeddings E1[bt] + E2[bd] of every layer, tabulated in one launch
         Ec = ops.edge_tables_combine([g.edge_embedding1.weight for g in self.gnns],
                                      [g.edge_embedding2.weight for g in self.gnns])

@@ -12,8 +12,14 @@ checkpoint is tolerated.
 
 Differences (all additive): the optimiser is :class:`FusedAdam` (same update
 rule, one kernel); optional config keys ``world_size`` (data parallel via
-torchrun), ``seed``; the scalar writer is TensorBoard when installed,
-otherwise a JSONL file with the same tags.
+torchrun), ``seed``, ``dataset.views`` ('device', the default: both views of
+every batch are built on the GPU from the resident molecules, for every
+``aug`` mode; 'host': the reference's DataLoader, node masking only); the
+scalar writer is TensorBoard when installed, otherwise a JSONL file with the
+same tags.  ``data_path`` may be the reference's SMILES text file (featurised
+once into a cached binary shard), a shard, or ``synthetic:<count>``.
+Invalid inputs raise at the next log step (``check_inputs``), as the
+reference's embedding lookup would.
 """
 from __future__ import annotations
 
@@ -110,6 +116,12 @@ class MolCLR(object):
             model = GINet(**self.config["model"], precision=prec).to(self.device)
         elif self.config['model_type'] == 'gcn':
             from .gcn_molclr import GCN
+            if self.config.get('fp16_precision', False):
+                # the reference's apex O2 switch wraps whichever model is built
+                # (molclr.py:93-96); the GCN kernels have no bf16 storage path
+                raise NotImplementedError(
+                    "fp16_precision: True with model_type: gcn -- the GCN encoder runs in fp32 "
+                    "only (set fp16_precision: False)")
             model = GCN(**self.config["model"]).to(self.device)
         else:
             raise ValueError('Undefined GNN model.')
@@ -140,6 +152,7 @@ class MolCLR(object):
         if reducer is not None:
             reducer.arm()
         loss = self._step(model, xis, xjs, n_iter)
+        self._last_inputs = xis
         loss.backward()
         if reducer is not None:
             reducer.finish()
@@ -167,6 +180,7 @@ class MolCLR(object):
             for bn, (xis, xjs) in enumerate(train_loader):
                 loss = self.train_step(model, optimizer, xis, xjs, n_iter)
                 if n_iter % self.config['log_every_n_steps'] == 0 and self.rank == 0:
+                    self.check_inputs()
                     self.writer.add_scalar('train_loss', loss, global_step=n_iter)
                     self.writer.add_scalar('cosine_lr_decay', scheduler.get_last_lr()[0],
                                            global_step=n_iter)
@@ -192,6 +206,16 @@ class MolCLR(object):
                 scheduler.step()
         return model
 
+    def check_inputs(self) -> None:
+        """Raise on the last step's invalid inputs (out-of-range edges, or atom
+        features outside the embedding tables, where the reference's
+        nn.Embedding raises IndexError).  Reads the graph's device status word
+        (a sync: called where the loop syncs anyway, at the log steps)."""
+        xi = getattr(self, "_last_inputs", None)
+        g = getattr(xi, "_molclr_pair_graph", None) or (None, getattr(xi, "_molclr_graph", None))
+        if g[1] is not None:
+            g[1].check()
+
     def _load_pre_trained_weights(self, model):
         try:
             checkpoints_folder = os.path.join('./ckpt', str(self.config['load_model']), 'checkpoints')
@@ -212,7 +236,9 @@ class MolCLR(object):
                 xis = xis.to(self.device)
                 xjs = xjs.to(self.device)
                 loss = self._step(model, xis, xjs, counter)
+                self._last_inputs = xis
                 valid_loss += loss.item()
+                self.check_inputs()
                 counter += 1
             valid_loss /= max(counter, 1)
         model.train()
@@ -220,13 +246,20 @@ class MolCLR(object):
 
 
 def main(config_path: str = "config.yaml"):
+    """molclr.py:180-195: the data module is chosen by ``config['aug']``."""
     with open(config_path, "r") as f:
         config = yaml.safe_load(f)
     print(config)
-    if config['aug'] != 'node':
-        raise ValueError("only aug: node (dataset/dataset.py) is provided; "
-                         "subgraph / mix augmentations are out of this build's scope")
-    from .dataset import MoleculeDatasetWrapper
+
+    if config['aug'] == 'node':
+        from .dataset import MoleculeDatasetWrapper
+    elif config['aug'] == 'subgraph':
+        from .dataset_subgraph import MoleculeDatasetWrapper
+    elif config['aug'] == 'mix':
+        from .dataset_mix import MoleculeDatasetWrapper
+    else:
+        raise ValueError('Not defined molecule augmentation!')
+
     dataset = MoleculeDatasetWrapper(config['batch_size'], **config['dataset'])
     molclr = MolCLR(dataset, config)
     molclr.train()

@@ -438,14 +438,14 @@ def edge_tables_combine(E1s, E2s) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 class _AtomEmbed(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x_idx, X1, X2):
+    def forward(ctx, x_idx, X1, X2, status=None):
         _check(x_idx, X1, X2)
         x_idx = _c(x_idx.to(torch.long))
         N = x_idx.shape[0]
         D = X1.shape[1]
         h = torch.empty(N, D, dtype=torch.float32, device=X1.device)
         _lib.call("molclr_atom_embed_fwd", x_idx.data_ptr(), X1.data_ptr(), X2.data_ptr(),
-                  h.data_ptr(), N, D, X1.shape[0], X2.shape[0], _stream(X1))
+                  h.data_ptr(), N, D, X1.shape[0], X2.shape[0], _lib.ptr(status), _stream(X1))
         ctx.save_for_backward(x_idx)
         ctx.shapes = (X1.shape[0], X2.shape[0], D)
         ctx.params = (X1, X2)
@@ -467,7 +467,7 @@ class _AtomEmbed(torch.autograd.Function):
         ws = _ws(ws_bytes, dh.device)
         _lib.call("molclr_atom_embed_bwd", x_idx.data_ptr(), dh.data_ptr(), b1.data_ptr(),
                   b2.data_ptr(), N, D, n1, n2, acc1, ws.data_ptr(), ws_bytes, _stream(dh))
-        return None, r1, r2
+        return None, r1, r2, None
 
 
 class _GINEAggregate(torch.autograd.Function):
@@ -948,6 +948,7 @@ class _GINEncoder(torch.autograd.Function):
         kind = "h3" if h3 and H3_FORWARD else "x6"
         kind_t = "h3" if h3 else "x6"
         enc.fp32_gemm = (1 | (2 if H3_FORWARD else 0)) if h3 else 0
+        enc.status = graph.status.data_ptr()  # out-of-vocabulary atoms: MOLCLR_STATUS_ATOM_RANGE
         enc.n_atom, enc.n_chiral = params[0].shape[0], params[1].shape[0]
         enc.momentum, enc.eps = float(bns[0].momentum), float(bns[0].eps)
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
@@ -1052,6 +1053,7 @@ class _GCNEncoder(torch.autograd.Function):
         enc.x_embedding1, enc.x_embedding2 = params[0].data_ptr(), params[1].data_ptr()
         h3 = gcn_h3_ok(N, D)  # the form _GCNConv uses on these shapes
         enc.fp32_gemm = int(h3)
+        enc.status = graph.status.data_ptr()
         for l in range(L):
             W, b, E1, E2, g, bb = params[2 + GCN_PARAMS_PER_LAYER * l:
                                          2 + GCN_PARAMS_PER_LAYER * (l + 1)]
@@ -1138,8 +1140,10 @@ def gin_encoder(x_idx, graph, bns, params, precision: str = "fp32"):
 
 
 # public functional API -------------------------------------------------------
-def atom_embed(x_idx, X1, X2):
-    return _AtomEmbed.apply(x_idx, X1, X2)
+def atom_embed(x_idx, X1, X2, status=None):
+    """ginet_molclr.py:103.  An out-of-vocabulary atom gives a NaN row and
+    sets MOLCLR_STATUS_ATOM_RANGE in ``status`` (e.g. the graph's word)."""
+    return _AtomEmbed.apply(x_idx, X1, X2, status)
 
 
 def gine_aggregate(h, E1, E2, graph, Ec=None):

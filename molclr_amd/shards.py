@@ -11,7 +11,7 @@ a pre-featurised, memory-mappable shard that loads straight into a
 Layout (little endian, every array 64-byte aligned)::
 
     magic  b"MOLCLRG1"          8 bytes
-    header u32 version (1), u32 flags (0),
+    header u32 version (1), u32 flags (bit 0: hydrogens explicit, Chem.AddHs),
            u64 num_mols, u64 num_atoms, u64 num_bonds
     atom_ptr  i64 [num_mols + 1]     atoms of molecule g: [atom_ptr[g], atom_ptr[g+1])
     bond_ptr  i64 [num_mols + 1]     bonds of molecule g
@@ -41,6 +41,8 @@ VERSION = 1
 _HDR = struct.Struct("<8sIIQQQ")
 _ALIGN = 64
 
+FLAG_EXPLICIT_H = 1   # molecules featurised after Chem.AddHs (dataset_mix.py:87-88)
+
 MAX_ATOM_TYPE = 119   # 118 elements + the mask token (ginet_molclr.py:9)
 MAX_CHIRALITY = 4     # CHIRALITY_LIST (dataset.py:27-32)
 MAX_BOND_TYPE = 4     # BOND_LIST (dataset.py:33)
@@ -63,10 +65,11 @@ def _layout(num_mols: int, num_atoms: int, num_bonds: int) -> dict:
     return lay
 
 
-def write_shard(path, molecules: Iterable) -> int:
+def write_shard(path, molecules: Iterable, flags: int = 0) -> int:
     """Write molecules (objects with ``x`` [N,2], ``edge_index`` [2,2M] local,
     ``edge_attr`` [2M,2] holding every bond as the consecutive directed pair
-    (s,e),(e,s), e.g. dataset.Molecule) as one shard; returns the count."""
+    (s,e),(e,s), e.g. dataset.Molecule) as one shard; returns the count.
+    ``flags``: FLAG_EXPLICIT_H when the molecules carry their hydrogens."""
     mols = list(molecules)
     xs, bonds, battr = [], [], []
     for m in mols:
@@ -100,7 +103,7 @@ def write_shard(path, molecules: Iterable) -> int:
     path = Path(path)
     tmp = path.with_suffix(path.suffix + ".tmp")
     with open(tmp, "wb") as f:
-        f.write(_HDR.pack(MAGIC, VERSION, 0, G, Na, Nb))
+        f.write(_HDR.pack(MAGIC, VERSION, int(flags), G, Na, Nb))
         for name, arr in (("atom_ptr", atom_ptr), ("bond_ptr", bond_ptr),
                           ("atoms", np.concatenate(xs, 0) if xs else np.zeros((0, 2), np.uint8)),
                           ("bonds", np.concatenate(bonds, 0) if bonds else np.zeros((0, 2), np.uint16)),
@@ -127,6 +130,8 @@ class GraphShard:
         mm = lambda name, dt, shape: np.memmap(self.path, dtype=dt, mode="r",  # noqa: E731
                                                offset=lay[name], shape=shape)
         self.num_molecules, self.num_atoms_total, self.num_bonds_total = G, Na, Nb
+        self.flags = int(flags)
+        self.explicit_h = bool(flags & FLAG_EXPLICIT_H)
         self.atom_ptr = mm("atom_ptr", np.int64, (G + 1,))
         self.bond_ptr = mm("bond_ptr", np.int64, (G + 1,))
         self.atoms = mm("atoms", np.uint8, (Na, 2)) if Na else np.zeros((0, 2), np.uint8)
@@ -205,24 +210,76 @@ def write_synthetic_shard(path, num_molecules: int, seed: int = 0, shape: str = 
     return write_shard(path, (random_molecule(rng, shape) for _ in range(num_molecules)))
 
 
-def featurise_smiles_file(smiles_path, shard_path, limit: int | None = None) -> tuple[int, int]:
-    """``read_smiles`` (dataset.py:46-53) + featurisation into a shard:
-    returns (molecules written, lines skipped by the SMILES subset parser)."""
+def read_smiles(data_path) -> list[str]:
+    """dataset/dataset.py:46-53 (and the subgraph / mix modules' copies): the
+    last comma-separated field of every line, read with ``csv.reader``.  Blank
+    lines, on which the reference's ``row[-1]`` raises, are skipped."""
+    import csv
+    out = []
+    with open(data_path) as f:
+        for row in csv.reader(f, delimiter=","):
+            if row:
+                out.append(row[-1])
+    return out
+
+
+NUM_CHIRALITY_TAG = 3   # rows of the model's x_embedding2 (ginet_molclr.py:10)
+
+
+def featurise_smiles_file(smiles_path, shard_path, limit: int | None = None,
+                          add_hs: bool = False) -> tuple[int, int]:
+    """``read_smiles`` + featurisation (dataset.py:61-109, with
+    ``Chem.AddHs`` first when ``add_hs``: dataset_mix.py:87-88) into a shard.
+    Returns (molecules written, molecules skipped).  Skipped: SMILES the
+    subset parser rejects, and molecules with a chirality tag the model has
+    no embedding row for (CHI_OTHER = 3: CHIRALITY_LIST has 4 entries, the
+    model's x_embedding2 3 -- the reference's nn.Embedding raises an
+    IndexError on such a molecule mid-training)."""
     from .smiles import featurise
     mols, skipped = [], 0
-    with open(smiles_path) as f:
-        for i, line in enumerate(f):
-            if limit is not None and i >= limit:
-                break
-            smi = line.strip().split()[0] if line.strip() else ""
-            if not smi:
-                continue
-            try:
-                mols.append(featurise(smi))
-            except ValueError:
-                skipped += 1
-    write_shard(shard_path, mols)
+    for i, smi in enumerate(read_smiles(smiles_path)):
+        if limit is not None and i >= limit:
+            break
+        smi = smi.strip()
+        if not smi:
+            continue
+        try:
+            m = featurise(smi, add_hs=add_hs)
+        except ValueError:
+            skipped += 1
+            continue
+        if m.x.size and int(m.x[:, 1].max()) >= NUM_CHIRALITY_TAG:
+            skipped += 1
+            continue
+        mols.append(m)
+    write_shard(shard_path, mols, flags=FLAG_EXPLICIT_H if add_hs else 0)
     return len(mols), skipped
+
+
+def is_shard(path) -> bool:
+    try:
+        with open(path, "rb") as f:
+            return f.read(len(MAGIC)) == MAGIC
+    except OSError:
+        return False
+
+
+def cached_smiles_shard(smiles_path, add_hs: bool = False) -> Path:
+    """The featurised shard of a SMILES file, built once next to it
+    (``<file>.molclr.molg``, ``<file>.molclr-h.molg`` with explicit
+    hydrogens) and rebuilt when the text file is newer.  With
+    torch.distributed initialised, rank 0 builds it and the others wait."""
+    import torch.distributed as dist
+    src = Path(smiles_path)
+    dst = src.with_name(src.name + (".molclr-h.molg" if add_hs else ".molclr.molg"))
+    stale = not dst.exists() or dst.stat().st_mtime < src.stat().st_mtime
+    dist_on = dist.is_available() and dist.is_initialized()
+    if stale and (not dist_on or dist.get_rank() == 0):
+        n, skipped = featurise_smiles_file(src, dst, add_hs=add_hs)
+        print(f"featurised {src}: {n} molecules, {skipped} skipped -> {dst}")
+    if dist_on:
+        dist.barrier()
+    return dst
 
 
 def molecules_of(shard: GraphShard, ids: Sequence[int]):

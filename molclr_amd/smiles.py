@@ -24,6 +24,12 @@ RDKit conventions restated (rdkit is unpinned in README.md:40, so this is
   kept only on bonds next to a double bond (the stereo cleanup clears the
   others).
 
+``featurise(..., add_hs=True)`` is ``Chem.AddHs`` on top (the mixed
+augmentation's input, dataset/dataset_mix.py:87-88), with RDKit's
+implicit-hydrogen rule for the organic subset (default valences B 3, C 4,
+N 3, O 2, P 3/5, S 2/4/6, halogens 1; aromatic bonds count 1.5 and an aromatic
+atom is capped at its first default valence) and the bracket H counts.
+
 Not restated: aromaticity *perception* of Kekulé input (``C1=CC=CC=C1``
 stays single/double; PubChem-10M-clean is RDKit canonical, i.e. already
 aromatic), and the removal of chirality tags from atoms that are not
@@ -70,8 +76,9 @@ def _chirality(tag: str | None) -> int:
 
 
 def parse(smiles: str):
-    """Atoms [(Z, chirality, aromatic, is_plain_H)], bonds [(begin, end, type|None, dir)]
-    (type None = unmarked) in RDKit bond order."""
+    """Atoms [(Z, chirality, aromatic, is_plain_H, bracket H count or None)],
+    bonds [(begin, end, type|None, dir)] (type None = unmarked) in RDKit bond
+    order.  The H count is None for organic-subset atoms (implicit Hs)."""
     atoms, chain, ring_bonds = [], [], []
     open_rings = {}   # ring number -> (atom, bond symbol or None, order of opening)
     closures = []     # (ring number, opening order, begin, end, symbol)
@@ -138,17 +145,18 @@ def parse(smiles: str):
             if Z is None:
                 raise ValueError(f"unknown element {sym!r}")
             plain_h = Z == 1 and iso is None
-            atoms.append((Z, _chirality(chi), arom, plain_h))
+            nh = 0 if not hs else (int(hs[1:]) if len(hs) > 1 else 1)
+            atoms.append((Z, _chirality(chi), arom, plain_h, nh))
             i = m.end()
         elif ch == "*":
             raise ValueError("dummy atom '*' (atomic number 0) is outside ATOM_LIST")
         else:
             sym = next((s for s in _ORGANIC if smiles.startswith(s, i)), None)
             if sym is not None:
-                atoms.append((Z_OF[sym], CHI_NONE, False, False))
+                atoms.append((Z_OF[sym], CHI_NONE, False, False, None))
                 i += len(sym)
             elif ch in _AROMATIC_ORGANIC:
-                atoms.append((Z_OF[ch.upper()], CHI_NONE, True, False))
+                atoms.append((Z_OF[ch.upper()], CHI_NONE, True, False, None))
                 i += 1
             else:
                 raise ValueError(f"unexpected character {ch!r} at {i}")
@@ -209,9 +217,41 @@ def _ring_bonds(n_atoms: int, bonds) -> np.ndarray:
     return on_ring
 
 
-def featurise(smiles: str):
+# RDKit's default valences of the organic subset (implicit hydrogens)
+_DEFAULT_VALENCE = {5: (3,), 6: (4,), 7: (3,), 8: (2,), 15: (3, 5), 16: (2, 4, 6), 9: (1,),
+                    17: (1,), 35: (1,), 53: (1,)}
+_BOND_ORDER = {SINGLE: 1.0, DOUBLE: 2.0, TRIPLE: 3.0, AROMATIC: 1.5}
+
+
+def _implicit_hs(Z: int, aromatic: bool, valence: float) -> int:
+    """RDKit's implicit-H count of an organic-subset atom: explicit valence
+    with aromatic bonds at 1.5 (an aromatic atom above its first default
+    valence is taken at it), rounded, then the smallest default valence that
+    is not below it minus the valence.  Above every default valence RDKit
+    rejects the molecule."""
+    allowed = _DEFAULT_VALENCE.get(Z)
+    if allowed is None:
+        raise ValueError(f"element {Z} is not in the SMILES organic subset")
+    if aromatic and valence > allowed[0]:
+        valence = float(allowed[0])
+    v = int(valence + 0.1 + 0.5)   # round(valence + 0.1), half up
+    for a in allowed:
+        if a >= v:
+            return a - v
+    raise ValueError(f"explicit valence {v} of element {Z} exceeds its default valences")
+
+
+def featurise(smiles: str, add_hs: bool = False):
     """A dataset.Molecule (x [N,2], edge_index [2,2M], edge_attr [2M,2],
-    numpy int64) with the reference's features (dataset.py:65-109)."""
+    numpy int64) with the reference's features (dataset.py:65-109).
+
+    ``add_hs`` adds the hydrogens explicitly, as ``Chem.AddHs(mol)`` does for
+    the mixed augmentation (dataset/dataset_mix.py:87-88): after the heavy
+    atoms, for every atom in order, its hydrogens (bracket count, implicit
+    count of an organic-subset atom, and the explicit ``[H]`` atoms that
+    RemoveHs folded into it) each become an atom [0, 0] (ATOM_LIST.index(1),
+    CHI_UNSPECIFIED) bonded to it by a SINGLE bond, direction NONE, begin atom
+    the heavy one, appended after the original bonds."""
     from .dataset import Molecule
     atoms, bonds = parse(smiles)
     # RemoveHs: drop plain [H] atoms that hang off another atom
@@ -221,7 +261,14 @@ def featurise(smiles: str):
         deg[b] += 1
     keep = [not (at[3] and deg[k] > 0) for k, at in enumerate(atoms)]
     remap = np.cumsum(keep) - 1
+    folded = np.zeros(len(atoms), dtype=np.int64)   # removed [H] per surviving atom
+    for a, b, _, _ in bonds:
+        if keep[a] and not keep[b]:
+            folded[a] += 1
+        if keep[b] and not keep[a]:
+            folded[b] += 1
     kept_atoms = [at for k, at in enumerate(atoms) if keep[k]]
+    folded = folded[np.asarray(keep, dtype=bool)]
     kept_bonds = [(int(remap[a]), int(remap[b]), t, d) for a, b, t, d in bonds
                   if keep[a] and keep[b]]
     if not kept_atoms:
@@ -240,12 +287,25 @@ def featurise(smiles: str):
     dbl_atoms = {x for (a, b, _, _), t in zip(kept_bonds, types) if t == DOUBLE for x in (a, b)}
     dirs = [d if (types[k] == SINGLE and (a in dbl_atoms or b in dbl_atoms)) else DIR_NONE
             for k, (a, b, _, d) in enumerate(kept_bonds)]
-    x = np.array([[Z - 1, chi] for Z, chi, _, _ in kept_atoms], dtype=np.int64).reshape(-1, 2)
-    M = len(kept_bonds)
+    xs = [[Z - 1, chi] for Z, chi, *_ in kept_atoms]
+    edges = [(a, b, types[k], dirs[k]) for k, (a, b, _, _) in enumerate(kept_bonds)]
+    if add_hs:
+        valence = np.zeros(len(kept_atoms))
+        for (a, b, _, _), t in zip(kept_bonds, types):
+            valence[a] += _BOND_ORDER[t]
+            valence[b] += _BOND_ORDER[t]
+        valence += folded  # the folded [H] atoms were single bonds
+        for k, (Z, _, ar, _, nh) in enumerate(kept_atoms):
+            h = (nh if nh is not None else _implicit_hs(Z, ar, valence[k])) + int(folded[k])
+            for _ in range(h):
+                xs.append([0, CHI_NONE])
+                edges.append((k, len(xs) - 1, SINGLE, DIR_NONE))
+    x = np.array(xs, dtype=np.int64).reshape(-1, 2)
+    M = len(edges)
     ei = np.empty((2, 2 * M), dtype=np.int64)
     ea = np.empty((2 * M, 2), dtype=np.int64)
-    for k, (a, b, _, _) in enumerate(kept_bonds):
+    for k, (a, b, t, d) in enumerate(edges):
         ei[:, 2 * k] = (a, b)
         ei[:, 2 * k + 1] = (b, a)
-        ea[2 * k] = ea[2 * k + 1] = (types[k], dirs[k])
+        ea[2 * k] = ea[2 * k + 1] = (t, d)
     return Molecule(x, ei, ea)

@@ -80,7 +80,7 @@ def _worker(rank, port, out_q):
     dR = ntxent_math.prep_bwd(drh, rh, nrm, True)
     # data sharding: disjoint, equally sized per-rank shards every epoch
     from molclr_amd.dataset import MoleculeDatasetWrapper
-    w = MoleculeDatasetWrapper(8, 0, 0.2, "synthetic:120", seed=3)
+    w = MoleculeDatasetWrapper(8, 0, 0.2, "synthetic:120", seed=3, views="host")
     tr, va = w.get_data_loaders()
     ids = []
     for epoch in range(2):

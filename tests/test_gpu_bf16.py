@@ -163,7 +163,7 @@ def test_bf16_aggregation_atom_pool_bit_exact(dev):
     xi = b.x.to(dev)
     hb2 = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
     assert lib.molclr_atom_embed_fwd_bf16(xi.data_ptr(), X1.data_ptr(), X2.data_ptr(),
-                                          hb2.data_ptr(), N, D, 119, 3, None) == 0
+                                          hb2.data_ptr(), N, D, 119, 3, None, None) == 0
     assert torch.equal(hb2, bf(X1[xi[:, 0]] + X2[xi[:, 1]]))
     wsa = lib.molclr_atom_embed_bwd_workspace_bytes(N, D, 119, 3)
     wa = torch.empty(wsa, dtype=torch.uint8, device=dev)
