@@ -234,18 +234,6 @@ int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32
                               const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
                               float* out, int64_t num_nodes, int64_t dim,
                               molclr_stream_t stream);
-/* molclr_gine_aggregate_fwd over x = BatchNorm(z) (+ReLU), the normalised
- * output applied per gathered element instead of materialised: x[i][c] =
- * max?(z[i][c] * sc[c] + sh[c]) with sc = gamma * invstd, sh = beta - mean * sc
- * -- the expression molclr_batchnorm_fwd applies, so the sums are identical to
- * molclr_batchnorm_fwd followed by molclr_gine_aggregate_fwd.  mean / invstd
- * are molclr_batchnorm_fwd's save_mean / save_invstd (gamma / beta may be NULL:
- * 1 / 0). */
-int molclr_gine_aggregate_bn_fwd(const float* z, const float* mean, const float* invstd,
-                                 const float* gamma, const float* beta, int relu,
-                                 const int32_t* rowptr, const int32_t* col, const uint8_t* ecode,
-                                 const uint32_t* nbr, const float* Ec, float* out,
-                                 int64_t num_nodes, int64_t dim, molclr_stream_t stream);
 /* Backward: dx[j] = Σ_{k in out(j), edge order} g[dst_k] + g[j];
  * dE1[t] = Σ_i ecount[i][t] g[i], dE2[d] = Σ_i ecount[i][5+d] g[i].
  * dx may be NULL (first layer input needs no grad); dE1/dE2 may be NULL. */
@@ -454,8 +442,7 @@ int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64_t cols, in
  * training == 0: running statistics are used and nothing is updated.
  * relu != 0 applies max(y, 0) to the output.  y may be NULL: the statistics
  * (save_mean / save_invstd, running stats) are computed and the normalised
- * output is not written -- for a consumer that applies it on the fly
- * (molclr_gine_aggregate_bn_fwd). */
+ * output is not written. */
 size_t molclr_batchnorm_workspace_bytes(int64_t rows, int64_t dim);
 int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,
                          float* running_mean, float* running_var,

@@ -41,8 +41,6 @@ SIGNATURES = {
                                       _P]),
     "molclr_edge_tables_combine": (c_int, [c_int, _P, _P, _P, _I64, _P]),
     "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
-    "molclr_gine_aggregate_bn_fwd": (c_int, [_P, _P, _P, _P, _P, c_int, _P, _P, _P, _P, _P, _P,
-                                             _I64, _I64, _P]),
     "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
                                           c_size_t, _P]),

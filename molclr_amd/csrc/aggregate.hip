@@ -302,52 +302,17 @@ __device__ __forceinline__ float4 gine_msg(const float4* __restrict__ x, const f
 // costs two dependent memory latencies (slots, then features).  Rows of
 // higher degree walk the CSR.  Order of the adds: in-edges in edge order,
 // self loop last — the reference's, so the sums are bit-identical.
-// BN (+ReLU) of a gathered element: molclr_batchnorm_fwd's bn_coeffs / k_bn_apply
-// expression (z * sc + sh, then max(., 0)), so values match a materialised output
-struct BnIn {
-  float4 sc, sh;
-  bool relu;
-  __device__ __forceinline__ float4 operator()(float4 v) const {
-    float4 o = make_float4(__fmaf_rn(v.x, sc.x, sh.x), __fmaf_rn(v.y, sc.y, sh.y),
-                           __fmaf_rn(v.z, sc.z, sh.z), __fmaf_rn(v.w, sc.w, sh.w));
-    if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
-    return o;
-  }
-};
-__device__ __forceinline__ float bn_scale1(float g, float is) { return g * is; }
-__device__ __forceinline__ float bn_shift1(float b, float m, float sc) { return __fmaf_rn(-m, sc, b); }
-
-// BN = true: x holds z, and every x element read goes through BatchNorm
-// (+ReLU) first (molclr_gine_aggregate_bn_fwd); the adds are unchanged.
-template <bool BN, typename St = StF32>
+template <typename St = StF32>
 __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     const typename St::T* __restrict__ x, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
     const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
-    int64_t N, int d4, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ gamma, const float* __restrict__ beta, int relu) {
+    int64_t N, int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
-  BnIn bn;
-  if constexpr (BN) {
-    const float4 mu = reinterpret_cast<const float4*>(mean)[c];
-    const float4 is = reinterpret_cast<const float4*>(invstd)[c];
-    const float4 g = gamma ? reinterpret_cast<const float4*>(gamma)[c]
-                           : make_float4(1.f, 1.f, 1.f, 1.f);
-    const float4 b = beta ? reinterpret_cast<const float4*>(beta)[c] : f4zero();
-    bn.sc = make_float4(bn_scale1(g.x, is.x), bn_scale1(g.y, is.y), bn_scale1(g.z, is.z),
-                        bn_scale1(g.w, is.w));
-    bn.sh = make_float4(bn_shift1(b.x, mu.x, bn.sc.x), bn_shift1(b.y, mu.y, bn.sc.y),
-                        bn_shift1(b.z, mu.z, bn.sc.z), bn_shift1(b.w, mu.w, bn.sc.w));
-    bn.relu = relu != 0;
-  }
-  auto X = [&](int64_t idx) {
-    const float4 v = St::ld(x, idx);
-    if constexpr (BN) return bn(v);
-    return v;
-  };
+  auto X = [&](int64_t idx) { return St::ld(x, idx); };
   auto msg = [&](uint32_t w) {
     return f4add(X((int64_t)nbr_node(w) * d4 + c), Ec[nbr_ecomb(w) * d4 + c]);
   };
@@ -376,7 +341,7 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
 // dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC).
 // Unlike the forward, the self row is read last and the gathers stay in
 // branches: measured 14.0 us against 17.3 us for the forward's structure here
-// (tools/agg_bench.py transpose).
+// (round 1, unpaired c2 launch).
 template <typename St = StF32>
 __global__ __launch_bounds__(kT) void k_transpose_gather(const typename St::T* __restrict__ g,
                                                          const int32_t* __restrict__ rowptr_t,
@@ -815,31 +780,9 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
-  const float* nf = nullptr;
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StF32>,
+  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<StF32>,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, nf,
-                       nf, nf, nf, 0);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
-}
-
-MOLCLR_API int molclr_gine_aggregate_bn_fwd(const float* z, const float* mean,
-                                            const float* invstd, const float* gamma,
-                                            const float* beta, int relu, const int32_t* rowptr,
-                                            const int32_t* col, const uint8_t* ecode,
-                                            const uint32_t* nbr, const float* Ec, float* out,
-                                            int64_t N, int64_t D, molclr_stream_t stream) {
-  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_bn_fwd: dim %lld must be a multiple of 4",
-                 (long long)D);
-  if (N == 0) return MOLCLR_OK;
-  MOLCLR_REQUIRE(z && mean && invstd && rowptr && nbr && Ec && out,
-                 "gine_aggregate_bn_fwd: null pointer");
-  int d4 = (int)(D / 4);
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<true, StF32>,
-                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       z, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4, mean,
-                       invstd, gamma, beta, relu);
+                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -979,11 +922,9 @@ MOLCLR_API int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* 
                          (const uint4*)nbr, (const float4*)Ec, out, N, d8);
   } else {
     const int d4 = (int)(D / 4);
-    const float* nf = nullptr;
-    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<false, StBF16>,
+    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<StBF16>,
                          dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                         x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
-                         nf, nf, nf, nf, 0);
+                         x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4);
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;

@@ -200,7 +200,7 @@ __global__ void k_bn_stats_partial(const typename St::T* __restrict__ z, int d4,
 __device__ __forceinline__ void bn_coeffs(float gamma, float beta, float mean, float invstd,
                                           float& scale, float& shift) {
   scale = gamma * invstd;
-  shift = __fmaf_rn(-mean, scale, beta);  // explicit: molclr_gine_aggregate_bn_fwd repeats it
+  shift = __fmaf_rn(-mean, scale, beta);
 }
 
 __device__ __forceinline__ void chan1(float& n, float& mean, float& m2, float nb, float mb, float qb) {

@@ -444,13 +444,14 @@ constexpr int64_t kBwdWaves = 1024;
 
 namespace {
 
-// workspace of the GEMM formulation: the column planes, S / W, and the two
-// GEMMs' split-K space
+// workspace of the GEMM formulation: the column planes, S / W, and both
+// GEMMs' split-K space side by side (the backward without a kept S takes the
+// similarity GEMM's and then the dR GEMM's from one workspace)
 size_t ntx_gemm_ws(int64_t nrows, int64_t ncols, int64_t C) {
   size_t g1 = molclr_gemm_f32_workspace_bytes(nrows, ncols, C);
   size_t g2 = molclr_gemm_f32_workspace_bytes(nrows, C, ncols);
-  return molclr_bplanes_bytes(ncols, C) + (size_t)nrows * ncols * sizeof(float) +
-         (g1 > g2 ? g1 : g2) + 3 * 256;
+  return molclr_bplanes_bytes(ncols, C) + (size_t)nrows * ncols * sizeof(float) + g1 + g2 +
+         4 * 256;
 }
 // automatic choice: the GEMM formulation once S has >= 2^20 elements (c2's
 // 1024 x 1024 and up), the fused kernels below that
@@ -469,6 +470,10 @@ int ntx_similarity(const float* rows, const float* cols, int64_t nrows, int64_t 
   if (sim) S = sim;
   const size_t gws = molclr_gemm_f32_workspace_bytes(nrows, ncols, C);
   void* g = w.take<char>(gws);
+  if (!w.ok()) {
+    molclr::set_error("ntxent: workspace too small");
+    return MOLCLR_ERR_WORKSPACE;
+  }
   int rc = molclr_bplanes_make(cols, ncols, C, C, 0, planes, s);
   if (rc) return rc;
   rc = molclr_gemm_f32_bplanes(rows, planes, S, nrows, ncols, C, C, ncols, 0, MOLCLR_EPI_NONE,
@@ -578,6 +583,10 @@ MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, co
     // dR[r][k] = Σ_c W[r][c] cols[c][k]: A = W (row-major, K = ncols), B = cols ([K][N])
     const size_t gws = molclr_gemm_f32_workspace_bytes(nrows, C, ncols);
     void* g = w.take<char>(gws);
+    if (!w.ok()) {
+      molclr::set_error("ntxent_bwd: workspace too small");
+      return MOLCLR_ERR_WORKSPACE;
+    }
     {
       molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
       rc = molclr_gemm_f32(W, cols, drows, nrows, C, ncols, ncols, C, C, 0, 1, MOLCLR_EPI_NONE,

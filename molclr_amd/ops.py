@@ -211,9 +211,11 @@ def weight_planes(W, N, K, ldb, b_kmajor, kind: str = "x6") -> torch.Tensor:
         ent = _PLANES.get(key)
         if ent is not None and ent[0] == (W._version, gen):
             return ent[3]
-    if len(_PLANES) > 512:  # drop entries of dead tensors
-        for k in [k for k, e in _PLANES.items() if e[1]() is None]:
-            del _PLANES[k]
+    # drop entries of dead tensors on every insert: a padded weight (emb_dim
+    # not a multiple of the kernels' width) is a new tensor each call, and its
+    # planes must not stay pinned in HBM
+    for k in [k for k, e in _PLANES.items() if e[1]() is None]:
+        del _PLANES[k]
     nbytes = _wsq(_PLANE_FNS[kind][0], N, K)
     planes = torch.empty(nbytes // 2, dtype=torch.int16, device=W.device)
     _make_planes(kind, [(W, (N, K, ldb, int(b_kmajor)), planes)])

@@ -522,6 +522,53 @@ def test_ntxent_large_vs_oracle(dev, B, C):
     assert rel(zis.grad, dzi_ref) < TOL and rel(zjs.grad, dzj_ref) < TOL
 
 
+@pytest.mark.parametrize("B,C", [(512, 512), (512, 256)])
+def test_ntxent_bwd_without_kept_similarity(dev, B, C):
+    """The public molclr_ntxent_bwd (sim = NULL: S recomputed inside, both
+    GEMMs' split-K space from one workspace of molclr_ntxent_workspace_bytes)
+    against the backward that reuses the forward's S, and the fp64 oracle.
+    C = 512 makes both GEMMs split K (the workspace overflowed)."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(C)
+    z = rng.standard_normal((2 * B, C)).astype(np.float32)
+    z /= np.linalg.norm(z, axis=1, keepdims=True)
+    R = torch.from_numpy(z).to(dev)
+    n = 2 * B
+    gidx = torch.arange(n, dtype=torch.int32, device=dev)
+    lse, lossr = torch.empty(n, device=dev), torch.empty(n, device=dev)
+    wsb = lib.molclr_ntxent_workspace_bytes(n, n, C)
+    # guard bytes after the workspace catch an overflow
+    ws = torch.full((wsb + 4096,), 0x5A, dtype=torch.uint8, device=dev)
+    simb = lib.molclr_ntxent_sim_bytes(n, n, C, -1)
+    assert simb > 0
+    sim = torch.empty(simb // 4, device=dev)
+    st = _lib.stream_of(dev)
+    assert lib.molclr_ntxent_fwd_impl(R.data_ptr(), gidx.data_ptr(), R.data_ptr(), n, n, C, B,
+                                      0.1, lse.data_ptr(), lossr.data_ptr(), sim.data_ptr(),
+                                      ws.data_ptr(), wsb, st, -1) == 0
+    g = torch.ones(1, device=dev)
+    d_kept, d_pub = torch.empty_like(R), torch.empty_like(R)
+    assert lib.molclr_ntxent_bwd_impl(R.data_ptr(), gidx.data_ptr(), R.data_ptr(), lse.data_ptr(),
+                                      g.data_ptr(), n, n, C, B, 0.1, sim.data_ptr(),
+                                      d_kept.data_ptr(), ws.data_ptr(), wsb, st, -1) == 0
+    assert lib.molclr_ntxent_bwd(R.data_ptr(), gidx.data_ptr(), R.data_ptr(), lse.data_ptr(),
+                                 g.data_ptr(), n, n, C, B, 0.1, d_pub.data_ptr(), ws.data_ptr(),
+                                 wsb, st) == 0
+    torch.cuda.synchronize()
+    assert (ws[wsb:] == 0x5A).all(), "molclr_ntxent_bwd wrote past its workspace"
+    assert torch.equal(d_pub, d_kept)
+    z64 = z.astype(np.float64)
+    gi = np.arange(n)
+    lse_ref, lr_ref = ntxent_math.rows_forward(z64, gi, z64, B, 0.1)
+    assert abs(lossr.sum().item() - lr_ref.sum()) <= TOL * abs(lr_ref.sum())
+    assert rel(d_pub, ntxent_math.rows_backward(z64, gi, z64, lse_ref, B, 0.1)) < TOL
+    # a workspace one byte short is refused, not overrun
+    assert lib.molclr_ntxent_bwd(R.data_ptr(), gidx.data_ptr(), R.data_ptr(), lse.data_ptr(),
+                                 g.data_ptr(), n, n, C, B, 0.1, d_pub.data_ptr(), ws.data_ptr(),
+                                 wsb - 1, st) != 0
+
+
 def test_ntxent_matches_reference_module_at_b512(dev):
     """Full reference formulation (broadcast cosine + mask + CE) at the c2 batch."""
     from molclr_amd.nt_xent import NTXentLoss
@@ -573,53 +620,6 @@ def test_fused_adam_matches_torch_adam(dev):
         d = (a.detach() - c.detach()).abs().max().item()
         assert d <= 32 * torch.finfo(torch.float32).eps * c.detach().abs().max().item(), d
     assert o_mine.steps_taken == 20
-
-
-@pytest.mark.parametrize("training,relu,D", [(1, 1, 300), (1, 0, 128), (0, 1, 300)])
-def test_gine_aggregate_bn_fwd_matches_materialised(dev, training, relu, D):
-    """molclr_gine_aggregate_bn_fwd(z) == molclr_gine_aggregate_fwd(BatchNorm(z)),
-    bit for bit (the executor's fused path)."""
-    from molclr_amd import _lib
-    lib = _lib.load()
-    b = batch(96, 4)
-    g = dgraph(b, dev)
-    N = b.x.shape[0]
-    torch.manual_seed(D + relu)
-    z = (torch.randn(N, D) * 3 + 1).to(dev)
-    gamma = torch.randn(D).to(dev)
-    beta = torch.randn(D).to(dev)
-    rm, rv = torch.randn(D).to(dev), (torch.rand(D) + 0.5).to(dev)
-    y = torch.empty(N, D, device=dev)
-    mean, invstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
-    wsb = lib.molclr_batchnorm_workspace_bytes(N, D)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    assert lib.molclr_batchnorm_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(), rm.data_ptr(),
-                                    rv.data_ptr(), None, y.data_ptr(), mean.data_ptr(),
-                                    invstd.data_ptr(), N, D, 0.1, 1e-5, training, relu,
-                                    ws.data_ptr(), wsb, None) == 0
-    Ec = torch.randn(15, D).to(dev)
-    ref = torch.empty(N, D, device=dev)
-    out = torch.empty(N, D, device=dev)
-    assert lib.molclr_gine_aggregate_fwd(y.data_ptr(), g.rowptr.data_ptr(), g.col.data_ptr(),
-                                         g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
-                                         ref.data_ptr(), N, D, None) == 0
-    assert lib.molclr_gine_aggregate_bn_fwd(z.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
-                                            gamma.data_ptr(), beta.data_ptr(), relu,
-                                            g.rowptr.data_ptr(), g.col.data_ptr(),
-                                            g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
-                                            out.data_ptr(), N, D, None) == 0
-    torch.cuda.synchronize()
-    assert torch.equal(out, ref)
-    # statistics only (y = NULL) gives the same saved statistics
-    m2, i2 = torch.empty(D, device=dev), torch.empty(D, device=dev)
-    rm2, rv2 = torch.randn(D).to(dev), (torch.rand(D) + 0.5).to(dev)
-    if not training:
-        rm2, rv2 = rm, rv
-    assert lib.molclr_batchnorm_fwd(z.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
-                                    rm2.data_ptr(), rv2.data_ptr(), None, None, m2.data_ptr(),
-                                    i2.data_ptr(), N, D, 0.1, 1e-5, training, relu,
-                                    ws.data_ptr(), wsb, None) == 0
-    assert torch.equal(m2, mean) and torch.equal(i2, invstd)
 
 
 # ---------------------------------------------------------------------------
