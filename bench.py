@@ -101,7 +101,14 @@ def log(rank, *a):
 
 
 def cpu_baseline(cfg, batches_cpu, steps):
-    """Oracle step (reference restatement) timed on this host's cores."""
+    """Oracle step (reference restatement) timed on this host's cores, with its
+    calibration against the survey's timing of the reference modules
+    (tools/cpu_calibrate.py): the reference's own
+    NT-Xent (utils/nt_xent.py, restated op for op and pinned by the goldens)
+    is timed alone on the same host, and the step / NT-Xent ratio is compared
+    with the survey's (c2: 3.8-4.2 s / 2.6-3.2 s = 1.19-1.62; c3 0.91-1.38).  A host slower
+    than the survey's container scales both; the ratio says whether the
+    restatement costs what the reference does."""
     import torch
 
     from oracle.reference_cpu import RefGCN, RefGINet, RefNTXentLoss, ref_train_step
@@ -119,10 +126,36 @@ def cpu_baseline(cfg, batches_cpu, steps):
         ref_train_step(model, crit, opt, xi, xj)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times[1:])
-    return {"value": round(cfg["batch"] / med, 2), "unit": "molecules/s", "cores": threads,
-            "kind": "port", "ms_per_step": round(med * 1e3, 1),
-            "sample": f"{steps} steps (+1 warm-up) of {cfg['desc']}, oracle/reference_cpu.py, "
-                      f"torch CPU fp32, {threads} threads, median step"}
+    out = {"value": round(cfg["batch"] / med, 2), "unit": "molecules/s", "cores": threads,
+           "kind": "port", "ms_per_step": round(med * 1e3, 1),
+           "sample": f"{steps} steps (+1 warm-up) of {cfg['desc']}, oracle/reference_cpu.py, "
+                     f"torch CPU fp32, {threads} threads, median step"}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                out["cpu_model"] = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    if cfg["batch"] == 512:
+        nt = []
+        for _ in range(2):
+            zi = torch.nn.functional.normalize(torch.randn(512, 256), dim=1).requires_grad_(True)
+            zj = torch.nn.functional.normalize(torch.randn(512, 256), dim=1).requires_grad_(True)
+            t0 = time.perf_counter()
+            crit(zi, zj).backward()
+            nt.append(time.perf_counter() - t0)
+        ntx = min(nt)
+        out["calibration"] = {
+            "ntxent_fwd_bwd_ms": round(ntx * 1e3, 1),
+            "step_over_ntxent": round(med / ntx, 3),
+            "survey_step_over_ntxent": {"c2": [1.19, 1.62], "c3": [0.91, 1.38]}.get(
+                cfg["desc"][:2]),
+            "survey_ms_per_step": {"c2": [3800, 4200], "c3": [2900, 3600]}.get(
+                cfg["desc"][:2]),
+            "note": "survey timings: the reference modules on the 8-core build container; "
+                    "tools/cpu_calibrate.py there gave c2 4844 ms / NT-Xent 3688 ms = 1.31"}
+    return out
 
 
 def split_ceiling(tfs, model_type) -> dict:

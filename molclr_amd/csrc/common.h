@@ -17,6 +17,21 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
 inline hipStream_t as_stream(molclr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Compute units of the current device (cached per device): the grid of a
+// persistent kernel.
+inline int cu_count() {
+  static int cached[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

@@ -1199,19 +1199,9 @@ int launch_tb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
 #undef MOLCLR_TB
 }
 
-// one persistent k_gemm_tp block per CU (160 KB of LDS: one block fits)
-int cu_count() {
-  static int cached[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
+// one persistent k_gemm_tp block per CU (160 KB of LDS: one block fits):
+// molclr::cu_count()
+using molclr::cu_count;
 
 template <int NW>
 int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,

@@ -83,51 +83,63 @@ __global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
 }
 
 // Exclusive scan of deg[0..n) into ptr[0..n]; blockIdx.x selects one of two
-// arrays.  Tiles of 1024 elements (coalesced), 8 tiles' loads in flight per
-// thread, block-wide scan per tile with a running carry.
+// arrays.  Tiles of 1024 x 8 elements: the tile is loaded coalesced (8 loads in
+// flight per thread) into LDS, each thread sums 8 consecutive elements, one
+// block-wide scan of the 1024 thread sums (wave scans + a scan of the 16 wave
+// totals), then each thread writes its 8 prefixes: three barriers per tile
+// (the per-1024-element scan it replaces took three per 1024 elements).
+constexpr int kScanPer = 8;
 __global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ degA,
                                                         int32_t* __restrict__ ptrA,
                                                         const int32_t* __restrict__ degB,
                                                         int32_t* __restrict__ ptrB, int64_t n) {
-  constexpr int CH = 8;
+  constexpr int TILE = kScanPer * kScanThreads;
   const int32_t* deg = blockIdx.x == 0 ? degA : degB;
   int32_t* ptr = blockIdx.x == 0 ? ptrA : ptrB;
+  __shared__ int32_t tile[TILE];
   __shared__ int32_t wsum[kScanThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int32_t carry = 0;
-  for (int64_t base = 0; base < n; base += (int64_t)CH * kScanThreads) {
-    int32_t v[CH];
+  for (int64_t base = 0; base < n; base += TILE) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      int64_t idx = base + (int64_t)c * kScanThreads + tid;
-      v[c] = idx < n ? deg[idx] : 0;
+    for (int c = 0; c < kScanPer; ++c) {
+      const int64_t idx = base + (int64_t)c * kScanThreads + tid;
+      tile[c * kScanThreads + tid] = idx < n ? deg[idx] : 0;
     }
+    __syncthreads();
+    int32_t v[kScanPer], x = 0;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      int32_t x = v[c];
+    for (int j = 0; j < kScanPer; ++j) {
+      v[j] = tile[kScanPer * tid + j];
+      x += v[j];
+    }
+    const int32_t own = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t u = __shfl_up(x, o, 64);
+      if (lane >= o) x += u;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+      int32_t w = lane < kScanThreads / 64 ? wsum[lane] : 0;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
-        int32_t u = __shfl_up(x, o, 64);
-        if (lane >= o) x += u;
+        const int32_t u = __shfl_up(w, o, 64);
+        if (lane >= o) w += u;
       }
-      if (lane == 63) wsum[wid] = x;
-      __syncthreads();
-      if (wid == 0) {
-        int32_t w = lane < kScanThreads / 64 ? wsum[lane] : 0;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          int32_t u = __shfl_up(w, o, 64);
-          if (lane >= o) w += u;
-        }
-        if (lane < kScanThreads / 64) wsum[lane] = w;
-      }
-      __syncthreads();
-      const int32_t before = (wid > 0 ? wsum[wid - 1] : 0) + x - v[c];
-      const int64_t idx = base + (int64_t)c * kScanThreads + tid;
-      if (idx < n) ptr[idx] = carry + before;
-      carry += wsum[kScanThreads / 64 - 1];
-      __syncthreads();
+      if (lane < kScanThreads / 64) wsum[lane] = w;
     }
+    __syncthreads();
+    int32_t run = carry + (wid > 0 ? wsum[wid - 1] : 0) + x - own;
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j) {
+      const int64_t idx = base + (int64_t)kScanPer * tid + j;
+      if (idx < n) ptr[idx] = run;
+      run += v[j];
+    }
+    carry += wsum[kScanThreads / 64 - 1];
+    __syncthreads();  // tile and wsum are rewritten by the next tile
   }
   if (tid == 0) ptr[n] = carry;
 }

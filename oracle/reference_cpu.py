@@ -21,6 +21,13 @@ models/ginet_molclr.py:16-117 and models/gcn_molclr.py:27-158 so that the same
 CosineSimilarity that materialises a (2B, 2B, C) tensor — that is the
 reference's CPU cost, which the bench's ``cpu_baseline`` leg measures.
 
+``RefGINet(..., emulate_bf16=True)`` is the same model with the HIP bf16
+path's storage points (the c5 configuration, include/molclr.h "bf16
+storage"): node features, aggregation outputs, MLP activations, BatchNorm
+inputs and outputs and their gradients are rounded to bf16 where the kernels
+store them, and the MLP weights enter their products as bf16; everything in
+between stays in the oracle's precision (the kernels accumulate in fp32).
+
 Parity status: the NT-Xent restatement is pinned by golden vectors produced
 by importing the reference's own utils/nt_xent.py (tests/golden/).  The
 encoder restatement cannot be pinned by reference outputs (the reference
@@ -98,6 +105,44 @@ def global_max_pool(h: torch.Tensor, batch: torch.Tensor, size: int | None = Non
 
 
 # ---------------------------------------------------------------------------
+# bf16 storage points of the HIP c5 path (emulate_bf16)
+# ---------------------------------------------------------------------------
+def _to_bf16(t: torch.Tensor) -> torch.Tensor:
+    """Round to the nearest bf16 (even on ties), via fp32 as the kernels do."""
+    return t.float().to(torch.bfloat16).to(t.dtype)
+
+
+class _StoreBF16(torch.autograd.Function):
+    """A tensor the kernels store in bf16: the value rounded in the forward,
+    its gradient (also stored in bf16 by the backward kernels) in the backward."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _to_bf16(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _to_bf16(g)
+
+
+class _OperandBF16(torch.autograd.Function):
+    """A weight used as a bf16 GEMM operand (the fp32 master is rounded; its
+    gradient is fp32)."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return _to_bf16(w)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+def _identity(t):
+    return t
+
+
+# ---------------------------------------------------------------------------
 # models/ginet_molclr.py
 # ---------------------------------------------------------------------------
 class RefGINEConv(nn.Module):
@@ -119,12 +164,19 @@ class RefGINEConv(nn.Module):
         edge_attr = torch.cat((edge_attr, self_loop_attr), dim=0)
         edge_embeddings = self.edge_embedding1(edge_attr[:, 0]) + self.edge_embedding2(edge_attr[:, 1])
         aggr = propagate_add(x, edge_index, N, lambda x_j: x_j + edge_embeddings)  # :43-44
-        return self.mlp(aggr)                                          # :46-47
+        if not getattr(self, "emulate_bf16", False):
+            return self.mlp(aggr)                                      # :46-47
+        st, op = _StoreBF16.apply, _OperandBF16.apply
+        lin1, lin2 = self.mlp[0], self.mlp[2]
+        a1 = st(F.relu(F.linear(st(aggr), op(lin1.weight), lin1.bias)))
+        return st(F.linear(a1, op(lin2.weight), lin2.bias))
 
 
 class RefGINet(nn.Module):
-    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean'):
+    def __init__(self, num_layer=5, emb_dim=300, feat_dim=256, drop_ratio=0, pool='mean',
+                 emulate_bf16=False):
         super().__init__()
+        self.emulate_bf16 = emulate_bf16
         self.num_layer = num_layer
         self.emb_dim = emb_dim
         self.feat_dim = feat_dim
@@ -134,6 +186,8 @@ class RefGINet(nn.Module):
         nn.init.xavier_uniform_(self.x_embedding1.weight.data)
         nn.init.xavier_uniform_(self.x_embedding2.weight.data)
         self.gnns = nn.ModuleList([RefGINEConv(emb_dim) for _ in range(num_layer)])
+        for g in self.gnns:
+            g.emulate_bf16 = emulate_bf16
         self.batch_norms = nn.ModuleList([nn.BatchNorm1d(emb_dim) for _ in range(num_layer)])
         self.pool = {'mean': global_mean_pool, 'add': global_add_pool,
                      'max': global_max_pool}[pool]                      # ginet_molclr.py:83-88
@@ -142,8 +196,9 @@ class RefGINet(nn.Module):
                                      nn.Linear(self.feat_dim, self.feat_dim // 2))
 
     def forward(self, data):                                          # ginet_molclr.py:98-117
+        st = _StoreBF16.apply if getattr(self, "emulate_bf16", False) else _identity
         x, edge_index, edge_attr = data.x, data.edge_index, data.edge_attr
-        h = self.x_embedding1(x[:, 0]) + self.x_embedding2(x[:, 1])
+        h = st(self.x_embedding1(x[:, 0]) + self.x_embedding2(x[:, 1]))
         for layer in range(self.num_layer):
             h = self.gnns[layer](h, edge_index, edge_attr)
             h = self.batch_norms[layer](h)
@@ -151,6 +206,7 @@ class RefGINet(nn.Module):
                 h = F.dropout(h, self.drop_ratio, training=self.training)
             else:
                 h = F.dropout(F.relu(h), self.drop_ratio, training=self.training)
+            h = st(h)
         h = self.pool(h, data.batch)
         h = self.feat_lin(h)
         out = self.out_lin(h)

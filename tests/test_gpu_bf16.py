@@ -273,6 +273,115 @@ def test_ginet_bf16_vs_fp64_reference(dev, L, D, B):
             assert rel(mb, buf) < BF16_TOL["h"], name
 
 
+EMU_TOL = 1e-2  # vs the oracle that rounds where the kernels store bf16
+
+
+def _emu_models(L, D, seed=7):
+    from molclr_amd.ginet_molclr import GINet
+    from oracle.reference_cpu import RefGINet
+    torch.manual_seed(seed)
+    emu = RefGINet(L, D, 512, emulate_bf16=True)
+    mine = GINet(L, D, 512, precision="bf16")
+    mine.load_state_dict(emu.state_dict())
+    return emu, mine
+
+
+@pytest.mark.parametrize("L,D,B", [(5, 512, 256), (3, 128, 64)])
+def test_ginet_bf16_encoder_vs_bf16_emulating_oracle(dev, L, D, B):
+    """The c5 encoder arithmetic against oracle/reference_cpu.py with
+    emulate_bf16: the same rounding points as the HIP bf16 path (node
+    features, aggregation outputs, MLP activations, BatchNorm in/outputs and
+    the gradients of all of them stored as bf16; bf16 weight operands), fp64
+    everywhere else.  What remains is the kernels' fp32 accumulation and the
+    elements whose bf16 rounding an fp32 vs fp64 sum flips (one bf16 ulp
+    each).  Both views through the paired pass, backward of a fixed random
+    functional of the node embeddings.  Node embeddings and BatchNorm running
+    statistics within 1e-2 norm-wise.  The parameter gradients are sensitive
+    to those one-ulp flips (BatchNorm's backward projects them out of a
+    gradient that is largely mean / x_hat-aligned): the SAME emulation run in
+    fp32 instead of fp64 moves them by 3-4e-2 at L=3 and ~0.12 at L=5, so
+    each gradient is held to 1e-2 or 1.5x that self-noise, whichever is
+    larger (measured: 2.4e-2 at L=3, vs 4.1e-2 self-noise)."""
+    from oracle.reference_cpu import _StoreBF16
+    emu32, mine = _emu_models(L, D)
+    emu64 = copy.deepcopy(emu32).double()
+    mine = mine.to(dev)
+    xi, xj = SyntheticPairBatches(B, seed=3, shape="pubchem").next()
+    g = torch.Generator().manual_seed(1)
+    refs = []
+    for emu in (emu64, emu32):
+        hs = []
+        for x in (xi, xj):  # the oracle's encoder: ginet_molclr.py:103-111, per view
+            h = _StoreBF16.apply(emu.x_embedding1(x.x[:, 0]) + emu.x_embedding2(x.x[:, 1]))
+            for layer in range(L):
+                h = emu.batch_norms[layer](emu.gnns[layer](h, x.edge_index, x.edge_attr))
+                h = _StoreBF16.apply(h if layer == L - 1 else torch.relu(h))
+            hs.append(h)
+        refs.append(torch.cat(hs))
+    w = torch.randn(refs[0].shape, generator=g, dtype=torch.float64)
+    (refs[0] * w).sum().backward()
+    (refs[1] * w.float()).sum().backward()
+    from molclr_amd.data import pair_graph
+    xi_d, xj_d = xi.to(dev), xj.to(dev)
+    h = mine._run_encoder(torch.cat([xi_d.x, xj_d.x]), pair_graph(xi_d, xj_d))
+    (h.float() * w.float().to(dev)).sum().backward()
+    assert rel(h, refs[0]) < EMU_TOL
+    g64, g32 = dict(emu64.named_parameters()), dict(emu32.named_parameters())
+    checked, bad = 0, {}
+    for n, p in mine.named_parameters():
+        if p.grad is None or n.endswith("mlp.2.bias"):  # pre-BN bias: exact gradient 0
+            continue
+        checked += 1
+        e, e32 = rel(p.grad, g64[n].grad), rel(g32[n].grad, g64[n].grad)
+        if e > max(EMU_TOL, 1.5 * e32) or e > BF16_TOL["grad"]:
+            bad[n] = (e, e32)
+    assert checked == 2 + 7 * L and not bad, bad
+    for name, buf in emu64.named_buffers():
+        if not name.endswith("num_batches_tracked"):
+            assert rel(dict(mine.named_buffers())[name], buf) < EMU_TOL, name
+
+
+@pytest.mark.parametrize("L,D,B", [(5, 512, 256), (3, 128, 64)])
+def test_ginet_bf16_step_vs_bf16_emulating_oracle(dev, L, D, B):
+    """The whole c5 step (paired pass, heads, NT-Xent) against the emulating
+    oracle: h, out and the loss within 1e-2.  The step's parameter gradients
+    at random init are ill-conditioned (the projections are nearly parallel:
+    NT-Xent's gradient is a small difference of large terms), so one-ulp bf16
+    rounding differences are amplified; each gradient is held to twice what
+    the SAME emulation run in fp32 instead of fp64 moves (its own conditioning
+    at these rounding points), and to 0.35 as before."""
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from oracle.reference_cpu import RefNTXentLoss
+    emu32, mine = _emu_models(L, D)
+    emu64 = copy.deepcopy(emu32).double()
+    mine = mine.to(dev)
+    xi, xj = SyntheticPairBatches(B, seed=3, shape="pubchem").next()
+    outs = []
+    for m in (emu64, emu32):
+        hi, zi = m(xi)
+        hj, zj = m(xj)
+        loss = RefNTXentLoss("cpu", B, 0.1, True)(torch.nn.functional.normalize(zi, dim=1),
+                                                  torch.nn.functional.normalize(zj, dim=1))
+        loss.backward()
+        outs.append((torch.cat([hi, hj]), torch.cat([zi, zj]), loss))
+    hp, op = mine.forward_pair(xi.to(dev), xj.to(dev))
+    lm = NTXentLoss(dev, B, 0.1, True).forward_pair(l2_normalize(op))
+    lm.backward()
+    h64, o64, l64 = outs[0]
+    assert rel(hp, h64) < EMU_TOL and rel(op, o64) < EMU_TOL
+    assert abs(lm.item() - l64.item()) / abs(l64.item()) < EMU_TOL
+    g64, g32 = dict(emu64.named_parameters()), dict(emu32.named_parameters())
+    bad = {}
+    for n, p in mine.named_parameters():
+        if n.endswith("mlp.2.bias"):  # exact gradient 0: rounding noise on every side
+            continue
+        e, e32 = rel(p.grad, g64[n].grad), rel(g32[n].grad, g64[n].grad)
+        if e > max(EMU_TOL, 2 * e32) or e > BF16_TOL["grad"]:
+            bad[n] = (e, e32)
+    assert not bad, bad
+
+
 def test_ginet_bf16_training_step_runs_and_is_deterministic(dev):
     from molclr_amd.ginet_molclr import GINet
     from molclr_amd.nt_xent import NTXentLoss

@@ -48,9 +48,18 @@ def check_grads(mine, ref64, err32=None, tol=TOL, record=None):
     """Gradient parity against the oracle evaluated in fp64 (the exact result
     of the reference algorithm).  Per parameter, either
         ||g - g64|| <= tol * ||g64||                              (well-conditioned)
-    or, where ``err32`` (the reference's OWN fp32 error ||g32 - g64|| in the
-    identity molecule order, tests/golden/c2_grad_conditioning.json) shows the
-    gradient is ill-conditioned, no further from fp64 than twice that.
+    or, where ``err32`` (the reference's OWN fp32 error ||g32 - g64||,
+    tests/golden/c2_grad_conditioning.json) shows the gradient is
+    ill-conditioned:
+      GIN: no further from fp64 than the reference's own fp32 step lands in
+           the worst of 4 molecule orders of the same batch (err32) -- the
+           spread any fp32 evaluation of the reference shows.  Measured: every
+           GIN gradient of the paired and the two-call pass within 0.77 of it
+           (the paired pass's 2.2e-3 and the two-call pass's 1.1e-3 on
+           gnns.2.edge_embedding2 both sit inside the reference's own
+           1.97e-3 .. 3.05e-3);
+      GCN: twice the identity-order error (its tiny scalar edge tables reach
+           1.2-1.9x the worst-order error; see the exemptions).
     Pre-BN biases (exact gradient 0) must be at rounding-noise level.  The
     parameters listed in tests/golden/grad_exemptions.json (with the reason)
     are held to 8x the reference's worst fp32 error over molecule orders."""
@@ -69,7 +78,8 @@ def check_grads(mine, ref64, err32=None, tol=TOL, record=None):
         err = (a - b).norm().item()
         bound = tol * b.norm().item()
         if err32 is not None:
-            bound = max(bound, 2.0 * err32[name]["err32_identity"])
+            gin = record is not None and "gin" in record
+            bound = max(bound, err32[name]["err32"] if gin else 2.0 * err32[name]["err32_identity"])
             if name in exempt:
                 bound = max(bound, 8.0 * err32[name]["err32"])
         errs[name] = {"rel": err / max(b.norm().item(), 1e-30),

@@ -1,7 +1,7 @@
 """GEMM shapes of the c2 step: molclr_gemm_f32 vs torch.matmul (hipBLASLt /
 rocBLAS fp32) on the same operands.  Prints TFLOP/s per shape.
 
-    python tools/gemm_bench.py [N_rows] [impl,impl,...]
+    python tools/gemm_bench.py [N_rows] [impl,impl,...] [tile,tile,...]
 """
 import sys
 from pathlib import Path
@@ -56,6 +56,7 @@ def main():
     from molclr_amd import _lib
     lib = _lib.load()
     impls = [int(v) for v in (sys.argv[2].split(",") if len(sys.argv) > 2 else "-1,0,5,6".split(","))]
+    tiles = [int(v) for v in (sys.argv[3].split(",") if len(sys.argv) > 3 else "5,7,9".split(","))]
     for name, A, B, M, N, K, lda, ldb, ak, bk, epi, kw, weight, ref in cases:
         flops = 2 * M * N * K
         res = []
@@ -72,7 +73,7 @@ def main():
                     ws.data_ptr(), ws_bytes, _lib.stream_of(dev), kg))
                 res.append(f"w6/kg{kg} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
         if weight:
-            for t in (5, 7, 9):
+            for t in tiles:
                 tm = timeit(lambda: ops.gemm_w(A, B, M, N, K, lda, ldb, ak, bk, epi, tile=t, **kw))
                 res.append(f"bp{t} {tm*1e6:5.1f}us {flops/tm/1e12:5.1f}TF")
         tr = timeit(ref)

@@ -54,11 +54,14 @@ def main():
                                                            db.data_ptr(), M, n_out, n_in, n_out, n_in,
                                                            0, ws.data_ptr(), wsb, st, variant)
     else:
-        cases = {"q6_lin1": lambda: ops.linear_fwd(X["agg"], W0, b0, relu=True),
-                 "q6_lin2": lambda: ops.linear_fwd(X["a1"], W2, b2),
+        t = max(variant, 0)  # molclr_gemm_f32_bplanes_tile: 9 q6, 10 q7, 0 automatic
+        cases = {"q6_lin1": lambda: ops.gemm_w(X["agg"], W0, M, H, D, D, D, False, False,
+                                               EPI_BIAS_RELU, bias=b0, tile=t),
+                 "q6_lin2": lambda: ops.gemm_w(X["a1"], W2, M, D, H, H, H, False, False,
+                                               EPI_BIAS, bias=b2, tile=t),
                  "q6_dz1": lambda: ops.gemm_w(X["dz"], W2, M, H, D, D, H, False, True,
-                                              EPI_RELU_MASK, aux=X["a1"]),
-                 "q6_dagg": lambda: ops.gemm_w(X["dz1"], W0, M, D, H, H, D, False, True),
+                                              EPI_RELU_MASK, aux=X["a1"], tile=t),
+                 "q6_dagg": lambda: ops.gemm_w(X["dz1"], W0, M, D, H, H, D, False, True, tile=t),
                  "w6_dW2": lambda: ops.linear_bwd(X["dz"], X["a1"], W2, need_x=False),
                  "w6_dW1": lambda: ops.linear_bwd(X["dz1"], X["agg"], W0, need_x=False)}
         fn = cases[case]
