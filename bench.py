@@ -92,6 +92,10 @@ def parse():
                         "built inside every step by molclr_mask_views from a resident "
                         "molecule store; subgraph / mix: the same with molclr_aug_views "
                         "(dataset_subgraph.py / dataset_mix.py views)")
+    p.add_argument("--no-hip-graph", action="store_true",
+                   help="run every step eagerly (host-enqueued launches) instead of replaying "
+                        "the HIP graph captured per batch-size bucket (molclr_amd.graph_step; "
+                        "single process, paired pass only)")
     return p.parse_args()
 
 
@@ -235,7 +239,12 @@ def main():
         id_sets = [perm_rng.permutation(nmol)[:B].astype(np.int64) for _ in range(args.batches)]
         id_sets_dev = [torch.from_numpy(v).to(dev) for v in id_sets]
 
-    def step(i):
+    captured = None
+    if world == 1 and not args.two_pass and not args.no_hip_graph:
+        from molclr_amd.graph_step import CapturedTrainStep
+        captured = CapturedTrainStep(model, opt, crit)
+
+    def step(i, eager=False):
         if store is not None:
             k = i % len(id_sets)
             if args.augment == "device":
@@ -245,6 +254,10 @@ def main():
                                          host_ids=id_sets[k])
         else:
             xi, xj = batches[i % len(batches)]
+        if captured is not None and not eager:
+            # staging copy + one graph launch: the graph build, both views'
+            # encoder pass, NT-Xent, backward and Adam replay on the device
+            return captured(xi, xj)
         for g in (xi, xj):  # rebuild the graph every step: it is part of the work
             g.__dict__.pop("_molclr_graph", None)
             g.__dict__.pop("_molclr_pair_graph", None)
@@ -281,8 +294,11 @@ def main():
     torch.cuda.synchronize()
 
     # the timed region carries dispatch events on the scatter-add launches only
-    # (10 per step); timing every GEMM launch too costs ~13 % of the step
-    timer = None if args.no_kernel_timing else ops.KernelTimer(kinds=("gine_aggregate_fwd",))
+    # (10 per step); timing every GEMM launch too costs ~13 % of the step.  A
+    # replayed graph cannot carry them: the scatter-add is then timed over
+    # extra eager steps after the timed region, like the GEMMs
+    timer = None if args.no_kernel_timing or captured is not None else \
+        ops.KernelTimer(kinds=("gine_aggregate_fwd",))
     ops.set_kernel_timer(timer)
     if world > 1:
         torch.distributed.barrier()
@@ -309,12 +325,23 @@ def main():
 
     # (the library keeps one timer: read the scatter-add samples before the GEMM pass)
     s = timer.summary() if timer is not None else {}
+    agg_timing = "hipExtLaunchKernelGGL dispatch events in the timed region"
+    if captured is not None and not args.no_kernel_timing and args.mfma_steps > 0:
+        timer = ops.KernelTimer(kinds=("gine_aggregate_fwd",))
+        ops.set_kernel_timer(timer)
+        for i in range(args.mfma_steps):
+            step(args.warmup + args.steps + 3 + i, eager=True)
+        torch.cuda.synchronize()
+        ops.set_kernel_timer(None)
+        s = timer.summary()
+        agg_timing = (f"hipExtLaunchKernelGGL dispatch events over {args.mfma_steps} eager steps "
+                      f"after the timed region (the timed region replays HIP graphs)")
     # GEMM durations: dispatch events over extra steps after the timed region
     if timer is not None and args.mfma_steps > 0:
         gemm_timer = ops.KernelTimer(kinds=("gemm_f32", "ntxent"))
         ops.set_kernel_timer(gemm_timer)
         for i in range(args.mfma_steps):
-            step(args.warmup + args.steps + 3 + i)
+            step(args.warmup + args.steps + 3 + i, eager=True)
         torch.cuda.synchronize()
         ops.set_kernel_timer(None)
         s.update({k: v for k, v in gemm_timer.summary().items() if k in ("gemm_f32", "ntxent")})
@@ -334,7 +361,7 @@ def main():
                         "bytes_per_launch": int(per_launch_bytes),
                         "us_per_launch": round(per_launch_s * 1e6, 2),
                         "launches": agg["launches"],
-                        "timing": "hipExtLaunchKernelGGL dispatch events"}
+                        "timing": agg_timing}
         gm = s.get("gemm_f32")
         if gm:
             tfs = gm["work"] / (gm["ms"] / 1e3) / 1e12
@@ -391,6 +418,9 @@ def main():
                        "parallelism": f"dp{world}",
                        "views": ("two encoder calls (molclr.py:57,60)" if args.two_pass else
                                  "one paired encoder pass, per-view BatchNorm statistics"),
+                       "launch": ("HIP graph per batch-size bucket (molclr_amd.graph_step): "
+                                  f"{captured.captures} captured, staged + replayed every step"
+                                  if captured is not None else "eager (host-enqueued)"),
                        "augment": ("host: pre-built resident batch pairs" if store is None else
                                    "device: molclr_mask_views inside the step"
                                    if args.augment == "device" else

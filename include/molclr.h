@@ -134,6 +134,43 @@ int molclr_graph_build_multi(int nseg, const molclr_graph_segment* segs, int32_t
                              int32_t* status, void* workspace, size_t workspace_bytes,
                              molclr_stream_t stream);
 
+/* Device-sized graph build: molclr_graph_build_multi over fixed-capacity
+ * buffers, for a training step captured once as a HIP graph and replayed for
+ * every batch that fits (molclr_amd/graph_step.py; the reference's per-step
+ * loop, molclr.py:107-128).  Two calls:
+ *   molclr_stage_segments (outside the captured region; one launch): copies
+ *     segment s's PyG fields -- x [n_s,2], edge_index [2,e_s], edge_attr
+ *     [e_s,2], batch [n_s] -- into its staging buffers dst[s] (edge_index
+ *     rows edge_cap apart), x into x_all [num_nodes_cap,2] at row
+ *     n_0 + .. + n_{s-1}, fills the remaining rows of x_all with atom (0, 0),
+ *     and writes counts [2*nseg] = n_0..n_{nseg-1}, e_0..e_{nseg-1}.
+ *   molclr_graph_build_dev (inside it): the build, reading the counts on the
+ *     device.  Outputs sized for num_nodes_cap rows / num_edges_cap edges
+ *     (workspace: molclr_graph_build_workspace_bytes of those); rows past the
+ *     real nodes are padding: no edges, ecount = the self loop only, outside
+ *     every graph (graph_ptr[G] = the real node count).  G = sum of num_graphs
+ *     is fixed. */
+typedef struct molclr_stage_source {
+  const int64_t *x, *edge_index, *edge_attr, *batch;
+  int64_t num_nodes, num_edges;
+} molclr_stage_source;
+typedef struct molclr_graph_staged_segment {
+  const int64_t* edge_index; /* [2, edge_cap] */
+  const int64_t* edge_attr;  /* [edge_cap, 2] */
+  const int64_t* batch;      /* [node_cap] */
+  int64_t node_cap, edge_cap, num_graphs;
+} molclr_graph_staged_segment;
+int molclr_stage_segments(int nseg, const molclr_stage_source* src,
+                          const molclr_graph_staged_segment* dst, int64_t* x_all,
+                          int64_t num_nodes_cap, int64_t num_edges_cap, int64_t* counts,
+                          molclr_stream_t stream);
+int molclr_graph_build_dev(int nseg, const molclr_graph_staged_segment* segs, const int64_t* counts,
+                           int64_t num_nodes_cap, int64_t num_edges_cap, int32_t* rowptr,
+                           int32_t* col, uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t,
+                           uint32_t* nbr, uint32_t* nbr_t, int32_t* ecount, int32_t* graph_ptr,
+                           int32_t* status, void* workspace, size_t workspace_bytes,
+                           molclr_stream_t stream);
+
 /* On-device node-mask augmentation + collate: one contrastive view of a batch
  * of molecules, replacing MoleculeDataset.__getitem__'s masking
  * (dataset/dataset.py:111-145) and the DataLoader's PyG collate
@@ -487,6 +524,27 @@ int molclr_batchnorm_seg_bwd(const void* dy, const void* z, const float* gamma,
  * NULL; the caller zeroes it): the scales of the h3 products that consume dz
  * (molclr_gemm_f32_h3 row-wise, molclr_linear_wgrad_h3). */
 int molclr_bn_row_parts(int64_t dim);
+/* Device-sized segments (a captured step over padded buffers): the rows of
+ * every segment are read from seg_rows_dev [nseg] on the device; z / y / dy /
+ * dz hold rows_cap rows, and rows past the segments' sum are padding (y and dz
+ * zero there, no statistics).  Same per-segment plan as the host-sized calls,
+ * so the real rows' results are bit-identical to theirs.  The backward's
+ * rowmax / slot (fp32 only, may be NULL) as molclr_batchnorm_seg_bwd_max. */
+size_t molclr_batchnorm_seg_dev_workspace_bytes(int nseg, int64_t rows_cap, int64_t dim);
+int molclr_batchnorm_seg_fwd_dev(const void* z, const float* gamma, const float* beta,
+                                 float* running_mean, float* running_var,
+                                 int64_t* num_batches_tracked, void* y, float* save_mean,
+                                 float* save_invstd, int nseg, const int64_t* seg_rows_dev,
+                                 int64_t rows_cap, int64_t dim, int dtype, double momentum,
+                                 double eps, int training, int relu, void* workspace,
+                                 size_t workspace_bytes, molclr_stream_t stream);
+int molclr_batchnorm_seg_bwd_dev(const void* dy, const void* z, const float* gamma,
+                                 const float* beta, const float* save_mean,
+                                 const float* save_invstd, void* dz, float* dgamma, float* dbeta,
+                                 int nseg, const int64_t* seg_rows_dev, int64_t rows_cap,
+                                 int64_t dim, int dtype, int relu, int accumulate, float* rowmax,
+                                 float* slot, void* workspace, size_t workspace_bytes,
+                                 molclr_stream_t stream);
 int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, const float* gamma,
                                  const float* beta, const float* save_mean,
                                  const float* save_invstd, float* dz, float* dgamma, float* dbeta,
@@ -683,6 +741,10 @@ typedef struct molclr_device_graph {
   const uint32_t *nbr, *nbr_t;
   int32_t num_segments;
   int64_t segment_nodes[MOLCLR_MAX_SEGMENTS];
+  /* NULL, or (molclr_graph_build_dev) the segments' node counts on the device:
+   * num_nodes is then the capacity, segment_nodes is unused and the rows past
+   * the counts' sum are padding */
+  const int64_t* segment_nodes_dev;
 } molclr_device_graph;
 
 /* Saved activations of one forward (kept for the backward): arena of

@@ -32,6 +32,9 @@ SIGNATURES = {
                                    _P, _P, _P, c_size_t, _P]),
     "molclr_graph_build_multi": (c_int, [c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                          c_size_t, _P]),
+    "molclr_stage_segments": (c_int, [c_int, _P, _P, _P, _I64, _I64, _P, _P]),
+    "molclr_graph_build_dev": (c_int, [c_int, _P, _P, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
+                                       _P, _P, _P, c_size_t, _P]),
     "molclr_mask_views_workspace_bytes": (c_size_t, [_I64]),
     "molclr_mask_views": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, c_uint64, c_int, _P, _P,
                                   _P, _P, _P, _I64, _I64, _P, _P, c_size_t, _P]),
@@ -93,6 +96,12 @@ SIGNATURES = {
                                          c_double, c_double, c_int, c_int, _P, c_size_t, _P]),
     "molclr_batchnorm_seg_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P, _I64, c_int,
                                          c_int, c_int, _P, c_size_t, _P]),
+    "molclr_batchnorm_seg_dev_workspace_bytes": (c_size_t, [c_int, _I64, _I64]),
+    "molclr_batchnorm_seg_fwd_dev": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P, _I64,
+                                             _I64, c_int, c_double, c_double, c_int, c_int, _P,
+                                             c_size_t, _P]),
+    "molclr_batchnorm_seg_bwd_dev": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P, c_int, _P, _I64,
+                                             _I64, c_int, c_int, c_int, _P, _P, _P, c_size_t, _P]),
     "molclr_segment_pool_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
     "molclr_segment_pool_bwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_l2norm_fwd": (c_int, [_P, _P, _P, _I64, _I64, c_double, _P]),
@@ -208,13 +217,26 @@ class DeviceGraphC(ctypes.Structure):
     _fields_ = [("num_nodes", c_int64), ("num_edges", c_int64), ("num_graphs", c_int64)] + [
         (f, c_void_p) for f in ("rowptr", "col", "rowptr_t", "col_t", "ecount", "graph_ptr",
                                 "ecode", "nbr", "nbr_t")] + [
-        ("num_segments", ctypes.c_int32), ("segment_nodes", c_int64 * 8)]
+        ("num_segments", ctypes.c_int32), ("segment_nodes", c_int64 * 8),
+        ("segment_nodes_dev", c_void_p)]
 
 
 class GraphSegmentC(ctypes.Structure):
     """struct molclr_graph_segment."""
     _fields_ = [("edge_index", c_void_p), ("edge_attr", c_void_p), ("batch", c_void_p),
                 ("num_nodes", c_int64), ("num_edges", c_int64), ("num_graphs", c_int64)]
+
+
+class StageSourceC(ctypes.Structure):
+    """struct molclr_stage_source."""
+    _fields_ = [("x", c_void_p), ("edge_index", c_void_p), ("edge_attr", c_void_p),
+                ("batch", c_void_p), ("num_nodes", c_int64), ("num_edges", c_int64)]
+
+
+class StagedSegmentC(ctypes.Structure):
+    """struct molclr_graph_staged_segment."""
+    _fields_ = [("edge_index", c_void_p), ("edge_attr", c_void_p), ("batch", c_void_p),
+                ("node_cap", c_int64), ("edge_cap", c_int64), ("num_graphs", c_int64)]
 
 
 class MolclrError(RuntimeError):

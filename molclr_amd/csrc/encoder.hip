@@ -88,13 +88,23 @@ int check_encoder(const molclr_gin_encoder* e, const molclr_device_graph* g) {
 }
 
 // BatchNorm segments of a graph (the views of a paired forward), checked
+// (device-sized graph: the rows of every segment are read on the device,
+// g->num_nodes rows in all, the rest padding)
 struct SegRows {
   int n;
   const int64_t* rows;
+  const int64_t* dev;
+  int64_t cap;
 };
 int graph_segments(const molclr_device_graph* g, const int64_t* N, SegRows& out) {
+  if (g->segment_nodes_dev) {
+    MOLCLR_REQUIRE(g->num_segments >= 1 && g->num_segments <= MOLCLR_MAX_SEGMENTS,
+                   "encoder: %d graph segments", g->num_segments);
+    out = {g->num_segments, nullptr, g->segment_nodes_dev, *N};
+    return MOLCLR_OK;
+  }
   if (g->num_segments <= 1) {
-    out = {1, N};
+    out = {1, N, nullptr, *N};
     return MOLCLR_OK;
   }
   MOLCLR_REQUIRE(g->num_segments <= MOLCLR_MAX_SEGMENTS, "encoder: %d graph segments",
@@ -103,8 +113,38 @@ int graph_segments(const molclr_device_graph* g, const int64_t* N, SegRows& out)
   for (int s = 0; s < g->num_segments; ++s) tot += g->segment_nodes[s];
   MOLCLR_REQUIRE(tot == *N, "encoder: segment nodes sum to %lld, graph has %lld", (long long)tot,
                  (long long)*N);
-  out = {g->num_segments, g->segment_nodes};
+  out = {g->num_segments, g->segment_nodes, nullptr, *N};
   return MOLCLR_OK;
+}
+
+// the segmented BatchNorm of a graph, host- or device-sized
+int seg_bn_fwd(const SegRows& sg, const void* z, const float* gamma, const float* beta,
+               float* rmean, float* rvar, int64_t* nbt, void* y, float* mean, float* invstd,
+               int64_t D, int dtype, double momentum, double eps, int training, int relu,
+               void* ws, size_t ws_bytes, molclr_stream_t stream) {
+  if (sg.dev)
+    return molclr_batchnorm_seg_fwd_dev(z, gamma, beta, rmean, rvar, nbt, y, mean, invstd, sg.n,
+                                        sg.dev, sg.cap, D, dtype, momentum, eps, training, relu,
+                                        ws, ws_bytes, stream);
+  return molclr_batchnorm_seg_fwd(z, gamma, beta, rmean, rvar, nbt, y, mean, invstd, sg.n,
+                                  sg.rows, D, dtype, momentum, eps, training, relu, ws, ws_bytes,
+                                  stream);
+}
+// rowmax != NULL (fp32): also dz's row maxima and max slot (the h3 scales)
+int seg_bn_bwd(const SegRows& sg, const void* dy, const void* z, const float* gamma,
+               const float* beta, const float* mean, const float* invstd, void* dz, float* dgamma,
+               float* dbeta, int64_t D, int dtype, int relu, int accumulate, float* rowmax,
+               float* slot, void* ws, size_t ws_bytes, molclr_stream_t stream) {
+  if (sg.dev)
+    return molclr_batchnorm_seg_bwd_dev(dy, z, gamma, beta, mean, invstd, dz, dgamma, dbeta, sg.n,
+                                        sg.dev, sg.cap, D, dtype, relu, accumulate, rowmax, slot,
+                                        ws, ws_bytes, stream);
+  if (rowmax)
+    return molclr_batchnorm_seg_bwd_max((const float*)dy, (const float*)z, gamma, beta, mean,
+                                        invstd, (float*)dz, dgamma, dbeta, sg.n, sg.rows, D, relu,
+                                        accumulate, rowmax, slot, ws, ws_bytes, stream);
+  return molclr_batchnorm_seg_bwd(dy, z, gamma, beta, mean, invstd, dz, dgamma, dbeta, sg.n,
+                                  sg.rows, D, dtype, relu, accumulate, ws, ws_bytes, stream);
 }
 
 #define MOLCLR_TRY(expr)      \
@@ -201,11 +241,10 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
                                   MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, stream));
       MOLCLR_TRY(molclr_gemm_bf16(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D,
                                   MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, stream));
-      MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                          e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                          F(lay.mean[l]), F(lay.invstd[l]), seg.n, seg.rows, D,
-                                          MOLCLR_DTYPE_BF16, e->momentum, e->eps, e->training,
-                                          last ? 0 : 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(seg_bn_fwd(seg, z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                            e->bn_running_var[l], e->bn_num_batches_tracked[l], y, F(lay.mean[l]),
+                            F(lay.invstd[l]), D, MOLCLR_DTYPE_BF16, e->momentum, e->eps,
+                            e->training, last ? 0 : 1, kws, kws_bytes, stream));
     } else {
       float *agg = F(lay.agg[l]), *a1 = F(lay.a1[l]), *z = F(lay.z[l]);
       MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
@@ -242,11 +281,10 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
                                            MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, kws,
                                            kws_bytes, stream));
       }
-      MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                          e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                          F(lay.mean[l]), F(lay.invstd[l]), seg.n, seg.rows, D,
-                                          MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
-                                          last ? 0 : 1, kws, kws_bytes, stream));
+      MOLCLR_TRY(seg_bn_fwd(seg, z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                            e->bn_running_var[l], e->bn_num_batches_tracked[l], y, F(lay.mean[l]),
+                            F(lay.invstd[l]), D, MOLCLR_DTYPE_F32, e->momentum, e->eps,
+                            e->training, last ? 0 : 1, kws, kws_bytes, stream));
     }
     h = y;
   }
@@ -306,15 +344,14 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
     if (h3) {
       // dz's row maxima and max slot for the h3 products
-      MOLCLR_TRY(molclr_batchnorm_seg_bwd_max(
-          (const float*)dy, (const float*)z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
-          F(lay.invstd[l]), (float*)dz, gr->bn_weight[l], gr->bn_bias[l], seg.n, seg.rows, D,
-          last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotFloats, kws, kws_bytes, stream));
+      MOLCLR_TRY(seg_bn_bwd(seg, dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
+                            F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l], D,
+                            MOLCLR_DTYPE_F32, last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotFloats,
+                            kws, kws_bytes, stream));
     } else {
-      MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
-                                          F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l],
-                                          seg.n, seg.rows, D, dt, last ? 0 : 1, 1, kws, kws_bytes,
-                                          stream));
+      MOLCLR_TRY(seg_bn_bwd(seg, dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
+                            F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l], D, dt,
+                            last ? 0 : 1, 1, nullptr, nullptr, kws, kws_bytes, stream));
     }
     if (bf) {
       const uint16_t *hz = (const uint16_t*)dz, *ha1 = (const uint16_t*)a1;
@@ -538,11 +575,10 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
     MOLCLR_TRY(molclr_gcn_aggregate_fwd(xw, g->rowptr, g->col, g->ecode, g->nbr,
                                         e->edge_embedding1[l], e->edge_embedding2[l], e->bias[l],
                                         z, N, D, stream));
-    MOLCLR_TRY(molclr_batchnorm_seg_fwd(z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
-                                        e->bn_running_var[l], e->bn_num_batches_tracked[l], y,
-                                        A + lay.mean[l], A + lay.invstd[l], seg.n, seg.rows, D,
-                                        MOLCLR_DTYPE_F32, e->momentum, e->eps, e->training,
-                                        last ? 0 : 1, kws, kws_bytes, stream));
+    MOLCLR_TRY(seg_bn_fwd(seg, z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
+                          e->bn_running_var[l], e->bn_num_batches_tracked[l], y, A + lay.mean[l],
+                          A + lay.invstd[l], D, MOLCLR_DTYPE_F32, e->momentum, e->eps,
+                          e->training, last ? 0 : 1, kws, kws_bytes, stream));
     h = y;
   }
   return MOLCLR_OK;
@@ -584,10 +620,10 @@ MOLCLR_API int molclr_gcn_encoder_bwd(const molclr_gcn_encoder* e,
     const float* xin = l == 0 ? A + lay.h0 : A + lay.h[l - 1];
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gcn_encoder_bwd: BatchNorm grads needed");
-    MOLCLR_TRY(molclr_batchnorm_seg_bwd(dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
-                                        A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l],
-                                        seg.n, seg.rows, D, MOLCLR_DTYPE_F32, last ? 0 : 1, 1,
-                                        kws, kws_bytes, stream));
+    MOLCLR_TRY(seg_bn_bwd(seg, dy, z, e->bn_weight[l], e->bn_bias[l], A + lay.mean[l],
+                          A + lay.invstd[l], dz, gr->bn_weight[l], gr->bn_bias[l], D,
+                          MOLCLR_DTYPE_F32, last ? 0 : 1, 1, nullptr, nullptr, kws, kws_bytes,
+                          stream));
     // ops._GCNConv.backward order: aggregation (dxw, edge tables, bias), dW, dx
     MOLCLR_TRY(molclr_gcn_aggregate_bwd(dz, g->rowptr_t, g->col_t, g->nbr_t, g->ecount, dxw,
                                         gr->edge_embedding1[l], gr->edge_embedding2[l],

@@ -20,18 +20,48 @@ constexpr int kScanThreads = 1024;
 // The inputs as up to MOLCLR_MAX_SEGMENTS concatenated PyG batches (the two
 // contrastive views of a step built as one graph): segment s's nodes, edges
 // and graphs follow those of segments 0..s-1.
+// Device-sized (molclr_graph_build_dev, a captured step): the node and edge
+// counts of every segment are read on the device (dcount), the outputs have a
+// fixed capacity and segment s's edge_index rows are eld[s] apart.
 struct GSegs {
   int n;
   const int64_t* ei[MOLCLR_MAX_SEGMENTS];
   const int64_t* ea[MOLCLR_MAX_SEGMENTS];
   const int64_t* batch[MOLCLR_MAX_SEGMENTS];
   int64_t n0[MOLCLR_MAX_SEGMENTS + 1], e0[MOLCLR_MAX_SEGMENTS + 1], g0[MOLCLR_MAX_SEGMENTS + 1];
+  int64_t eld[MOLCLR_MAX_SEGMENTS];
+  const int64_t* dcount;  // [nseg] nodes, then [nseg] edges; NULL = host-sized
 };
 
 __device__ __forceinline__ int gseg(const int64_t* off, int n, int64_t k) {
   int s = 0;
   while (s + 1 < n && k >= off[s + 1]) ++s;
   return s;
+}
+
+// count of segment s: which = 0 nodes, 1 edges
+__device__ __forceinline__ int64_t gcount(const GSegs& sg, int which, int s) {
+  if (sg.dcount) return sg.dcount[which * sg.n + s];
+  return which ? sg.e0[s + 1] - sg.e0[s] : sg.n0[s + 1] - sg.n0[s];
+}
+__device__ __forceinline__ int64_t gbase(const GSegs& sg, int which, int s) {
+  if (!sg.dcount) return which ? sg.e0[s] : sg.n0[s];
+  int64_t b = 0;
+  for (int q = 0; q < s; ++q) b += sg.dcount[which * sg.n + q];
+  return b;
+}
+struct GLoc {
+  int s;  // -1: past the last segment
+  int64_t base, cnt;
+};
+__device__ __forceinline__ GLoc glocate(const GSegs& sg, int which, int64_t k) {
+  int64_t b = 0;
+  for (int s = 0; s < sg.n; ++s) {
+    const int64_t c = gcount(sg, which, s);
+    if (k < b + c) return {s, b, c};
+    b += c;
+  }
+  return {-1, b, 0};
 }
 
 __global__ void k_graph_init(int32_t* __restrict__ ecount, int32_t* __restrict__ counters,
@@ -52,12 +82,14 @@ __global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
                               int32_t* __restrict__ ecount, int32_t* __restrict__ status) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= E) return;
-  const int g = gseg(sg.e0, sg.n, k);
-  const int64_t kk = k - sg.e0[g], Eg = sg.e0[g + 1] - sg.e0[g];
-  const int64_t Ng = sg.n0[g + 1] - sg.n0[g];
+  const GLoc le = glocate(sg, 1, k);
+  if (le.s < 0) return;  // past the real edges of a device-sized build
+  const int g = le.s;
+  const int64_t kk = k - le.base, Eg = le.cnt;
+  const int64_t Ng = gcount(sg, 0, g), nb = gbase(sg, 0, g);
   const int64_t* ei = sg.ei[g];
   const int64_t* ea = sg.ea[g];
-  int64_t s = ei[kk], d = ei[Eg + kk];
+  int64_t s = ei[kk], d = ei[(sg.dcount ? sg.eld[g] : Eg) + kk];
   int64_t bt = ea[2 * kk], bd = ea[2 * kk + 1];
   int bad = 0;
   if (s < 0 || s >= Ng || d < 0 || d >= Ng) {
@@ -71,8 +103,8 @@ __global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
     bd = bd < 0 ? 0 : (bd >= MOLCLR_NUM_BOND_DIR ? MOLCLR_NUM_BOND_DIR - 1 : bd);
   }
   if (bad) atomicOr(status, bad);
-  s += sg.n0[g];
-  d += sg.n0[g];
+  s += nb;
+  d += nb;
   src32[k] = (int32_t)s;
   dst32[k] = (int32_t)d;
   code8[k] = (uint8_t)(bt | (bd << 3));
@@ -144,13 +176,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restric
   if (tid == 0) ptr[n] = carry;
 }
 
-__global__ void k_graph_fill(const int32_t* __restrict__ src32, const int32_t* __restrict__ dst32,
-                             int64_t E, const int32_t* __restrict__ rowptr,
+__global__ void k_graph_fill(GSegs sg, const int32_t* __restrict__ src32,
+                             const int32_t* __restrict__ dst32, int64_t E,
+                             const int32_t* __restrict__ rowptr,
                              const int32_t* __restrict__ rowptr_t, int32_t* __restrict__ cur,
                              int32_t* __restrict__ cur_t, int32_t* __restrict__ perm,
                              int32_t* __restrict__ perm_t) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= E) return;
+  if (k >= E || (sg.dcount && k >= gbase(sg, 1, sg.n))) return;
   int32_t s = src32[k], d = dst32[k];
   perm[rowptr[d] + atomicAdd(&cur[d], 1)] = (int32_t)k;
   perm_t[rowptr_t[s] + atomicAdd(&cur_t[s], 1)] = (int32_t)k;
@@ -207,29 +240,82 @@ __global__ void k_graph_ptr(GSegs sg, int64_t N, int64_t G, int32_t* __restrict_
                             int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < N) {
-    const int g = gseg(sg.n0, sg.n, t);
-    const int64_t* batch = sg.batch[g];
-    const int64_t i = t - sg.n0[g], Gg = sg.g0[g + 1] - sg.g0[g];
-    const int64_t b = batch[i];
-    if (b < 0 || b >= Gg || (i > 0 && batch[i - 1] > b)) atomicOr(status, 4);
+    const GLoc ln = glocate(sg, 0, t);
+    if (ln.s >= 0) {  // (padding rows of a device-sized build have no batch entry)
+      const int g = ln.s;
+      const int64_t* batch = sg.batch[g];
+      const int64_t i = t - ln.base, Gg = sg.g0[g + 1] - sg.g0[g];
+      const int64_t b = batch[i];
+      if (b < 0 || b >= Gg || (i > 0 && batch[i - 1] > b)) atomicOr(status, 4);
+    }
   }
   if (t <= G) {
     if (t == G) {
-      graph_ptr[t] = (int32_t)N;
+      graph_ptr[t] = (int32_t)gbase(sg, 0, sg.n);  // the real node count
     } else {
       // lower_bound(batch of t's segment, local graph id) + the segment's first node
       const int g = gseg(sg.g0, sg.n, t);
       const int64_t* batch = sg.batch[g];
       const int64_t want = t - sg.g0[g];
-      int64_t lo = 0, hi = sg.n0[g + 1] - sg.n0[g];
+      int64_t lo = 0, hi = gcount(sg, 0, g);
       while (lo < hi) {
         int64_t mid = (lo + hi) >> 1;
         if (batch[mid] < want) lo = mid + 1;
         else hi = mid;
       }
-      graph_ptr[t] = (int32_t)(sg.n0[g] + lo);
+      graph_ptr[t] = (int32_t)(gbase(sg, 0, g) + lo);
     }
   }
+}
+
+// The kernels of a build over N rows / E edge slots (host-sized: the real
+// counts; device-sized: the capacities, the kernels read the real counts).
+int build_launch(const GSegs& sg, int64_t N, int64_t E, int64_t G, int32_t* rowptr, int32_t* col,
+                 uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t, uint32_t* nbr, uint32_t* nbr_t,
+                 int32_t* ecount, int32_t* graph_ptr, int32_t* status, void* workspace,
+                 size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status && (N == 0 || (nbr && nbr_t)),
+                 "graph_build: null output");
+  MOLCLR_REQUIRE(E == 0 || (col && ecode && col_t), "graph_build: null edge buffer");
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_graph_build_workspace_bytes(N, E));
+  hipStream_t s = molclr::as_stream(stream);
+  molclr::Workspace w(workspace, workspace_bytes);
+  int32_t* src32 = w.take<int32_t>(E);
+  int32_t* dst32 = w.take<int32_t>(E);
+  uint8_t* code8 = w.take<uint8_t>(E);
+  int32_t* counters = w.take<int32_t>(4 * N);
+  int32_t* indeg = counters;
+  int32_t* outdeg = counters + N;
+  int32_t* cur = counters + 2 * N;
+  int32_t* cur_t = counters + 3 * N;
+  int32_t* perm = w.take<int32_t>(E);
+  int32_t* perm_t = w.take<int32_t>(E);
+
+  const int T = 256;
+  int64_t n_init = 8 * N > 4 * N ? 8 * N : 4 * N;
+  if (n_init < 1) n_init = 1;
+  hipLaunchKernelGGL(k_graph_init, dim3(molclr::ceil_div(n_init, T)), dim3(T), 0, s, ecount,
+                     counters, 4 * N, N, status);
+  if (E > 0) {
+    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, sg, E, src32,
+                       dst32, code8, indeg, outdeg, ecount, status);
+  }
+  hipLaunchKernelGGL(k_scan2, dim3(2), dim3(kScanThreads), 0, s, indeg, rowptr, outdeg, rowptr_t,
+                     N);
+  if (E > 0) {
+    hipLaunchKernelGGL(k_graph_fill, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, sg, src32, dst32,
+                       E, rowptr, rowptr_t, cur, cur_t, perm, perm_t);
+  }
+  if (N > 0) {
+    hipLaunchKernelGGL(k_graph_rows, dim3(molclr::ceil_div(2 * N, T)), dim3(T), 0, s, N, src32,
+                       dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t,
+                       (uint4*)nbr, (uint4*)nbr_t);
+  }
+  int64_t n_ptr = N > G + 1 ? N : G + 1;
+  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, sg, N, G,
+                     graph_ptr, status);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
 }
 
 }  // namespace
@@ -281,48 +367,8 @@ MOLCLR_API int molclr_graph_build_multi(int nseg, const molclr_graph_segment* se
     MOLCLR_REQUIRE(segs[g].num_nodes == 0 || segs[g].batch, "graph_build: null batch in segment %d",
                    g);
   }
-  MOLCLR_REQUIRE(rowptr && rowptr_t && ecount && graph_ptr && status && (N == 0 || (nbr && nbr_t)),
-                 "graph_build: null output");
-  MOLCLR_REQUIRE(E == 0 || (col && ecode && col_t), "graph_build: null edge buffer");
-  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_graph_build_workspace_bytes(N, E));
-  hipStream_t s = molclr::as_stream(stream);
-  molclr::Workspace w(workspace, workspace_bytes);
-  int32_t* src32 = w.take<int32_t>(E);
-  int32_t* dst32 = w.take<int32_t>(E);
-  uint8_t* code8 = w.take<uint8_t>(E);
-  int32_t* counters = w.take<int32_t>(4 * N);
-  int32_t* indeg = counters;
-  int32_t* outdeg = counters + N;
-  int32_t* cur = counters + 2 * N;
-  int32_t* cur_t = counters + 3 * N;
-  int32_t* perm = w.take<int32_t>(E);
-  int32_t* perm_t = w.take<int32_t>(E);
-
-  const int T = 256;
-  int64_t n_init = 8 * N > 4 * N ? 8 * N : 4 * N;
-  if (n_init < 1) n_init = 1;
-  hipLaunchKernelGGL(k_graph_init, dim3(molclr::ceil_div(n_init, T)), dim3(T), 0, s, ecount,
-                     counters, 4 * N, N, status);
-  if (E > 0) {
-    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, sg, E, src32,
-                       dst32, code8, indeg, outdeg, ecount, status);
-  }
-  hipLaunchKernelGGL(k_scan2, dim3(2), dim3(kScanThreads), 0, s, indeg, rowptr, outdeg, rowptr_t,
-                     N);
-  if (E > 0) {
-    hipLaunchKernelGGL(k_graph_fill, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, src32, dst32, E,
-                       rowptr, rowptr_t, cur, cur_t, perm, perm_t);
-  }
-  if (N > 0) {
-    hipLaunchKernelGGL(k_graph_rows, dim3(molclr::ceil_div(2 * N, T)), dim3(T), 0, s, N, src32,
-                       dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t,
-                       (uint4*)nbr, (uint4*)nbr_t);
-  }
-  int64_t n_ptr = N > G + 1 ? N : G + 1;
-  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, sg, N, G,
-                     graph_ptr, status);
-  MOLCLR_LAUNCHED();
-  return MOLCLR_OK;
+  return build_launch(sg, N, E, G, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount,
+                      graph_ptr, status, workspace, workspace_bytes, stream);
 }
 
 MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge_attr,
@@ -335,4 +381,124 @@ MOLCLR_API int molclr_graph_build(const int64_t* edge_index, const int64_t* edge
   const molclr_graph_segment seg{edge_index, edge_attr, batch, N, E, G};
   return molclr_graph_build_multi(1, &seg, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount,
                                   graph_ptr, status, workspace, workspace_bytes, stream);
+}
+
+// ---------------------------------------------------------------------------
+// Device-sized build (a captured training step, molclr_amd/graph_step.py):
+// the batch arrives in fixed-capacity staging buffers and the kernels read
+// the real counts on the device, so one launch sequence serves every batch
+// whose sizes fit the capacities.
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kStageJobs = 5 * MOLCLR_MAX_SEGMENTS + 1;
+struct StageJob {
+  const int64_t* src;  // NULL: fill with 0
+  int64_t* dst;
+  int64_t count;
+};
+struct StageJobs {
+  StageJob j[kStageJobs];
+  int64_t counts[2 * MOLCLR_MAX_SEGMENTS];
+  int64_t* counts_dst;
+  int ncounts;
+};
+
+// blockIdx.y: the job; grid-stride over its elements
+__global__ void k_stage(StageJobs jb) {
+  const StageJob& j = jb.j[blockIdx.y];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.count;
+       i += (int64_t)gridDim.x * blockDim.x)
+    j.dst[i] = j.src ? j.src[i] : 0;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < jb.ncounts)
+    jb.counts_dst[threadIdx.x] = jb.counts[threadIdx.x];
+}
+
+}  // namespace
+
+MOLCLR_API int molclr_stage_segments(int nseg, const molclr_stage_source* src,
+                                     const molclr_graph_staged_segment* dst, int64_t* x_all,
+                                     int64_t num_nodes_cap, int64_t num_edges_cap,
+                                     int64_t* counts, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && src && dst && x_all && counts,
+                 "stage_segments: %d segments (1..%d) / null pointer", nseg, MOLCLR_MAX_SEGMENTS);
+  StageJobs jb{};
+  int nj = 0;
+  int64_t row = 0, edges = 0, most = 1;
+  auto job = [&](const int64_t* from, int64_t* to, int64_t n) {
+    jb.j[nj++] = {from, to, n};
+    if (n > most) most = n;
+  };
+  for (int s = 0; s < nseg; ++s) {
+    const molclr_stage_source& a = src[s];
+    const molclr_graph_staged_segment& b = dst[s];
+    MOLCLR_REQUIRE(a.num_nodes >= 0 && a.num_edges >= 0 && a.num_nodes <= b.node_cap &&
+                       a.num_edges <= b.edge_cap,
+                   "stage_segments: segment %d has %lld nodes / %lld edges, capacity %lld / %lld", s,
+                   (long long)a.num_nodes, (long long)a.num_edges, (long long)b.node_cap,
+                   (long long)b.edge_cap);
+    MOLCLR_REQUIRE((a.num_nodes == 0 || (a.x && a.batch && b.batch)) &&
+                       (a.num_edges == 0 || (a.edge_index && a.edge_attr && b.edge_index &&
+                                             b.edge_attr)),
+                   "stage_segments: null buffer in segment %d", s);
+    job(a.x, x_all + 2 * row, 2 * a.num_nodes);
+    job(a.edge_index, const_cast<int64_t*>(b.edge_index), a.num_edges);
+    job(a.edge_index + a.num_edges, const_cast<int64_t*>(b.edge_index) + b.edge_cap, a.num_edges);
+    job(a.edge_attr, const_cast<int64_t*>(b.edge_attr), 2 * a.num_edges);
+    job(a.batch, const_cast<int64_t*>(b.batch), a.num_nodes);
+    jb.counts[s] = a.num_nodes;
+    jb.counts[nseg + s] = a.num_edges;
+    row += a.num_nodes;
+    edges += a.num_edges;
+  }
+  MOLCLR_REQUIRE(edges <= num_edges_cap, "stage_segments: %lld edges exceed the capacity %lld",
+                 (long long)edges, (long long)num_edges_cap);
+  MOLCLR_REQUIRE(row <= num_nodes_cap, "stage_segments: %lld nodes exceed the capacity %lld",
+                 (long long)row, (long long)num_nodes_cap);
+  job(nullptr, x_all + 2 * row, 2 * (num_nodes_cap - row));  // padding atoms: type 0, chirality 0
+  jb.counts_dst = counts;
+  jb.ncounts = 2 * nseg;
+  const int T = 256;
+  int64_t bx = molclr::ceil_div(most, T);
+  if (bx > 256) bx = 256;
+  hipLaunchKernelGGL(k_stage, dim3((unsigned)bx, nj), dim3(T), 0, molclr::as_stream(stream), jb);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_graph_build_dev(int nseg, const molclr_graph_staged_segment* segs,
+                                      const int64_t* counts, int64_t num_nodes_cap,
+                                      int64_t num_edges_cap, int32_t* rowptr, int32_t* col,
+                                      uint8_t* ecode, int32_t* rowptr_t, int32_t* col_t,
+                                      uint32_t* nbr, uint32_t* nbr_t, int32_t* ecount,
+                                      int32_t* graph_ptr, int32_t* status, void* workspace,
+                                      size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && segs && counts,
+                 "graph_build_dev: %d segments (1..%d)", nseg, MOLCLR_MAX_SEGMENTS);
+  GSegs sg{};
+  sg.n = nseg;
+  sg.dcount = counts;
+  int64_t ecap = 0;
+  for (int g = 0; g < nseg; ++g) {
+    const molclr_graph_staged_segment& q = segs[g];
+    MOLCLR_REQUIRE(q.node_cap >= 0 && q.edge_cap >= 0 && q.num_graphs >= 0 &&
+                       q.edge_index && q.edge_attr && q.batch,
+                   "graph_build_dev: bad segment %d", g);
+    sg.ei[g] = q.edge_index;
+    sg.ea[g] = q.edge_attr;
+    sg.batch[g] = q.batch;
+    sg.eld[g] = q.edge_cap;
+    sg.g0[g + 1] = sg.g0[g] + q.num_graphs;
+    ecap += q.edge_cap;
+  }
+  for (int g = nseg; g < MOLCLR_MAX_SEGMENTS; ++g) sg.g0[g + 1] = sg.g0[nseg];
+  const int64_t N = num_nodes_cap, E = num_edges_cap, G = sg.g0[nseg];
+  MOLCLR_REQUIRE(E >= 1 && E <= ecap,
+                 "graph_build_dev: num_edges_cap %lld must be in [1, sum of edge_cap %lld]",
+                 (long long)E, (long long)ecap);
+  MOLCLR_REQUIRE(N >= 1 && N <= MOLCLR_NBR_MAX_NODES && E < (int64_t)1 << 31,
+                 "graph_build_dev: %lld nodes exceed the neighbour-slot limit %d (or E > int32)",
+                 (long long)N, MOLCLR_NBR_MAX_NODES);
+  return build_launch(sg, N, E, G, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount,
+                      graph_ptr, status, workspace, workspace_bytes, stream);
 }

@@ -17,12 +17,22 @@ namespace {
 
 constexpr int kT = 256;
 
-int64_t band_parts(int64_t rows, int band) {
+__host__ __device__ __forceinline__ int64_t band_parts(int64_t rows, int band) {
   // ~16 row-iterations per thread: many blocks keep enough loads in flight;
   // the final merge over the partitions is parallel (k_*_final)
-  int64_t P = molclr::ceil_div(rows, (int64_t)band * 16);
+  const int64_t unit = (int64_t)band * 16;
+  int64_t P = (rows + unit - 1) / unit;
   if (P > 1024) P = 1024;
   if (P < 1) P = 1;
+  return P;
+}
+
+// an upper bound of sum_s band_parts(n_s) over any split of `rows` rows into
+// nseg segments: ceil(a / u) + ceil(b / u) <= ceil((a + b) / u) + 1, and an
+// empty segment still takes one partition
+int64_t band_parts_bound(int64_t rows, int band, int nseg) {
+  int64_t P = band_parts(rows, band) + nseg;
+  if (P > (int64_t)nseg * 1024) P = (int64_t)nseg * 1024;
   return P;
 }
 
@@ -111,21 +121,53 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_colsum_final(
 // (StF32 / StBF16); the statistics are always fp32.
 // ---------------------------------------------------------------------------
 struct Segs {
-  int n;
-  int64_t row0[MOLCLR_MAX_SEGMENTS + 1];   // segment s: rows [row0[s], row0[s+1])
-  int64_t part0[MOLCLR_MAX_SEGMENTS + 1];  // its partitions: [part0[s], part0[s+1])
-  int64_t rpp[MOLCLR_MAX_SEGMENTS];        // rows per partition
+  int n;     // segments
+  int band;  // the partition plan's row unit (make_band(D).band)
+  int64_t rows[MOLCLR_MAX_SEGMENTS];  // host-sized: rows of every segment
+  // device-sized (a captured step over padded buffers): the rows of every
+  // segment live on the device and rows[] is unused; rows past the last
+  // segment are padding -- zero output, zero gradient, no statistics
+  const int64_t* drows;
 };
 
-__device__ __forceinline__ int seg_of_part(const Segs& sg, int64_t b) {
-  int s = 0;
-  while (s + 1 < sg.n && b >= sg.part0[s + 1]) ++s;
-  return s;
+__device__ __forceinline__ int64_t seg_n(const Segs& sg, int s) {
+  return sg.drows ? sg.drows[s] : sg.rows[s];
+}
+
+// Segment s's rows [row0, row1) and partitions [part0, part0 + P), each
+// partition rpp rows: exactly a one-segment call's plan over its rows.  s = -1
+// for a spare partition / padding row of a device-sized plan.
+struct SegAt {
+  int s;
+  int64_t row0, row1, part0, P, rpp;
+};
+__device__ __forceinline__ SegAt seg_info(const Segs& sg, int s) {
+  int64_t r = 0, p = 0;
+  for (int q = 0; q < s; ++q) {
+    const int64_t n = seg_n(sg, q);
+    r += n;
+    p += band_parts(n, sg.band);
+  }
+  const int64_t n = seg_n(sg, s), P = band_parts(n, sg.band);
+  return {s, r, r + n, p, P, (n > 0 ? n + P - 1 : P) / P};
+}
+__device__ __forceinline__ SegAt seg_of_part(const Segs& sg, int64_t b) {
+  int64_t r = 0, p = 0;
+  for (int s = 0; s < sg.n; ++s) {
+    const int64_t n = seg_n(sg, s), P = band_parts(n, sg.band);
+    if (b < p + P) return {s, r, r + n, p, P, (n > 0 ? n + P - 1 : P) / P};
+    r += n;
+    p += P;
+  }
+  return {-1, r, r, p, 0, 1};
 }
 __device__ __forceinline__ int seg_of_row(const Segs& sg, int64_t i) {
-  int s = 0;
-  while (s + 1 < sg.n && i >= sg.row0[s + 1]) ++s;
-  return s;
+  int64_t r = 0;
+  for (int s = 0; s < sg.n; ++s) {
+    r += seg_n(sg, s);
+    if (i < r) return s;
+  }
+  return -1;
 }
 
 struct Welford4 {
@@ -160,10 +202,11 @@ __global__ void k_bn_stats_partial(const typename St::T* __restrict__ z, int d4,
   const int tid = threadIdx.x;
   const bool live = tid < band * d4;
   const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
-  const int s = seg_of_part(sg, blockIdx.x);
-  const int64_t beg = sg.row0[s] + (blockIdx.x - sg.part0[s]) * sg.rpp[s];
-  int64_t end = beg + sg.rpp[s];
-  if (end > sg.row0[s + 1]) end = sg.row0[s + 1];
+  const SegAt at = seg_of_part(sg, blockIdx.x);
+  if (at.s < 0) return;  // spare partition of a device-sized plan (block-uniform)
+  const int64_t beg = at.row0 + (blockIdx.x - at.part0) * at.rpp;
+  int64_t end = beg + at.rpp;
+  if (end > at.row1) end = at.row1;
   float n = 0.f;
   float4 mean = f4zero(), m2 = f4zero();
   if (live) {
@@ -243,10 +286,11 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
     const int s = s0 + half;
     float n = 0.f, mean = 0.f, m2 = 0.f;
     if (s < sg.n && c < D) {
-      const int64_t P = sg.part0[s + 1] - sg.part0[s];
-      const float* sm = pmean + sg.part0[s] * D;
-      const float* sq = pm2 + sg.part0[s] * D;
-      const float* sn = pn + sg.part0[s];
+      const SegAt at = seg_info(sg, s);
+      const int64_t P = at.P;
+      const float* sm = pmean + at.part0 * D;
+      const float* sq = pm2 + at.part0 * D;
+      const float* sn = pn + at.part0;
       int64_t p = sl;
       for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
         float bn[4], bm[4], bq[4];
@@ -334,6 +378,10 @@ __global__ __launch_bounds__(kT) void k_bn_apply(const typename St::T* __restric
   const int64_t i = t / d4;
   const int c = (int)(t - i * d4);
   const int s = seg_of_row(sg, i);
+  if (s < 0) {  // padding row of a device-sized plan
+    St::st(y, t, f4zero());
+    return;
+  }
   float4 v = St::ld(z, t), sc = scale[s * d4 + c], sh = shift[s * d4 + c];
   float4 o = make_float4(bn_apply1(v.x, sc.x, sh.x), bn_apply1(v.y, sc.y, sh.y),
                          bn_apply1(v.z, sc.z, sh.z), bn_apply1(v.w, sc.w, sh.w));
@@ -363,10 +411,12 @@ __global__ void k_bn_bwd_partial(const typename St::T* __restrict__ dy,
   const int tid = threadIdx.x;
   const bool live = tid < band * d4;
   const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
-  const int s = seg_of_part(sg, blockIdx.x);
-  const int64_t beg = sg.row0[s] + (blockIdx.x - sg.part0[s]) * sg.rpp[s];
-  int64_t end = beg + sg.rpp[s];
-  if (end > sg.row0[s + 1]) end = sg.row0[s + 1];
+  const SegAt at = seg_of_part(sg, blockIdx.x);
+  if (at.s < 0) return;  // spare partition of a device-sized plan (block-uniform)
+  const int s = at.s;
+  const int64_t beg = at.row0 + (blockIdx.x - at.part0) * at.rpp;
+  int64_t end = beg + at.rpp;
+  if (end > at.row1) end = at.row1;
   float4 s1 = f4zero(), s2 = f4zero();
   if (live) {
     float4 mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
@@ -431,9 +481,10 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
     const int s = s0 + half;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
     if (s < sg.n && c < D) {
-      const int64_t P = sg.part0[s + 1] - sg.part0[s];
-      const float* q1 = p1 + sg.part0[s] * D;
-      const float* q2 = p2 + sg.part0[s] * D;
+      const SegAt at = seg_info(sg, s);
+      const int64_t P = at.P;
+      const float* q1 = p1 + at.part0 * D;
+      const float* q2 = p2 + at.part0 * D;
       int64_t p = sl;
       for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
         a0 += q1[p * D + c];
@@ -467,7 +518,7 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
       for (int h = 0; h < 2 && s0 + h < sg.n; ++h) {  // segment order
         const int ss = s0 + h;
         const float sa = ra[h * kSegLanes][cl], sb = rb[h * kSegLanes][cl];
-        const float inv_rows = 1.0f / (float)(sg.row0[ss + 1] - sg.row0[ss]);
+        const float inv_rows = 1.0f / (float)seg_n(sg, ss);
         const bool add = accumulate || ss > 0;
         if (dbeta) dbeta[c] = add ? dbeta[c] + sa : sa;
         if (dgamma) dgamma[c] = add ? dgamma[c] + sb : sb;
@@ -489,6 +540,10 @@ __device__ __forceinline__ float4 bn_bwd_elem(
   const int64_t i = t / d4;
   const int c = (int)(t - i * d4);
   const int s = seg_of_row(sg, i);
+  if (s < 0) {  // padding row of a device-sized plan: no gradient
+    St::st(dz, t, f4zero());
+    return f4zero();
+  }
   float4 g = St::ld(dy, t), x = St::ld(z, t), mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
   bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
   float4 a = k1[s * d4 + c], b = k2[s * d4 + c];
@@ -749,28 +804,32 @@ MOLCLR_API int molclr_colsum_f32(const float* X, float* out, int64_t rows, int64
 namespace {
 
 // host-side segment plan: partitions of every segment exactly as a one-segment
-// call over its rows would have them
-int make_segs(int nseg, const int64_t* seg_rows, int64_t D, Segs& sg, int64_t& P, int64_t& rows) {
-  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && seg_rows,
+// call over its rows would have them.  Device-sized (drows != NULL): the
+// segments' rows are read on the device, `cap` rows in all; P covers any
+// split of cap rows into nseg segments (spare partitions exit at once).
+int make_segs(int nseg, const int64_t* seg_rows, const int64_t* drows, int64_t cap, int64_t D,
+              Segs& sg, int64_t& P, int64_t& rows) {
+  MOLCLR_REQUIRE(nseg >= 1 && nseg <= MOLCLR_MAX_SEGMENTS && (seg_rows || drows),
                  "batchnorm: %d segments (1..%d)", nseg, MOLCLR_MAX_SEGMENTS);
   const molclr::Band b = molclr::make_band(D);
   sg.n = nseg;
-  sg.row0[0] = 0;
-  sg.part0[0] = 0;
+  sg.band = b.band;
+  sg.drows = drows;
+  P = 0;
+  rows = 0;
+  for (int s = 0; s < MOLCLR_MAX_SEGMENTS; ++s) sg.rows[s] = 0;
+  if (drows) {
+    MOLCLR_REQUIRE(cap >= 0, "batchnorm: negative row capacity");
+    P = band_parts_bound(cap, b.band, nseg);
+    rows = cap;
+    return MOLCLR_OK;
+  }
   for (int s = 0; s < nseg; ++s) {
     MOLCLR_REQUIRE(seg_rows[s] >= 0, "batchnorm: negative segment rows");
-    const int64_t Ps = band_parts(seg_rows[s], b.band);
-    sg.row0[s + 1] = sg.row0[s] + seg_rows[s];
-    sg.part0[s + 1] = sg.part0[s] + Ps;
-    sg.rpp[s] = molclr::ceil_div(seg_rows[s] > 0 ? seg_rows[s] : 1, Ps);
+    sg.rows[s] = seg_rows[s];
+    P += band_parts(seg_rows[s], b.band);
+    rows += seg_rows[s];
   }
-  for (int s = nseg; s < MOLCLR_MAX_SEGMENTS; ++s) {
-    sg.row0[s + 1] = sg.row0[nseg];
-    sg.part0[s + 1] = sg.part0[nseg];
-    sg.rpp[s] = 1;
-  }
-  P = sg.part0[nseg];
-  rows = sg.row0[nseg];
   return MOLCLR_OK;
 }
 
@@ -790,12 +849,13 @@ template <typename St>
 int bn_fwd(const void* zv, const float* gamma, const float* beta, float* running_mean,
            float* running_var, int64_t* nbt, void* yv, float* save_mean, float* save_invstd,
            int nseg, const int64_t* seg_rows, int64_t D, double momentum, double eps, int training,
-           int relu, void* workspace, size_t workspace_bytes, hipStream_t s) {
+           int relu, void* workspace, size_t workspace_bytes, hipStream_t s,
+           const int64_t* drows = nullptr, int64_t cap = 0) {
   Segs sg;
   int64_t P = 0, rows = 0;
-  if (int rc = make_segs(nseg, seg_rows, D, sg, P, rows)) return rc;
+  if (int rc = make_segs(nseg, seg_rows, drows, cap, D, sg, P, rows)) return rc;
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_fwd: dim must be a multiple of 4");
-  for (int q = 0; q < nseg; ++q)
+  for (int q = 0; q < nseg && !drows; ++q)  // device-sized: the caller's contract
     MOLCLR_REQUIRE(!training || seg_rows[q] > 1,
                    "batchnorm_fwd: need more than 1 row per segment when training");
   MOLCLR_REQUIRE(training || (running_mean && running_var), "batchnorm_fwd: eval needs running stats");
@@ -840,13 +900,14 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
            const float* save_mean, const float* save_invstd, void* dzv, float* dgamma,
            float* dbeta, int nseg, const int64_t* seg_rows, int64_t D, int relu, int accumulate,
            void* workspace, size_t workspace_bytes, hipStream_t s, float* rowparts = nullptr,
-           float* slot = nullptr) {
+           float* slot = nullptr, const int64_t* drows = nullptr, int64_t cap = 0) {
   Segs sg;
   int64_t P = 0, rows = 0;
-  if (int rc = make_segs(nseg, seg_rows, D, sg, P, rows)) return rc;
+  if (int rc = make_segs(nseg, seg_rows, drows, cap, D, sg, P, rows)) return rc;
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "batchnorm_bwd: dim must be a multiple of 4");
   MOLCLR_REQUIRE(rows > 0 && dyv && zv && save_mean && save_invstd && dzv, "batchnorm_bwd: bad args");
-  for (int q = 0; q < nseg; ++q) MOLCLR_REQUIRE(seg_rows[q] > 0, "batchnorm_bwd: empty segment");
+  for (int q = 0; q < nseg && !drows; ++q)
+    MOLCLR_REQUIRE(seg_rows[q] > 0, "batchnorm_bwd: empty segment");
   MOLCLR_REQUIRE_WS(workspace_bytes, bn_ws_bytes(P, D, nseg));
   const auto* dy = static_cast<const typename St::T*>(dyv);
   const auto* z = static_cast<const typename St::T*>(zv);
@@ -884,16 +945,14 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
 // segments (the encoder executors size their scratch before knowing it).
 size_t molclr_batchnorm_ws_bound(int64_t rows, int64_t D) {
   const molclr::Band b = molclr::make_band(D > 0 ? D : 4);
-  int64_t P = molclr::ceil_div(rows, (int64_t)b.band * 16) + MOLCLR_MAX_SEGMENTS;
-  if (P > (int64_t)MOLCLR_MAX_SEGMENTS * 1024) P = (int64_t)MOLCLR_MAX_SEGMENTS * 1024;
-  return bn_ws_bytes(P, D, MOLCLR_MAX_SEGMENTS);
+  return bn_ws_bytes(band_parts_bound(rows, b.band, MOLCLR_MAX_SEGMENTS), D, MOLCLR_MAX_SEGMENTS);
 }
 
 MOLCLR_API size_t molclr_batchnorm_seg_workspace_bytes(int nseg, const int64_t* seg_rows,
                                                        int64_t D) {
   Segs sg;
   int64_t P = 0, rows = 0;
-  if (make_segs(nseg, seg_rows, D > 0 ? D : 4, sg, P, rows)) return 0;
+  if (make_segs(nseg, seg_rows, nullptr, 0, D > 0 ? D : 4, sg, P, rows)) return 0;
   return bn_ws_bytes(P, D, nseg);
 }
 
@@ -947,6 +1006,58 @@ MOLCLR_API int molclr_batchnorm_seg_bwd_max(const float* dy, const float* z, con
   return bn_bwd<StF32>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
                        seg_rows, D, relu, accumulate, workspace, workspace_bytes,
                        molclr::as_stream(stream), rowmax, slot);
+}
+
+// Device-sized segments (a captured training step over padded buffers):
+// seg_rows_dev [nseg] on the device, rows_cap rows in z / y / dy / dz; rows
+// past the segments' sum are padding (zero output and gradient).  Same plan
+// per segment as the host-sized calls, so the results are bit-identical to
+// them on the real rows.  Workspace: molclr_batchnorm_seg_dev_workspace_bytes.
+MOLCLR_API size_t molclr_batchnorm_seg_dev_workspace_bytes(int nseg, int64_t rows_cap, int64_t D) {
+  if (nseg < 1 || nseg > MOLCLR_MAX_SEGMENTS) return 0;
+  const molclr::Band b = molclr::make_band(D > 0 ? D : 4);
+  return bn_ws_bytes(band_parts_bound(rows_cap, b.band, nseg), D, nseg);
+}
+
+MOLCLR_API int molclr_batchnorm_seg_fwd_dev(const void* z, const float* gamma, const float* beta,
+                                            float* running_mean, float* running_var,
+                                            int64_t* num_batches_tracked, void* y, float* save_mean,
+                                            float* save_invstd, int nseg,
+                                            const int64_t* seg_rows_dev, int64_t rows_cap,
+                                            int64_t D, int dtype, double momentum, double eps,
+                                            int training, int relu, void* workspace,
+                                            size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(seg_rows_dev, "batchnorm_seg_fwd_dev: null seg_rows_dev");
+  hipStream_t s = molclr::as_stream(stream);
+  if (dtype == MOLCLR_DTYPE_F32)
+    return bn_fwd<StF32>(z, gamma, beta, running_mean, running_var, num_batches_tracked, y,
+                         save_mean, save_invstd, nseg, nullptr, D, momentum, eps, training, relu,
+                         workspace, workspace_bytes, s, seg_rows_dev, rows_cap);
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_BF16, "batchnorm_seg_fwd_dev: dtype %d", dtype);
+  return bn_fwd<StBF16>(z, gamma, beta, running_mean, running_var, num_batches_tracked, y,
+                        save_mean, save_invstd, nseg, nullptr, D, momentum, eps, training, relu,
+                        workspace, workspace_bytes, s, seg_rows_dev, rows_cap);
+}
+
+MOLCLR_API int molclr_batchnorm_seg_bwd_dev(const void* dy, const void* z, const float* gamma,
+                                            const float* beta, const float* save_mean,
+                                            const float* save_invstd, void* dz, float* dgamma,
+                                            float* dbeta, int nseg, const int64_t* seg_rows_dev,
+                                            int64_t rows_cap, int64_t D, int dtype, int relu,
+                                            int accumulate, float* rowmax, float* slot,
+                                            void* workspace, size_t workspace_bytes,
+                                            molclr_stream_t stream) {
+  MOLCLR_REQUIRE(seg_rows_dev, "batchnorm_seg_bwd_dev: null seg_rows_dev");
+  MOLCLR_REQUIRE(!rowmax || dtype == MOLCLR_DTYPE_F32, "batchnorm_seg_bwd_dev: row maxima are fp32 only");
+  hipStream_t s = molclr::as_stream(stream);
+  if (dtype == MOLCLR_DTYPE_F32)
+    return bn_bwd<StF32>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
+                         nullptr, D, relu, accumulate, workspace, workspace_bytes, s, rowmax, slot,
+                         seg_rows_dev, rows_cap);
+  MOLCLR_REQUIRE(dtype == MOLCLR_DTYPE_BF16, "batchnorm_seg_bwd_dev: dtype %d", dtype);
+  return bn_bwd<StBF16>(dy, z, gamma, beta, save_mean, save_invstd, dz, dgamma, dbeta, nseg,
+                        nullptr, D, relu, accumulate, workspace, workspace_bytes, s, nullptr,
+                        nullptr, seg_rows_dev, rows_cap);
 }
 
 MOLCLR_API int molclr_batchnorm_fwd(const float* z, const float* gamma, const float* beta,

@@ -188,6 +188,15 @@ class GCN(nn.Module):
         h, graph = self.encode(data)
         return self._readout(h, graph)
 
+    def forward_staged(self, graph):
+        """forward_pair over a StagedPairGraph (molclr_amd.graph_step): the
+        views' atoms are graph.x, fixed-capacity buffers whose padding rows
+        carry no gradient -- the capturable form of the paired pass."""
+        if not self._executor_ok() or self._dim_pad():
+            raise NotImplementedError("forward_staged needs the encoder executor at a width "
+                                      "the kernels take unpadded")
+        return self._readout(self._run_encoder(graph.x, graph), graph)
+
     def forward_pair(self, xi, xj):
         """Both views in one pass, per-view BatchNorm statistics (see
         GINet.forward_pair): rows of forward(xi) then forward(xj)."""

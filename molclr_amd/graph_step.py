@@ -1,0 +1,223 @@
+"""The pre-training step captured as HIP graphs.
+
+The reference's hot loop (molclr.py:107-128) enqueues, per step: the graph of
+both views, the encoder forward, F.normalize, NT-Xent, the backward and the
+Adam update.  Here that is ~150 kernel launches (the encoder executors issue
+most of them from C++), ~1.5 ms of host time per step.  This module captures
+the whole step ONCE per batch-size bucket as a HIP graph (torch.cuda.CUDAGraph
+over the library's launches) and replays it: the host cost per step becomes
+one staging launch plus one graph launch.
+
+Batches vary in size, a graph does not.  The step therefore runs over
+fixed-capacity buffers:
+
+* ``StagedPairGraph`` holds staging buffers for both views' PyG fields and the
+  graph outputs, sized by a bucket's capacities (nodes rounded up to
+  ``node_quantum``, edges to ``edge_quantum``).  Before a replay,
+  ``molclr_stage_segments`` copies the batch in (one launch) and writes the
+  views' real node / edge counts to the device; inside the graph
+  ``molclr_graph_build_dev`` and the BatchNorm kernels read those counts.
+* Rows past the real nodes are padding: atoms (0, 0) without edges, outside
+  every graph, zero BatchNorm output and zero gradient, so they change no
+  parameter gradient, statistic or loss (tests/test_gpu_graph_step.py holds
+  the replayed step to the eager one).
+* The learning rate and Adam's step counter already live on the device
+  (FusedAdam); the weight planes are regenerated inside the graph.
+
+Single-process only: the data-parallel step keeps its eager path (its RCCL
+collectives overlap the backward through events on a side stream).
+"""
+from __future__ import annotations
+
+import ctypes
+from collections import OrderedDict
+
+import torch
+
+from . import _lib, ops
+from .data import DeviceGraph, _num_graphs_of
+
+
+def _round_up(n: int, q: int) -> int:
+    return max(q, (int(n) + q - 1) // q * q)
+
+
+class StagedPairGraph(DeviceGraph):
+    """A DeviceGraph over fixed capacities (node_cap rows, edge_cap edge slots)
+    whose views are staged in before every use (``stage``) and whose build
+    (``build``) reads the real sizes on the device -- both capturable."""
+
+    def __init__(self, device, node_cap: int, edge_cap: int, graphs_per_segment):
+        self.device = device
+        self.nseg = len(graphs_per_segment)
+        i64 = dict(dtype=torch.long, device=device)
+        i32 = dict(dtype=torch.int32, device=device)
+        N, E, G = int(node_cap), int(edge_cap), int(sum(graphs_per_segment))
+        self.num_nodes, self.num_edges, self.num_graphs = N, E, G
+        self.graphs_per_segment = [int(g) for g in graphs_per_segment]
+        self.segment_nodes = None  # on the device: self.counts[:nseg]
+        # staging: every segment gets the full capacity (a few MB)
+        self.st_ei = [torch.zeros(2, E, **i64) for _ in range(self.nseg)]
+        self.st_ea = [torch.zeros(E, 2, **i64) for _ in range(self.nseg)]
+        self.st_batch = [torch.zeros(N, **i64) for _ in range(self.nseg)]
+        self.x = torch.zeros(N, 2, **i64)
+        self.counts = torch.zeros(2 * self.nseg, **i64)
+        self._dst = (_lib.StagedSegmentC * self.nseg)()
+        for q in range(self.nseg):
+            self._dst[q] = _lib.StagedSegmentC(self.st_ei[q].data_ptr(), self.st_ea[q].data_ptr(),
+                                               self.st_batch[q].data_ptr(), N, E,
+                                               self.graphs_per_segment[q])
+        self.rowptr = torch.empty(N + 1, **i32)
+        self.col = torch.empty(E, **i32)
+        self.ecode = torch.empty(E, dtype=torch.uint8, device=device)
+        self.rowptr_t = torch.empty(N + 1, **i32)
+        self.col_t = torch.empty(E, **i32)
+        self.nbr = torch.empty(N * 4, **i32)
+        self.nbr_t = torch.empty(N * 4, **i32)
+        self.ecount = torch.empty(N * 8, **i32)
+        self.graph_ptr = torch.empty(G + 1, **i32)
+        self.status = torch.zeros(1, **i32)
+        self._ws_bytes = _lib.query("molclr_graph_build_workspace_bytes", N, E)
+        self._ws = torch.empty(self._ws_bytes, dtype=torch.uint8, device=device)
+        self._keep = []
+
+    def fits(self, views) -> bool:
+        n = sum(int(v.x.shape[0]) for v in views)
+        e = sum(int(v.edge_index.shape[1]) for v in views)
+        return (n <= self.num_nodes and e <= self.num_edges
+                and [_num_graphs_of(v) for v in views] == self.graphs_per_segment)
+
+    def stage(self, views) -> None:
+        """Copy the views' x / edge_index / edge_attr / batch in (one launch on
+        the current stream); the inputs must stay alive until it has run."""
+        if len(views) != self.nseg:
+            raise ValueError(f"StagedPairGraph: {len(views)} views, built for {self.nseg}")
+        src = (_lib.StageSourceC * self.nseg)()
+        keep = []
+        for q, d in enumerate(views):
+            if _num_graphs_of(d) != self.graphs_per_segment[q]:
+                raise ValueError("StagedPairGraph: a view's graph count changed "
+                                 f"({_num_graphs_of(d)} vs {self.graphs_per_segment[q]})")
+            x = d.x.to(torch.long).contiguous()
+            ei = d.edge_index.to(torch.long).contiguous()
+            ea = d.edge_attr.to(torch.long).contiguous()
+            b = getattr(d, "batch", None)
+            if b is None:
+                b = torch.zeros(x.shape[0], dtype=torch.long, device=x.device)
+            b = b.to(torch.long).contiguous()
+            keep += [x, ei, ea, b]
+            src[q] = _lib.StageSourceC(x.data_ptr(), ei.data_ptr(), ea.data_ptr(), b.data_ptr(),
+                                       int(x.shape[0]), int(ei.shape[1]))
+        _lib.call("molclr_stage_segments", self.nseg, ctypes.addressof(src),
+                  ctypes.addressof(self._dst), self.x.data_ptr(), self.num_nodes, self.num_edges,
+                  self.counts.data_ptr(), _lib.stream_of(self.device))
+        self._keep = keep  # until the next stage: the copy is asynchronous
+
+    def build(self) -> None:
+        """molclr_graph_build_dev on the current stream (capturable)."""
+        _lib.call("molclr_graph_build_dev", self.nseg, ctypes.addressof(self._dst),
+                  self.counts.data_ptr(), self.num_nodes, self.num_edges,
+                  self.rowptr.data_ptr(), self.col.data_ptr(), self.ecode.data_ptr(),
+                  self.rowptr_t.data_ptr(), self.col_t.data_ptr(), self.nbr.data_ptr(),
+                  self.nbr_t.data_ptr(), self.ecount.data_ptr(), self.graph_ptr.data_ptr(),
+                  self.status.data_ptr(), self._ws.data_ptr(), self._ws_bytes,
+                  _lib.stream_of(self.device))
+
+    def cstruct(self):
+        c = getattr(self, "_cstruct", None)
+        if c is None:
+            c = _lib.DeviceGraphC(self.num_nodes, self.num_edges, self.num_graphs, *[
+                t.data_ptr() for t in (self.rowptr, self.col, self.rowptr_t, self.col_t,
+                                       self.ecount, self.graph_ptr, self.ecode, self.nbr,
+                                       self.nbr_t)])
+            c.num_segments = self.nseg
+            c.segment_nodes_dev = self.counts.data_ptr()
+            self._cstruct = c
+        return c
+
+
+class _Captured:
+    def __init__(self, graph: StagedPairGraph, cuda_graph):
+        self.graph = graph
+        self.cuda_graph = cuda_graph
+
+
+class CapturedTrainStep:
+    """``step(xis, xjs) -> loss``: one MolCLR training step (molclr.py:108-128:
+    zero_grad, the paired encoder pass, normalize, NT-Xent, backward, Adam)
+    replayed from a HIP graph captured per (node, edge) capacity bucket.
+
+    The returned loss tensor is this object's own buffer, overwritten by the
+    next step.  Requirements: a model with the paired executor path
+    (``forward_staged``), a FusedAdam optimizer, one process."""
+
+    def __init__(self, model, optimizer, criterion, node_quantum: int = 256,
+                 edge_quantum: int = 2048, max_graphs: int = 16):
+        from .optim import FusedAdam
+        if not isinstance(optimizer, FusedAdam):
+            raise TypeError("CapturedTrainStep needs molclr_amd.optim.FusedAdam "
+                            "(learning rate and step counter on the device)")
+        if not hasattr(model, "forward_staged"):
+            raise TypeError("CapturedTrainStep: the model has no forward_staged")
+        if getattr(criterion, "group", None) is not None:
+            raise ValueError("CapturedTrainStep runs one process; the data-parallel step is eager")
+        self.model, self.optimizer, self.criterion = model, optimizer, criterion
+        self.node_quantum, self.edge_quantum = int(node_quantum), int(edge_quantum)
+        self.max_graphs = int(max_graphs)
+        self.device = optimizer.flat.device
+        self._graphs: OrderedDict = OrderedDict()
+        self._pool = torch.cuda.graph_pool_handle()
+        self.loss = torch.zeros((), dtype=torch.float32, device=self.device)
+        self.captures = 0
+        self.last_graph: StagedPairGraph | None = None
+
+    def bucket(self, xis, xjs) -> tuple:
+        n = int(xis.x.shape[0]) + int(xjs.x.shape[0])
+        e = int(xis.edge_index.shape[1]) + int(xjs.edge_index.shape[1])
+        return (_round_up(n, self.node_quantum), _round_up(e, self.edge_quantum),
+                _num_graphs_of(xis), _num_graphs_of(xjs))
+
+    def _capture(self, key, xis, xjs) -> _Captured:
+        if not self.model._executor_ok() or self.model._dim_pad():
+            raise NotImplementedError(
+                "CapturedTrainStep: the model must run through the encoder executor with "
+                "emb_dim a multiple of the kernels' width (dropout 0, tracked BatchNorm)")
+        ops._check_no_timer()
+        graph = StagedPairGraph(self.device, key[0], key[1], key[2:])
+        graph.stage([xis, xjs])
+        opt = self.optimizer
+        opt.sync_lr()
+        # the capture must record the weight-plane regeneration: make every
+        # cached image stale so the forward's first lookup refreshes them all
+        ops.bump_param_generation()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g, pool=self._pool):
+            graph.build()
+            opt.zero_grad()
+            _, z = self.model.forward_staged(graph)
+            loss = self.criterion.forward_pair(ops.l2_normalize(z))
+            loss.backward()
+            opt.step(sync_lr=False)
+            self.loss.copy_(loss)
+        del loss, z
+        self.captures += 1
+        return _Captured(graph, g)
+
+    def __call__(self, xis, xjs) -> torch.Tensor:
+        key = self.bucket(xis, xjs)
+        ent = self._graphs.get(key)
+        if ent is None:
+            ent = self._capture(key, xis, xjs)  # stages this batch too
+            self._graphs[key] = ent
+            if len(self._graphs) > self.max_graphs:
+                self._graphs.popitem(last=False)
+        else:
+            self._graphs.move_to_end(key)
+            ent.graph.stage([xis, xjs])
+            self.optimizer.sync_lr()
+        ent.cuda_graph.replay()
+        # the replay's Adam step changed the weights behind Python's back
+        ops.bump_param_generation()
+        self.last_graph = ent.graph
+        return self.loss

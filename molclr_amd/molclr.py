@@ -14,7 +14,9 @@ Differences (all additive): the optimiser is :class:`FusedAdam` (same update
 rule, one kernel); optional config keys ``world_size`` (data parallel via
 torchrun), ``seed``, ``dataset.views`` ('device', the default: both views of
 every batch are built on the GPU from the resident molecules, for every
-``aug`` mode; 'host': the reference's DataLoader, node masking only); the
+``aug`` mode; 'host': the reference's DataLoader, node masking only),
+``hip_graph`` (True: one process replays the whole step from HIP graphs
+captured per batch-size bucket, molclr_amd.graph_step); the
 scalar writer is TensorBoard when installed, otherwise a JSONL file with the
 same tags.  ``data_path`` may be the reference's SMILES text file (featurised
 once into a cached binary shard), a shard, or ``synthetic:<count>``.
@@ -144,10 +146,32 @@ class MolCLR(object):
                                       eta_min=0, last_epoch=-1)
         return optimizer, scheduler
 
+    def _graph_step(self, model, optimizer):
+        """The HIP-graph step (molclr_amd.graph_step) when the config asks for
+        it (``hip_graph: True``) and the run allows it: one process, the
+        paired executor pass at an unpadded width; else None (eager)."""
+        if not self.config.get('hip_graph', False) or self.world > 1:
+            return None
+        if not getattr(self, "paired", True) or not hasattr(model, "forward_staged"):
+            return None
+        if not model._executor_ok() or model._dim_pad():
+            return None
+        cs = getattr(self, "_captured", None)
+        if cs is None or cs.model is not model or cs.optimizer is not optimizer:
+            from .graph_step import CapturedTrainStep
+            cs = self._captured = CapturedTrainStep(model, optimizer, self.nt_xent_criterion)
+        return cs
+
     def train_step(self, model, optimizer, xis, xjs, n_iter):
-        optimizer.zero_grad()
         xis = xis.to(self.device, non_blocking=True)
         xjs = xjs.to(self.device, non_blocking=True)
+        cs = self._graph_step(model, optimizer)
+        if cs is not None:  # zero_grad .. Adam replayed as one HIP graph
+            loss = cs(xis, xjs)
+            self._last_graph = cs.last_graph
+            return loss
+        self._last_graph = None
+        optimizer.zero_grad()
         reducer = getattr(self, "reducer", None)
         if reducer is not None:
             reducer.arm()
@@ -211,6 +235,9 @@ class MolCLR(object):
         features outside the embedding tables, where the reference's
         nn.Embedding raises IndexError).  Reads the graph's device status word
         (a sync: called where the loop syncs anyway, at the log steps)."""
+        if getattr(self, "_last_graph", None) is not None:  # the captured step's graph
+            self._last_graph.check()
+            return
         xi = getattr(self, "_last_inputs", None)
         g = getattr(xi, "_molclr_pair_graph", None) or (None, getattr(xi, "_molclr_graph", None))
         if g[1] is not None:
@@ -237,6 +264,7 @@ class MolCLR(object):
                 xjs = xjs.to(self.device)
                 loss = self._step(model, xis, xjs, counter)
                 self._last_inputs = xis
+                self._last_graph = None
                 valid_loss += loss.item()
                 self.check_inputs()
                 counter += 1

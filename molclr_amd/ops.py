@@ -127,6 +127,12 @@ def set_kernel_timer(timer: KernelTimer | None) -> None:
     _TIMER = timer
 
 
+def _check_no_timer() -> None:
+    """A HIP-graph capture cannot hold the timer's dispatch events."""
+    if _TIMER is not None:
+        raise RuntimeError("molclr_amd: stop the kernel timer before capturing a step")
+
+
 # Gradient-ready hook of the data-parallel reducer
 # (molclr_amd.distributed.OverlappedGradReducer): told when an encoder
 # backward starts, given per-layer events the executor records, and told when

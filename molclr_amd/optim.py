@@ -73,13 +73,22 @@ class FusedAdam(torch.optim.Optimizer):
                 p.grad = self.flat_grad[off:off + n].view_as(p)
 
     @torch.no_grad()
-    def step(self, closure=None):
-        loss = closure() if closure is not None else None
-        g = self.param_groups[0]
-        lr = float(g["lr"])
+    def sync_lr(self) -> None:
+        """Copy the param group's learning rate (a scheduler may have changed
+        it) to the device value the kernel reads."""
+        lr = float(self.param_groups[0]["lr"])
         if lr != self._lr_host:
             self._lr_dev.fill_(lr)
             self._lr_host = lr
+
+    @torch.no_grad()
+    def step(self, closure=None, sync_lr: bool = True):
+        """``sync_lr=False`` while capturing a HIP graph: the replays read the
+        device learning rate, which the caller syncs before each replay."""
+        loss = closure() if closure is not None else None
+        g = self.param_groups[0]
+        if sync_lr:
+            self.sync_lr()
         b1, b2 = g["betas"]
         _lib.call("molclr_adam_step", self.flat.data_ptr(), self.flat_grad.data_ptr(),
                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,

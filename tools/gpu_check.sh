@@ -32,6 +32,10 @@ for s in $steps; do
     gpmc)    for c in ${PMC_CASES:-qb_lin2:1}; do
                CASE=${c%%:*} VARIANT=${c##*:} run "gpmc_${c%%:*}_${c##*:}" 400 bash tools/gemm_pmc.sh; rc=$?; [ $rc -eq 0 ] || exit $rc
              done ;;
+    graph)   run graph 600 python -m pytest tests/test_gpu_graph_step.py -m gpu -q --maxfail=50 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    trainer) run trainer 600 python -m pytest tests/test_gpu_trainer.py -m gpu -q --maxfail=50 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    benche)  run benche 600 python bench.py --no-cpu-baseline --no-hip-graph; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    bench3e) run bench3e 600 python bench.py --no-cpu-baseline --config c3 --no-hip-graph; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     smoke)   run smoke 300 python __graft_entry__.py smoke; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench)   run bench 600 python bench.py --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench2)  run bench2 600 python bench.py --no-cpu-baseline --two-pass; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
