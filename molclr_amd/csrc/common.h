@@ -161,6 +161,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
+// LDS written by this wave, then read back by it (a wave-private tile): order
+// the wave's own accesses, no block barrier
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------------------
 // Storage types of node-feature matrices.  Kernels over [rows, D] matrices are
 // templated on one of these: a "column unit" is 4 consecutive elements, read

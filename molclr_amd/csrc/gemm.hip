@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
         tw[row * 32 + li] = H3 ? __builtin_ldexpf(acc[b][r], -(sr + shb)) : acc[b][r];
       }
     }
-    __syncthreads();
+    wave_lds_sync();  // tw is this wave's own 4 KB: no block barrier
     if (grp == 0) {
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
         }
       }
     }
-    __syncthreads();  // the wave's tile is rewritten by the next block
+    wave_lds_sync();  // the wave's tile is rewritten by the next block
   }
   {
     if (crow != nullptr && grp == 0) {
@@ -1301,7 +1301,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
         tw[((r & 3) + 8 * (r >> 2) + 4 * lh) * 32 + li] =
             H3 ? __builtin_ldexpf(acc[b][r], -(sha + shb)) : acc[b][r];
     }
-    __syncthreads();
+    wave_lds_sync();  // tw is this wave's own 4 KB: no block barrier
     if (grp == 0) {
 #pragma unroll
       for (int it = 0; it < 4; ++it) {
@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
               *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
       }
     }
-    __syncthreads();
+    wave_lds_sync();
   }
 }
 

@@ -24,11 +24,6 @@ using namespace molclr;
 
 // LDS written by a wave and read back by other lanes of the SAME wave: wait
 // for the wave's LDS operations, no workgroup barrier
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // One K step of B: a [BN][32] image (xoff swizzle) of the weight plane,
 // rows clamped into the padded planes (columns >= N are never stored).

@@ -58,6 +58,9 @@ def main():
         ("dz1 = dz W2 * (a1>0)", dz, p2t, out_h, H, D, EPI_RELU_MASK, None, a1,
          lambda: (dz @ W2b).mul_(a1 > 0)),
         ("dagg = dz1 W0", dz1, p0t, out_d, D, H, EPI_NONE, None, None, lambda: dz1 @ W0b),
+        # the lin1 / dz1 shapes without their epilogues: what the epilogue costs
+        ("lin1 shape, no epilogue", agg, p0, out_h, H, D, EPI_NONE, None, None,
+         lambda: agg @ W0b.t()),
     ]
     for name, A, P, C, N, K, epi, bias, aux, ref in cases:
         fl = 2.0 * M * N * K
