@@ -876,6 +876,17 @@ int molclr_gemm_bf16_impl(const uint16_t* A, const uint16_t* planes, uint16_t* C
                           int64_t N, int64_t K, int64_t lda, int64_t ldc, int epilogue,
                           const float* bias, const uint16_t* aux, int64_t ldaux,
                           molclr_stream_t stream, int impl);
+/* molclr_gemm_bf16 (the persistent 256 x 256 kernel; K % 64 == 0) with the
+ * ReLU mask as bits -- column-block-major words bits[n / 32][m], bit n % 32 =
+ * (C[m][n] > 0), ceil(N / 32) x M words (molclr_gemm_f32_bplanes_max's
+ * layout): epilogue MOLCLR_EPI_BIAS_RELU writes them to bits_out (the GIN
+ * MLP's first Linear, ginet_molclr.py:19-23), MOLCLR_EPI_RELU_MASK takes its
+ * mask from bits_in instead of a bf16 aux matrix (the ReLU backward): 1/16 of
+ * the mask bytes.  Results equal the aux form's bit for bit. */
+int molclr_gemm_bf16_bits(const uint16_t* A, const uint16_t* planes, uint16_t* C, int64_t M,
+                          int64_t N, int64_t K, int64_t lda, int64_t ldc, int epilogue,
+                          const float* bias, uint32_t* bits_out, const uint32_t* bits_in,
+                          molclr_stream_t stream);
 /* Linear weight / bias gradients from bf16 operands into fp32:
  * dW[n_out][n_in] (+)= Σ_r dy[r][o] x[r][i], db (+)= Σ_r dy[r][o] (db may be
  * NULL); n_out, n_in, ld_dy, ld_x multiples of 8.  Split-K partials summed in

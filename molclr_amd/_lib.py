@@ -146,6 +146,8 @@ SIGNATURES = {
     "molclr_segment_pool_bwd_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, c_int, _P]),
     "molclr_gemm_bf16": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P, _I64,
                                  _P]),
+    "molclr_gemm_bf16_bits": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P, _P,
+                                      _P]),
     "molclr_gemm_bf16_impl": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P, _P,
                                       _I64, _P, c_int]),
     "molclr_linear_wgrad_bf16_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),

@@ -236,9 +236,15 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
       uint16_t *agg = H(lay.agg[l]), *a1 = H(lay.a1[l]), *z = H(lay.z[l]);
       MOLCLR_TRY(molclr_gine_aggregate_fwd_bf16((const uint16_t*)h, g->rowptr, g->col, g->ecode,
                                                 g->nbr, Ecl, agg, N, D, stream));
-      // GINEConv.update in bf16: one MFMA per product, fp32 accumulation
-      MOLCLR_TRY(molclr_gemm_bf16(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
-                                  MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, stream));
+      // GINEConv.update in bf16: one MFMA per product, fp32 accumulation; the
+      // first product also writes a1's ReLU mask as bits for the backward
+      if (D % 64 == 0)
+        MOLCLR_TRY(molclr_gemm_bf16_bits(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
+                                         MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l],
+                                         (uint32_t*)(A + lay.bits[l]), nullptr, stream));
+      else
+        MOLCLR_TRY(molclr_gemm_bf16(agg, e->mlp0_planes[l], a1, N, 2 * D, D, D, 2 * D,
+                                    MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, stream));
       MOLCLR_TRY(molclr_gemm_bf16(a1, e->mlp2_planes[l], z, N, D, 2 * D, 2 * D, D,
                                   MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0, stream));
       MOLCLR_TRY(seg_bn_fwd(seg, z, e->bn_weight[l], e->bn_bias[l], e->bn_running_mean[l],
@@ -361,8 +367,13 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
         MOLCLR_TRY(molclr_linear_wgrad_bf16(hz, ha1, gr->mlp2_weight[l], gr->mlp2_bias[l], N, D,
                                             2 * D, D, 2 * D, 1, kws, kws_bytes, stream));
       }
-      MOLCLR_TRY(molclr_gemm_bf16(hz, e->mlp2_planes_t[l], (uint16_t*)dz1, N, 2 * D, D, D, 2 * D,
-                                  MOLCLR_EPI_RELU_MASK, nullptr, ha1, 2 * D, stream));
+      if (D % 64 == 0)  // the mask from the forward's bits
+        MOLCLR_TRY(molclr_gemm_bf16_bits(hz, e->mlp2_planes_t[l], (uint16_t*)dz1, N, 2 * D, D, D,
+                                         2 * D, MOLCLR_EPI_RELU_MASK, nullptr, nullptr,
+                                         (const uint32_t*)(A + lay.bits[l]), stream));
+      else
+        MOLCLR_TRY(molclr_gemm_bf16(hz, e->mlp2_planes_t[l], (uint16_t*)dz1, N, 2 * D, D, D, 2 * D,
+                                    MOLCLR_EPI_RELU_MASK, nullptr, ha1, 2 * D, stream));
       if (gr->mlp0_weight[l] || gr->mlp0_bias[l]) {
         MOLCLR_REQUIRE(gr->mlp0_weight[l], "gin_encoder_bwd: bf16 needs the weight gradient");
         MOLCLR_TRY(molclr_linear_wgrad_bf16((const uint16_t*)dz1, (const uint16_t*)agg,

@@ -24,6 +24,8 @@
 // once per XCD rather than once per column tile.
 #include "mfma.h"
 
+#include <stdlib.h>
+
 namespace {
 
 using namespace molclr;
@@ -831,6 +833,40 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   const int64_t m0 = (int64_t)(tile / ntn) * kQ6BM;
   const int64_t n0 = (int64_t)(tile % ntn) * BN;
 
+  // What the epilogue reads -- bias columns, ReLU-mask words -- is loaded
+  // here, ahead of the main loop: CDNA4's vmcnt counts stores too, so a load
+  // issued among the epilogue's stores waits for all of them.  Epilogue lane
+  // (row, c4): columns nb + 4 c4 .. +3 of rows mw + 8 it + lane / 8.
+  constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
+  constexpr int BVN = HAS_BIAS ? TN : 1, MWN = EPI == MOLCLR_EPI_RELU_MASK ? TN : 1;
+  float4 bvq[BVN];
+  uint32_t mwq[MWN][4];
+  if (grp == 0) {
+    const int c4l = lane & 7;
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int64_t n = n0 + 32 * b + 4 * c4l;
+        bvq[b] = (n + 4 <= N && (reinterpret_cast<uintptr_t>(bias) & 15) == 0)
+                     ? *reinterpret_cast<const float4*>(bias + n) : f4zero();
+      }
+    }
+    if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+      if (bits_in != nullptr) {  // block-uniform
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            int64_t m = m0 + 32 * wm + 8 * it + (lane >> 3);
+            m = m < M ? m : M - 1;
+            int64_t nb = n0 + 32 * b;
+            nb = nb < N ? nb : 0;
+            mwq[b][it] = bits_in[(nb >> 5) * bits_ld + m];
+          }
+      }
+    }
+  }
+
   int64_t arow_i = m0 + 32 * wm + li;
   arow_i = arow_i < M ? arow_i : M - 1;
   const float* __restrict__ arow = A + arow_i * lda;
@@ -1016,12 +1052,12 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
           float* o = C + m * ldc + n;
           // the mask nibble of this lane's columns (RELU_MASK with bits_in)
           uint32_t mk = 15u;
-          if (EPI == MOLCLR_EPI_RELU_MASK && bits_in != nullptr)
-            mk = (bits_in[(nb >> 5) * bits_ld + m] >> (4 * c4)) & 15u;
+          if constexpr (EPI == MOLCLR_EPI_RELU_MASK)
+            if (bits_in != nullptr) mk = (mwq[b][it] >> (4 * c4)) & 15u;
           if (vec && n + 4 <= N) {
             float4 v = v4;
-            if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
-              v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
+            if constexpr (HAS_BIAS) {
+              v = f4add(v, bvq[b]);
               if (EPI == MOLCLR_EPI_BIAS_RELU)
                 v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
             }
@@ -1687,9 +1723,17 @@ int64_t q6_blocks(int64_t M, int64_t N) {
 }
 
 // in-block K groups: two for narrow products (fewer than 1.5 blocks per CU)
-// with at least 8 K steps, else one
+// with at least 8 K steps, else one.  MOLCLR_Q6_GROUPS = 1 / 2 forces the
+// count for products of at least 8 K steps (a diagnostic: the K-chain length
+// of the fp32 sums, tools/order_spread.py).
 int q6_groups(int64_t M, int64_t N, int64_t K) {
-  return (q6_blocks(M, N) < 384 && (K + BK - 1) / BK >= 8) ? 2 : 1;
+  static const int forced = [] {
+    const char* e = getenv("MOLCLR_Q6_GROUPS");
+    return e ? atoi(e) : 0;
+  }();
+  if ((K + BK - 1) / BK < 8) return 1;
+  if (forced == 1 || forced == 2) return forced;
+  return q6_blocks(M, N) < 384 ? 2 : 1;
 }
 
 template <int TN, int EPI, int KG, bool MASK, int H3>

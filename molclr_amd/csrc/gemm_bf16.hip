@@ -393,6 +393,9 @@ __global__ __launch_bounds__(512) void k_gemm_tb(
   }
 }
 
+// bf16 bit pattern h (low 16 bits) > 0: +denormal .. +inf, not +0, NaN or negative
+__device__ __forceinline__ bool bf16_pos(uint32_t h) { return h - 1u < 0x7F80u; }
+
 // ---------------------------------------------------------------------------
 // k_gemm_tp: k_gemm_tb as a persistent kernel.  One block per CU walks its
 // share of the output tiles; the first K step of the NEXT tile is DMA-staged
@@ -404,12 +407,23 @@ __global__ __launch_bounds__(512) void k_gemm_tb(
 // Tiles: XCD x's blocks own a contiguous range of logical tiles (row slab
 // major), in proportion to their number; block p of the XCD takes every P-th.
 // Results are identical to k_gemm_tb (same fragments, same MFMA order).
+// BITS: the ReLU mask as bits, column-block-major words [n / 32][m] (bits_ld
+// = M; k_gemm_q6's layout): a BIAS_RELU product writes bit (n % 32) = (C > 0)
+// to bits_out, a RELU_MASK product reads its mask from bits_in instead of aux
+// (1/16 of the bytes).  Everything the epilogue reads -- bias, mask words --
+// is loaded at the start of the tile, ahead of the K loop: CDNA4's vmcnt
+// counts stores too, so a load issued among the epilogue's stores would wait
+// for them all.
 // ---------------------------------------------------------------------------
-template <int EPI, int NW>
+template <int EPI, int NW, bool BITS = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bp, uint16_t* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
-    const float* __restrict__ bias, const uint16_t* __restrict__ aux, int64_t ldaux) {
+    const float* __restrict__ bias, const uint16_t* __restrict__ aux, int64_t ldaux,
+    uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in, int64_t bits_ld) {
+  constexpr bool MASK_BITS = BITS && EPI == MOLCLR_EPI_RELU_MASK;
+  constexpr bool OUT_BITS = BITS && EPI == MOLCLR_EPI_BIAS_RELU;
+  constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
   constexpr int BM = 256, BN = 256, KT = 64;
   constexpr int SI = BM * KT * 2;       // bytes per operand image per stage (32 KB)
   constexpr int WMW = NW == 8 ? 4 : 2;  // waves along M (8 waves: 4 x 2, 4 waves: 2 x 2)
@@ -492,8 +506,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
   // this lane's epilogue pieces of a 32 x 32 block: rows (lane >> 3) + 8 it,
   // columns 4 (lane & 7) .. +3
   const int erow = lane >> 3, ec4 = lane & 7;
-  uint2 am[2][TJ][4];  // ReLU-mask operand of one row of blocks, one row ahead
-  auto fetch_mask = [&](int64_t m0, int64_t n0, int i, uint2(&dst)[TJ][4]) {
+  constexpr bool AUX_MASK = EPI == MOLCLR_EPI_RELU_MASK && !MASK_BITS;
+  constexpr int AMI = AUX_MASK ? 2 : 1, AMJ = AUX_MASK ? TJ : 1;
+  uint2 am[AMI][AMJ][4];  // ReLU-mask operand of one row of blocks, one row ahead
+  auto fetch_mask = [&](int64_t m0, int64_t n0, int i, uint2(&dst)[AMJ][4]) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j)
 #pragma unroll
@@ -513,10 +529,21 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
   stage(0, asrc, bsrc, 0);
   __syncthreads();
   int buf = 0;
+  constexpr int BVJ = HAS_BIAS ? TJ : 1, MWI = MASK_BITS ? TI : 1, MWJ = MASK_BITS ? TJ : 1;
+  float4 bv[BVJ];           // this lane's bias columns of the tile
+  uint32_t mw[MWI][MWJ][4];  // this lane's mask words of the tile (MASK_BITS)
   for (;;) {
     const int64_t m0 = (int64_t)(t / ntn) * BM, n0 = (int64_t)(t % ntn) * BN;
     const int tn = t + P;
     const bool more = tn < hi;
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int64_t n = n0 + 32 * TJ * wn + 32 * j + 4 * ec4;
+        bv[j] = n + 4 <= N ? *reinterpret_cast<const float4*>(bias + n) : f4zero();
+      }
+    }
+
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -537,10 +564,27 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
       buf ^= 1;
     }
 
-    if (EPI == MOLCLR_EPI_RELU_MASK) fetch_mask(m0, n0, 0, am[0]);
+    if constexpr (MASK_BITS) {
+      // the tile's mask words, all loaded before the first store (then one
+      // latency per tile); held through the K loop they would spill
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            int64_t m = m0 + 32 * TI * wm + 32 * i + erow + 8 * it;
+            m = m < M ? m : M - 1;
+            int64_t nb = n0 + 32 * TJ * wn + 32 * j;
+            nb = nb < N ? nb : 0;
+            mw[i][j][it] = bits_in[(nb >> 5) * bits_ld + m];
+          }
+    }
+    if constexpr (AUX_MASK) fetch_mask(m0, n0, 0, am[0]);
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
-      if (EPI == MOLCLR_EPI_RELU_MASK && i + 1 < TI) fetch_mask(m0, n0, i + 1, am[(i + 1) & 1]);
+      if constexpr (AUX_MASK)
+        if (i + 1 < TI) fetch_mask(m0, n0, i + 1, am[(i + 1) & (AMI - 1)]);
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int64_t mb = m0 + 32 * TI * wm + 32 * i, nb = n0 + 32 * TJ * wn + 32 * j;
@@ -552,28 +596,61 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
         for (int it = 0; it < 4; ++it) {
           const int row = erow + 8 * it;
           const int64_t m = mb + row, n = nb + 4 * ec4;
-          if (m >= M || n >= N) continue;
-          float4 v = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * ec4);
-          if (n + 4 <= N) {
-            if (EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU) {
-              v = f4add(v, *reinterpret_cast<const float4*>(bias + n));
-              if (EPI == MOLCLR_EPI_BIAS_RELU)
-                v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          uint32_t pos = 0;  // OUT_BITS: this lane's nibble of C > 0
+          if (m < M && n < N) {
+            float4 v = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * ec4);
+            uint32_t mk = 15u;  // MASK_BITS: this lane's mask nibble
+            if constexpr (MASK_BITS) mk = (mw[i][j][it] >> (4 * ec4)) & 15u;
+            if (n + 4 <= N) {
+              if constexpr (HAS_BIAS) {
+                v = f4add(v, bv[j]);
+                if (EPI == MOLCLR_EPI_BIAS_RELU)
+                  v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+              }
+              if constexpr (MASK_BITS) {
+                v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                                mk & 8u ? v.w : 0.f);
+              } else if constexpr (AUX_MASK) {
+                const float4 xm = bf16x4_to_f4(am[i & (AMI - 1)][j][it]);
+                v = make_float4(xm.x > 0.f ? v.x : 0.f, xm.y > 0.f ? v.y : 0.f,
+                                xm.z > 0.f ? v.z : 0.f, xm.w > 0.f ? v.w : 0.f);
+              }
+              const uint2 o = f4_to_bf16x4(v);
+              *reinterpret_cast<uint2*>(C + m * ldc + n) = o;
+              if constexpr (OUT_BITS)  // the stored bf16 values > 0 (what the aux mask tests)
+                pos = (bf16_pos(o.x & 0xFFFFu) ? 1u : 0u) | (bf16_pos(o.x >> 16) ? 2u : 0u) |
+                      (bf16_pos(o.y & 0xFFFFu) ? 4u : 0u) | (bf16_pos(o.y >> 16) ? 8u : 0u);
+            } else {
+              const float e[4] = {v.x, v.y, v.z, v.w};
+              for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+                float xv = e[jj];
+                if (EPI == MOLCLR_EPI_BIAS) xv = xv + bias[n + jj];
+                if (EPI == MOLCLR_EPI_BIAS_RELU) xv = fmaxf(xv + bias[n + jj], 0.f);
+                if constexpr (MASK_BITS) xv = ((mk >> jj) & 1u) ? xv : 0.f;
+                if constexpr (AUX_MASK)
+                  xv = bf16_to_f32(aux[m * ldaux + n + jj]) > 0.f ? xv : 0.f;
+                const uint16_t h = (uint16_t)(f32x2_to_bf16x2(xv, 0.f) & 0xFFFFu);
+                C[m * ldc + n + jj] = h;
+                if constexpr (OUT_BITS) pos |= (bf16_pos(h) ? 1u : 0u) << jj;
+              }
             }
-            if (EPI == MOLCLR_EPI_RELU_MASK) {
-              const float4 xm = bf16x4_to_f4(am[i & 1][j][it]);
-              v = make_float4(xm.x > 0.f ? v.x : 0.f, xm.y > 0.f ? v.y : 0.f, xm.z > 0.f ? v.z : 0.f,
-                              xm.w > 0.f ? v.w : 0.f);
-            }
-            *reinterpret_cast<uint2*>(C + m * ldc + n) = f4_to_bf16x4(v);
-          } else {
-            const float e[4] = {v.x, v.y, v.z, v.w};
-            for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
-              float xv = e[jj];
-              if (EPI == MOLCLR_EPI_BIAS) xv = xv + bias[n + jj];
-              if (EPI == MOLCLR_EPI_BIAS_RELU) xv = fmaxf(xv + bias[n + jj], 0.f);
-              if (EPI == MOLCLR_EPI_RELU_MASK) xv = bf16_to_f32(aux[m * ldaux + n + jj]) > 0.f ? xv : 0.f;
-              C[m * ldc + n + jj] = (uint16_t)(f32x2_to_bf16x2(xv, 0.f) & 0xFFFFu);
+          }
+          if constexpr (OUT_BITS) {
+            // a row's 8 lanes (lane / 8) hold its 32 columns as nibbles: one
+            // ballot per nibble bit, interleaved into the row's word
+            const uint64_t bj[4] = {__ballot((pos & 1u) != 0u), __ballot((pos & 2u) != 0u),
+                                    __ballot((pos & 4u) != 0u), __ballot((pos & 8u) != 0u)};
+            if (ec4 == 0 && m < M && nb < N) {
+              uint32_t w = 0;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                uint32_t x = (uint32_t)(bj[q] >> (8 * erow)) & 0xFFu;  // bit c -> bit 4 c
+                x = (x | (x << 12)) & 0x000F000Fu;
+                x = (x | (x << 6)) & 0x03030303u;
+                x = (x | (x << 3)) & 0x11111111u;
+                w |= x << q;
+              }
+              bits_out[(nb >> 5) * bits_ld + m] = w;
             }
           }
         }
@@ -1201,14 +1278,30 @@ using molclr::cu_count;
 template <int NW>
 int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,
               int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc, const float* bias,
-              const uint16_t* aux, int64_t ldaux, hipStream_t s) {
+              const uint16_t* aux, int64_t ldaux, hipStream_t s, uint32_t* bits_out = nullptr,
+              const uint32_t* bits_in = nullptr) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   MOLCLR_REQUIRE(tiles < (1ll << 31) / 256, "gemm_bf16: too many tiles");
   const int64_t cus = cu_count();
   const dim3 g((unsigned)(tiles < cus ? tiles : cus)), b(64 * NW);
+  if (bits_out || bits_in) {
+    MOLCLR_REQUIRE(bits_out ? epi == MOLCLR_EPI_BIAS_RELU : epi == MOLCLR_EPI_RELU_MASK,
+                   "gemm_bf16: ReLU bits go out of a bias+ReLU product / into a ReLU-mask one");
+    if (bits_out)
+      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<MOLCLR_EPI_BIAS_RELU, NW, true>, g, b, 0, s,
+                           A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, bits_out,
+                           bits_in, M);
+    else
+      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true>, g, b, 0, s,
+                           A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, bits_out,
+                           bits_in, M);
+    return MOLCLR_OK;
+  }
+  uint32_t* no_out = nullptr;
+  const uint32_t* no_in = nullptr;
 #define MOLCLR_TP(EPV)                                                                          \
   molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<EPV, NW>, g, b, 0, s, A, Bp, C, M, N, K, lda, kp, \
-                       npad, ldc, bias, aux, ldaux)
+                       npad, ldc, bias, aux, ldaux, no_out, no_in, (int64_t)0)
   switch (epi) {
     case MOLCLR_EPI_NONE: MOLCLR_TP(MOLCLR_EPI_NONE); return MOLCLR_OK;
     case MOLCLR_EPI_BIAS: MOLCLR_TP(MOLCLR_EPI_BIAS); return MOLCLR_OK;
@@ -1375,6 +1468,26 @@ MOLCLR_API int molclr_gemm_bf16(const uint16_t* A, const uint16_t* planes, uint1
                                 molclr_stream_t stream) {
   return molclr_gemm_bf16_impl(A, planes, C, M, N, K, lda, ldc, epilogue, bias, aux, ldaux, stream,
                                -1);
+}
+
+MOLCLR_API int molclr_gemm_bf16_bits(const uint16_t* A, const uint16_t* planes, uint16_t* C,
+                                     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc,
+                                     int epilogue, const float* bias, uint32_t* bits_out,
+                                     const uint32_t* bits_in, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(M >= 0 && N >= 0 && K > 0 && A && planes && C, "gemm_bf16_bits: bad operands");
+  MOLCLR_REQUIRE((epilogue == MOLCLR_EPI_BIAS_RELU && bias && bits_out && !bits_in) ||
+                     (epilogue == MOLCLR_EPI_RELU_MASK && bits_in && !bits_out),
+                 "gemm_bf16_bits: bias+ReLU with bits_out, or ReLU-mask with bits_in");
+  MOLCLR_REQUIRE(K % 64 == 0 && lda % 8 == 0 && lda >= K && ldc >= N && ldc % 4 == 0,
+                 "gemm_bf16_bits: K %% 64 == 0, lda %% 8 == 0, ldc %% 4 == 0 (%lld, %lld, %lld)",
+                 (long long)K, (long long)lda, (long long)ldc);
+  if (M == 0 || N == 0) return MOLCLR_OK;
+  const int64_t npad = (N + 127) / 128 * 128, kp = (K + BK - 1) / BK * BK;
+  const int rc = launch_tp<8>(epilogue, A, planes, C, M, N, K, lda, kp, npad, ldc, bias, nullptr, 0,
+                              molclr::as_stream(stream), bits_out, bits_in);
+  if (rc) return rc;
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
 }
 
 MOLCLR_API size_t molclr_linear_wgrad_bf16_workspace_bytes(int64_t rows, int64_t n_out,

@@ -92,6 +92,48 @@ def test_gemm_bf16(dev, M, N, K):
             assert torch.equal(C, outs[0]), (epi, impl)
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 1024, 512), (20000, 1024, 512), (333, 1000, 64),
+                                   (17001, 96, 128), (55342, 1024, 512)])
+def test_gemm_bf16_bits(dev, M, N, K):
+    """molclr_gemm_bf16_bits: the bias+ReLU product writes the ReLU mask as
+    column-block-major bits (bit n % 32 of word [n / 32][m] = C > 0), and the
+    ReLU-mask product given those bits equals the aux form bit for bit."""
+    from molclr_amd._lib import EPI_BIAS_RELU, EPI_RELU_MASK
+    lib = _lib.load()
+    torch.manual_seed(M + N)
+    A = bf(torch.randn(M, K)).to(dev)
+    W = torch.randn(N, K, device=dev)
+    b = torch.randn(N, device=dev)
+    dz = bf(torch.randn(M, K)).to(dev)
+    Wt = torch.randn(K, N, device=dev)
+    planes = ops.weight_planes(W, N, K, K, 0)
+    planes_t = ops.weight_planes(Wt, N, K, N, 1)
+    nw = (N + 31) // 32
+    bits = torch.full((nw, M), -1, dtype=torch.int32, device=dev)
+    C1 = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    C0 = torch.empty_like(C1)
+    assert lib.molclr_gemm_bf16_bits(A.data_ptr(), planes.data_ptr(), C1.data_ptr(), M, N, K, K, N,
+                                     EPI_BIAS_RELU, b.data_ptr(), bits.data_ptr(), None, None) == 0
+    assert lib.molclr_gemm_bf16_impl(A.data_ptr(), planes.data_ptr(), C0.data_ptr(), M, N, K, K, N,
+                                     EPI_BIAS_RELU, b.data_ptr(), None, 0, None, 8) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(C1, C0)
+    pos = torch.zeros(M, nw * 32, dtype=torch.bool, device=dev)
+    pos[:, :N] = C1.float() > 0
+    w = (pos.view(M, nw, 32).long() << torch.arange(32, device=dev)).sum(2)  # [M, nw]
+    want = w.t().contiguous().to(torch.int64) & 0xFFFFFFFF
+    assert torch.equal(bits.to(torch.int64) & 0xFFFFFFFF, want)
+    D1 = torch.empty_like(C1)
+    D0 = torch.empty_like(C1)
+    assert lib.molclr_gemm_bf16_bits(dz.data_ptr(), planes_t.data_ptr(), D1.data_ptr(), M, N, K, K,
+                                     N, EPI_RELU_MASK, None, None, bits.data_ptr(), None) == 0
+    assert lib.molclr_gemm_bf16_impl(dz.data_ptr(), planes_t.data_ptr(), D0.data_ptr(), M, N, K, K,
+                                     N, EPI_RELU_MASK, None, C1.data_ptr(), N, None, 8) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(D1, D0)
+    assert rel(D1, (dz.double() @ bf(Wt).double()) * (C1.double() > 0)) < EPS_BF16
+
+
 @pytest.mark.parametrize("rows,n_out,n_in", [(55000, 1024, 512), (55000, 512, 1024), (777, 64, 128),
                                              (8, 8, 16), (4096, 512, 256), (3001, 264, 520)])
 @pytest.mark.parametrize("acc", [0, 1])
