@@ -1,0 +1,209 @@
+// Ablation copy of k_gemm_q6 (molclr_amd/csrc/gemm.hip: x6, no epilogue, one
+// K group, TN = 5) for tools/q6_abl.py: which part of the main loop bounds it.
+// ABL bits remove one part each (results are garbage when any bit is set):
+//   1 A loads (A comes from registers)      2 the A split (VALU)
+//   4 B staging (global loads + LDS stores) 8 the MFMAs
+//  16 the epilogue stores                   32 the per-K-step barrier
+//  64 B LDS fragment reads (fragments from registers)
+// Build: tools/exp/build_q6_abl.sh (-> tools/exp/libq6_abl.so).  Experiment
+// only; nothing in the product links it.
+#include "../../molclr_amd/csrc/mfma.h"
+
+using namespace molclr;
+
+namespace {
+
+constexpr int kW = 4, kBM = 32 * kW, TN = 5, BN = 32 * TN, NP = 3, BI = NP * BN * XK;
+constexpr int T = 64 * kW;
+
+template <int ABL>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q6_abl(
+    const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C, int64_t M,
+    int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BI];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wm = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int ntn = (int)((N + BN - 1) / BN), ntm = (int)((M + kBM - 1) / kBM);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int64_t m0 = (int64_t)(tile / ntn) * kBM, n0 = (int64_t)(tile % ntn) * BN;
+  int64_t ai = m0 + 32 * wm + li;
+  ai = ai < M ? ai : M - 1;
+  const float* __restrict__ arow = A + ai * lda;
+  const int rounds = (int)(kp / BK);
+
+  // B staging units (QStageB<BN, T, 3>)
+  constexpr int UNITS = NP * BN * 4, PER = (UNITS + T - 1) / T;
+  u32x4 br[PER];
+  int goff[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int u = tid + j * T;
+    const int pl = u / (BN * 4), rem = u % (BN * 4);
+    int64_t row = n0 + (rem >> 2);
+    row = row < npad ? row : npad - 1;
+    goff[j] = (UNITS % T && u >= UNITS) ? 0 : (int)((pl * npad + row) * kp + 8 * (rem & 3));
+  }
+  auto bload = [&](int r) {
+    if (ABL & 4) return;
+    r = r < rounds ? r : rounds - 1;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (j == PER - 1 && UNITS % T && tid + j * T >= UNITS) continue;
+      br[j] = *reinterpret_cast<const u32x4*>(Bp + goff[j] + (int64_t)r * BK);
+    }
+  };
+  auto bstore = [&](uint16_t* img) {
+    if (ABL & 4) return;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int u = tid + j * T;
+      if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
+      const int pl = u / (BN * 4), rem = u % (BN * 4);
+      *reinterpret_cast<u32x4*>(img + pl * BN * XK + xoff(rem >> 2, rem & 3)) = br[j];
+    }
+  };
+  auto aload = [&](int r, float4(&v)[4]) {
+    if (ABL & 1) {
+      v[0] = make_float4(1.f + r, 2.f, 3.f, 4.f);
+      v[1] = v[2] = v[3] = v[0];
+      return;
+    }
+    r = r < rounds ? r : rounds - 1;
+    const int64_t k = (int64_t)r * BK + 16 * lh;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int64_t kj = k + 4 * j;
+      kj = kj < K - 4 ? kj : K - 4;
+      v[j] = *reinterpret_cast<const float4*>(arow + kj);
+    }
+  };
+  f32x16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[b][q] = 0.f;
+  const bf16x8 bconst = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u,
+                                                          0x3f803f80u});
+  auto compute = [&](const uint16_t* Bs, const float4(&a)[4]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 h, m, l;
+      if (ABL & 2) {
+        h = __builtin_bit_cast(u32x4, a[2 * s]);
+        m = __builtin_bit_cast(u32x4, a[2 * s + 1]);
+        l = h ^ m;
+      } else {
+        split8(a[2 * s], a[2 * s + 1], h, m, l);
+      }
+      const bf16x8 ah = __builtin_bit_cast(bf16x8, h), am = __builtin_bit_cast(bf16x8, m),
+                   al = __builtin_bit_cast(bf16x8, l);
+      const int ch = 2 * lh + s;
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int row = 32 * b + li;
+        bf16x8 bh = bconst, bm = bconst, bl = bconst;
+        if (!(ABL & 64)) {
+          bh = xfrag(Bs, row, ch);
+          bm = xfrag(Bs + BN * XK, row, ch);
+          bl = xfrag(Bs + 2 * BN * XK, row, ch);
+        }
+        if (ABL & 8) {
+          acc[b][0] += (float)ah[0] * (float)bh[0] + (float)am[1] * (float)bm[1] +
+                       (float)al[2] * (float)bl[2];
+          continue;
+        }
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[b], 0, 0, 0);
+      }
+    }
+  };
+  auto bar = [&]() {
+    if (ABL & 32) __builtin_amdgcn_wave_barrier();
+    else __syncthreads();
+  };
+  uint16_t* buf0 = lds;
+  uint16_t* buf1 = lds + BI;
+  float4 a0[4], a1[4];
+  bload(0);
+  aload(0, a0);
+  bstore(buf0);
+  bload(1);
+  aload(1, a1);
+  __syncthreads();
+  int i = 0;
+  for (; i + 2 <= rounds; i += 2) {
+    bstore(buf1);
+    bload(i + 2);
+    compute(buf0, a0);
+    aload(i + 2, a0);
+    bar();
+    bstore(buf0);
+    bload(i + 3);
+    compute(buf1, a1);
+    aload(i + 3, a1);
+    bar();
+  }
+  if (i < rounds) compute(buf0, a0);
+  __syncthreads();
+  if (ABL & 16) {  // keep the sums alive without storing the tile
+    float s = 0.f;
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += acc[b][q];
+    if (s == 12345.678f) C[0] = s;
+    return;
+  }
+  float* tw = reinterpret_cast<float*>(lds) + wm * 32 * 32;
+  const int64_t mw = m0 + 32 * wm;
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t nb = n0 + 32 * b;
+    if (nb >= N) break;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tw[((q & 3) + 8 * (q >> 2) + 4 * lh) * 32 + li] = acc[b][q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = it * 64 + lane, row = idx >> 3, c4 = idx & 7;
+      const int64_t m = mw + row, n = nb + 4 * c4;
+      if (m < M && n + 4 <= N)
+        *reinterpret_cast<float4*>(C + m * ldc + n) =
+            *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+template <int ABL>
+void launch(const float* A, const uint16_t* Bp, float* C, int64_t M, int64_t N, int64_t K,
+            int64_t lda, int64_t kp, int64_t npad, int64_t ldc, hipStream_t s) {
+  const int64_t blocks = ((M + kBM - 1) / kBM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL(k_q6_abl<ABL>, dim3((unsigned)blocks), dim3(T), 0, s, A, Bp, C, M, N, K, lda,
+                     kp, npad, ldc);
+}
+
+}  // namespace
+
+extern "C" int q6_abl(int abl, const float* A, const uint16_t* Bp, float* C, int64_t M, int64_t N,
+                      int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (abl) {
+#define Q6A(v) \
+  case v: launch<v>(A, Bp, C, M, N, K, lda, kp, npad, ldc, s); break;
+    Q6A(0) Q6A(1) Q6A(2) Q6A(3) Q6A(4) Q6A(8) Q6A(16) Q6A(32) Q6A(64) Q6A(7) Q6A(68) Q6A(36)
+    Q6A(12) Q6A(24) Q6A(72) Q6A(39) Q6A(103)
+#undef Q6A
+    default: return -1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
