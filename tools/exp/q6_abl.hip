@@ -5,6 +5,10 @@
 //   4 B staging (global loads + LDS stores) 8 the MFMAs
 //  16 the epilogue stores                   32 the per-K-step barrier
 //  64 B LDS fragment reads (fragments from registers)
+// and three additions (not removals):
+// 128 the product's MASK zeroing of A beyond K (k_gemm_q6<..., MASK = true>)
+// 256 B loaded two K steps ahead (a second register set)
+// 512 B global loads kept, their LDS stores dropped
 // Build: tools/exp/build_q6_abl.sh (-> tools/exp/libq6_abl.so).  Experiment
 // only; nothing in the product links it.
 #include "../../molclr_amd/csrc/mfma.h"
@@ -34,7 +38,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
 
   // B staging units (QStageB<BN, T, 3>)
   constexpr int UNITS = NP * BN * 4, PER = (UNITS + T - 1) / T;
-  u32x4 br[PER];
+  u32x4 br[PER], br2[(ABL & 256) ? PER : 1];
   int goff[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -44,17 +48,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
     row = row < npad ? row : npad - 1;
     goff[j] = (UNITS % T && u >= UNITS) ? 0 : (int)((pl * npad + row) * kp + 8 * (rem & 3));
   }
-  auto bload = [&](int r) {
+  auto bload_to = [&](int r, u32x4* dst) {
     if (ABL & 4) return;
     r = r < rounds ? r : rounds - 1;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       if (j == PER - 1 && UNITS % T && tid + j * T >= UNITS) continue;
-      br[j] = *reinterpret_cast<const u32x4*>(Bp + goff[j] + (int64_t)r * BK);
+      dst[j] = *reinterpret_cast<const u32x4*>(Bp + goff[j] + (int64_t)r * BK);
     }
   };
+  auto bload = [&](int r) { bload_to(r, br); };
   auto bstore = [&](uint16_t* img) {
-    if (ABL & 4) return;
+    if (ABL & (4 | 512)) return;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * T;
@@ -85,7 +90,15 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
     for (int q = 0; q < 16; ++q) acc[b][q] = 0.f;
   const bf16x8 bconst = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u,
                                                           0x3f803f80u});
-  auto compute = [&](const uint16_t* Bs, const float4(&a)[4]) {
+  auto compute = [&](const uint16_t* Bs, const float4(&a0_)[4], int rr) {
+    float4 a[4] = {a0_[0], a0_[1], a0_[2], a0_[3]};
+    if (ABL & 128) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t kj = (int64_t)rr * BK + 16 * lh + 4 * j;
+        if (kj >= K) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       u32x4 h, m, l;
@@ -129,26 +142,61 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
   uint16_t* buf0 = lds;
   uint16_t* buf1 = lds + BI;
   float4 a0[4], a1[4];
-  bload(0);
-  aload(0, a0);
-  bstore(buf0);
-  bload(1);
-  aload(1, a1);
-  __syncthreads();
   int i = 0;
-  for (; i + 2 <= rounds; i += 2) {
-    bstore(buf1);
-    bload(i + 2);
-    compute(buf0, a0);
-    aload(i + 2, a0);
-    bar();
+  if constexpr ((ABL & 256) != 0) {
+    // B two K steps ahead: br holds B(i + 1), br2 B(i + 2) at the top of step i
+    bload(0);
+    aload(0, a0);
     bstore(buf0);
-    bload(i + 3);
-    compute(buf1, a1);
-    aload(i + 3, a1);
-    bar();
+    bload_to(1, br);
+    bload_to(2, br2);
+    aload(1, a1);
+    __syncthreads();
+    for (; i + 2 <= rounds; i += 2) {
+      bstore(buf1);                         // B(i + 1)
+      bload_to(i + 3, br);
+      compute(buf0, a0, i);
+      aload(i + 2, a0);
+      bar();
+      {
+        // B(i + 2) from br2
+        for (int j = 0; j < PER; ++j) br[j] = br[j];
+      }
+      if (!(ABL & (4 | 512))) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+          const int u = tid + j * T;
+          if (j == PER - 1 && UNITS % T && u >= UNITS) continue;
+          const int pl = u / (BN * 4), rem = u % (BN * 4);
+          *reinterpret_cast<u32x4*>(buf0 + pl * BN * XK + xoff(rem >> 2, rem & 3)) = br2[j];
+        }
+      }
+      bload_to(i + 4, br2);
+      compute(buf1, a1, i + 1);
+      aload(i + 3, a1);
+      bar();
+    }
+  } else {
+    bload(0);
+    aload(0, a0);
+    bstore(buf0);
+    bload(1);
+    aload(1, a1);
+    __syncthreads();
+    for (; i + 2 <= rounds; i += 2) {
+      bstore(buf1);
+      bload(i + 2);
+      compute(buf0, a0, i);
+      aload(i + 2, a0);
+      bar();
+      bstore(buf0);
+      bload(i + 3);
+      compute(buf1, a1, i + 1);
+      aload(i + 3, a1);
+      bar();
+    }
   }
-  if (i < rounds) compute(buf0, a0);
+  if (i < rounds) compute(buf0, a0, i);
   __syncthreads();
   if (ABL & 16) {  // keep the sums alive without storing the tile
     float s = 0.f;
@@ -201,7 +249,7 @@ extern "C" int q6_abl(int abl, const float* A, const uint16_t* Bp, float* C, int
 #define Q6A(v) \
   case v: launch<v>(A, Bp, C, M, N, K, lda, kp, npad, ldc, s); break;
     Q6A(0) Q6A(1) Q6A(2) Q6A(3) Q6A(4) Q6A(8) Q6A(16) Q6A(32) Q6A(64) Q6A(7) Q6A(68) Q6A(36)
-    Q6A(12) Q6A(24) Q6A(72) Q6A(39) Q6A(103)
+    Q6A(12) Q6A(24) Q6A(72) Q6A(39) Q6A(103) Q6A(128) Q6A(256) Q6A(512) Q6A(384)
 #undef Q6A
     default: return -1;
   }
