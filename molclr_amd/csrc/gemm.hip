@@ -774,6 +774,32 @@ struct QStageB {
   }
 };
 
+// B by LDS-DMA (global_load_lds): the pre-split planes need no conversion, so
+// a K step's image is copied straight into LDS -- no staging registers, no
+// ds_write (measured: the register round trip and its LDS stores were 25-35 %
+// of the kernel, tools/q6_abl.py).  One K step = NP x BN / 16 chunks of 1 KB
+// (16 image rows of 64 B); wave w of the group issues chunks w, w + 4, ...;
+// lane l writes physical chunk l % 4 of its image row, which xoff() gives
+// the logical chunk (l % 4) ^ ((row >> 2) & 3) -- the swizzle is applied to
+// the source address.  Rows past the planes are clamped (never stored).
+template <int BN, int NP>
+__device__ __forceinline__ void q6_dma_b(const uint16_t* __restrict__ Bp, int64_t n0, int64_t npad,
+                                         int64_t kp, int64_t k0, uint16_t* img, int wm, int lane) {
+  constexpr int RPB = BN / 16, CH = NP * RPB, PERW = (CH + kQ6Waves - 1) / kQ6Waves;
+  static_assert(BN % 16 == 0, "q6 DMA: 16-row chunks");
+#pragma unroll
+  for (int qq = 0; qq < PERW; ++qq) {
+    const int q = wm + kQ6Waves * qq;
+    if (CH % kQ6Waves && q >= CH) break;  // wave-uniform
+    const int pl = q / RPB, row = (q % RPB) * 16 + (lane >> 2), c = lane & 3;
+    int64_t gr = n0 + row;
+    gr = gr < npad ? gr : npad - 1;
+    __builtin_amdgcn_global_load_lds(
+        (gbl_as_ptr)(Bp + (pl * npad + gr) * kp + k0 + 8 * (c ^ ((row >> 2) & 3))),
+        (lds_as_ptr)(img + (pl * BN + (q % RPB) * 16) * XK), 16, 0, 0);
+  }
+}
+
 // KG > 1 splits K inside the block: KG groups of 4 waves take the K steps
 // g, g + KG, ... of the same tile, each with its own B ring, and group 0 adds
 // the other groups' sums (in group order, through LDS) before the epilogue.
@@ -960,32 +986,27 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     }
   };
 
-  QStageB<BN, T, NP> sb;
-  sb.init(n0, npad, kp, gt);
   uint16_t* buf0 = lds + grp * 2 * BI;
   uint16_t* buf1 = buf0 + BI;
   float4 a0[4], a1[4];
-  sb.load(Bp, kb(0), gt);
+  (void)gt;
+  q6_dma_b<BN, NP>(Bp, n0, npad, kp, kb(0), buf0, wm, lane);
   load_a(0, a0);
-  sb.store(buf0, gt);
-  sb.load(Bp, kb(1), gt);
-  load_a(1, a1);
   __syncthreads();
-  // At the top of an iteration (i even): buf0 holds B(i) (visible), sb holds
-  // B(i+1) in flight, a0 = A(i), a1 = A(i+1) in flight.  B(i+1) is written
-  // right after the barrier into the buffer the previous step read; one
-  // barrier per K step.  Loads past the last round re-read a clamped step.
+  // Step i: its top issues every load it leaves for step i + 1 -- the DMA of
+  // B(i + 1) into the other buffer and A(i + 1) into the other register set
+  // -- then the MFMAs of step i, then the barrier (whose vmcnt(0) the compute
+  // phase has already covered).  One barrier per K step.  Loads past the
+  // last round re-read a clamped step.
   int i = 0;
   for (; i + 2 <= rounds; i += 2) {
-    sb.store(buf1, gt);
-    sb.load(Bp, kb(i + 2), gt);
+    q6_dma_b<BN, NP>(Bp, n0, npad, kp, kb(i + 1), buf1, wm, lane);
+    load_a(i + 1, a1);
     compute(buf0, a0, i);
-    load_a(i + 2, a0);
     __syncthreads();
-    sb.store(buf0, gt);
-    sb.load(Bp, kb(i + 3), gt);
+    q6_dma_b<BN, NP>(Bp, n0, npad, kp, kb(i + 2), buf0, wm, lane);
+    load_a(i + 2, a0);
     compute(buf1, a1, i + 1);
-    load_a(i + 3, a1);
     __syncthreads();
   }
   if (i < rounds) compute(buf0, a0, i);  // odd count: B(i) is in buf0

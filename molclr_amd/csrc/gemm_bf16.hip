@@ -250,8 +250,6 @@ __global__ __launch_bounds__(64 * WM * WN) void k_gemm_qb(
 // hits 16 distinct 16-byte slots.  Requires K % 64 == 0 (the host falls back
 // to k_gemm_qb otherwise).
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void* lds_as_ptr;
-typedef const __attribute__((address_space(1))) void* gbl_as_ptr;
 
 __device__ __forceinline__ int t128(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
 

@@ -18,6 +18,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+// LDS-DMA operands of __builtin_amdgcn_global_load_lds
+typedef __attribute__((address_space(3))) void* lds_as_ptr;
+typedef const __attribute__((address_space(1))) void* gbl_as_ptr;
+
 constexpr int BK = 32;  // K per staged slice
 constexpr int XK = 32;  // bf16 per [row][k] image row (64 B, unpadded, chunk-swizzled)
 

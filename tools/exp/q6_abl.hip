@@ -9,6 +9,13 @@
 // 128 the product's MASK zeroing of A beyond K (k_gemm_q6<..., MASK = true>)
 // 256 B loaded two K steps ahead (a second register set)
 // 512 B global loads kept, their LDS stores dropped
+// 1024 B staged by LDS-DMA (global_load_lds, source-side swizzle): no B
+//      registers, no ds_write; the DMA for step i + 1 waited for before the
+//      step's barrier
+// 2048 K steps taken from step blockIdx % rounds on (wrapping): blocks of one
+//      column tile read different B slices at a time (L2 hot-spot test)
+// 4096 8 waves per block (256 rows) sharing each B stage: half the B staging
+//      per MFMA, one block per CU
 // Build: tools/exp/build_q6_abl.sh (-> tools/exp/libq6_abl.so).  Experiment
 // only; nothing in the product links it.
 #include "../../molclr_amd/csrc/mfma.h"
@@ -17,13 +24,16 @@ using namespace molclr;
 
 namespace {
 
-constexpr int kW = 4, kBM = 32 * kW, TN = 5, BN = 32 * TN, NP = 3, BI = NP * BN * XK;
-constexpr int T = 64 * kW;
+typedef __attribute__((address_space(3))) void* lds_as_ptr;
+typedef const __attribute__((address_space(1))) void* gbl_as_ptr;
 
-template <int ABL>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q6_abl(
+constexpr int TN = 5, BN = 32 * TN, NP = 3, BI = NP * BN * XK;
+
+template <int ABL, int kW = (ABL & 4096) ? 8 : 4>
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(2))) void k_q6_abl(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C, int64_t M,
     int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc) {
+  constexpr int kBM = 32 * kW, T = 64 * kW;
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BI];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wm = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -35,6 +45,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
   ai = ai < M ? ai : M - 1;
   const float* __restrict__ arow = A + ai * lda;
   const int rounds = (int)(kp / BK);
+  const int rot = (ABL & 2048) ? (int)(blockIdx.x % rounds) : 0;
+  auto kstep = [&](int r) {  // logical step r -> the K slice it reads
+    r = r < rounds ? r : rounds - 1;
+    r += rot;
+    return r >= rounds ? r - rounds : r;
+  };
 
   // B staging units (QStageB<BN, T, 3>)
   constexpr int UNITS = NP * BN * 4, PER = (UNITS + T - 1) / T;
@@ -50,7 +66,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
   }
   auto bload_to = [&](int r, u32x4* dst) {
     if (ABL & 4) return;
-    r = r < rounds ? r : rounds - 1;
+    r = kstep(r);
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       if (j == PER - 1 && UNITS % T && tid + j * T >= UNITS) continue;
@@ -58,8 +74,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
     }
   };
   auto bload = [&](int r) { bload_to(r, br); };
+  uint32_t sink = 0;  // ABL 512: the loaded B consumed without an LDS store
   auto bstore = [&](uint16_t* img) {
-    if (ABL & (4 | 512)) return;
+    if (ABL & 4) return;
+    if (ABL & 512) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) sink ^= br[j].x ^ br[j].w;
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int u = tid + j * T;
@@ -68,13 +90,31 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
       *reinterpret_cast<u32x4*>(img + pl * BN * XK + xoff(rem >> 2, rem & 3)) = br[j];
     }
   };
+  // LDS-DMA of B(r) into img: 30 chunks of 1 KB (16 image rows each), wave w
+  // issues chunks w, w + 4, ...; lane l writes physical chunk l % 4 of image
+  // row 16 q' + l / 4, which holds the logical chunk (l % 4) ^ ((row >> 2) & 3)
+  auto bdma = [&](int r, uint16_t* img) {
+    r = kstep(r);
+#pragma unroll
+    for (int qq = 0; qq < (NP * BN / 16 + kW - 1) / kW; ++qq) {
+      const int q = wm + kW * qq;
+      if (q >= NP * BN / 16) break;  // wave-uniform
+      const int pl = q / (BN / 16), row = (q % (BN / 16)) * 16 + (lane >> 2), c = lane & 3;
+      int64_t gr = n0 + row;
+      gr = gr < npad ? gr : npad - 1;
+      const uint16_t* src = Bp + (pl * npad + gr) * kp + (int64_t)r * BK + 8 * (c ^ ((row >> 2) & 3));
+      __builtin_amdgcn_global_load_lds((gbl_as_ptr)src,
+                                       (lds_as_ptr)(img + (pl * BN + (q % (BN / 16)) * 16) * XK),
+                                       16, 0, 0);
+    }
+  };
   auto aload = [&](int r, float4(&v)[4]) {
     if (ABL & 1) {
       v[0] = make_float4(1.f + r, 2.f, 3.f, 4.f);
       v[1] = v[2] = v[3] = v[0];
       return;
     }
-    r = r < rounds ? r : rounds - 1;
+    r = kstep(r);
     const int64_t k = (int64_t)r * BK + 16 * lh;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -143,7 +183,26 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
   uint16_t* buf1 = lds + BI;
   float4 a0[4], a1[4];
   int i = 0;
-  if constexpr ((ABL & 256) != 0) {
+  if constexpr ((ABL & 1024) != 0) {
+    // B(i + 1) DMA'd into the other buffer at the top of step i, landed by
+    // the step's barrier; A two register sets as the product
+    // every load of step i (the DMA of B(i + 1), the registers of A(i + 1))
+    // is issued at its top and lands by its barrier: the barrier's vmcnt(0)
+    // then costs nothing the compute phase did not already cover
+    bdma(0, buf0);
+    aload(0, a0);
+    __syncthreads();
+    for (; i + 2 <= rounds; i += 2) {
+      bdma(i + 1, buf1);
+      aload(i + 1, a1);
+      compute(buf0, a0, i);
+      bar();
+      bdma(i + 2, buf0);
+      aload(i + 2, a0);
+      compute(buf1, a1, i + 1);
+      bar();
+    }
+  } else if constexpr ((ABL & 256) != 0) {
     // B two K steps ahead: br holds B(i + 1), br2 B(i + 2) at the top of step i
     bload(0);
     aload(0, a0);
@@ -198,6 +257,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
   }
   if (i < rounds) compute(buf0, a0, i);
   __syncthreads();
+  if ((ABL & 512) && sink == 0x12345678u) C[1] = 1.f;
   if (ABL & 16) {  // keep the sums alive without storing the tile
     float s = 0.f;
 #pragma unroll
@@ -235,9 +295,10 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2))) void k_q
 template <int ABL>
 void launch(const float* A, const uint16_t* Bp, float* C, int64_t M, int64_t N, int64_t K,
             int64_t lda, int64_t kp, int64_t npad, int64_t ldc, hipStream_t s) {
+  constexpr int kW = (ABL & 4096) ? 8 : 4, kBM = 32 * kW;
   const int64_t blocks = ((M + kBM - 1) / kBM) * ((N + BN - 1) / BN);
-  hipLaunchKernelGGL(k_q6_abl<ABL>, dim3((unsigned)blocks), dim3(T), 0, s, A, Bp, C, M, N, K, lda,
-                     kp, npad, ldc);
+  hipLaunchKernelGGL(k_q6_abl<ABL>, dim3((unsigned)blocks), dim3(64 * kW), 0, s, A, Bp, C, M, N,
+                     K, lda, kp, npad, ldc);
 }
 
 }  // namespace
@@ -249,7 +310,7 @@ extern "C" int q6_abl(int abl, const float* A, const uint16_t* Bp, float* C, int
 #define Q6A(v) \
   case v: launch<v>(A, Bp, C, M, N, K, lda, kp, npad, ldc, s); break;
     Q6A(0) Q6A(1) Q6A(2) Q6A(3) Q6A(4) Q6A(8) Q6A(16) Q6A(32) Q6A(64) Q6A(7) Q6A(68) Q6A(36)
-    Q6A(12) Q6A(24) Q6A(72) Q6A(39) Q6A(103) Q6A(128) Q6A(256) Q6A(512) Q6A(384)
+    Q6A(12) Q6A(24) Q6A(72) Q6A(39) Q6A(103) Q6A(128) Q6A(256) Q6A(512) Q6A(384) Q6A(1024) Q6A(2048) Q6A(3072) Q6A(4096) Q6A(5120)
 #undef Q6A
     default: return -1;
   }

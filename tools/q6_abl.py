@@ -21,7 +21,10 @@ NAMES = {0: "full copy", 1: "no A loads", 2: "no A split", 3: "no A loads+split"
          12: "no B staging, no MFMA", 24: "no MFMA, no epilogue", 72: "no MFMA, no B reads",
          39: "MFMA + B reads only (no barrier)", 103: "MFMA only",
          128: "+ the product's MASK zeroing", 256: "+ B loaded two K steps ahead",
-         512: "B loads kept, LDS stores dropped", 384: "+ MASK zeroing, B two steps ahead"}
+         512: "B loads kept, LDS stores dropped", 384: "+ MASK zeroing, B two steps ahead",
+         1024: "B staged by LDS-DMA", 2048: "K order rotated per block",
+         3072: "LDS-DMA + K rotation", 4096: "8 waves x 32 rows share a B stage",
+         5120: "8 waves + LDS-DMA"}
 
 
 def timeit(fn, reps=30):
@@ -61,16 +64,25 @@ def main():
             ws.data_ptr(), ws_b, st, 9))
         ref = C.clone()
         print(f"M={M} N={N} K={K}: product q6 {t*1e6:6.1f} us ({fl/t/1e12:5.1f} TF)", flush=True)
-        for abl, name in NAMES.items():
+        same = {}
+        for abl in NAMES:
             rc = exp.q6_abl(abl, A.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N, K, K, kp,
                             npad, N, st)
             assert rc == 0, (abl, rc)
             torch.cuda.synchronize()
-            same = torch.equal(C, ref) if abl in (0, 128, 256, 384) else None
-            t = timeit(lambda: exp.q6_abl(abl, A.data_ptr(), planes.data_ptr(), C.data_ptr(), M,
-                                          N, K, K, kp, npad, N, st))
+            same[abl] = torch.equal(C, ref) if abl in (0, 128, 256, 384, 1024, 4096, 5120) else None
+        # rounds of all variants interleaved, median per variant (box noise ~5-10 %)
+        times = {abl: [] for abl in NAMES}
+        for _ in range(5):
+            for abl in NAMES:
+                times[abl].append(timeit(lambda: exp.q6_abl(
+                    abl, A.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N, K, K, kp, npad, N,
+                    st), reps=10))
+        for abl, name in NAMES.items():
+            t = sorted(times[abl])[2]
             print(f"  abl {abl:3d} {name:40s} {t*1e6:6.1f} us"
-                  + ("" if same is None else f"  (bit-identical to product: {same})"), flush=True)
+                  + ("" if same[abl] is None else f"  (bit-identical to product: {same[abl]})"),
+                  flush=True)
 
 
 if __name__ == "__main__":
