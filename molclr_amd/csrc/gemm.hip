@@ -840,12 +840,18 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   constexpr int BN = 32 * TN;
   constexpr int NP = H3 ? 2 : 3;    // B planes
   constexpr int BI = NP * BN * XK;  // 16-bit elements per B image
-  static_assert(kQ6Waves * 32 * 32 * (int)sizeof(float) <= 2 * BI * (int)sizeof(uint16_t),
-                "epilogue tiles exceed the LDS images");
+  constexpr int EPI_ELEMS = kQ6Waves * 32 * 32 * 2;  // the epilogue's wave tiles (fp32)
+  constexpr int L0 = KG == 1 ? (BI > EPI_ELEMS ? BI : EPI_ELEMS) : KG * 2 * BI;
   static_assert(KG == 1 || (kQ6Waves * 32 * BN * (int)sizeof(float) <=
                             KG * 2 * BI * (int)sizeof(uint16_t)),
                 "group sums exceed the LDS images");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[KG * 2 * BI];
+  // One K group: the two B buffers are separate __shared__ arrays, so the
+  // compiler sees that the LDS-DMA in flight into one does not alias the
+  // fragment reads of the other (one array: it waited vmcnt(0) -- the whole
+  // prefetch of the next step -- before the first read of every step).
+  // K groups: one array (their group sums need it contiguous).
+  __shared__ __attribute__((aligned(16))) uint16_t lds[L0];
+  __shared__ __attribute__((aligned(16))) uint16_t lds_b1[KG == 1 ? BI : 8];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -986,8 +992,8 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
     }
   };
 
-  uint16_t* buf0 = lds + grp * 2 * BI;
-  uint16_t* buf1 = buf0 + BI;
+  uint16_t* buf0 = KG == 1 ? lds : lds + grp * 2 * BI;
+  uint16_t* buf1 = KG == 1 ? lds_b1 : buf0 + BI;
   float4 a0[4], a1[4];
   (void)gt;
   q6_dma_b<BN, NP>(Bp, n0, npad, kp, kb(0), buf0, wm, lane);

@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B: q6 B buffers in two __shared__ arrays (in-tree) vs one (tools/ab/lib_base.so)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ]; }
+rm -rf gpurun_out/pa gpurun_out/pb
+step kq 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -x --timeout 300 --timeout-method thread -k "gemm or q6 or h3 or bplanes or linear" &&
+step pb 400 rocprofv3 --kernel-trace --stats -d gpurun_out/pb -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing &&
+MOLCLR_LIB=tools/ab/lib_base.so step pa 400 rocprofv3 --kernel-trace --stats -d gpurun_out/pa -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing &&
+step bb 300 python bench.py --no-cpu-baseline --no-kernel-timing &&
+MOLCLR_LIB=tools/ab/lib_base.so step ba 300 python bench.py --no-cpu-baseline --no-kernel-timing &&
+step bb2 300 python bench.py --no-cpu-baseline --no-kernel-timing &&
+MOLCLR_LIB=tools/ab/lib_base.so step ba2 300 python bench.py --no-cpu-baseline --no-kernel-timing
+tail -2 gpurun_out/kq.log
+for f in ba bb ba2 bb2; do echo $f; grep -o '"value": [0-9.]*' gpurun_out/$f.log; done
