@@ -535,10 +535,16 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
     const int tn = t + P;
     const bool more = tn < hi;
     if constexpr (HAS_BIAS) {
+      // unconditional loads from a clamped column (bv[j] is used only where
+      // n + 4 <= N): a zero-initialised conditional load wrote its registers
+      // by VALU, which made the compiler drain the previous tile's stores
+      // (vmcnt(0)) at the tile head
+      // (N >= 4: launch_tp)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const int64_t n = n0 + 32 * TJ * wn + 32 * j + 4 * ec4;
-        bv[j] = n + 4 <= N ? *reinterpret_cast<const float4*>(bias + n) : f4zero();
+        int64_t n = n0 + 32 * TJ * wn + 32 * j + 4 * ec4;
+        n = n + 4 <= N ? n : N - 4;
+        bv[j] = *reinterpret_cast<const float4*>(bias + n);
       }
     }
 
@@ -1280,6 +1286,10 @@ int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
               const uint32_t* bits_in = nullptr) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   MOLCLR_REQUIRE(tiles < (1ll << 31) / 256, "gemm_bf16: too many tiles");
+  // k_gemm_tp reads its bias columns as float4s from a column clamped to N - 4
+  MOLCLR_REQUIRE(N >= 4 || (epi != MOLCLR_EPI_BIAS && epi != MOLCLR_EPI_BIAS_RELU),
+                 "gemm_bf16: the persistent tile kernel needs N >= 4 with a bias (N = %lld)",
+                 (long long)N);
   const int64_t cus = cu_count();
   const dim3 g((unsigned)(tiles < cus ? tiles : cus)), b(64 * NW);
   if (bits_out || bits_in) {
@@ -1339,7 +1349,7 @@ constexpr int kQbImpls = 10;
 // 2-5 % faster than k_gemm_tb on the plain products and ~20 % on the ReLU-mask
 // one; its 4-wave 128 x 128 form, 9, is 10-25 % slower), k_gemm_tc for K % 32 == 0
 int qb_default(int64_t N, int64_t K) {
-  if (K % 64 == 0) return 8;
+  if (K % 64 == 0 && N >= 4) return 8;
   if (K % 32 == 0) return 7;
   return N > 512 ? 5 : 2;
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B: q6 B buffers in two __shared__ arrays (in-tree) vs one (tools/ab/lib_base.so)
+# A/B: in-tree vs tools/ab/lib_base.so (the previous commit)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
