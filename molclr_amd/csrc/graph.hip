@@ -119,7 +119,9 @@ __global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
 // flight per thread) into LDS, each thread sums 8 consecutive elements, one
 // block-wide scan of the 1024 thread sums (wave scans + a scan of the 16 wave
 // totals), then each thread writes its 8 prefixes: three barriers per tile
-// (the per-1024-element scan it replaces took three per 1024 elements).
+// (the per-1024-element scan it replaces took three per 1024 elements).  The
+// next tile's loads are issued into registers while the current tile is
+// scanned, so only the first tile waits for memory.
 constexpr int kScanPer = 8;
 __global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restrict__ degA,
                                                         int32_t* __restrict__ ptrA,
@@ -132,12 +134,19 @@ __global__ __launch_bounds__(kScanThreads) void k_scan2(const int32_t* __restric
   __shared__ int32_t wsum[kScanThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int32_t carry = 0;
-  for (int64_t base = 0; base < n; base += TILE) {
+  int32_t nx[kScanPer];
+  auto load = [&](int64_t base) {
 #pragma unroll
     for (int c = 0; c < kScanPer; ++c) {
       const int64_t idx = base + (int64_t)c * kScanThreads + tid;
-      tile[c * kScanThreads + tid] = idx < n ? deg[idx] : 0;
+      nx[c] = idx < n ? deg[idx] : 0;
     }
+  };
+  load(0);
+  for (int64_t base = 0; base < n; base += TILE) {
+#pragma unroll
+    for (int c = 0; c < kScanPer; ++c) tile[c * kScanThreads + tid] = nx[c];
+    if (base + TILE < n) load(base + TILE);
     __syncthreads();
     int32_t v[kScanPer], x = 0;
 #pragma unroll
