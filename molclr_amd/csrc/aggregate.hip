@@ -192,7 +192,16 @@ __global__ __launch_bounds__(64) void k_emb_chunk_sum(const typename St::T* __re
   const int32_t beg = cbeg[ch], end = cend[ch];
   float4 acc = f4zero();
   int32_t i = beg;
-  for (; i + 4 <= end; i += 4) {  // four rows in flight; adds in item order
+  // sixteen rows in flight (four left a 128-item chunk 32 round trips long);
+  // adds in item order
+  for (; i + 16 <= end; i += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = St::ld(dh, (int64_t)perm[i + u] * d4 + c);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = f4add(acc, v[u]);
+  }
+  for (; i + 4 <= end; i += 4) {
     float4 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = St::ld(dh, (int64_t)perm[i + u] * d4 + c);
