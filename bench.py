@@ -19,7 +19,8 @@ BatchNorm statistics (the reference's two calls).  N > 1 runs under torchrun,
 one rank per GPU over RCCL: the NT-Xent batch is global (512 N), weak scaling.
 
 The JSON line adds:
-  roofline      — the GIN scatter-add (molclr_gine_aggregate_fwd), HBM-bound:
+  roofline      — the GIN scatter-add (molclr_gine_aggregate_fwd; GCN's
+                  molclr_gcn_aggregate_fwd for c3), HBM-bound:
                   algorithmic bytes per launch / mean kernel duration in the
                   timed region, against 8.0 TB/s.  Durations are the
                   dispatch-recorded events of hipExtLaunchKernelGGL
@@ -116,7 +117,8 @@ def cpu_baseline(cfg, batches_cpu, steps):
     import torch
 
     from oracle.reference_cpu import RefGCN, RefGINet, RefNTXentLoss, ref_train_step
-    threads = min(16, os.cpu_count() or 1)
+    hw = host_cores()
+    threads = hw["threads_used"]
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     M = RefGINet if cfg["model_type"] == "gin" else RefGCN
@@ -131,9 +133,11 @@ def cpu_baseline(cfg, batches_cpu, steps):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times[1:])
     out = {"value": round(cfg["batch"] / med, 2), "unit": "molecules/s", "cores": threads,
+           "host": hw,
            "kind": "port", "ms_per_step": round(med * 1e3, 1),
            "sample": f"{steps} steps (+1 warm-up) of {cfg['desc']}, oracle/reference_cpu.py, "
-                     f"torch CPU fp32, {threads} threads, median step"}
+                     f"torch CPU fp32, {threads} threads (one per physical core available "
+                     f"to this process), median step"}
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -162,6 +166,50 @@ def cpu_baseline(cfg, batches_cpu, steps):
     return out
 
 
+def host_cores() -> dict:
+    """Physical cores of this host (unique (package, core) pairs of
+    /proc/cpuinfo), the logical CPUs this process may run on (affinity) and
+    the cgroup CPU quota; the CPU baseline uses one thread per physical core
+    within the affinity set, capped by the quota (all physical
+    cores; on a shared GPU box the job's share is what it can actually use)."""
+    import math
+    logical = os.cpu_count() or 1
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = list(range(logical))
+    core_of, phys, cur = {}, set(), {}
+    try:
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if "processor" in cur:
+                    key = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                    core_of[int(cur["processor"])] = key
+                    phys.add(key)
+                cur = {}
+                continue
+            k, v = (t.strip() for t in line.split(":", 1))
+            cur[k] = v
+        if "processor" in cur:
+            key = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+            core_of[int(cur["processor"])] = key
+            phys.add(key)
+    except OSError:
+        pass
+    phys_allowed = len({core_of[c] for c in allowed if c in core_of}) or len(allowed)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    used = phys_allowed if quota is None else max(1, min(phys_allowed, math.floor(quota)))
+    return {"physical_cores": len(phys) or logical, "logical_cpus": logical,
+            "affinity_cpus": len(allowed), "physical_cores_in_affinity": phys_allowed,
+            "cgroup_cpu_quota": quota, "threads_used": used}
+
+
 def split_ceiling(tfs, model_type) -> dict:
     """fp32 GEMMs: fraction of their own MFMA ceiling.  Forward products run as
     split-bf16 x6 (six bf16 MFMAs: 2.5 PF / 6); with ops.FP32_GEMM == "h3" the
@@ -169,9 +217,14 @@ def split_ceiling(tfs, model_type) -> dict:
     (three fp16 MFMAs: 2.5 PF / 3), so the ceiling is their flop-weighted
     harmonic mean."""
     from molclr_amd import ops
-    x6 = BF16_MFMA_PEAK_TFS / 6
+    x6, h3 = BF16_MFMA_PEAK_TFS / 6, BF16_MFMA_PEAK_TFS / 3
     if model_type == "gin" and ops.FP32_GEMM == "h3":
-        ceil = 1.0 / ((2 / 6) / x6 + (4 / 6) / (BF16_MFMA_PEAK_TFS / 3))
+        ceil = 1.0 / ((2 / 6) / x6 + (4 / 6) / h3)
+        form = "x6 forward, h3 backward"
+    elif model_type == "gcn" and ops.FP32_GEMM == "h3":
+        # GCN: one forward product per layer (x6), its weight and data
+        # gradients in h3 (DESIGN §4): 1 of every 3 equal-size products is x6
+        ceil = 1.0 / ((1 / 3) / x6 + (2 / 3) / h3)
         form = "x6 forward, h3 backward"
     else:
         ceil, form = x6, "x6"
@@ -239,21 +292,15 @@ def main():
         id_sets = [perm_rng.permutation(nmol)[:B].astype(np.int64) for _ in range(args.batches)]
         id_sets_dev = [torch.from_numpy(v).to(dev) for v in id_sets]
 
+    # the scatter-add timed for the HBM roofline: GINE's, or GCN's for c3
+    agg_kind = "gcn_aggregate_fwd" if cfg["model_type"] == "gcn" else "gine_aggregate_fwd"
     captured = None
     if world == 1 and not args.two_pass and not args.no_hip_graph:
         from molclr_amd.graph_step import CapturedTrainStep
         captured = CapturedTrainStep(model, opt, crit)
 
     def step(i, eager=False):
-        if store is not None:
-            k = i % len(id_sets)
-            if args.augment == "device":
-                xi, xj = store.mask_views(id_sets_dev[k], seed=i, host_ids=id_sets[k])
-            else:
-                xi, xj = store.aug_views(id_sets_dev[k], seed=i, mode=args.augment,
-                                         host_ids=id_sets[k])
-        else:
-            xi, xj = batches[i % len(batches)]
+        xi, xj = views_of(i)
         if captured is not None and not eager:
             # staging copy + one graph launch: the graph build, both views'
             # encoder pass, NT-Xent, backward and Adam replay on the device
@@ -279,6 +326,27 @@ def main():
         opt.step()
         return loss
 
+    def views_of(i):
+        if store is None:
+            return batches[i % len(batches)]
+        k = i % len(id_sets)
+        if args.augment == "device":
+            return store.mask_views(id_sets_dev[k], seed=i, host_ids=id_sets[k])
+        return store.aug_views(id_sets_dev[k], seed=i, mode=args.augment, host_ids=id_sets[k])
+
+    if captured is not None:
+        # capture every graph the run's batches need BEFORE the warm-up, so no
+        # capture lands in the timed region: the resident batches, or (device
+        # augmentation) the views of every step index the run will use
+        t0 = time.perf_counter()
+        if store is None:
+            captured.prepare(batches)
+        else:
+            for i in list(range(args.warmup + args.steps + 3)):
+                captured.prepare([views_of(i)])
+        torch.cuda.synchronize()
+        log(rank, f"captured {captured.captures} graphs in {time.perf_counter() - t0:.1f}s "
+                  f"(node/edge capacities {sorted(captured.buckets)})")
     for i in range(args.warmup):
         loss = step(i)
     torch.cuda.synchronize()
@@ -298,12 +366,13 @@ def main():
     # replayed graph cannot carry them: the scatter-add is then timed over
     # extra eager steps after the timed region, like the GEMMs
     timer = None if args.no_kernel_timing or captured is not None else \
-        ops.KernelTimer(kinds=("gine_aggregate_fwd",))
+        ops.KernelTimer(kinds=(agg_kind,))
     ops.set_kernel_timer(timer)
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    captures_before = captured.captures if captured is not None else 0
     t0 = time.perf_counter()
     marks[0].record()
     for i in range(args.steps):
@@ -313,6 +382,7 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
+    captures_timed = (captured.captures - captures_before) if captured is not None else 0
     ops.set_kernel_timer(None)
     elapsed = mdist.max_over_ranks(elapsed, dev)
     final_loss = float(loss.item())
@@ -327,7 +397,7 @@ def main():
     s = timer.summary() if timer is not None else {}
     agg_timing = "hipExtLaunchKernelGGL dispatch events in the timed region"
     if captured is not None and not args.no_kernel_timing and args.mfma_steps > 0:
-        timer = ops.KernelTimer(kinds=("gine_aggregate_fwd",))
+        timer = ops.KernelTimer(kinds=(agg_kind,))
         ops.set_kernel_timer(timer)
         for i in range(args.mfma_steps):
             step(args.warmup + args.steps + 3 + i, eager=True)
@@ -348,13 +418,16 @@ def main():
 
     roofline = roofline_mfma = roofline_ntxent = None
     if timer is not None:
-        agg = s.get("gine_aggregate_fwd")
+        agg = s.get(agg_kind)
         if agg:
             per_launch_s = agg["ms"] / agg["launches"] / 1e3
             per_launch_bytes = agg["work"] / agg["launches"]
             achieved = per_launch_bytes / per_launch_s / 1e9
-            roofline = {"kernel": ("molclr_gine_aggregate_fwd_bf16" if precision == "bf16" else
-                                   "molclr_gine_aggregate_fwd") + " (k_gine_agg_fwd)", "bound": "hbm",
+            roofline = {"kernel": ("molclr_gcn_aggregate_fwd (k_gcn_agg_fwd)" if agg_kind ==
+                                   "gcn_aggregate_fwd" else
+                                   ("molclr_gine_aggregate_fwd_bf16" if precision == "bf16" else
+                                    "molclr_gine_aggregate_fwd") + " (k_gine_agg_fwd)"),
+                        "bound": "hbm",
                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 4),
                         "traffic": load_pmc_traffic(args.config, args.two_pass),
@@ -365,16 +438,26 @@ def main():
         gm = s.get("gemm_f32")
         if gm:
             tfs = gm["work"] / (gm["ms"] / 1e3) / 1e12
-            peak = BF16_MFMA_PEAK_TFS if precision == "bf16" else FP32_MFMA_PEAK_TFS
+            if precision == "bf16":
+                peak, extra = BF16_MFMA_PEAK_TFS, {}
+            else:
+                # fp32 at fp32 accuracy from split bf16 / fp16 MFMAs: the
+                # headline fraction is against that form's own ceiling; the
+                # native fp32 MFMA peak is reported beside it
+                sc = split_ceiling(tfs, cfg["model_type"])
+                peak = sc["split_ceiling_tfs"]
+                extra = {**sc, "fp32_mfma_peak": FP32_MFMA_PEAK_TFS,
+                         "frac_of_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFS, 4)}
             roofline_mfma = {"kernel": ("molclr_gemm_bf16 / _linear_wgrad_bf16 encoder GEMMs + "
                                         "the fp32 head GEMMs" if precision == "bf16" else
                                         "molclr_gemm_f32 (all launches)"), "bound": "mfma",
                              "achieved": round(tfs, 2), "peak": peak,
-                             "unit": "TFLOP/s", "frac": round(tfs / peak, 4),
+                             "unit": "TFLOP/s" + ("" if precision == "bf16" else
+                                                  " (fp32-equivalent)"),
+                             "frac": round(tfs / peak, 4),
                              "traffic": None, "launches": gm["launches"],
                              "ms_per_step": round(gm["ms"] / args.mfma_steps, 3),
-                             **({} if precision == "bf16" else
-                                split_ceiling(tfs, cfg["model_type"])),
+                             **extra,
                              "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                        f"after the timed region"}
         nx = s.get("ntxent")
@@ -418,8 +501,9 @@ def main():
                        "parallelism": f"dp{world}",
                        "views": ("two encoder calls (molclr.py:57,60)" if args.two_pass else
                                  "one paired encoder pass, per-view BatchNorm statistics"),
-                       "launch": ("HIP graph per batch-size bucket (molclr_amd.graph_step): "
-                                  f"{captured.captures} captured, staged + replayed every step"
+                       "launch": ("HIP graph per batch-size capacity bucket "
+                                  "(molclr_amd.graph_step): captured before the warm-up, "
+                                  "staged + replayed every step"
                                   if captured is not None else "eager (host-enqueued)"),
                        "augment": ("host: pre-built resident batch pairs" if store is None else
                                    "device: molclr_mask_views inside the step"
@@ -427,6 +511,8 @@ def main():
                                    f"device: molclr_aug_views ({args.augment}) inside the step")},
             "final_loss": round(final_loss, 5),
             "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
+            "captures": captured.captures if captured is not None else 0,
+            "captures_in_timed_region": captures_timed,
             "roofline": roofline, "roofline_mfma": roofline_mfma,
             "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
         }

@@ -911,10 +911,11 @@ int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t* x, float* 
  * itself, so each sample is the kernel's own execution window (the figure
  * rocprofv3 --kernel-trace reports).  Kinds (a bit mask): 1 = k_gine_agg_fwd,
  * 2 = every kernel of molclr_gemm_f32 (main GEMM + split-K reduce), 4 = the
- * NT-Xent similarity kernels. */
+ * NT-Xent similarity kernels, 8 = k_gcn_agg_fwd. */
 #define MOLCLR_KTIMER_GINE_AGG 1
 #define MOLCLR_KTIMER_GEMM 2
 #define MOLCLR_KTIMER_NTXENT 4 /* k_ntxent_fwd_partial / k_ntxent_bwd_partial */
+#define MOLCLR_KTIMER_GCN_AGG 8
 int molclr_ktimer_start(int kinds_mask);
 /* Waits for the recorded launches of `kind`, returns their summed duration
  * and count, and forgets them. */

@@ -170,6 +170,7 @@ STATUS_ATOM_RANGE = 8  # MOLCLR_STATUS_ATOM_RANGE
 KTIMER_GINE_AGG = 1
 KTIMER_GEMM = 2
 KTIMER_NTXENT = 4
+KTIMER_GCN_AGG = 8
 AUG_SUBGRAPH, AUG_MIX = 0, 1
 
 

@@ -841,10 +841,10 @@ MOLCLR_API int molclr_gcn_aggregate_fwd(const float* xw, const int32_t* rowptr,
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(xw && rowptr && nbr && E1 && E2 && bias && out, "gcn_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_gcn_agg_fwd, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), (const float4*)xw, rowptr, col, ecode,
-                     (const uint4*)nbr, E1, E2,
-                     (const float4*)bias, (float4*)out, N, d4);
+  molclr::launch_timed(molclr::kTimeGcnAgg, k_gcn_agg_fwd,
+                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
+                       (const float4*)xw, rowptr, col, ecode, (const uint4*)nbr, E1, E2,
+                       (const float4*)bias, (float4*)out, N, d4);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

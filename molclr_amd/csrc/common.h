@@ -76,7 +76,12 @@ inline Band make_band(int64_t dim) {
 // written by the kernel dispatch itself: the elapsed time is the kernel's own
 // execution window (what rocprofv3's kernel trace reports), not a bracket of
 // separately queued event packets.
-enum { kTimeGineAgg = MOLCLR_KTIMER_GINE_AGG, kTimeGemm = MOLCLR_KTIMER_GEMM, kTimeNtxent = MOLCLR_KTIMER_NTXENT };
+enum {
+  kTimeGineAgg = MOLCLR_KTIMER_GINE_AGG,
+  kTimeGemm = MOLCLR_KTIMER_GEMM,
+  kTimeNtxent = MOLCLR_KTIMER_NTXENT,
+  kTimeGcnAgg = MOLCLR_KTIMER_GCN_AGG
+};
 bool timer_wants(int kind);
 void timer_record(int kind, hipEvent_t start, hipEvent_t stop);
 // Launches made while a TimerKindScope is alive on the calling thread are

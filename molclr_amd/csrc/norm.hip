@@ -29,9 +29,13 @@ __host__ __device__ __forceinline__ int64_t band_parts(int64_t rows, int band) {
 
 // an upper bound of sum_s band_parts(n_s) over any split of `rows` rows into
 // nseg segments: ceil(a / u) + ceil(b / u) <= ceil((a + b) / u) + 1, and an
-// empty segment still takes one partition
+// empty segment still takes one partition.  The per-segment cap (1024) applies
+// to each segment, so the uncapped total is bounded first and only then
+// capped at nseg * 1024 (capping the total at 1024 first undercounts: two
+// segments of 865 partitions each need 1730).
 int64_t band_parts_bound(int64_t rows, int band, int nseg) {
-  int64_t P = band_parts(rows, band) + nseg;
+  const int64_t unit = (int64_t)band * 16;
+  int64_t P = (rows + unit - 1) / unit + nseg;
   if (P > (int64_t)nseg * 1024) P = (int64_t)nseg * 1024;
   return P;
 }

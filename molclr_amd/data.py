@@ -190,19 +190,23 @@ class DeviceGraph:
 
     def check(self) -> None:
         """Synchronising validity check of the input indices (tests / debug)."""
-        st = int(self.status.item())
-        if st:
-            what = []
-            if st & 1:
-                what.append("edge_index out of range")
-            if st & 2:
-                what.append("edge_attr out of range")
-            if st & 4:
-                what.append("batch not ascending / out of range")
-            if st & _lib.STATUS_ATOM_RANGE:
-                what.append("atom type / chirality outside the model's embedding tables "
-                            "(the reference's nn.Embedding raises IndexError)")
-            raise ValueError("invalid graph batch: " + ", ".join(what))
+        raise_for_status(int(self.status.item()))
+
+
+def raise_for_status(st: int) -> None:
+    """ValueError naming every invalid-input bit of a graph status word."""
+    if st:
+        what = []
+        if st & 1:
+            what.append("edge_index out of range")
+        if st & 2:
+            what.append("edge_attr out of range")
+        if st & 4:
+            what.append("batch not ascending / out of range")
+        if st & _lib.STATUS_ATOM_RANGE:
+            what.append("atom type / chirality outside the model's embedding tables "
+                        "(the reference's nn.Embedding raises IndexError)")
+        raise ValueError("invalid graph batch: " + ", ".join(what))
 
 
 def pair_graph(xi, xj) -> DeviceGraph:

@@ -145,14 +145,38 @@ class _Captured:
 class CapturedTrainStep:
     """``step(xis, xjs) -> loss``: one MolCLR training step (molclr.py:108-128:
     zero_grad, the paired encoder pass, normalize, NT-Xent, backward, Adam)
-    replayed from a HIP graph captured per (node, edge) capacity bucket.
+    replayed from a HIP graph captured per capacity bucket.
+
+    Lookup is by capacity, not by exact size: a batch pair runs on the
+    smallest captured graph whose node / edge capacities hold it (same
+    graphs per view), provided the node padding stays within ``node_slack``
+    rows of the batch's own rounded size -- padding rows cost GEMM / BatchNorm
+    / aggregation time, padding edge slots almost nothing.  Otherwise a new
+    graph is captured at the batch's node count rounded up to
+    ``node_quantum`` and its edge count plus ``edge_headroom`` rounded up to
+    ``edge_quantum``.  Over an epoch the set of captures converges to a short
+    ladder covering the batch-size spread (a handful of graphs at B = 512);
+    ``prepare(pairs)`` captures what a known set of batches needs ahead of
+    time.
+
+    Memory invariant (all captures share ONE graph memory pool): every replay
+    runs on the same stream as every other replay and eager step, and no
+    tensor allocated inside a capture is read by a replay before that replay
+    has written it.  Cross-replay state lives outside the pool (parameters,
+    gradients, Adam moments, BatchNorm running statistics, the loss and status
+    buffers below, the staging buffers); pool blocks of one capture that a
+    later capture reuses are therefore only ever scratch of one replay at a
+    time.  tests/test_gpu_graph_step.py alternates buckets against eager steps.
 
     The returned loss tensor is this object's own buffer, overwritten by the
-    next step.  Requirements: a model with the paired executor path
-    (``forward_staged``), a FusedAdam optimizer, one process."""
+    next step.  ``status`` ORs every replayed batch's input-validity word
+    (sticky: ``check()`` raises for an invalid batch at any earlier step).
+    Requirements: a model with the paired executor path (``forward_staged``),
+    a FusedAdam optimizer, one process."""
 
     def __init__(self, model, optimizer, criterion, node_quantum: int = 256,
-                 edge_quantum: int = 2048, max_graphs: int = 16):
+                 edge_quantum: int = 2048, max_graphs: int = 32, node_slack: int | None = None,
+                 edge_headroom: float = 0.04):
         from .optim import FusedAdam
         if not isinstance(optimizer, FusedAdam):
             raise TypeError("CapturedTrainStep needs molclr_amd.optim.FusedAdam "
@@ -163,19 +187,43 @@ class CapturedTrainStep:
             raise ValueError("CapturedTrainStep runs one process; the data-parallel step is eager")
         self.model, self.optimizer, self.criterion = model, optimizer, criterion
         self.node_quantum, self.edge_quantum = int(node_quantum), int(edge_quantum)
+        self.node_slack = 2 * self.node_quantum if node_slack is None else int(node_slack)
+        self.edge_headroom = float(edge_headroom)
         self.max_graphs = int(max_graphs)
         self.device = optimizer.flat.device
         self._graphs: OrderedDict = OrderedDict()
         self._pool = torch.cuda.graph_pool_handle()
         self.loss = torch.zeros((), dtype=torch.float32, device=self.device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.captures = 0
+        self.replays = 0
         self.last_graph: StagedPairGraph | None = None
 
-    def bucket(self, xis, xjs) -> tuple:
+    @staticmethod
+    def _need(xis, xjs) -> tuple:
         n = int(xis.x.shape[0]) + int(xjs.x.shape[0])
         e = int(xis.edge_index.shape[1]) + int(xjs.edge_index.shape[1])
-        return (_round_up(n, self.node_quantum), _round_up(e, self.edge_quantum),
-                _num_graphs_of(xis), _num_graphs_of(xjs))
+        return n, e, _num_graphs_of(xis), _num_graphs_of(xjs)
+
+    def bucket(self, xis, xjs) -> tuple:
+        """(node_cap, edge_cap, G_i, G_j) a new capture for this pair gets."""
+        n, e, gi, gj = self._need(xis, xjs)
+        e_cap = _round_up(int(e * (1.0 + self.edge_headroom)) + 1, self.edge_quantum)
+        return (_round_up(n, self.node_quantum), e_cap, gi, gj)
+
+    def lookup(self, xis, xjs):
+        """The captured entry this pair would replay on, or None."""
+        n, e, gi, gj = self._need(xis, xjs)
+        limit = _round_up(n, self.node_quantum) + self.node_slack
+        best = None
+        for ent in self._graphs.values():
+            g = ent.graph
+            if (g.num_nodes >= n and g.num_edges >= e and g.num_nodes <= limit
+                    and g.graphs_per_segment == [gi, gj]):
+                if best is None or (g.num_nodes, g.num_edges) < (best.graph.num_nodes,
+                                                                 best.graph.num_edges):
+                    best = ent
+        return best
 
     def _capture(self, key, xis, xjs) -> _Captured:
         if not self.model._executor_ok() or self.model._dim_pad():
@@ -200,24 +248,53 @@ class CapturedTrainStep:
             loss.backward()
             opt.step(sync_lr=False)
             self.loss.copy_(loss)
+            # graph build and atom embedding write the batch's validity bits
+            torch.bitwise_or(self.status, graph.status, out=self.status)
         del loss, z
         self.captures += 1
+        # a capture only records: the cached images must be regenerated by
+        # the next eager use as well
+        ops.bump_param_generation()
         return _Captured(graph, g)
 
-    def __call__(self, xis, xjs) -> torch.Tensor:
-        key = self.bucket(xis, xjs)
-        ent = self._graphs.get(key)
+    def _entry(self, xis, xjs):
+        ent = self.lookup(xis, xjs)
         if ent is None:
+            key = self.bucket(xis, xjs)
             ent = self._capture(key, xis, xjs)  # stages this batch too
-            self._graphs[key] = ent
+            self._graphs[id(ent)] = ent
             if len(self._graphs) > self.max_graphs:
                 self._graphs.popitem(last=False)
-        else:
-            self._graphs.move_to_end(key)
+            return ent, True
+        self._graphs.move_to_end(id(ent))
+        return ent, False
+
+    def prepare(self, pairs) -> int:
+        """Capture (without running) every graph the given batch pairs need;
+        returns the number of new captures."""
+        before = self.captures
+        for xis, xjs in pairs:
+            self._entry(xis, xjs)
+        return self.captures - before
+
+    def __call__(self, xis, xjs) -> torch.Tensor:
+        ent, fresh = self._entry(xis, xjs)
+        if not fresh:
             ent.graph.stage([xis, xjs])
             self.optimizer.sync_lr()
         ent.cuda_graph.replay()
+        self.replays += 1
         # the replay's Adam step changed the weights behind Python's back
         ops.bump_param_generation()
         self.last_graph = ent.graph
         return self.loss
+
+    @property
+    def buckets(self) -> list:
+        """(node_cap, edge_cap) of every live capture."""
+        return [(e.graph.num_nodes, e.graph.num_edges) for e in self._graphs.values()]
+
+    def check(self) -> None:
+        """Raise ValueError if any replayed batch so far had invalid inputs."""
+        from .data import raise_for_status
+        raise_for_status(int(self.status.item()))

@@ -15,13 +15,15 @@ rule, one kernel); optional config keys ``world_size`` (data parallel via
 torchrun), ``seed``, ``dataset.views`` ('device', the default: both views of
 every batch are built on the GPU from the resident molecules, for every
 ``aug`` mode; 'host': the reference's DataLoader, node masking only),
-``hip_graph`` (True: one process replays the whole step from HIP graphs
-captured per batch-size bucket, molclr_amd.graph_step); the
+``hip_graph`` (default True: one process replays the whole step from HIP
+graphs captured per batch-size capacity bucket, molclr_amd.graph_step, when
+the run allows it -- one process, the paired executor pass; False: eager); the
 scalar writer is TensorBoard when installed, otherwise a JSONL file with the
 same tags.  ``data_path`` may be the reference's SMILES text file (featurised
 once into a cached binary shard), a shard, or ``synthetic:<count>``.
 Invalid inputs raise at the next log step (``check_inputs``), as the
-reference's embedding lookup would.
+reference's embedding lookup would: every step's graph status word is ORed
+into a sticky device accumulator, so a bad batch between log steps is caught.
 """
 from __future__ import annotations
 
@@ -78,6 +80,8 @@ class MolCLR(object):
         self.writer = _summary_writer(log_dir) if self.rank == 0 else None
         self.log_dir = log_dir
         self.dataset = dataset
+        # sticky OR of every eager step's graph status word (check_inputs)
+        self._status = torch.zeros(1, dtype=torch.int32, device=self.device)
         group = torch.distributed.group.WORLD if self.world > 1 else None
         global_batch = config['batch_size'] * self.world
         self.nt_xent_criterion = NTXentLoss(self.device, global_batch, group=group,
@@ -147,10 +151,10 @@ class MolCLR(object):
         return optimizer, scheduler
 
     def _graph_step(self, model, optimizer):
-        """The HIP-graph step (molclr_amd.graph_step) when the config asks for
-        it (``hip_graph: True``) and the run allows it: one process, the
-        paired executor pass at an unpadded width; else None (eager)."""
-        if not self.config.get('hip_graph', False) or self.world > 1:
+        """The HIP-graph step (molclr_amd.graph_step) unless the config turns
+        it off (``hip_graph: False``), when the run allows it: one process,
+        the paired executor pass at an unpadded width; else None (eager)."""
+        if not self.config.get('hip_graph', True) or self.world > 1:
             return None
         if not getattr(self, "paired", True) or not hasattr(model, "forward_staged"):
             return None
@@ -177,6 +181,7 @@ class MolCLR(object):
             reducer.arm()
         loss = self._step(model, xis, xjs, n_iter)
         self._last_inputs = xis
+        self._accumulate_status(xis, xjs)
         loss.backward()
         if reducer is not None:
             reducer.finish()
@@ -230,18 +235,25 @@ class MolCLR(object):
                 scheduler.step()
         return model
 
+    def _accumulate_status(self, xi, xj) -> None:
+        """OR the step's graph status words (the paired graph, or each view's
+        own) into the sticky accumulator (tiny device ops, no sync)."""
+        pg = getattr(xi, "_molclr_pair_graph", None)
+        graphs = [pg[1]] if pg is not None else [getattr(v, "_molclr_graph", None) for v in (xi, xj)]
+        for g in graphs:
+            if g is not None:
+                torch.bitwise_or(self._status, g.status, out=self._status)
+
     def check_inputs(self) -> None:
-        """Raise on the last step's invalid inputs (out-of-range edges, or atom
-        features outside the embedding tables, where the reference's
-        nn.Embedding raises IndexError).  Reads the graph's device status word
-        (a sync: called where the loop syncs anyway, at the log steps)."""
-        if getattr(self, "_last_graph", None) is not None:  # the captured step's graph
-            self._last_graph.check()
-            return
-        xi = getattr(self, "_last_inputs", None)
-        g = getattr(xi, "_molclr_pair_graph", None) or (None, getattr(xi, "_molclr_graph", None))
-        if g[1] is not None:
-            g[1].check()
+        """Raise if any step so far had invalid inputs (out-of-range edges, or
+        atom features outside the embedding tables, where the reference's
+        nn.Embedding raises IndexError).  Reads the sticky device status words
+        of the eager steps and of the captured step (a sync: called where the
+        loop syncs anyway, at the log steps)."""
+        from .data import raise_for_status
+        cs = getattr(self, "_captured", None)
+        st = int(self._status.item()) | (int(cs.status.item()) if cs is not None else 0)
+        raise_for_status(st)
 
     def _load_pre_trained_weights(self, model):
         try:
@@ -265,6 +277,7 @@ class MolCLR(object):
                 loss = self._step(model, xis, xjs, counter)
                 self._last_inputs = xis
                 self._last_graph = None
+                self._accumulate_status(xis, xjs)
                 valid_loss += loss.item()
                 self.check_inputs()
                 counter += 1

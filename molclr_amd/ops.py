@@ -86,7 +86,7 @@ class KernelTimer:
     NT-Xent: 2 n 2B C forward, twice that backward)."""
 
     KINDS = {"gine_aggregate_fwd": _lib.KTIMER_GINE_AGG, "gemm_f32": _lib.KTIMER_GEMM,
-             "ntxent": _lib.KTIMER_NTXENT}
+             "ntxent": _lib.KTIMER_NTXENT, "gcn_aggregate_fwd": _lib.KTIMER_GCN_AGG}
 
     def __init__(self, kinds=None):
         """``kinds``: the subset of KINDS to time (default all).  Every timed
@@ -768,6 +768,8 @@ class _GCNConv(torch.autograd.Function):
                   graph.col.data_ptr(), graph.ecode.data_ptr(), graph.nbr.data_ptr(),
                   E1.data_ptr(), E2.data_ptr(),
                   bias.data_ptr(), out.data_ptr(), N, Dout, _stream(x))
+        if _TIMER is not None:
+            _TIMER.add("gcn_aggregate_fwd", gine_aggregate_bytes(N, Dout, graph.num_edges))
         ctx.save_for_backward(x, W)
         ctx.graph = graph
         ctx.params = (W, bias, E1, E2)
@@ -1089,6 +1091,8 @@ class _GCNEncoder(torch.autograd.Function):
         if _TIMER is not None:
             for _ in range(L):
                 _TIMER.add("gemm_f32", 2.0 * N * D * D)
+                # the GCN scatter-add moves the same compulsory bytes as GINE's
+                _TIMER.add("gcn_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges))
         ctx.enc, ctx.graph, ctx.arena, ctx.arena_bytes = enc, graph, arena, arena_bytes
         ctx.x_idx, ctx.params, ctx.training = x_idx, params, training
         return h

@@ -83,7 +83,10 @@ def test_stage_rejects_overflow(dev):
 
 
 @pytest.mark.parametrize("dtype", [_lib.DTYPE_F32, _lib.DTYPE_BF16])
-@pytest.mark.parametrize("rows,pad,D", [((700, 900), 300, 64), ((15000, 15300), 1200, 300)])
+@pytest.mark.parametrize("rows,pad,D", [((700, 900), 300, 64), ((15000, 15300), 1200, 300),
+                                        # c5-sized: > 512 partitions per segment (band 2 at
+                                        # D = 512: 32 rows per partition), 1730 in all
+                                        ((27700, 27650), 600, 512)])
 def test_batchnorm_dev_matches_host(dev, dtype, rows, pad, D):
     lib = _lib.load()
     st = ops._stream(torch.empty(1, device=dev))
@@ -183,7 +186,7 @@ def test_captured_step_follows_eager(dev, kind):
     opt_c = FusedAdam(cap.parameters(), 5e-4, weight_decay=1e-5)
     crit = NTXentLoss(dev, B, 0.1, True)
     # small quanta: several buckets, several captures, replays of each
-    step = CapturedTrainStep(cap, opt_c, crit, node_quantum=128, edge_quantum=512)
+    step = CapturedTrainStep(cap, opt_c, crit, node_quantum=128, edge_quantum=512, node_slack=0)
     tol_grad = 1e-5 if kind != "bf16" else 1e-4
     for i, (xi, xj) in enumerate(batches + batches[:3]):
         _sync(ref, opt_r, cap, opt_c)
@@ -223,3 +226,46 @@ def test_captured_step_lr_follows_scheduler(dev):
     torch.cuda.synchronize()
     assert torch.equal(opt.flat, before)
     assert opt.steps_taken == 2
+
+
+def test_capacity_fit_lookup_and_prepare(dev):
+    """A pair replays on the smallest captured graph that holds it within the
+    node slack; prepare() captures ahead of time, so the steps after it
+    capture nothing; a replay on a larger graph (padding rows) still follows
+    the eager step."""
+    B = 32
+    pairs = [_to(p, dev) for p in SyntheticPairBatches(B, seed=21).take(8)]
+    ref = _make("gin", 3).to(dev)
+    cap = copy.deepcopy(ref)
+    opt_r = FusedAdam(ref.parameters(), 5e-4, weight_decay=1e-5)
+    opt_c = FusedAdam(cap.parameters(), 5e-4, weight_decay=1e-5)
+    crit = NTXentLoss(dev, B, 0.1, True)
+    step = CapturedTrainStep(cap, opt_c, crit, node_quantum=64, edge_quantum=256,
+                             node_slack=4096)
+    # with a wide slack the largest pair's graph serves every smaller one
+    order = sorted(pairs, key=lambda p: -(p[0].x.shape[0] + p[1].x.shape[0]))
+    assert step.prepare(order[:1]) == 1
+    biggest = step.lookup(*order[0])
+    for p in order:
+        ent = step.lookup(*p)
+        if ent is not None:
+            assert ent is biggest
+    n_before = step.captures
+    step.prepare(pairs)
+    n_prepared = step.captures
+    for xi, xj in pairs + pairs[:2]:
+        _sync(ref, opt_r, cap, opt_c)
+        lr_ = _eager_step(ref, opt_r, crit, xi, xj)
+        lc = step(xi, xj).clone()
+        torch.cuda.synchronize()
+        assert abs(lc.item() - lr_.item()) <= 1e-6 * abs(lr_.item())
+        assert rel(opt_c.flat_grad, opt_r.flat_grad) < 1e-5
+    assert step.captures == n_prepared  # nothing captured after prepare()
+    assert step.replays == len(pairs) + 2
+    # a tight slack refuses the oversized graph and captures an exact one
+    tight = CapturedTrainStep(cap, opt_c, crit, node_quantum=64, edge_quantum=256, node_slack=0)
+    tight.prepare(order[:1])
+    small = order[-1]
+    assert tight.lookup(*small) is None
+    tight.prepare([small])
+    assert tight.captures == 2 and tight.lookup(*small) is not None

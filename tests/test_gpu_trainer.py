@@ -174,3 +174,34 @@ def test_trainer_hip_graph_matches_eager(dev, tmp_path, monkeypatch, aug):
             # rounding noise in either run (tests/test_gpu_models.py:pre_bn_bias)
             continue
         assert (a - b).norm().item() <= 1e-2 * max(b.norm().item(), 1e-12), k
+
+
+@pytest.mark.parametrize("hg", [False, True])
+def test_invalid_batch_between_log_steps_raises(dev, tmp_path, monkeypatch, hg):
+    """The status word is sticky: a batch with an out-of-vocabulary atom that
+    is NOT the logged one (valid batches after it) still makes the next
+    check_inputs raise, in the eager and in the captured step."""
+    from molclr_amd.data import Batch
+    from molclr_amd.dataset import SyntheticPairBatches
+    from molclr_amd.molclr import MolCLR
+    monkeypatch.chdir(tmp_path)
+    config = _config("node", "synthetic:64", tmp_path)
+    config["hip_graph"] = hg
+    trainer = MolCLR(_wrapper(config), config)
+    torch.manual_seed(0)
+    model = trainer.build_model()
+    opt, _ = trainer.build_optimizer(model)
+    pairs = SyntheticPairBatches(16, seed=4).take(4)
+    x = pairs[1][0].x.clone()
+    x[3, 1] = 3  # CHI_OTHER: no embedding row
+    xi = pairs[1][0]
+    bad = Batch(x=x, edge_index=xi.edge_index, edge_attr=xi.edge_attr, batch=xi.batch)
+    bad._num_graphs = 16
+    pairs[1] = (bad, pairs[1][1])
+    trainer.train_step(model, opt, *pairs[0], 0)
+    trainer.check_inputs()  # clean so far
+    for i, (a, b) in enumerate(pairs[1:]):
+        trainer.train_step(model, opt, a, b, i + 1)
+    assert (getattr(trainer, "_captured", None) is not None) == hg
+    with pytest.raises(ValueError, match="embedding tables"):
+        trainer.check_inputs()

@@ -43,6 +43,12 @@ for s in $steps; do
     bench5)  run bench5 600 python bench.py --no-cpu-baseline --config c5; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench3)  run bench3 600 python bench.py --no-cpu-baseline --config c3; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchfull) run benchfull 900 python bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    benchd)  run benchd 600 python bench.py --steps 20 --warmup 5; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    benchd5) run benchd5 600 python bench.py --steps 20 --warmup 5 --config c5 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    benchd3) run benchd3 600 python bench.py --steps 20 --warmup 5 --config c3 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    tbench)  for c in ${TB_CASES:-c2:node c2:subgraph c2:mix c3:node}; do
+               run "tbench_${c%%:*}_${c##*:}" 600 python -u tools/trainer_bench.py --config ${c%%:*} --aug ${c##*:}; rc=$?; [ $rc -eq 0 ] || exit $rc
+             done ;;
     prof5)   export TMPDIR=/tmp; rm -rf gpurun_out/prof5
              run prof5 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof5 -o run --output-format csv -- python bench.py --config c5 --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     prof)    export TMPDIR=/tmp; rm -rf gpurun_out/prof
