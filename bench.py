@@ -93,10 +93,13 @@ def parse():
                         "built inside every step by molclr_mask_views from a resident "
                         "molecule store; subgraph / mix: the same with molclr_aug_views "
                         "(dataset_subgraph.py / dataset_mix.py views)")
+    p.add_argument("--dp", action="store_true",
+                   help="at N = 1, run the data-parallel code path anyway (an RCCL group of one: "
+                        "group NT-Xent, bucketed gradient all-reduce)")
     p.add_argument("--no-hip-graph", action="store_true",
                    help="run every step eagerly (host-enqueued launches) instead of replaying "
                         "the HIP graph captured per batch-size bucket (molclr_amd.graph_step; "
-                        "single process, paired pass only)")
+                        "paired pass only; N > 1 captures the RCCL collectives too)")
     return p.parse_args()
 
 
@@ -242,6 +245,17 @@ def main():
     from molclr_amd.nt_xent import NTXentLoss
     from molclr_amd.optim import FusedAdam
 
+    if args.dp and int(os.environ.get("WORLD_SIZE", 1)) == 1:
+        # the data-parallel code path on one GPU: an RCCL process group of one
+        import socket
+        import torch.distributed as dist
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(s.getsockname()[1]))
+        s.close()
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     rank, world, dev = mdist.init()
     if world != args.gpus:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
@@ -271,12 +285,14 @@ def main():
         model = GCN(cfg["num_layer"], cfg["emb_dim"], cfg["feat_dim"]).to(dev)
     # parameters in gradient-bucket order: the overlapped all-reduce's buckets
     # are slices of the flat gradient buffer (DP only)
-    opt = FusedAdam(mdist.bucketed_parameters(model) if world > 1 else model.parameters(), 5e-4,
+    # data-parallel code path: N > 1, or --dp at N = 1 (an RCCL group of one)
+    dp = world > 1 or args.dp
+    opt = FusedAdam(mdist.bucketed_parameters(model) if dp else model.parameters(), 5e-4,
                     weight_decay=1e-5)
     mdist.broadcast_params(opt.flat)
     reducer = (mdist.OverlappedGradReducer(model, opt, torch.distributed.group.WORLD)
-               if world > 1 and not args.two_pass else None)
-    group = torch.distributed.group.WORLD if world > 1 else None
+               if dp and not args.two_pass else None)
+    group = torch.distributed.group.WORLD if dp else None
     crit = NTXentLoss(dev, B * world, 0.1, True, group=group)
 
     store = None
@@ -295,9 +311,11 @@ def main():
     # the scatter-add timed for the HBM roofline: GINE's, or GCN's for c3
     agg_kind = "gcn_aggregate_fwd" if cfg["model_type"] == "gcn" else "gine_aggregate_fwd"
     captured = None
-    if world == 1 and not args.two_pass and not args.no_hip_graph:
+    if not args.two_pass and not args.no_hip_graph:
+        # N > 1: the step's RCCL collectives (NT-Xent all-gathers, bucketed
+        # gradient all-reduces) are captured with it
         from molclr_amd.graph_step import CapturedTrainStep
-        captured = CapturedTrainStep(model, opt, crit)
+        captured = CapturedTrainStep(model, opt, crit, reducer=reducer)
 
     def step(i, eager=False):
         xi, xj = views_of(i)
@@ -321,7 +339,7 @@ def main():
         loss.backward()
         if reducer is not None:  # bucketed, overlapped with the encoder backward
             reducer.finish()
-        elif world > 1:
+        elif dp:
             mdist.allreduce_grads(opt.flat_grad)
         opt.step()
         return loss
@@ -498,7 +516,8 @@ def main():
                        f"{cfg['num_layer']}x{cfg['emb_dim']} feat {cfg['feat_dim']}",
                        "global_batch": B * world, "per_gpu_batch": B,
                        "mean_nodes_per_view": round(n_nodes), "mean_edges_per_view": round(n_edges),
-                       "parallelism": f"dp{world}",
+                       "parallelism": f"dp{world}" + (" (RCCL group of one)" if dp and world == 1
+                                                      else ""),
                        "views": ("two encoder calls (molclr.py:57,60)" if args.two_pass else
                                  "one paired encoder pass, per-view BatchNorm statistics"),
                        "launch": ("HIP graph per batch-size capacity bucket "
@@ -517,7 +536,7 @@ def main():
             "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

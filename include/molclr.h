@@ -215,8 +215,9 @@ int molclr_mask_views(const int64_t* store_x, const int64_t* store_atom_ptr,
  * bits: 0 molecule id out of range, 1 num_nodes mismatch, 2 edge index out
  * of its molecule (clamped), 3 the frontier emptied before the quota (the
  * subgraph module would not terminate; dataset_mix.py:55-56's guard is
- * applied), 4 a molecule over 256 atoms / 512 bonds (left un-augmented),
- * 5 a centre atom without bonds (the reference raises). */
+ * applied), 4 a molecule over 256 atoms / 512 bonds (left un-augmented; with
+ * molclr_aug_views_plan_big: over its large-molecule caps), 5 a centre atom
+ * without bonds (the reference raises). */
 enum { MOLCLR_AUG_SUBGRAPH = 0, MOLCLR_AUG_MIX = 1 };
 size_t molclr_aug_views_workspace_bytes(int64_t batch_size, int64_t num_nodes, int64_t num_bonds);
 int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
@@ -225,6 +226,25 @@ int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_ed
                           int mode, int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
                           int64_t* num_edges_out, int32_t* status, void* workspace,
                           size_t workspace_bytes, molclr_stream_t stream);
+/* The plan with molecules beyond the in-LDS caps (256 atoms / 512 bonds)
+ * augmented too, the reference's behaviour for every molecule
+ * (dataset_subgraph.py:96-177 and dataset_mix.py:86-217 have no size limit):
+ * they run the same plan over int32 tables in `big_workspace`, one slot per
+ * such molecule of the batch.  big_slots >= the batch's count of such
+ * molecules, big_atoms / big_bonds >= their largest atom / bond counts
+ * (molecules past these caps pass unchanged, status bit 4).  Results are
+ * identical to molclr_aug_views_plan's on every molecule within its caps. */
+size_t molclr_aug_views_big_workspace_bytes(int64_t big_slots, int64_t big_atoms,
+                                            int64_t big_bonds);
+int molclr_aug_views_plan_big(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
+                              const int64_t* store_bond_ptr, int64_t store_mols,
+                              int64_t store_edges, const int64_t* mol_ids, int64_t batch_size,
+                              uint64_t seed, int view, int mode, int64_t num_nodes,
+                              int64_t num_bonds, int64_t* ptr_out, int64_t* num_edges_out,
+                              int32_t* status, void* workspace, size_t workspace_bytes,
+                              int64_t big_slots, int64_t big_atoms, int64_t big_bonds,
+                              void* big_workspace, size_t big_workspace_bytes,
+                              molclr_stream_t stream);
 int molclr_aug_views_write(const int64_t* store_x, const int64_t* store_atom_ptr,
                            const int64_t* store_edge_index, const int64_t* store_edge_attr,
                            const int64_t* store_bond_ptr, int64_t store_mols, int64_t store_edges,

@@ -132,6 +132,10 @@ SIGNATURES = {
     "molclr_aug_views_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_aug_views_plan": (c_int, [_P, _P, _P, _I64, _I64, _P, _I64, ctypes.c_uint64, c_int,
                                       c_int, _I64, _I64, _P, _P, _P, _P, c_size_t, _P]),
+    "molclr_aug_views_big_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
+    "molclr_aug_views_plan_big": (c_int, [_P, _P, _P, _I64, _I64, _P, _I64, ctypes.c_uint64,
+                                          c_int, c_int, _I64, _I64, _P, _P, _P, _P, c_size_t,
+                                          _I64, _I64, _I64, _P, c_size_t, _P]),
     "molclr_aug_views_write": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I64,
                                        _I64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "molclr_atom_embed_fwd_bf16": (c_int, [_P, _P, _P, _P, _I64, _I64, _I64, _I64, _P, _P]),

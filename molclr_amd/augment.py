@@ -83,6 +83,13 @@ class DeviceMoleculeStore:
         return {k: getattr(self, k).cpu().numpy()
                 for k in ("x", "atom_ptr", "edge_index", "edge_attr", "bond_ptr")}
 
+    def mask_view_size(self, ids_h) -> tuple[int, int]:
+        """(nodes, directed edges) of one node-masked view of the host ids:
+        every atom, and the bonds left after dropping floor(M / 4) of each
+        molecule's M (dataset.py:133-145) in both directions."""
+        m = self.num_bonds[ids_h]
+        return int(self.num_atoms[ids_h].sum()), int((2 * (m - m // 4)).sum())
+
     def mask_view(self, mol_ids, seed: int, view: int, check: bool = False,
                   host_ids=None) -> Batch:
         """One collated, node-masked view of the molecules ``mol_ids``.
@@ -96,10 +103,7 @@ class DeviceMoleculeStore:
         if ids_h.size and (ids_h.min() < 0 or ids_h.max() >= self.num_molecules):
             raise IndexError("molecule id out of range")
         B = int(ids_h.shape[0])
-        n = self.num_atoms[ids_h]
-        m = self.num_bonds[ids_h]
-        N = int(n.sum())
-        E = int((2 * (m - m // 4)).sum())
+        N, E = self.mask_view_size(ids_h)
         dev = self.device
         i64 = dict(dtype=torch.int64, device=dev)
         ids = (mol_ids.to(torch.int64).contiguous() if on_dev
@@ -139,8 +143,9 @@ class DeviceMoleculeStore:
     AUG_MAX_ATOMS, AUG_MAX_BONDS = 256, 512   # augment.hip kAugMaxAtoms / kAugMaxBonds
 
     def aug_capable(self) -> np.ndarray:
-        """Per molecule: small enough for the subgraph / mix kernels (larger
-        molecules come back unaugmented with status bit 4)."""
+        """Per molecule: small enough for the in-LDS subgraph / mix plan;
+        larger ones run the same plan from a global workspace
+        (molclr_aug_views_plan_big): every molecule is augmented."""
         return (self.num_atoms <= self.AUG_MAX_ATOMS) & (self.num_bonds <= self.AUG_MAX_BONDS)
 
     def aug_view(self, mol_ids, seed: int, view: int, mode: str = "subgraph",
@@ -169,10 +174,20 @@ class DeviceMoleculeStore:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         st = _lib.stream_of(dev)
         E_store = int(self.edge_index.shape[1])
-        _lib.call("molclr_aug_views_plan", self.atom_ptr.data_ptr(), self.edge_index.data_ptr(),
-                  self.bond_ptr.data_ptr(), self.num_molecules, E_store, ids.data_ptr(), B,
-                  int(seed) & 0xFFFFFFFFFFFFFFFF, int(view), self.AUG_MODES[mode], N, Mb,
-                  ptr.data_ptr(), ne.data_ptr(), status.data_ptr(), ws.data_ptr(), ws_bytes, st)
+        # molecules beyond the in-LDS caps: one global-workspace slot each
+        na, nb = self.num_atoms[ids_h], self.num_bonds[ids_h]
+        big = (na > self.AUG_MAX_ATOMS) | (nb > self.AUG_MAX_BONDS)
+        nbig = int(big.sum())
+        big_atoms = int(na[big].max()) if nbig else 0
+        big_bonds = int(nb[big].max()) if nbig else 0
+        bws_bytes = _lib.query("molclr_aug_views_big_workspace_bytes", nbig, big_atoms, big_bonds)
+        bws = torch.empty(max(bws_bytes, 1), dtype=torch.uint8, device=dev)
+        _lib.call("molclr_aug_views_plan_big", self.atom_ptr.data_ptr(),
+                  self.edge_index.data_ptr(), self.bond_ptr.data_ptr(), self.num_molecules,
+                  E_store, ids.data_ptr(), B, int(seed) & 0xFFFFFFFFFFFFFFFF, int(view),
+                  self.AUG_MODES[mode], N, Mb, ptr.data_ptr(), ne.data_ptr(), status.data_ptr(),
+                  ws.data_ptr(), ws_bytes, nbig, big_atoms, big_bonds, bws.data_ptr(), bws_bytes,
+                  st)
         E = int(ne.item())  # the data-dependent edge count sizes the outputs
         x = torch.empty(N, 2, **i64)
         ei = torch.empty(2, E, **i64)

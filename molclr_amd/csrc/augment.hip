@@ -219,40 +219,67 @@ __global__ __launch_bounds__(64 * kMolsPerBlock) void k_mask_views(
 // top 53 bits of a per-view key; mix's extra atom / bond masks are the
 // k-smallest-key subsets of the remaining atoms / surviving bonds.
 // ---------------------------------------------------------------------------
-constexpr int kAugMaxAtoms = 256;  // per molecule (LDS tables); larger: status bit 4
+constexpr int kAugMaxAtoms = 256;  // per molecule in the LDS plan; larger: k_aug_plan_big
 constexpr int kAugMaxBonds = 512;
 constexpr int kSetSlots = 2048;    // the emulated set never exceeds this for <= 256 keys
+
+// The plan's tables: in LDS (int16 indices) for molecules within the caps
+// above, or (int32 indices) in a global workspace slot for larger ones.
+template <typename I>
+struct AugTabs {
+  I* adj_off;      // [n + 1]
+  I* adj;          // [2 M]
+  I* first;        // [n] position in nx node order, -1: not in the bond graph
+  I* removed;      // [n]
+  I* in_temp;      // [n]
+  I* temp;         // [n]
+  I* nbr;          // [2 M]
+  I* table;        // [set slots]
+  I* fill_cursor;  // [n]
+};
 
 struct AugLds {
   int16_t adj_off[kAugMaxAtoms + 1];
   int16_t adj[2 * kAugMaxBonds];
-  int16_t first[kAugMaxAtoms];   // position in nx node order, -1: not in the bond graph
-  uint8_t removed[kAugMaxAtoms];
-  uint8_t in_temp[kAugMaxAtoms];
+  int16_t first[kAugMaxAtoms];
+  int16_t removed[kAugMaxAtoms];
+  int16_t in_temp[kAugMaxAtoms];
   int16_t temp[kAugMaxAtoms];
   int16_t nbr[2 * kAugMaxBonds];
   int16_t table[kSetSlots];
   int16_t fill_cursor[kAugMaxAtoms];
 };
 
+// set slots a molecule of n atoms can need: CPython grows to the power of two
+// above 4 x fill (fill <= n), from 8
+__host__ __device__ inline int64_t aug_set_slots(int64_t n) {
+  int64_t s = 8;
+  while (s <= 4 * n) s <<= 1;
+  return s;
+}
+// int32 elements of one global-workspace slot for n atoms / M bonds
+__host__ __device__ inline int64_t aug_big_slot_elems(int64_t n, int64_t M) {
+  return (n + 1) + 2 * M + 5 * n + 2 * M + aug_set_slots(n) + n + 4;
+}
+
 // CPython set(list) of non-negative ints: iteration order into out, returns
 // its length.  `scratch` holds the old keys during a resize (it may be `out`:
 // out is written only at the end).
-__device__ int pyset_order(const int16_t* items, int n_items, int16_t* table, int16_t* out,
-                           int16_t* scratch) {
+template <typename I>
+__device__ int pyset_order(const I* items, int n_items, I* table, I* out, I* scratch) {
   int mask = 7, fill = 0;
   for (int t = 0; t <= mask; ++t) table[t] = -1;
   auto insert_clean = [&](int k) {
     uint32_t i = (uint32_t)k & mask, perturb = (uint32_t)k;
     while (true) {
       if (table[i] < 0) {
-        table[i] = (int16_t)k;
+        table[i] = (I)k;
         return;
       }
       if (i + 9 <= (uint32_t)mask)
         for (uint32_t j = i + 1; j <= i + 9; ++j)
           if (table[j] < 0) {
-            table[j] = (int16_t)k;
+            table[j] = (I)k;
             return;
           }
       perturb >>= 5;
@@ -268,7 +295,7 @@ __device__ int pyset_order(const int16_t* items, int n_items, int16_t* table, in
       bool done = false;
       for (uint32_t j = i; j <= last; ++j) {
         if (table[j] < 0) {
-          table[j] = (int16_t)k;
+          table[j] = (I)k;
           inserted = done = true;
           break;
         }
@@ -299,12 +326,14 @@ __device__ int pyset_order(const int16_t* items, int n_items, int16_t* table, in
 }
 
 // pass 1: per batch slot atom and bond offsets (ptr_out, bond_off), sizes
-// checked against the caps
+// checked against the caps (big_caps: the large-molecule slots' atoms / bonds,
+// 0 / 0 without a large-molecule pass); zeroes the large-molecule slot counter
 __global__ void k_aug_offsets(const int64_t* __restrict__ atom_ptr,
                               const int64_t* __restrict__ bond_ptr,
                               const int64_t* __restrict__ mol_ids, int64_t B, int64_t G,
                               int64_t* __restrict__ ptr_out, int64_t* __restrict__ bond_off,
-                              int64_t num_nodes, int32_t* __restrict__ status) {
+                              int64_t num_nodes, int32_t* __restrict__ status, int64_t big_atoms,
+                              int64_t big_bonds, int32_t* __restrict__ big_counter) {
   __shared__ int64_t sa[1024], se[1024];
   __shared__ int64_t carry_a, carry_e;
   const int t = threadIdx.x;
@@ -312,6 +341,7 @@ __global__ void k_aug_offsets(const int64_t* __restrict__ atom_ptr,
     carry_a = 0;
     carry_e = 0;
     *status = 0;
+    if (big_counter) *big_counter = 0;
   }
   __syncthreads();
   int bad = 0;
@@ -325,7 +355,8 @@ __global__ void k_aug_offsets(const int64_t* __restrict__ atom_ptr,
       } else {
         n = atom_ptr[id + 1] - atom_ptr[id];
         m = bond_ptr[id + 1] - bond_ptr[id];
-        if (n > kAugMaxAtoms || m > kAugMaxBonds) bad |= 16;
+        if ((n > kAugMaxAtoms || m > kAugMaxBonds) && (n > big_atoms || m > big_bonds))
+          bad |= 16;
       }
     }
     sa[t] = n;
@@ -358,30 +389,15 @@ __global__ void k_aug_offsets(const int64_t* __restrict__ atom_ptr,
   if (bad) atomicOr(status, bad);
 }
 
-// pass 2: one wave per molecule (lane 0 runs the reference loop in LDS):
-// drop[atom] = masked to [118, 0], keep[bond] = the bond survives, cnt[b] =
-// surviving bonds.  mode 0: dataset_subgraph (25 %), 1: dataset_mix.
-__global__ __launch_bounds__(64) void k_aug_plan(
-    const int64_t* __restrict__ atom_ptr, const int64_t* __restrict__ sei,
-    const int64_t* __restrict__ bond_ptr, int64_t store_edges, const int64_t* __restrict__ mol_ids,
-    int64_t B, int64_t G, uint64_t seed, int view, int mode, const int64_t* __restrict__ ptr,
-    const int64_t* __restrict__ bond_off, uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
-    int64_t* __restrict__ cnt, int32_t* __restrict__ status) {
-  __shared__ AugLds L;
-  const int64_t b = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int64_t id = mol_ids[b];
-  if (id < 0 || id >= G) return;  // flagged by k_aug_offsets
-  const int64_t a0 = atom_ptr[id], n = atom_ptr[id + 1] - a0;
-  const int64_t m0 = bond_ptr[id], M = bond_ptr[id + 1] - m0;
-  const int64_t aoff = ptr[b], boff = bond_off[b];
-  if (n > kAugMaxAtoms || M > kAugMaxBonds) {  // flagged; the molecule passes unchanged
-    for (int64_t i = lane; i < n; i += 64) drop[aoff + i] = 0;
-    for (int64_t m = lane; m < M; m += 64) keep[boff + m] = 1;
-    if (lane == 0) cnt[b] = M;
-    return;
-  }
-  if (lane != 0) return;
+// One molecule's plan, run by a single lane over the tables L: drop[atom] =
+// masked to [118, 0], keep[bond] = the bond survives, cnt[b] = surviving
+// bonds.  mode 0: dataset_subgraph (25 %), 1: dataset_mix.
+template <typename I>
+__device__ void aug_plan_one(const AugTabs<I>& L, const int64_t* __restrict__ sei,
+                             int64_t store_edges, int64_t id, int64_t n, int64_t m0, int64_t M,
+                             uint64_t seed, int view, int mode, int64_t aoff, int64_t boff, int64_t b,
+                             uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
+                             int64_t* __restrict__ cnt, int32_t* __restrict__ status) {
   int bad = 0;
   // bond endpoints (molecule-local, clamped), nx node order, adjacency in bond order
   auto ends = [&](int64_t m, int& s, int& e) {
@@ -405,8 +421,8 @@ __global__ __launch_bounds__(64) void k_aug_plan(
   for (int64_t m = 0; m < M; ++m) {
     int s, e;
     ends(m, s, e);
-    if (L.first[s] < 0) L.first[s] = (int16_t)nodes++;
-    if (L.first[e] < 0) L.first[e] = (int16_t)nodes++;
+    if (L.first[s] < 0) L.first[s] = (I)nodes++;
+    if (L.first[e] < 0) L.first[e] = (I)nodes++;
     ++L.adj_off[s + 1];
     if (e != s) ++L.adj_off[e + 1];
   }
@@ -421,8 +437,8 @@ __global__ __launch_bounds__(64) void k_aug_plan(
     bool dup = false;
     for (int q = L.adj_off[s]; q < L.fill_cursor[s]; ++q) dup |= L.adj[q] == e;
     if (dup) continue;
-    L.adj[L.fill_cursor[s]++] = (int16_t)e;
-    if (e != s) L.adj[L.fill_cursor[e]++] = (int16_t)s;
+    L.adj[L.fill_cursor[s]++] = (I)e;
+    if (e != s) L.adj[L.fill_cursor[e]++] = (I)s;
   }
   // Graph.copy() reorders every neighbour list: the neighbours earlier in node
   // order first (in node order), then the later ones in bond order
@@ -441,7 +457,7 @@ __global__ __launch_bounds__(64) void k_aug_plan(
     for (int q = 0; q < d; ++q)
       if (L.first[L.adj[a + q]] > L.first[w]) L.nbr[k++] = L.adj[a + q];
     for (int q = 0; q < k; ++q) L.adj[a + q] = L.nbr[q];
-    L.fill_cursor[w] = (int16_t)(a + k);  // a self-loop drops out of the walk
+    L.fill_cursor[w] = (I)(a + k);  // a self-loop drops out of the walk
   }
   // centres: smallest / second smallest key of the molecule's centre stream
   int centre = 0;
@@ -470,7 +486,7 @@ __global__ __launch_bounds__(64) void k_aug_plan(
   }
   const int num = (int)floor((double)nodes * pct);
   int nrem = 0, nt = 1;
-  L.temp[0] = (int16_t)centre;
+  L.temp[0] = (I)centre;
   if (num > 0 && L.first[centre] < 0) bad |= 32;  // the reference raises (centre not in G)
   while (nrem < num) {
     if (nt < 1) {  // dataset_mix.py:55-56; dataset_subgraph.py would not terminate
@@ -483,7 +499,7 @@ __global__ __launch_bounds__(64) void k_aug_plan(
       const int u = L.temp[q];
       for (int a = L.adj_off[u]; a < L.fill_cursor[u]; ++a) {
         const int v = L.adj[a];
-        if (!L.removed[v] && !L.in_temp[v]) L.nbr[nn++] = (int16_t)v;
+        if (!L.removed[v] && !L.in_temp[v]) L.nbr[nn++] = (I)v;
       }
     }
     for (int q = 0; q < nt; ++q) {
@@ -495,7 +511,7 @@ __global__ __launch_bounds__(64) void k_aug_plan(
       }
     }
     for (int q = 0; q < nt; ++q) L.in_temp[L.temp[q]] = 0;
-    nt = pyset_order(L.nbr, nn, L.table, L.temp, L.temp);  // temp is free here: scratch, then out
+    nt = pyset_order<I>(L.nbr, nn, L.table, L.temp, L.temp);  // temp is free here: scratch, then out
   }
   // bonds surviving the removal
   int64_t kept = 0;
@@ -507,7 +523,7 @@ __global__ __launch_bounds__(64) void k_aug_plan(
     keep[boff + m] = k ? 1 : 0;
     kept += k ? 1 : 0;
   }
-  for (int i = 0; i < n; ++i) drop[aoff + i] = L.removed[i];
+  for (int i = 0; i < n; ++i) drop[aoff + i] = L.removed[i] ? 1 : 0;
   if (mode == 1) {
     // extra atom masks among the remaining atoms, extra bond masks among the
     // surviving bonds (dataset_mix.py:174-181)
@@ -534,6 +550,99 @@ __global__ __launch_bounds__(64) void k_aug_plan(
   }
   cnt[b] = kept;
   if (bad) atomicOr(status, bad);
+}
+
+// a molecule the plan leaves unchanged (flagged: beyond every cap)
+__device__ void aug_passthrough(int lane, int64_t n, int64_t M, int64_t aoff, int64_t boff,
+                                int64_t b, uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
+                                int64_t* __restrict__ cnt) {
+  for (int64_t i = lane; i < n; i += 64) drop[aoff + i] = 0;
+  for (int64_t m = lane; m < M; m += 64) keep[boff + m] = 1;
+  if (lane == 0) cnt[b] = M;
+}
+
+// pass 2: one wave per molecule (lane 0 runs the reference loop in LDS).
+// Molecules beyond the LDS caps are left to k_aug_plan_big when `big` is set,
+// else they pass unchanged (flagged by k_aug_offsets).
+__global__ __launch_bounds__(64) void k_aug_plan(
+    const int64_t* __restrict__ atom_ptr, const int64_t* __restrict__ sei,
+    const int64_t* __restrict__ bond_ptr, int64_t store_edges, const int64_t* __restrict__ mol_ids,
+    int64_t B, int64_t G, uint64_t seed, int view, int mode, const int64_t* __restrict__ ptr,
+    const int64_t* __restrict__ bond_off, uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
+    int64_t* __restrict__ cnt, int32_t* __restrict__ status, int big) {
+  __shared__ AugLds S;
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t id = mol_ids[b];
+  if (id < 0 || id >= G) return;  // flagged by k_aug_offsets
+  const int64_t a0 = atom_ptr[id], n = atom_ptr[id + 1] - a0;
+  const int64_t m0 = bond_ptr[id], M = bond_ptr[id + 1] - m0;
+  const int64_t aoff = ptr[b], boff = bond_off[b];
+  if (n > kAugMaxAtoms || M > kAugMaxBonds) {
+    if (!big) aug_passthrough(lane, n, M, aoff, boff, b, drop, keep, cnt);
+    return;
+  }
+  if (lane != 0) return;
+  const AugTabs<int16_t> L{S.adj_off, S.adj, S.first, S.removed, S.in_temp,
+                           S.temp, S.nbr, S.table, S.fill_cursor};
+  aug_plan_one<int16_t>(L, sei, store_edges, id, n, m0, M, seed, view, mode, aoff, boff, b, drop,
+                        keep, cnt, status);
+}
+
+// pass 2, molecules beyond the LDS caps: the same plan over int32 tables in a
+// global workspace slot (slots handed out by an atomic counter; a molecule's
+// result does not depend on its slot).  Molecules beyond big_atoms /
+// big_bonds or past big_slots pass unchanged (status bit 4 from k_aug_offsets,
+// or set here).
+__global__ __launch_bounds__(64) void k_aug_plan_big(
+    const int64_t* __restrict__ atom_ptr, const int64_t* __restrict__ sei,
+    const int64_t* __restrict__ bond_ptr, int64_t store_edges, const int64_t* __restrict__ mol_ids,
+    int64_t B, int64_t G, uint64_t seed, int view, int mode, const int64_t* __restrict__ ptr,
+    const int64_t* __restrict__ bond_off, uint8_t* __restrict__ drop, uint8_t* __restrict__ keep,
+    int64_t* __restrict__ cnt, int32_t* __restrict__ status, int64_t big_atoms, int64_t big_bonds,
+    int64_t big_slots, int32_t* __restrict__ counter, int32_t* __restrict__ slots) {
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int64_t id = mol_ids[b];
+  if (id < 0 || id >= G) return;
+  const int64_t a0 = atom_ptr[id], n = atom_ptr[id + 1] - a0;
+  const int64_t m0 = bond_ptr[id], M = bond_ptr[id + 1] - m0;
+  if (n <= kAugMaxAtoms && M <= kAugMaxBonds) return;  // k_aug_plan's
+  const int64_t aoff = ptr[b], boff = bond_off[b];
+  if (n > big_atoms || M > big_bonds) {
+    aug_passthrough(lane, n, M, aoff, boff, b, drop, keep, cnt);
+    return;
+  }
+  if (lane != 0) return;
+  const int slot = atomicAdd(counter, 1);
+  if (slot >= big_slots) {
+    for (int64_t i = 0; i < n; ++i) drop[aoff + i] = 0;
+    for (int64_t m = 0; m < M; ++m) keep[boff + m] = 1;
+    cnt[b] = M;
+    atomicOr(status, 16);
+    return;
+  }
+  int32_t* w = slots + (int64_t)slot * aug_big_slot_elems(big_atoms, big_bonds);
+  AugTabs<int32_t> L;
+  L.adj_off = w;
+  w += big_atoms + 1;
+  L.adj = w;
+  w += 2 * big_bonds;
+  L.first = w;
+  w += big_atoms;
+  L.removed = w;
+  w += big_atoms;
+  L.in_temp = w;
+  w += big_atoms;
+  L.temp = w;
+  w += big_atoms;
+  L.fill_cursor = w;
+  w += big_atoms;
+  L.nbr = w;
+  w += 2 * big_bonds;
+  L.table = w;
+  aug_plan_one<int32_t>(L, sei, store_edges, id, n, m0, M, seed, view, mode, aoff, boff, b, drop,
+                        keep, cnt, status);
 }
 
 // exclusive scan of the surviving-bond counts into edge offsets (2 per bond)
@@ -681,13 +790,14 @@ MOLCLR_API size_t molclr_aug_views_workspace_bytes(int64_t batch_size, int64_t n
          6 * 256;
 }
 
-MOLCLR_API int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
-                                     const int64_t* store_bond_ptr, int64_t store_mols,
-                                     int64_t store_edges, const int64_t* mol_ids,
-                                     int64_t batch_size, uint64_t seed, int view, int mode,
-                                     int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
-                                     int64_t* num_edges_out, int32_t* status, void* workspace,
-                                     size_t workspace_bytes, molclr_stream_t stream) {
+namespace {
+int aug_plan_impl(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
+                  const int64_t* store_bond_ptr, int64_t store_mols, int64_t store_edges,
+                  const int64_t* mol_ids, int64_t batch_size, uint64_t seed, int view, int mode,
+                  int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out, int64_t* num_edges_out,
+                  int32_t* status, void* workspace, size_t workspace_bytes, int64_t big_slots,
+                  int64_t big_atoms, int64_t big_bonds, void* big_ws, size_t big_ws_bytes,
+                  hipStream_t s) {
   MOLCLR_REQUIRE(batch_size >= 0 && store_mols >= 0 && store_edges >= 0 && num_nodes >= 0 &&
                      num_bonds >= 0,
                  "aug_views_plan: negative size");
@@ -701,15 +811,35 @@ MOLCLR_API int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_
   MOLCLR_REQUIRE(batch_size <= (1ll << 31), "aug_views_plan: batch too large");
   MOLCLR_REQUIRE_WS(workspace_bytes,
                     molclr_aug_views_workspace_bytes(batch_size, num_nodes, num_bonds));
-  hipStream_t s = molclr::as_stream(stream);
+  MOLCLR_REQUIRE(big_slots >= 0 && big_atoms >= 0 && big_bonds >= 0 && big_atoms < (1ll << 30) &&
+                     big_bonds < (1ll << 29),
+                 "aug_views_plan_big: bad large-molecule caps");
+  const bool big = big_slots > 0;
+  if (big) {
+    MOLCLR_REQUIRE(big_ws != nullptr, "aug_views_plan_big: null workspace");
+    MOLCLR_REQUIRE_WS(big_ws_bytes,
+                      molclr_aug_views_big_workspace_bytes(big_slots, big_atoms, big_bonds));
+  }
+  int32_t* counter = big ? static_cast<int32_t*>(big_ws) : nullptr;
+  int32_t* slots = big ? static_cast<int32_t*>(big_ws) + 64 : nullptr;  // counter on its own line
   const AugWs a = aug_ws(workspace, workspace_bytes, batch_size, num_nodes, num_bonds);
   hipLaunchKernelGGL(k_aug_offsets, dim3(1), dim3(1024), 0, s, store_atom_ptr, store_bond_ptr,
-                     mol_ids, batch_size, store_mols, ptr_out, a.bond_off, num_nodes, status);
-  if (batch_size > 0)
+                     mol_ids, batch_size, store_mols, ptr_out, a.bond_off, num_nodes, status,
+                     big ? big_atoms : (int64_t)0, big ? big_bonds : (int64_t)0, counter);
+  if (batch_size > 0) {
     hipLaunchKernelGGL(k_aug_plan, dim3((unsigned)batch_size), dim3(64), 0, s, store_atom_ptr,
                        store_edge_index, store_bond_ptr, store_edges, mol_ids, batch_size,
                        store_mols, seed, view, mode, static_cast<const int64_t*>(ptr_out),
-                       static_cast<const int64_t*>(a.bond_off), a.drop, a.keep, a.cnt, status);
+                       static_cast<const int64_t*>(a.bond_off), a.drop, a.keep, a.cnt, status,
+                       big ? 1 : 0);
+    if (big)
+      hipLaunchKernelGGL(k_aug_plan_big, dim3((unsigned)batch_size), dim3(64), 0, s,
+                         store_atom_ptr, store_edge_index, store_bond_ptr, store_edges, mol_ids,
+                         batch_size, store_mols, seed, view, mode,
+                         static_cast<const int64_t*>(ptr_out),
+                         static_cast<const int64_t*>(a.bond_off), a.drop, a.keep, a.cnt, status,
+                         big_atoms, big_bonds, big_slots, counter, slots);
+  }
   hipLaunchKernelGGL(k_aug_edge_offsets, dim3(1), dim3(1024), 0, s,
                      static_cast<const int64_t*>(a.cnt), batch_size, a.edge_off);
   if (hipMemcpyAsync(num_edges_out, a.edge_off + batch_size, sizeof(int64_t),
@@ -719,6 +849,40 @@ MOLCLR_API int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
+}
+}  // namespace
+
+MOLCLR_API size_t molclr_aug_views_big_workspace_bytes(int64_t big_slots, int64_t big_atoms,
+                                                       int64_t big_bonds) {
+  if (big_slots <= 0) return 0;
+  return (size_t)(64 + big_slots * aug_big_slot_elems(big_atoms, big_bonds)) * sizeof(int32_t) +
+         256;
+}
+
+MOLCLR_API int molclr_aug_views_plan(const int64_t* store_atom_ptr, const int64_t* store_edge_index,
+                                     const int64_t* store_bond_ptr, int64_t store_mols,
+                                     int64_t store_edges, const int64_t* mol_ids,
+                                     int64_t batch_size, uint64_t seed, int view, int mode,
+                                     int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
+                                     int64_t* num_edges_out, int32_t* status, void* workspace,
+                                     size_t workspace_bytes, molclr_stream_t stream) {
+  return aug_plan_impl(store_atom_ptr, store_edge_index, store_bond_ptr, store_mols, store_edges,
+                       mol_ids, batch_size, seed, view, mode, num_nodes, num_bonds, ptr_out,
+                       num_edges_out, status, workspace, workspace_bytes, 0, 0, 0, nullptr, 0,
+                       molclr::as_stream(stream));
+}
+
+MOLCLR_API int molclr_aug_views_plan_big(
+    const int64_t* store_atom_ptr, const int64_t* store_edge_index, const int64_t* store_bond_ptr,
+    int64_t store_mols, int64_t store_edges, const int64_t* mol_ids, int64_t batch_size,
+    uint64_t seed, int view, int mode, int64_t num_nodes, int64_t num_bonds, int64_t* ptr_out,
+    int64_t* num_edges_out, int32_t* status, void* workspace, size_t workspace_bytes,
+    int64_t big_slots, int64_t big_atoms, int64_t big_bonds, void* big_workspace,
+    size_t big_workspace_bytes, molclr_stream_t stream) {
+  return aug_plan_impl(store_atom_ptr, store_edge_index, store_bond_ptr, store_mols, store_edges,
+                       mol_ids, batch_size, seed, view, mode, num_nodes, num_bonds, ptr_out,
+                       num_edges_out, status, workspace, workspace_bytes, big_slots, big_atoms,
+                       big_bonds, big_workspace, big_workspace_bytes, molclr::as_stream(stream));
 }
 
 MOLCLR_API int molclr_aug_views_write(const int64_t* store_x, const int64_t* store_atom_ptr,

@@ -64,8 +64,9 @@ def _num_atoms(rng: np.random.Generator, shape: str) -> int:
     raise ValueError(f"unknown molecule size distribution {shape!r}")
 
 
-def random_molecule(rng: np.random.Generator, shape: str = "uniform") -> Molecule:
-    n = _num_atoms(rng, shape)
+def random_molecule(rng: np.random.Generator, shape: str = "uniform",
+                    num_atoms: int | None = None) -> Molecule:
+    n = _num_atoms(rng, shape) if num_atoms is None else int(num_atoms)
     bonds = []
     present = set()
     for i in range(1, n):
@@ -256,6 +257,12 @@ class DeviceViewLoader:
         self.store, self.sampler = store, sampler
         self.batch_size, self.aug, self.seed, self.rank = int(batch_size), aug, seed, rank
         self.epoch = 0
+        # optional callback(sizes, graphs_i, graphs_j) called when an epoch's
+        # batches are drawn, before the first is built, with the (nodes, edges)
+        # of every batch pair of the epoch (node masking: exact; subgraph / mix:
+        # exact nodes, the un-dropped bond count as the edge bound);
+        # MolCLR.train hands it to the HIP-graph step
+        self.on_epoch_plan = None
 
     def __len__(self):
         return len(self.sampler) // self.batch_size
@@ -265,7 +272,18 @@ class DeviceViewLoader:
         epoch = self.epoch
         self.epoch += 1
         bs = self.batch_size
-        for b in range(ids.shape[0] // bs):
+        nb = ids.shape[0] // bs
+        if self.on_epoch_plan is not None and nb:
+            sizes = []
+            for b in range(nb):
+                sel = ids[b * bs:(b + 1) * bs]
+                if self.aug == "node":
+                    n, e = self.store.mask_view_size(sel)
+                else:  # subgraph / mix keep every atom and drop bonds: e is a bound
+                    n, e = int(self.store.num_atoms[sel].sum()), 2 * int(self.store.num_bonds[sel].sum())
+                sizes.append((2 * n, 2 * e))
+            self.on_epoch_plan(sizes, bs, bs)
+        for b in range(nb):
             host = ids[b * bs:(b + 1) * bs]
             key = view_seed(self.seed, self.rank, epoch, b)
             self.last = (host, key)   # the batch's molecule ids and subset key
@@ -371,16 +389,8 @@ class MoleculeDatasetWrapper:
         rank, world = self._rank_world()
         num_train = len(train_dataset) if len_ is None else len_
         indices = np.random.default_rng(self.seed).permutation(num_train).tolist()
-        if self.views == "device" and self.aug != "node":
-            # subgraph / mix views hold a molecule in LDS: larger ones are left out
-            from .augment import DeviceMoleculeStore
-            ok = train_dataset.aug_capable()
-            dropped = int((~ok).sum())
-            if dropped:
-                print(f"{dropped} molecules above {DeviceMoleculeStore.AUG_MAX_ATOMS} atoms / "
-                      f"{DeviceMoleculeStore.AUG_MAX_BONDS} bonds left out of aug={self.aug}")
-                indices = [i for i in indices if ok[i]]
-                num_train = len(indices)
+        # every molecule takes part in every aug mode, as in the reference
+        # (large ones run the subgraph / mix plan from a global workspace)
         split = int(np.floor(self.valid_size * num_train))
         train_idx, valid_idx = indices[split:], indices[:split]
         train_sampler = ShardedSubsetSampler(train_idx, rank, world, seed=self.seed + 1)

@@ -24,8 +24,13 @@ fixed-capacity buffers:
 * The learning rate and Adam's step counter already live on the device
   (FusedAdam); the weight planes are regenerated inside the graph.
 
-Single-process only: the data-parallel step keeps its eager path (its RCCL
-collectives overlap the backward through events on a side stream).
+Data parallel (one process per GPU, RCCL): the step's collectives are
+captured with it -- NT-Xent's two all-gathers, and the bucketed gradient
+all-reduces of OverlappedGradReducer, which wait on the encoder backward's
+per-layer events from a side stream and are joined before Adam, exactly as
+in the eager step (RCCL kernels are captured into the HIP graph like any
+other launch).  Every rank must replay the same sequence of graphs in
+lockstep, as it would issue the same collectives eagerly.
 """
 from __future__ import annotations
 
@@ -172,19 +177,25 @@ class CapturedTrainStep:
     next step.  ``status`` ORs every replayed batch's input-validity word
     (sticky: ``check()`` raises for an invalid batch at any earlier step).
     Requirements: a model with the paired executor path (``forward_staged``),
-    a FusedAdam optimizer, one process."""
+    a FusedAdam optimizer.  Data parallel: a criterion with a process group,
+    and (optionally) an OverlappedGradReducer over the same optimizer --
+    without one, the flat gradient is all-reduced in one collective.  The
+    process group's communicator must exist before the first capture (any
+    collective, e.g. the initial parameter broadcast, creates it)."""
 
     def __init__(self, model, optimizer, criterion, node_quantum: int = 256,
                  edge_quantum: int = 2048, max_graphs: int = 32, node_slack: int | None = None,
-                 edge_headroom: float = 0.04):
+                 edge_headroom: float = 0.04, reducer=None):
         from .optim import FusedAdam
         if not isinstance(optimizer, FusedAdam):
             raise TypeError("CapturedTrainStep needs molclr_amd.optim.FusedAdam "
                             "(learning rate and step counter on the device)")
         if not hasattr(model, "forward_staged"):
             raise TypeError("CapturedTrainStep: the model has no forward_staged")
-        if getattr(criterion, "group", None) is not None:
-            raise ValueError("CapturedTrainStep runs one process; the data-parallel step is eager")
+        self.group = getattr(criterion, "group", None)
+        if reducer is not None and reducer.flat is not optimizer.flat_grad:
+            raise ValueError("CapturedTrainStep: the reducer must reduce this optimizer's gradients")
+        self.reducer = reducer
         self.model, self.optimizer, self.criterion = model, optimizer, criterion
         self.node_quantum, self.edge_quantum = int(node_quantum), int(edge_quantum)
         self.node_slack = 2 * self.node_quantum if node_slack is None else int(node_slack)
@@ -225,14 +236,17 @@ class CapturedTrainStep:
                     best = ent
         return best
 
-    def _capture(self, key, xis, xjs) -> _Captured:
+    def _capture(self, key, pair=None) -> _Captured:
+        """Capture a graph of capacities ``key``; ``pair`` (if given) is staged
+        into it first (the capture itself records, it runs nothing)."""
         if not self.model._executor_ok() or self.model._dim_pad():
             raise NotImplementedError(
                 "CapturedTrainStep: the model must run through the encoder executor with "
                 "emb_dim a multiple of the kernels' width (dropout 0, tracked BatchNorm)")
         ops._check_no_timer()
         graph = StagedPairGraph(self.device, key[0], key[1], key[2:])
-        graph.stage([xis, xjs])
+        if pair is not None:
+            graph.stage(list(pair))
         opt = self.optimizer
         opt.sync_lr()
         # the capture must record the weight-plane regeneration: make every
@@ -240,12 +254,22 @@ class CapturedTrainStep:
         ops.bump_param_generation()
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g, pool=self._pool):
+        # data parallel: the process group's watchdog thread polls its events
+        # while we capture; thread-local capture keeps those calls legal
+        mode = "global" if self.group is None else "thread_local"
+        with torch.cuda.graph(g, pool=self._pool, capture_error_mode=mode):
             graph.build()
             opt.zero_grad()
+            if self.reducer is not None:
+                self.reducer.arm()
             _, z = self.model.forward_staged(graph)
             loss = self.criterion.forward_pair(ops.l2_normalize(z))
             loss.backward()
+            if self.reducer is not None:  # bucketed, overlapped with the backward
+                self.reducer.finish()
+            elif self.group is not None:
+                from .distributed import allreduce_grads
+                allreduce_grads(opt.flat_grad, self.group)
             opt.step(sync_lr=False)
             self.loss.copy_(loss)
             # graph build and atom embedding write the batch's validity bits
@@ -257,14 +281,16 @@ class CapturedTrainStep:
         ops.bump_param_generation()
         return _Captured(graph, g)
 
+    def _insert(self, ent) -> None:
+        self._graphs[id(ent)] = ent
+        if len(self._graphs) > self.max_graphs:
+            self._graphs.popitem(last=False)
+
     def _entry(self, xis, xjs):
         ent = self.lookup(xis, xjs)
         if ent is None:
-            key = self.bucket(xis, xjs)
-            ent = self._capture(key, xis, xjs)  # stages this batch too
-            self._graphs[id(ent)] = ent
-            if len(self._graphs) > self.max_graphs:
-                self._graphs.popitem(last=False)
+            ent = self._capture(self.bucket(xis, xjs), (xis, xjs))  # stages this batch too
+            self._insert(ent)
             return ent, True
         self._graphs.move_to_end(id(ent))
         return ent, False
@@ -275,6 +301,31 @@ class CapturedTrainStep:
         before = self.captures
         for xis, xjs in pairs:
             self._entry(xis, xjs)
+        return self.captures - before
+
+    def prepare_sizes(self, sizes, graphs_i: int, graphs_j: int) -> int:
+        """Capture what batches of the given (nodes, edges) sizes -- both views
+        together, ``graphs_i`` / ``graphs_j`` molecules per view -- will need,
+        largest first, so that each capture serves every smaller size within
+        the node slack (captures spaced ~node_slack + node_quantum apart).
+        Nothing is staged: the first replay stages its batch.  Returns the
+        number of new captures."""
+        before = self.captures
+
+        class _V:  # the shape view lookup() / bucket() read
+            def __init__(self, n, e, g):
+                self.x = torch.empty(n, 0)
+                self.edge_index = torch.empty(2, e)
+                self._num_graphs = g
+
+            @property
+            def num_graphs(self):
+                return self._num_graphs
+
+        for n, e in sorted(((int(a), int(b)) for a, b in sizes), reverse=True):
+            vi, vj = _V(n, e, graphs_i), _V(0, 0, graphs_j)
+            if self.lookup(vi, vj) is None:
+                self._insert(self._capture(self.bucket(vi, vj)))
         return self.captures - before
 
     def __call__(self, xis, xjs) -> torch.Tensor:

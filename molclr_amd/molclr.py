@@ -154,7 +154,7 @@ class MolCLR(object):
         """The HIP-graph step (molclr_amd.graph_step) unless the config turns
         it off (``hip_graph: False``), when the run allows it: one process,
         the paired executor pass at an unpadded width; else None (eager)."""
-        if not self.config.get('hip_graph', True) or self.world > 1:
+        if not self.config.get('hip_graph', True):
             return None
         if not getattr(self, "paired", True) or not hasattr(model, "forward_staged"):
             return None
@@ -163,7 +163,9 @@ class MolCLR(object):
         cs = getattr(self, "_captured", None)
         if cs is None or cs.model is not model or cs.optimizer is not optimizer:
             from .graph_step import CapturedTrainStep
-            cs = self._captured = CapturedTrainStep(model, optimizer, self.nt_xent_criterion)
+            # data parallel: the RCCL collectives are captured with the step
+            cs = self._captured = CapturedTrainStep(model, optimizer, self.nt_xent_criterion,
+                                                    reducer=getattr(self, "reducer", None))
         return cs
 
     def train_step(self, model, optimizer, xis, xjs, n_iter):
@@ -201,6 +203,11 @@ class MolCLR(object):
         if self.rank == 0:
             _save_config_file(model_checkpoints_folder, self.config)
 
+        cs = self._graph_step(model, optimizer)
+        if cs is not None and hasattr(train_loader, "on_epoch_plan"):
+            # capture every graph an epoch's batches need when it is drawn
+            # (node masking: exact sizes), not in the middle of the epoch
+            train_loader.on_epoch_plan = cs.prepare_sizes
         n_iter = 0
         valid_n_iter = 0
         best_valid_loss = np.inf

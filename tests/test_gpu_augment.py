@@ -197,3 +197,28 @@ def test_aug_views_edge_cases(dev):
                     flags |= (8 if f["guard"] else 0) | (32 if f["centre_outside"] else 0)
                 _same_aug(b, ref, allowed_status=flags)
                 assert int(b.status.item()) == flags
+
+
+@pytest.mark.parametrize("mode", ["subgraph", "mix"])
+def test_aug_views_large_molecules(dev, mode):
+    """Molecules beyond the in-LDS plan's 256 atoms / 512 bonds (the
+    reference augments every molecule, dataset_subgraph.py:96-177,
+    dataset_mix.py:86-217) run the same plan from a global workspace
+    (molclr_aug_views_plan_big): bit-exact against the oracle, mixed in a
+    batch with ordinary molecules, status clean."""
+    from molclr_amd.augment import DeviceMoleculeStore
+    from molclr_amd.dataset import random_molecule
+    from oracle.augment_ref import AUG_MIX, AUG_SUBGRAPH, aug_views
+    rng = np.random.default_rng(17)
+    mols = _mols(40, seed=5)
+    for n in (257, 300, 480, 700, 1200):  # 1200 atoms: ~1350 bonds
+        mols.insert(int(rng.integers(0, len(mols))), random_molecule(rng, num_atoms=n))
+    store = DeviceMoleculeStore.from_molecules(mols, dev)
+    assert (~store.aug_capable()).sum() == 5
+    host = store.host_store()
+    ids = rng.permutation(len(mols))
+    m = AUG_SUBGRAPH if mode == "subgraph" else AUG_MIX
+    for seed in (0, 3):
+        bi, bj = store.aug_views(ids, seed, mode, check=True)
+        _same_aug(bi, aug_views(host, ids, seed, 0, m))
+        _same_aug(bj, aug_views(host, ids, seed, 1, m))

@@ -240,9 +240,10 @@ def test_capacity_fit_lookup_and_prepare(dev):
     opt_r = FusedAdam(ref.parameters(), 5e-4, weight_decay=1e-5)
     opt_c = FusedAdam(cap.parameters(), 5e-4, weight_decay=1e-5)
     crit = NTXentLoss(dev, B, 0.1, True)
+    # a slack of ~a quarter of the pairs' rows (B = 32: ~1.9k nodes per pair);
+    # the largest pair's graph serves every smaller one within it
     step = CapturedTrainStep(cap, opt_c, crit, node_quantum=64, edge_quantum=256,
-                             node_slack=4096)
-    # with a wide slack the largest pair's graph serves every smaller one
+                             node_slack=512)
     order = sorted(pairs, key=lambda p: -(p[0].x.shape[0] + p[1].x.shape[0]))
     assert step.prepare(order[:1]) == 1
     biggest = step.lookup(*order[0])
@@ -259,7 +260,21 @@ def test_capacity_fit_lookup_and_prepare(dev):
         lc = step(xi, xj).clone()
         torch.cuda.synchronize()
         assert abs(lc.item() - lr_.item()) <= 1e-6 * abs(lr_.item())
-        assert rel(opt_c.flat_grad, opt_r.flat_grad) < 1e-5
+        # per parameter; the pre-BatchNorm biases have an exact gradient of 0
+        # and hold rounding noise only (tests/test_gpu_models.py: pre_bn_bias).
+        # Bound: the padded rows change the weight gradients' split-K partition
+        # (w6_plan derives it from the row count), i.e. the fp32 summation
+        # order of dW = dY^T X over ~2k rows with cancellation: measured up to
+        # 2.8e-5 here, against ~1e-3 for the reference's own fp32 vs fp64
+        # (paired vs two-call gradients)
+        bad = []
+        for (name, pc), pr in zip(cap.named_parameters(), ref.parameters()):
+            if name.endswith("mlp.2.bias"):
+                continue
+            r = rel(pc.grad, pr.grad)
+            if r > 5e-5:
+                bad.append((name, r))
+        assert not bad, bad
     assert step.captures == n_prepared  # nothing captured after prepare()
     assert step.replays == len(pairs) + 2
     # a tight slack refuses the oversized graph and captures an exact one

@@ -33,6 +33,7 @@ for s in $steps; do
                CASE=${c%%:*} VARIANT=${c##*:} run "gpmc_${c%%:*}_${c##*:}" 400 bash tools/gemm_pmc.sh; rc=$?; [ $rc -eq 0 ] || exit $rc
              done ;;
     graph)   run graph 600 python -m pytest tests/test_gpu_graph_step.py -m gpu -q --maxfail=50 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
+    augment) run augment 600 python -m pytest tests/test_gpu_augment.py -m gpu -q --maxfail=50 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
     trainer) run trainer 600 python -m pytest tests/test_gpu_trainer.py -m gpu -q --maxfail=50 -rf --timeout 300 --timeout-method thread; rc=$? ; [ $rc -le 1 ] || exit $rc ;;
     benche)  run benche 600 python bench.py --no-cpu-baseline --no-hip-graph; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     bench3e) run bench3e 600 python bench.py --no-cpu-baseline --config c3 --no-hip-graph; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
@@ -44,6 +45,7 @@ for s in $steps; do
     bench3)  run bench3 600 python bench.py --no-cpu-baseline --config c3; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchfull) run benchfull 900 python bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchd)  run benchd 600 python bench.py --steps 20 --warmup 5; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+    benchdp) run benchdp 600 python bench.py --dp --steps 20 --warmup 5 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchd5) run benchd5 600 python bench.py --steps 20 --warmup 5 --config c5 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     benchd3) run benchd3 600 python bench.py --steps 20 --warmup 5 --config c3 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
     tbench)  for c in ${TB_CASES:-c2:node c2:subgraph c2:mix c3:node}; do

@@ -81,6 +81,9 @@ def main():
     model = trainer.build_model()
     optimizer, _ = trainer.build_optimizer(model)
 
+    cs0 = trainer._graph_step(model, optimizer)
+    if cs0 is not None and hasattr(train_loader, "on_epoch_plan"):
+        train_loader.on_epoch_plan = cs0.prepare_sizes  # as MolCLR.train sets it
     it = iter(train_loader)
     steps_in_epoch = len(train_loader)
     for i in range(args.warmup):
