@@ -26,6 +26,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace {
 
 using namespace molclr;
@@ -1161,6 +1163,352 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 }
 
 // ---------------------------------------------------------------------------
+// "pp": the q6 product (one K group) as a ping-pong over two wave groups.
+// A block of 8 waves owns 256 rows x BN columns: waves 0-3 (group 0) rows
+// m0 .. m0+127 and waves 4-7 (group 1) rows m0+128 .. m0+255, 32 rows each,
+// every SIMD holding one wave of each group; both groups read one shared B
+// image per K step.  Group 1 runs one phase behind group 0, so between two
+// block barriers one group issues its step's MFMAs -- the B fragments of the
+// next column block read from LDS under the current block's MFMAs, pinned by
+// sched_group_barrier -- while the other splits its next A step into bf16 /
+// fp16 fragments, issues the A loads two steps ahead and (group 1) the
+// LDS-DMA of the next B image:
+//   phase 2i+1: group 0 computes step i      | group 1 splits step i, loads
+//   phase 2i+2: group 0 splits step i+1      | group 1 computes step i
+// The matrix and vector pipes of a SIMD run the two waves' phases side by
+// side (q6: every wave splits and multiplies in turn, each K step behind a
+// barrier of its own group).  Loads use buffer addressing: fixed per-lane
+// offsets, one scalar offset per step.  The products, their order and the
+// epilogue are q6's: results are bit-identical to k_gemm_q6<TN, EPI, 1, *, H3>
+// (tests/test_gpu_kernels.py).  Measured at the c2 shapes (tools/q6x.py):
+// lin1 80 -> 72 us, lin2 69 -> 63, dz1 61 -> 57, dagg 50 -> 46.
+// ---------------------------------------------------------------------------
+constexpr int kPPRows = 256;
+
+template <int TN, int EPI, int H3>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_pp(
+    const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux,
+    int accumulate, const float* __restrict__ amax, const float* __restrict__ bmax,
+    float* __restrict__ cmax, float* __restrict__ crow, float* __restrict__ amax_out,
+    int arow_parts, uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in,
+    int64_t bits_ld) {
+  constexpr int BN = 32 * TN;
+  constexpr int NP = H3 ? 2 : 3;
+  constexpr int BI = NP * BN * XK;
+  // two B images (separate arrays: the LDS-DMA into one must not look like it
+  // aliases the fragment reads of the other) and the epilogue's wave tiles
+  __shared__ __attribute__((aligned(16))) uint16_t bimg0[BI];
+  __shared__ __attribute__((aligned(16))) uint16_t bimg1[BI];
+  __shared__ __attribute__((aligned(16))) float ep[8 * 32 * 32];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, wm = w & 3;
+  const int li = lane & 31, lh = lane >> 5;
+
+  const int ntn = (int)((N + BN - 1) / BN);
+  const int ntm = (int)((M + kPPRows - 1) / kPPRows);
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);  // a row slab's column tiles share an XCD
+  const int64_t m0 = (int64_t)(tile / ntn) * kPPRows;
+  const int64_t n0 = (int64_t)(tile % ntn) * BN;
+  const int64_t mw = m0 + 128 * grp + 32 * wm;  // this wave's first row
+
+  // epilogue operands ahead of the main loop (vmcnt counts stores too)
+  constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
+  constexpr int BVN = HAS_BIAS ? TN : 1, MWN = EPI == MOLCLR_EPI_RELU_MASK ? TN : 1;
+  float4 bvq[BVN];
+  uint32_t mwq[MWN][4];
+  {
+    const int c4l = lane & 7;
+    if constexpr (HAS_BIAS) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int64_t n = n0 + 32 * b + 4 * c4l;
+        bvq[b] = (n + 4 <= N && (reinterpret_cast<uintptr_t>(bias) & 15) == 0)
+                     ? *reinterpret_cast<const float4*>(bias + n) : f4zero();
+      }
+    }
+    if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+      if (bits_in != nullptr) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            int64_t m = mw + 8 * it + (lane >> 3);
+            m = m < M ? m : M - 1;
+            int64_t nb = n0 + 32 * b;
+            nb = nb < N ? nb : 0;
+            mwq[b][it] = bits_in[(nb >> 5) * bits_ld + m];
+          }
+      }
+    }
+  }
+
+  int64_t arow_i = mw + li;
+  arow_i = arow_i < M ? arow_i : M - 1;
+  const int S = (int)(kp / BK);  // K steps (the last may run past K: zeroed)
+  const __amdgpu_buffer_rsrc_t arsrc = make_rsrc(A, M * lda * 4);
+  const __amdgpu_buffer_rsrc_t brsrc = make_rsrc(Bp, (int64_t)NP * npad * kp * 2);
+  const uint32_t avoff = (uint32_t)((arow_i * lda + 16 * lh) * 4);
+  // this lane's 16 k of step r: float4 j holds k = 32 r + 16 lh + 4 j .. +3
+  auto load_a = [&](int r, float4(&v)[4]) {
+    const uint32_t soff = (uint32_t)(r * BK * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = buf_ld4(arsrc, avoff + 16 * j, soff);
+  };
+  // a step's B image: CH chunks of 1 KB (16 image rows of 64 B), issued by
+  // group 1; lane l writes physical chunk l % 4 of its image row, the source
+  // address carries the xoff swizzle (as q6_dma_b)
+  constexpr int RPB = BN / 16, CH = NP * RPB, PERW = (CH + 3) / 4;
+  uint32_t bvoff[PERW];
+#pragma unroll
+  for (int qq = 0; qq < PERW; ++qq) {
+    const int q = wm + 4 * qq;
+    const int qc = q < CH ? q : CH - 1;
+    const int pl = qc / RPB, row = (qc % RPB) * 16 + (lane >> 2), c = lane & 3;
+    int64_t gr = n0 + row;
+    gr = gr < npad ? gr : npad - 1;  // rows past the planes: never stored
+    bvoff[qq] = (uint32_t)(((pl * npad + gr) * kp + 8 * (c ^ ((row >> 2) & 3))) * 2);
+  }
+  auto dma_b = [&](int r, uint16_t* img) {
+    const uint32_t soff = (uint32_t)(r * BK * 2);
+#pragma unroll
+    for (int qq = 0; qq < PERW; ++qq) {
+      const int q = wm + 4 * qq;
+      if (CH % 4 && q >= CH) break;  // wave-uniform
+      buf_lds16(brsrc, img + ((q / RPB) * BN + (q % RPB) * 16) * XK, bvoff[qq], soff);
+    }
+  };
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  int sha = 0;
+  if constexpr (H3 == 1) sha = h3_shift(amax);
+  if constexpr (H3 == 2) {
+    float m = 0.f;
+    for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
+    sha = h3_shift_of(m);
+  }
+  const int shb = H3 ? h3_shift(bmax) : 0;
+  float ain = 0.f;  // max |A| of this lane's loads (amax_out)
+
+  u32x4 fr[2][NP];  // this step's A fragments [sub-step][plane]
+  auto split = [&](float4(&a)[4], int r) {
+    if (amax_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ain = fmaxf(ain, fmaxf(fmaxf(fabsf(a[j].x), fabsf(a[j].y)), fmaxf(fabsf(a[j].z), fabsf(a[j].w))));
+    }
+    if (r == S - 1) {  // k >= K of the last step: zero (wave-uniform branch)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((int64_t)r * BK + 16 * lh + 4 * j >= K) a[j] = f4zero();
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (H3) hsplit8(a[2 * s], a[2 * s + 1], sha, fr[s][0], fr[s][1]);
+      else split8(a[2 * s], a[2 * s + 1], fr[s][0], fr[s][1], fr[s][2]);
+    }
+  };
+  // the compute phase: 2 TN blocks of MFMAs (block k: sub-step k / TN, column
+  // block k % TN), block k + 1's B fragments read under block k's MFMAs
+  auto compute = [&](const uint16_t* Bs) {
+    constexpr int NB = 2 * TN;
+    auto rd = [&](int k, u32x4(&f)[NP]) {
+      const int s1 = k / TN, b1 = k % TN;
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+        f[p] = *reinterpret_cast<const u32x4*>(Bs + p * BN * XK + xoff(32 * b1 + li, 2 * lh + s1));
+    };
+    u32x4 q[2][NP];
+    rd(0, q[0]);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int s = k / TN, b = k % TN;
+      if (k + 1 < NB) rd(k + 1, q[(k + 1) & 1]);
+      const u32x4* cb = q[k & 1];
+      if constexpr (H3) {
+        acc[b] = mfma_h3(__builtin_bit_cast(f16x8, fr[s][0]), __builtin_bit_cast(f16x8, fr[s][1]),
+                         __builtin_bit_cast(f16x8, cb[0]), __builtin_bit_cast(f16x8, cb[1]), acc[b]);
+      } else {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, fr[s][0]);
+        const bf16x8 am = __builtin_bit_cast(bf16x8, fr[s][1]);
+        const bf16x8 al = __builtin_bit_cast(bf16x8, fr[s][2]);
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, cb[0]);
+        const bf16x8 bm = __builtin_bit_cast(bf16x8, cb[1]);
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, cb[2]);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh, acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[b], 0, 0, 0);
+      }
+    }
+    constexpr int NM = H3 ? 3 : 6;  // MFMAs per block
+    __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);  // block 0's reads
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        if (k + 1 < NB && m < NP) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // one read
+      }
+    }
+  };
+
+  // prologue: B(0), A(0) landed, A(1) in flight; A runs two steps ahead (two
+  // register sets), B one step (two images); the loop is unrolled by two so
+  // every register set and image is chosen at compile time
+  float4 ar0[4], ar1[4];
+  if (grp == 1) dma_b(0, bimg0);
+  load_a(0, ar0);
+  if (S > 1) {
+    load_a(1, ar1);
+    vm_wait<4>();
+  } else {
+    vm_wait<0>();
+  }
+  __syncthreads();
+  split(ar0, 0);
+  if (S > 1 && grp == 1) dma_b(1, bimg1);
+  if (S > 2) load_a(2, ar0);
+  if (grp == 1) __syncthreads();  // group 1 runs one phase behind
+  // step i (parity P): compute from image P, then the load phase of step
+  // i + 1: its A is in set 1 - P (issued two load phases ago), B(i + 1) in
+  // image 1 - P (issued one load phase ago, before A(i + 2): vmcnt(4) covers it)
+  auto body = [&](auto P, int i) -> bool {
+    constexpr int par = decltype(P)::value;
+    compute(par ? bimg1 : bimg0);
+    if (i + 1 >= S) return false;
+    if (i + 2 < S) vm_wait<4>();
+    else vm_wait<0>();
+    __syncthreads();
+    float4(&an)[4] = par ? ar0 : ar1;  // step i + 1's A
+    split(an, i + 1);
+    if (i + 2 < S && grp == 1) dma_b(i + 2, par ? bimg1 : bimg0);
+    if (i + 3 < S) load_a(i + 3, an);
+    __syncthreads();
+    return true;
+  };
+  for (int i = 0;; i += 2) {
+    if (!body(std::integral_constant<int, 0>{}, i)) break;
+    if (!body(std::integral_constant<int, 1>{}, i + 1)) break;
+  }
+  if (grp == 0) __syncthreads();  // the barrier count of both groups: 2 S
+
+  // Epilogue (q6's): per 32 x 32 block, the wave's accumulator goes through
+  // its own 4 KB of LDS so that rows leave as 16-byte pieces
+  const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
+                   (EPI != MOLCLR_EPI_RELU_MASK || bits_in != nullptr ||
+                    (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
+                   ((EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
+                    (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  float* tw = ep + w * 32 * 32;
+  float rm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int64_t nb = n0 + 32 * b;
+    if (nb >= N) break;  // block-uniform
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int sr = H3 == 2 ? __shfl(sha, row, 64) : sha;
+      tw[row * 32 + li] = H3 ? __builtin_ldexpf(acc[b][r], -(sr + shb)) : acc[b][r];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = it * 64 + lane;
+      const int row = idx >> 3, c4 = idx & 7;
+      const int64_t m = mw + row, n = nb + 4 * c4;
+      uint32_t pos = 0;
+      if (m < M && n < N) {
+        const float4 v4 = *reinterpret_cast<const float4*>(tw + row * 32 + 4 * c4);
+        float* o = C + m * ldc + n;
+        uint32_t mk = 15u;
+        if constexpr (EPI == MOLCLR_EPI_RELU_MASK)
+          if (bits_in != nullptr) mk = (mwq[b][it] >> (4 * c4)) & 15u;
+        if (vec && n + 4 <= N) {
+          float4 v = v4;
+          if constexpr (HAS_BIAS) {
+            v = f4add(v, bvq[b]);
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if (EPI == MOLCLR_EPI_RELU_MASK) {
+            if (bits_in != nullptr) {
+              v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                              mk & 8u ? v.w : 0.f);
+            } else {
+              const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+              v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f,
+                              x.z > 0.f ? v.z : 0.f, x.w > 0.f ? v.w : 0.f);
+            }
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+          *reinterpret_cast<float4*>(o) = v;
+          rm[it] = fmaxf(rm[it], fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          pos = (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+                (v.w > 0.f ? 8u : 0u);
+        } else {
+          const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+          for (int j = 0; j < 4 && n + j < N; ++j) {
+            float x = e[j];
+            if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+            if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+            if (EPI == MOLCLR_EPI_RELU_MASK)
+              x = (bits_in != nullptr ? ((mk >> j) & 1u) != 0u : aux[m * ldaux + n + j] > 0.f)
+                      ? x : 0.f;
+            if (accumulate) x += o[j];
+            o[j] = x;
+            rm[it] = fmaxf(rm[it], fabsf(x));
+            pos |= (x > 0.f ? 1u : 0u) << j;
+          }
+        }
+      }
+      if (bits_out != nullptr) {
+        const uint64_t bj[4] = {__ballot((pos & 1u) != 0u), __ballot((pos & 2u) != 0u),
+                                __ballot((pos & 4u) != 0u), __ballot((pos & 8u) != 0u)};
+        if (c4 == 0 && m < M) {
+          uint32_t wd = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint32_t x = (uint32_t)(bj[j] >> (8 * (lane >> 3))) & 0xFFu;
+            x = (x | (x << 12)) & 0x000F000Fu;
+            x = (x | (x << 6)) & 0x03030303u;
+            x = (x | (x << 3)) & 0x11111111u;
+            wd |= x << j;
+          }
+          bits_out[(nb >> 5) * bits_ld + m] = wd;
+        }
+      }
+    }
+    wave_lds_sync();
+  }
+  if (crow != nullptr) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      float v = rm[it];
+      v = fmaxf(v, __shfl_xor(v, 1, 64));
+      v = fmaxf(v, __shfl_xor(v, 2, 64));
+      v = fmaxf(v, __shfl_xor(v, 4, 64));
+      const int64_t m = mw + 8 * it + (lane >> 3);
+      if ((lane & 7) == 0 && m < M) crow[(n0 / BN) * M + m] = v;
+    }
+  }
+  if (cmax != nullptr) absmax_publish(fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3])), cmax);
+  if (amax_out != nullptr) absmax_publish(ain, amax_out);
+}
+
+// ---------------------------------------------------------------------------
 // "w6": the weight gradient of a Linear, C[m][n] = Σ_k A[k][m] B[k][n] with
 // both operands K-major (K = rows: dW = dY^T X), optionally with the column
 // sums Σ_k A[k][m] (the bias gradient, A = dY) taken from the staged tiles.
@@ -1787,10 +2135,36 @@ void launch_q6_t(const Args& a, int64_t npad, hipStream_t s) {
                        a.accumulate, a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts,
                        a.bits_out, a.bits_in, a.bits_ld);
 }
+// the ping-pong form: one K group, five-block tiles, byte ranges within the
+// buffer descriptors' 31-bit records (MOLCLR_Q6_PP=0 keeps k_gemm_q6)
+bool q6_pp_ok(const Args& a, int64_t npad, int tn, int kg, int h3) {
+  static const int off = [] {
+    const char* e = getenv("MOLCLR_Q6_PP");
+    return e && e[0] == '0';
+  }();
+  const int64_t kp = (a.K + BK - 1) / BK * BK;
+  return !off && kg == 1 && tn == 5 && a.M * a.lda * 4 < (1ll << 31) &&
+         (int64_t)(h3 ? 2 : 3) * npad * kp * 2 < (1ll << 31) && a.lda % 4 == 0;
+}
+template <int TN, int EPI, int H3>
+void launch_pp(const Args& a, int64_t npad, hipStream_t s) {
+  const int64_t bn = 32 * TN;
+  const int64_t blocks = ((a.M + kPPRows - 1) / kPPRows) * ((a.N + bn - 1) / bn);
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_pp<TN, EPI, H3>), dim3((unsigned)blocks),
+                       dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc,
+                       a.bias, a.aux, a.ldaux, a.accumulate, a.amax, a.bmax, a.cmax, a.crow,
+                       a.amax_out, a.arow_parts, a.bits_out, a.bits_in, a.bits_ld);
+}
 template <int TN, int EPI, int H3>
 void launch_q6(const Args& a, int64_t npad, hipStream_t s) {
   const int64_t nsteps = (a.K + BK - 1) / BK;
   const int kg = q6_groups(a.M, a.N, a.K);
+  if constexpr (TN == 5) {
+    if (q6_pp_ok(a, npad, TN, kg, H3)) {
+      launch_pp<TN, EPI, H3>(a, npad, s);
+      return;
+    }
+  }
   // steps that need their A tail zeroed: a partial last step, or rounds past
   // the end for some K groups
   const bool mask = a.K % BK != 0 || nsteps % kg != 0;

@@ -173,6 +173,47 @@ __device__ __forceinline__ void interleave_mfma_reads() {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Buffer-resource addressing (gfx9 descriptor word 3 = 0x00020000): a
+// per-lane 32-bit byte offset fixed for a whole tile plus a wave-uniform
+// (SGPR) offset per K step, so a main loop advances its loads with no 64-bit
+// address arithmetic; reads past num_records return zeros.  Device pass only
+// (the host pass compiles the launch stubs and has no AMDGPU builtins).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int64_t bytes) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int n = bytes > 0x7fffffffll ? 0x7fffffff : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, n, 0x00020000);
+#else
+  __builtin_unreachable();
+#endif
+}
+// 16 bytes at voff + soff (soff made wave-uniform: a divergent soffset would
+// turn every load into a readfirstlane loop)
+__device__ __forceinline__ float4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(
+      float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, __builtin_amdgcn_readfirstlane(soff), 0));
+#else
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+}
+// LDS-DMA of 16 bytes per lane (buffer_load_dwordx4 ... lds) into the
+// wave-uniform LDS address `lds` (+ 16 lane)
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t voff,
+                                          uint32_t soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_as_ptr)lds, 16, voff,
+                                           __builtin_amdgcn_readfirstlane(soff), 0, 0);
+#endif
+}
+// s_waitcnt vmcnt(N) alone (expcnt / lgkmcnt left at their maxima; gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 // row of register r of a 32x32 MFMA accumulator, lane half lh
 __device__ __forceinline__ int acc_row(int r, int lh) { return (r & 3) + 8 * (r >> 2) + 4 * lh; }
 

@@ -4,6 +4,7 @@
 
 CASE: qb_lin1 qb_lin2 qb_dz1 qb_dagg wb_dW2 wb_dW0 (bf16, c5 shapes, 55k rows)
       q6_lin1 q6_lin2 q6_dz1 q6_dagg w6_dW2 w6_dW1 (fp32 split-bf16, c2, 30.5k rows)
+      h3_dz1 h3_dagg w6h_dW2 w6h_dW1 (fp32 via three fp16 MFMAs: the c2 step's backward)
 """
 import sys
 from pathlib import Path
@@ -55,6 +56,19 @@ def main():
                                                            0, ws.data_ptr(), wsb, st, variant)
     else:
         t = max(variant, 0)  # molclr_gemm_f32_bplanes_tile: 9 q6, 10 q7, 0 automatic
+        # h3 inputs: row maxima (one partial array) and max slots, as the step has them
+        rdz = torch.empty(M, device=dev)
+        rdz1 = torch.empty(M, device=dev)
+        smax = {n: torch.zeros(ops.MAX_SLOT, device=dev) for n in X}
+        for n, r in (("dz", rdz), ("dz1", rdz1)):
+            lib.molclr_absmax_rows_f32(X[n].data_ptr(), M, X[n].shape[1], X[n].shape[1],
+                                       r.data_ptr(), smax[n].data_ptr(), 1, st)
+        for n in ("agg", "a1"):
+            ops.absmax(X[n], out=smax[n])
+        Wg0 = torch.nn.Parameter(W0.clone())
+        Wg2 = torch.nn.Parameter(W2.clone())
+        bg0 = torch.nn.Parameter(b0.clone())
+        bg2 = torch.nn.Parameter(b2.clone())
         cases = {"q6_lin1": lambda: ops.gemm_w(X["agg"], W0, M, H, D, D, D, False, False,
                                                EPI_BIAS_RELU, bias=b0, tile=t),
                  "q6_lin2": lambda: ops.gemm_w(X["a1"], W2, M, D, H, H, H, False, False,
@@ -62,6 +76,13 @@ def main():
                  "q6_dz1": lambda: ops.gemm_w(X["dz"], W2, M, H, D, D, H, False, True,
                                               EPI_RELU_MASK, aux=X["a1"], tile=t),
                  "q6_dagg": lambda: ops.gemm_w(X["dz1"], W0, M, D, H, H, D, False, True, tile=t),
+                 "h3_dz1": lambda: ops.gemm_h3(X["dz"], rdz, W2, H, D, H, 1, EPI_RELU_MASK,
+                                               aux=X["a1"], rowwise=1),
+                 "h3_dagg": lambda: ops.gemm_h3(X["dz1"], rdz1, W0, D, H, D, 1, rowwise=1),
+                 "w6h_dW2": lambda: ops.linear_wgrad_h3(X["dz"], smax["dz"], X["a1"], smax["a1"],
+                                                        Wg2, bg2),
+                 "w6h_dW1": lambda: ops.linear_wgrad_h3(X["dz1"], smax["dz1"], X["agg"],
+                                                        smax["agg"], Wg0, bg0),
                  "w6_dW2": lambda: ops.linear_bwd(X["dz"], X["a1"], W2, need_x=False),
                  "w6_dW1": lambda: ops.linear_bwd(X["dz1"], X["agg"], W0, need_x=False)}
         fn = cases[case]
