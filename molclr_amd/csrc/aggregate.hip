@@ -393,26 +393,28 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const typename St::T* _
 
 // Edge-table gradient partials: partial[p][s][c] = Σ_{i in part p} ecount[i][s] * g[i][c].
 // Band layout (a block covers `band` rows x all D/4 float4 columns, 1 KiB
-// contiguous per wave).  A thread takes its rows of the partition eight at a
-// time (all eight rows' loads in flight), sums each trip of eight in fp32 and
-// folds the trip sums into fp64 accumulators; the band's threads are added in
-// fp64 in row order through LDS.  Partitions are few (<= 256: one per CU), so
-// the fp64 partials (8 D per partition) stay small for k_reduce_partials_split.
+// contiguous per wave); fp32 within a partition, fp64 partials across.
 template <typename St = StF32>
-__global__ void k_ecount_weighted_partial(
-    const typename St::T* __restrict__ g, const int32_t* __restrict__ ecount, int64_t N, int d4,
-    int band, int64_t rows_per_part, double* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) double red64[];  // [8][d4][4]
+__global__ void k_ecount_weighted_partial(const typename St::T* __restrict__ g,
+                                          const int32_t* __restrict__ ecount, int64_t N, int d4,
+                                          int band, int64_t rows_per_part,
+                                          double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float4 red[];  // [band][8][d4]
   const int tid = threadIdx.x;
   const bool live = tid < band * d4;
   const int r = live ? tid / d4 : 0, c = live ? tid - r * d4 : 0;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_part;
   int64_t end = beg + rows_per_part;
   if (end > N) end = N;
-  double ax[8], ay[8], az[8], aw[8];
+  float4 acc[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) ax[q] = ay[q] = az[q] = aw[q] = 0.0;
+  for (int s = 0; s < 8; ++s) acc[s] = f4zero();
   if (live) {
+    // a partition is band x 8 rows (ecount_parts), so a thread's eight rows
+    // of it are ONE round trip with all eight loads in flight; past 1024
+    // partitions (N > 1024 band 8: the c2 paired pass) the cap makes the
+    // partitions longer and the loop takes a second, ragged trip.  The adds
+    // stay in row order
     constexpr int U = 8;
     for (int64_t i0 = beg + r; i0 < end; i0 += U * (int64_t)band) {
       int4 lo[U], hi[U];
@@ -426,54 +428,42 @@ __global__ void k_ecount_weighted_partial(
         hi[u] = ec[1];
         v[u] = St::ld(g, (in ? i : beg) * d4 + c);
       }
-      float4 acc[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] = f4zero();
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (i0 + (int64_t)u * band >= end) break;
         const int cnt[8] = {lo[u].x, lo[u].y, lo[u].z, lo[u].w, hi[u].x, hi[u].y, hi[u].z, hi[u].w};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float w = (float)cnt[q];
-          acc[q].x += w * v[u].x;
-          acc[q].y += w * v[u].y;
-          acc[q].z += w * v[u].z;
-          acc[q].w += w * v[u].w;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        ax[q] += acc[q].x;
-        ay[q] += acc[q].y;
-        az[q] += acc[q].z;
-        aw[q] += acc[q].w;
-      }
-    }
-  }
-  // band rows added in row order (fixed: deterministic)
-  for (int q = 0; q < band; ++q) {
-    if (live && r == q) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        double* o = red64 + ((int64_t)t * d4 + c) * 4;
-        if (q == 0) {
-          o[0] = ax[t];
-          o[1] = ay[t];
-          o[2] = az[t];
-          o[3] = aw[t];
-        } else {
-          o[0] += ax[t];
-          o[1] += ay[t];
-          o[2] += az[t];
-          o[3] += aw[t];
+        for (int s = 0; s < 8; ++s) {
+          const float w = (float)cnt[s];
+          acc[s].x += w * v[u].x;
+          acc[s].y += w * v[u].y;
+          acc[s].z += w * v[u].z;
+          acc[s].w += w * v[u].w;
         }
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 8; ++s) red[(r * 8 + s) * d4 + c] = acc[s];
   }
+  __syncthreads();
+  if (!live || r != 0) return;
   double* out = partial + (int64_t)blockIdx.x * 8 * (4 * d4);
-  for (int e = tid; e < 8 * 4 * d4; e += blockDim.x) out[e] = red64[e];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    double x = 0.0, y = 0.0, z = 0.0, w = 0.0;
+    for (int q = 0; q < band; ++q) {
+      const float4 v = red[(q * 8 + s) * d4 + c];
+      x += v.x;
+      y += v.y;
+      z += v.z;
+      w += v.w;
+    }
+    double* o = out + s * 4 * d4 + 4 * c;
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+    o[3] = w;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -673,7 +663,7 @@ __global__ __launch_bounds__(kT) void k_transpose_gather_b8(const uint16_t* __re
 
 int64_t ecount_parts(int64_t N, int band) {
   int64_t P = molclr::ceil_div(N, (int64_t)band * 8);
-  if (P > 256) P = 256;  // one partition per CU: few fp64 partials to reduce
+  if (P > 1024) P = 1024;
   if (P < 1) P = 1;
   return P;
 }
@@ -845,7 +835,7 @@ MOLCLR_API int molclr_gine_aggregate_bwd(const float* g, const int32_t* rowptr_t
     int64_t P = ecount_parts(N, b.band);
     int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
     double* partial = (double*)workspace;
-    size_t lds = (size_t)8 * b.d4 * 4 * sizeof(double);
+    size_t lds = (size_t)b.band * 8 * b.d4 * sizeof(float4);
     MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd: dim too large for the edge-table reduction");
     hipLaunchKernelGGL(k_ecount_weighted_partial<StF32>, dim3(P), dim3(b.threads), lds, s, g,
                        ecount, N, d4, b.band, rpp, partial);
@@ -988,7 +978,7 @@ MOLCLR_API int molclr_gine_aggregate_bwd_bf16(const uint16_t* g, const int32_t* 
     const int64_t P = ecount_parts(N, b.band);
     const int64_t rpp = molclr::ceil_div(N > 0 ? N : 1, P);
     double* partial = (double*)workspace;
-    const size_t lds = (size_t)8 * b.d4 * 4 * sizeof(double);
+    const size_t lds = (size_t)b.band * 8 * b.d4 * sizeof(float4);
     MOLCLR_REQUIRE(lds <= 65536, "gine_aggregate_bwd_bf16: dim too large for the edge-table reduction");
     hipLaunchKernelGGL(k_ecount_weighted_partial<StBF16>, dim3(P), dim3(b.threads), lds, s, g,
                        ecount, N, d4, b.band, rpp, partial);

@@ -1180,8 +1180,10 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 // barrier of its own group).  Loads use buffer addressing: fixed per-lane
 // offsets, one scalar offset per step.  The products, their order and the
 // epilogue are q6's: results are bit-identical to k_gemm_q6<TN, EPI, 1, *, H3>
-// (tests/test_gpu_kernels.py).  Measured at the c2 shapes (tools/q6x.py):
-// lin1 80 -> 72 us, lin2 69 -> 63, dz1 61 -> 57, dagg 50 -> 46.
+// (tests/test_gpu_kernels.py).  Measured at the c2 shapes in isolation
+// (tools/q6x.py): lin1 80 -> 72 us, lin2 69 -> 63, dz1 61 -> 57, dagg 50 -> 46;
+// in the step (rocprofv3, same box): lin1 88.1 -> 84.5, lin2 69.9 -> 67.5,
+// dz1 79.6 -> 75.0, dagg 53.0 -> 57.9 (so narrow h3 products stay on q6).
 // ---------------------------------------------------------------------------
 constexpr int kPPRows = 256;
 
@@ -2143,6 +2145,9 @@ bool q6_pp_ok(const Args& a, int64_t npad, int tn, int kg, int h3) {
     return e && e[0] == '0';
   }();
   const int64_t kp = (a.K + BK - 1) / BK * BK;
+  // narrow h3 products (<= 2 column tiles: 30 MFMAs per phase over 19 steps
+  // at K = 600) measured slower in the step (dagg 53.0 -> 57.9 us): q6
+  if (h3 && a.N <= 320) return false;
   return !off && kg == 1 && tn == 5 && a.M * a.lda * 4 < (1ll << 31) &&
          (int64_t)(h3 ? 2 : 3) * npad * kp * 2 < (1ll << 31) && a.lda % 4 == 0;
 }

@@ -176,6 +176,46 @@ __global__ __launch_bounds__(kT) void k_agg_persist(const float4* __restrict__ x
     s = sn;
   }
 }
+// chunked persistent: block b (XCD-remapped) owns the contiguous unit range
+// [b * per, (b + 1) * per); its threads walk it in strides of kT with the
+// next unit's slot word (and, COPY: the next unit) loaded before the current
+// unit's gathers.  COPY: the copy floor of the same structure.
+template <bool COPY, bool NT>
+__global__ __launch_bounds__(kT) void k_agg_chunk(const float4* __restrict__ x, const int32_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+                                                 const uint4* __restrict__ nbr, const float4* __restrict__ Ec,
+                                                 float4* __restrict__ out, int64_t N, int d4) {
+  const int64_t total = N * d4;
+  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t beg = b * per;
+  int64_t end = beg + per;
+  if (end > total) end = total;
+  int64_t t = beg + threadIdx.x;
+  if (t >= end) return;
+  if constexpr (COPY) {
+    float4 v = x[t];
+    while (t < end) {
+      const int64_t tn = t + kT;
+      const float4 vn = tn < end ? x[tn] : v;
+      store4<NT>(out + t, v);
+      v = vn;
+      t = tn;
+    }
+  } else {
+    int64_t i = t / d4;
+    uint4 s = nbr[i];
+    while (t < end) {
+      const int64_t tn = t + kT;
+      const int64_t in = tn < end ? tn / d4 : i;
+      const uint4 sn = nbr[in];
+      store4<NT>(out + t, agg_unit(x, rowptr, col, ecode, Ec, s, t, i, (int)(t - i * d4), d4));
+      t = tn;
+      i = in;
+      s = sn;
+    }
+  }
+}
 }  // namespace
 
 extern "C" int agg_exp(int v, const float* x, const int32_t* rowptr, const int32_t* col, const uint8_t* ecode,
@@ -215,6 +255,10 @@ extern "C" int agg_exp(int v, const float* x, const int32_t* rowptr, const int32
     case 23: args(k_agg_v<3, 1024>, (int)((total + 1023) / 1024), 1024); break;
     case 26: args(k_agg_v<6, 1024>, (int)((total + 1023) / 1024), 1024); break;
     case 30: args(k_agg_v<0, 128>, (int)((total + 127) / 128), 128); break;
+    case 50: args(k_agg_chunk<false, false>, 256 * blocks_per_cu); break;
+    case 51: args(k_agg_chunk<true, false>, 256 * blocks_per_cu); break;
+    case 52: args(k_agg_chunk<false, true>, 256 * blocks_per_cu); break;
+    case 53: args(k_agg_chunk<true, true>, 256 * blocks_per_cu); break;
     case 33: args(k_agg_v<3, 128>, (int)((total + 127) / 128), 128); break;
     default: return -1;
   }

@@ -645,7 +645,70 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
   if (grp == 0) __syncthreads();
   stamp();  // epilogue start
-
+  if constexpr ((ABL & 512) != 0) {
+    // direct epilogue: register r of block b holds row acc_row(r, lh) (the
+    // 32 lanes of a half share it) and column nb + li; no LDS round trip
+    int srow[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) srow[r] = H3 == 2 ? __shfl(sha, acc_row(r, lh), 64) + shb : sha + shb;
+    float rmx[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rmx[r] = 0.f;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int64_t nb = n0 + 32 * b;
+      if (nb >= N) break;  // block-uniform
+      const int64_t n = nb + li;
+      const bool nok = n < N;
+      float bv = 0.f;
+      if constexpr (HAS_BIAS) bv = nok ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = mw + acc_row(r, lh);
+        const bool ok = nok && m < M;
+        float v = acc[b][r];
+        if constexpr (H3) v = __builtin_ldexpf(v, -srow[r]);
+        if constexpr (HAS_BIAS) {
+          v = v + bv;
+          if (EPI == MOLCLR_EPI_BIAS_RELU) v = fmaxf(v, 0.f);
+        }
+        if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+          const int64_t mc = m < M ? m : M - 1;
+          bool keep;
+          if (bits_in != nullptr) keep = ((bits_in[(nb >> 5) * bits_ld + mc] >> li) & 1u) != 0u;
+          else keep = ok && aux[mc * ldaux + n] > 0.f;
+          v = keep ? v : 0.f;
+        }
+        float* o = C + m * ldc + n;
+        if (ok) {
+          // accumulate (the product's EPI_ACCUMULATE) is not taken by these shapes
+          if (!(ABL & 16) || v == 1.2345f) *o = v;
+          rmx[r] = fmaxf(rmx[r], fabsf(v));
+        }
+        if (bits_out != nullptr) {
+          const uint64_t bal = __ballot(ok && v > 0.f);
+          if (li == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = (uint32_t)(bal >> (32 * lh));
+        }
+      }
+    }
+    float cm = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float v = rmx[r];
+      v = fmaxf(v, __shfl_xor(v, 1, 64));
+      v = fmaxf(v, __shfl_xor(v, 2, 64));
+      v = fmaxf(v, __shfl_xor(v, 4, 64));
+      v = fmaxf(v, __shfl_xor(v, 8, 64));
+      v = fmaxf(v, __shfl_xor(v, 16, 64));
+      cm = fmaxf(cm, v);
+      const int64_t m = mw + acc_row(r, lh);
+      if (crow != nullptr && li == 0 && m < M) crow[(n0 / BN) * M + m] = v;
+    }
+    if (cmax != nullptr) absmax_publish(cm, cmax);
+    if (amax_out != nullptr) absmax_publish(ain, amax_out);
+    stamp();  // end
+    return;
+  }
   const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
                    (EPI != MOLCLR_EPI_RELU_MASK || bits_in != nullptr ||
                     (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
@@ -827,6 +890,8 @@ extern "C" int q6x(int variant, int epi, int h3, const float* A, const uint16_t*
     case 256: Q6PP_A(E, H, 256); break;                \
     case 384: Q6PP_A(E, H, 384); break;                \
     case 416: Q6PP_A(E, H, 416); break;                \
+    case 512: Q6PP_A(E, H, 512); break;                \
+    case 544: Q6PP_A(E, H, 544); break;                \
     default: return -4;                                \
   }
     if (h3 == 0 && epi == MOLCLR_EPI_BIAS_RELU) { Q6PP_L(MOLCLR_EPI_BIAS_RELU, 0) }

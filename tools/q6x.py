@@ -66,13 +66,28 @@ def main():
         kp = (K + 31) // 32 * 32
         bmax = planes[2 * npad * kp:] if h3 else None
         C = torch.empty(M, N, device=dev)
+        # the step's side outputs: lin1 writes a1's ReLU bits, max |a1| and
+        # max |agg|; dz1 writes dz1's row maxima per column tile and max |dz1|
+        bits_o = torch.zeros((N + 31) // 32, M, dtype=torch.int32, device=dev) if name.startswith("lin1") else None
+        crow = torch.zeros((N + 159) // 160, M, device=dev) if name.startswith("dz1") else None
+        cmax = torch.zeros(ops.MAX_SLOT, device=dev) if name.startswith(("lin1", "dz1")) else None
+        amo = torch.zeros(ops.MAX_SLOT, device=dev) if name.startswith("lin1") else None
 
         def run(v):
+            for t in (bits_o, crow, cmax, amo):
+                if t is not None:
+                    t.zero_()
             rc = exp.q6x(v, epi, h3, A.data_ptr(), planes.data_ptr(), C.data_ptr(), M, N, K, K, kp,
                          npad, N, _lib.ptr(bias), None, 0, _lib.ptr(rm),
-                         bmax.data_ptr() if bmax is not None else None, None, None, None,
-                         1 if h3 else 0, None, _lib.ptr(bi), M, st)
+                         bmax.data_ptr() if bmax is not None else None, _lib.ptr(cmax),
+                         _lib.ptr(crow), _lib.ptr(amo), 1 if h3 else 0, _lib.ptr(bits_o),
+                         _lib.ptr(bi), M, st)
             assert rc == 0, (v, rc)
+
+        def outs():
+            # max slots: compare their maxima (entries depend on the block count)
+            return [C.clone()] + [t.clone() for t in (bits_o, crow) if t is not None] + \
+                [t.max().reshape(1) for t in (cmax, amo) if t is not None]
 
         if h3:
             prod = lambda: lib.molclr_gemm_f32_h3(  # noqa: E731
@@ -86,16 +101,16 @@ def main():
                 _lib.ptr(bias), None, 0, ws.data_ptr(), wsb, st, 9)
         run(0)
         torch.cuda.synchronize()
-        ref = C.clone()
+        ref = outs()
         prod()
         torch.cuda.synchronize()
-        same_prod = torch.equal(C, ref)
+        same_prod = torch.equal(C, ref[0])
         same = {}
         for v in variants:
             C.zero_()
             run(v)
             torch.cuda.synchronize()
-            same[v] = torch.equal(C, ref)
+            same[v] = all(torch.equal(a, b) for a, b in zip(outs(), ref))
         times = {v: [] for v in variants}
         tp = []
         for _ in range(5):
