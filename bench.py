@@ -218,10 +218,13 @@ def split_ceiling(tfs, model_type) -> dict:
     split-bf16 x6 (six bf16 MFMAs: 2.5 PF / 6); with ops.FP32_GEMM == "h3" the
     GIN backward products (4 of every layer's 6 equal-size products) run as h3
     (three fp16 MFMAs: 2.5 PF / 3), so the ceiling is their flop-weighted
-    harmonic mean."""
+    harmonic mean; with ops.H3_FORWARD (the default) the GIN forward products
+    run as h3 too and the ceiling is h3's."""
     from molclr_amd import ops
     x6, h3 = BF16_MFMA_PEAK_TFS / 6, BF16_MFMA_PEAK_TFS / 3
-    if model_type == "gin" and ops.FP32_GEMM == "h3":
+    if model_type == "gin" and ops.FP32_GEMM == "h3" and ops.H3_FORWARD:
+        ceil, form = h3, "h3"
+    elif model_type == "gin" and ops.FP32_GEMM == "h3":
         ceil = 1.0 / ((2 / 6) / x6 + (4 / 6) / h3)
         form = "x6 forward, h3 backward"
     elif model_type == "gcn" and ops.FP32_GEMM == "h3":

@@ -291,6 +291,16 @@ int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32
                               const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
                               float* out, int64_t num_nodes, int64_t dim,
                               molclr_stream_t stream);
+/* molclr_gine_aggregate_fwd that also writes the output's row maxima as
+ * molclr_bn_row_parts(D) partial arrays rowparts[p][N] (plain stores; the row
+ * max is the max over p) and, when `slot` is not NULL, folds max |out| into
+ * it (zeroed by the caller): the row scales of the h3 product that consumes it
+ * (molclr_gemm_f32_h3 with a_row_parts = molclr_bn_row_parts(D)), with no
+ * pass of its own. */
+int molclr_gine_aggregate_fwd_rowmax(const float* x, const int32_t* rowptr, const int32_t* col,
+                                     const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
+                                     float* out, int64_t N, int64_t D, float* rowparts,
+                                     float* slot, molclr_stream_t stream);
 /* Backward: dx[j] = Σ_{k in out(j), edge order} g[dst_k] + g[j];
  * dE1[t] = Σ_i ecount[i][t] g[i], dE2[d] = Σ_i ecount[i][5+d] g[i].
  * dx may be NULL (first layer input needs no grad); dE1/dE2 may be NULL. */
@@ -471,6 +481,15 @@ int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
                        const uint32_t* mask_bits, float* cmax, float* crow, float* amax_out,
                        molclr_stream_t stream);
+/* molclr_gemm_f32_h3 whose BIAS_RELU product also writes C's ReLU mask as
+ * bits (relu_bits: molclr_gemm_f32_bplanes_max's layout, may be NULL): the h3
+ * forward's first GIN-MLP product, whose mask the dz1 product reads back. */
+int molclr_gemm_f32_h3_bits(const float* A, const float* amax, int a_row_parts,
+                            const uint16_t* hplanes, float* C, int64_t M, int64_t N, int64_t K,
+                            int64_t lda, int64_t ldc, int epilogue_flags, const float* bias,
+                            const float* aux, int64_t ldaux, const uint32_t* mask_bits,
+                            float* cmax, float* crow, float* amax_out, uint32_t* relu_bits,
+                            molclr_stream_t stream);
 /* molclr_linear_wgrad_h3 with the K groups per block chosen per call (the plain
  * call is groups = 2), as molclr_linear_wgrad_groups. */
 int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,

@@ -44,6 +44,8 @@ SIGNATURES = {
                                       _P]),
     "molclr_edge_tables_combine": (c_int, [c_int, _P, _P, _P, _I64, _P]),
     "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_gine_aggregate_fwd_rowmax": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P,
+                                                 _P]),
     "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),
     "molclr_gine_aggregate_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, c_int, _P,
                                           c_size_t, _P]),
@@ -80,6 +82,8 @@ SIGNATURES = {
                                             _P, _I64, _P, _P, _P, _P, _P, c_size_t, _P]),
     "molclr_gemm_f32_h3": (c_int, [_P, _P, c_int, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int, _P,
                                    _P, _I64, _P, _P, _P, _P, _P]),
+    "molclr_gemm_f32_h3_bits": (c_int, [_P, _P, c_int, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
+                                        _P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "molclr_linear_wgrad_h3_groups": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                                               c_int, _P, c_size_t, _P, c_int]),
     "molclr_linear_wgrad_h3": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,

@@ -19,6 +19,8 @@
 // are bit-identical to the reference CPU path.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace {
 
 constexpr int kT = 256;
@@ -324,15 +326,14 @@ __device__ __forceinline__ float4 gine_msg(const float4* __restrict__ x, const f
 // for degree <= 4 every gather is issued before the ordered adds, so the row
 // costs two dependent memory latencies (slots, then features).  Rows of
 // higher degree walk the CSR.  Order of the adds: in-edges in edge order,
-// self loop last — the reference's, so the sums are bit-identical.
-template <typename St = StF32>
-__global__ __launch_bounds__(kT) void k_gine_agg_fwd(
+// self loop last — the reference's, so the sums are bit-identical.  One
+// float4 of the aggregation, stored and returned.
+template <typename St, bool NT = false>
+__device__ __forceinline__ float4 gine_agg_elem(
     const typename St::T* __restrict__ x, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
     const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
-    int64_t N, int d4) {
-  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  if (t >= N * d4) return;
+    int64_t t, int d4) {
   int64_t i = t / d4;
   int c = (int)(t - i * d4);
   auto X = [&](int64_t idx) { return St::ld(x, idx); };
@@ -358,7 +359,43 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
       acc = f4add(acc, f4add(X((int64_t)col[k] * d4 + c), Ec[MOLCLR_ECOMB(ecode[k]) * d4 + c]));
   }
   acc = f4add(acc, f4add(self, es));
-  St::st(out, t, acc);
+  if constexpr (NT) {  // fp32 only
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{acc.x, acc.y, acc.z, acc.w}, reinterpret_cast<f4v*>(out) + t);
+  } else {
+    St::st(out, t, acc);
+  }
+  return acc;
+}
+
+// ROWMAX: also the output's row maxima as row parts (row_max_parts) and, when
+// `slot` is given, its max -- the row scales of the h3 product that consumes it.
+// NT: non-temporal output stores (fp32; MOLCLR_AGG_NT=1, an A/B switch).
+template <typename St, bool ROWMAX, bool NT = false>
+__global__ __launch_bounds__(kT) void k_gine_agg_fwd(
+    const typename St::T* __restrict__ x, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
+    const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
+    int64_t N, int d4, float* __restrict__ rowparts, int nparts, float* __restrict__ slot) {
+  int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  if constexpr (ROWMAX) {
+    // every lane reaches the shuffles and the block barrier
+    float m = 0.f;
+    int row = -1;
+    if (t < N * d4) {
+      const float4 v = gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, d4);
+      m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+      row = (int)(t / d4);
+    }
+    row_max_parts(m, row, t, N, d4, rowparts, nparts);
+    // the tensor max costs a block barrier (waves of one block then retire
+    // together): callers whose consumer can fold it (a GEMM's amax_out) pass
+    // no slot
+    if (slot != nullptr) absmax_publish(m, slot);
+    return;
+  }
+  if (t >= N * d4) return;
+  gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, d4);
 }
 
 // dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC).
@@ -795,6 +832,14 @@ MOLCLR_API int molclr_edge_tables_combine(int layers, const float* const* E1s,
   return MOLCLR_OK;
 }
 
+static bool agg_nt() {
+  static const bool on = [] {
+    const char* e = getenv("MOLCLR_AGG_NT");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
                                          const int32_t* col, const uint8_t* ecode,
                                          const uint32_t* nbr, const float* Ec, float* out,
@@ -804,9 +849,33 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out, "gine_aggregate_fwd: null pointer");
   int d4 = (int)(D / 4);
-  molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<StF32>,
+  molclr::launch_timed(molclr::kTimeGineAgg, agg_nt() ? k_gine_agg_fwd<StF32, false, true>
+                                                      : k_gine_agg_fwd<StF32, false, false>,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4);
+                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
+                       nullptr, 0, nullptr);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_gine_aggregate_fwd_rowmax(const float* x, const int32_t* rowptr,
+                                                const int32_t* col, const uint8_t* ecode,
+                                                const uint32_t* nbr, const float* Ec, float* out,
+                                                int64_t N, int64_t D, float* rowparts, float* slot,
+                                                molclr_stream_t stream) {
+  MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "gine_aggregate_fwd_rowmax: dim %lld must be a multiple of 4",
+                 (long long)D);
+  MOLCLR_REQUIRE(N < (1ll << 31), "gine_aggregate_fwd_rowmax: too many rows");
+  if (N == 0) return MOLCLR_OK;
+  MOLCLR_REQUIRE(x && rowptr && nbr && Ec && out && rowparts,
+                 "gine_aggregate_fwd_rowmax: null pointer");
+  const int d4 = (int)(D / 4);
+  static_assert(kT % 64 == 0, "row parts follow the waves");
+  molclr::launch_timed(molclr::kTimeGineAgg, agg_nt() ? k_gine_agg_fwd<StF32, true, true>
+                                                      : k_gine_agg_fwd<StF32, true, false>,
+                       dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
+                       x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
+                       rowparts, (int)molclr_bn_row_parts(D), slot);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -946,9 +1015,10 @@ MOLCLR_API int molclr_gine_aggregate_fwd_bf16(const uint16_t* x, const int32_t* 
                          (const uint4*)nbr, (const float4*)Ec, out, N, d8);
   } else {
     const int d4 = (int)(D / 4);
-    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<StBF16>,
+    molclr::launch_timed(molclr::kTimeGineAgg, k_gine_agg_fwd<StBF16, false>,
                          dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
-                         x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4);
+                         x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
+                         nullptr, 0, nullptr);
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;

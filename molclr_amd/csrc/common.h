@@ -234,6 +234,34 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Row maxima of a row-major [rows][d4] float4 tensor written by one thread per
+// float4 (t = row * d4 + c, blocks of whole waves): a row's float4s are
+// contiguous lanes spread over at most `nparts` waves; each wave's piece of a
+// row is reduced by a segmented shuffle and its first lane stores the piece's
+// max as rowparts[part][row], part = its wave - the row's first wave (plain
+// stores, no atomics; the row max is the max over parts).  The writer of part
+// 0 zeroes the parts the row does not reach.  m = this lane's max |.|, row =
+// -1 for a lane past the end.  Every lane of the wave must call it.
+__device__ __forceinline__ void row_max_parts(float m, int row, int64_t t, int64_t rows, int d4,
+                                              float* __restrict__ rowparts, int nparts) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float mv = __shfl_down(m, off, 64);
+    const int rv = __shfl_down(row, off, 64);
+    if (lane + off < 64 && rv == row) m = fmaxf(m, mv);
+  }
+  const int rp = __shfl_up(row, 1, 64);
+  if (row >= 0 && (lane == 0 || rp != row)) {
+    const int64_t rs = (int64_t)row * d4;  // the row's first float4
+    const int part = (int)((t >> 6) - (rs >> 6));
+    rowparts[part * rows + row] = m;
+    if (part == 0)  // parts this row does not reach
+      for (int q = (int)(((rs + d4 - 1) >> 6) - (rs >> 6)) + 1; q < nparts; ++q)
+        rowparts[q * rows + row] = 0.f;
+  }
+}
+
 // A tensor's max |x| "slot" (molclr_absmax_f32) is kMaxSlotParts entries, each
 // on its own 128-byte line, whose max is the value: producers spread their
 // atomics over the entries (atomics on one line serialise: thousands of them

@@ -207,7 +207,7 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   // h3: row maxima of agg and a1 (workspace row-maxima region)
   float* ragg = (float*)((char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) +
                          kSlotBytes);
-  float* ra1 = ragg + N;
+  float* ra1 = ragg + (size_t)molclr_bn_row_parts(D) * N;  // after agg's row-max parts
   void* kws = (char*)ragg + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const bool h3 = !bf && e->fp32_gemm != 0;
@@ -253,18 +253,24 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
                             e->training, last ? 0 : 1, kws, kws_bytes, stream));
     } else {
       float *agg = F(lay.agg[l]), *a1 = F(lay.a1[l]), *z = F(lay.z[l]);
-      MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
-                                           Ecl, agg, N, D, stream));
+      float* sl = fmax + 2 * l * kMaxSlotFloats;
+      if (h3f)  // agg's row maxima from the aggregation itself, max |agg| from lin1
+        MOLCLR_TRY(molclr_gine_aggregate_fwd_rowmax((const float*)h, g->rowptr, g->col, g->ecode,
+                                                    g->nbr, Ecl, agg, N, D, ragg, nullptr,
+                                                    stream));
+      else
+        MOLCLR_TRY(molclr_gine_aggregate_fwd((const float*)h, g->rowptr, g->col, g->ecode, g->nbr,
+                                             Ecl, agg, N, D, stream));
       if (h3f) {
-        // GINEConv.update in h3 (ops._MLP): max |agg| by a pass, max |a1| from
-        // the first GEMM's epilogue
-        float* sl = fmax + 2 * l * kMaxSlotFloats;
+        // GINEConv.update in h3 (ops._MLP), A scaled row by row; max |agg| (its
+        // A reads), max |a1|, a1's row maxima and its ReLU mask as bits from
+        // the first GEMM
         const uint16_t* p0 = e->mlp0_planes[l];
         const uint16_t* p2 = e->mlp2_planes[l];
-        MOLCLR_TRY(molclr_absmax_rows_f32(agg, N, D, D, ragg, sl, 1, stream));
-        MOLCLR_TRY(molclr_gemm_f32_h3(agg, ragg, 1, p0, a1, N, 2 * D, D, D, 2 * D,
-                                      MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr, 0, nullptr,
-                                      sl + kMaxSlotFloats, ra1, nullptr, stream));
+        MOLCLR_TRY(molclr_gemm_f32_h3_bits(agg, ragg, molclr_bn_row_parts(D), p0, a1, N, 2 * D, D,
+                                           D, 2 * D, MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr,
+                                           0, nullptr, sl + kMaxSlotFloats, ra1, sl,
+                                           (uint32_t*)(A + lay.bits[l]), stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, (int)molclr_gemm_row_parts(2 * D), p2, z, N, D,
                                       2 * D, 2 * D, D, MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0,
                                       nullptr,
@@ -330,9 +336,6 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;
   const bool h3 = !bf && e->fp32_gemm != 0;
-  // the forward wrote a1's ReLU bits unless its products ran in h3 (then the
-  // mask is read from a1 itself)
-  const bool fwd_h3 = h3 && (e->fp32_gemm & 2);
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
   if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
@@ -401,7 +404,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       // gradients
       MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, molclr_bn_row_parts(D), e->mlp2_planes_t[l],
                                     (float*)dz1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_RELU_MASK,
-                                    nullptr, fa1, 2 * D, fwd_h3 ? nullptr : (const uint32_t*)(A + lay.bits[l]),
+                                    nullptr, fa1, 2 * D, (const uint32_t*)(A + lay.bits[l]),
                                     sl + kMaxSlotFloats, rdz1, nullptr, stream));
       MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
                                         gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,

@@ -2742,12 +2742,13 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
   return MOLCLR_OK;
 }
 
-MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts,
-                                  const uint16_t* hplanes, float* C, int64_t M, int64_t N,
-                                  int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
-                                  const float* bias, const float* aux, int64_t ldaux,
-                                  const uint32_t* mask_bits, float* cmax, float* crow,
-                                  float* amax_out, molclr_stream_t stream) {
+MOLCLR_API int molclr_gemm_f32_h3_bits(const float* A, const float* amax, int a_row_parts,
+                                       const uint16_t* hplanes, float* C, int64_t M, int64_t N,
+                                       int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
+                                       const float* bias, const float* aux, int64_t ldaux,
+                                       const uint32_t* mask_bits, float* cmax, float* crow,
+                                       float* amax_out, uint32_t* relu_bits,
+                                       molclr_stream_t stream) {
   const int accumulate = (epilogue_flags & MOLCLR_EPI_ACCUMULATE) ? 1 : 0;
   const int epilogue = epilogue_flags & ~MOLCLR_EPI_ACCUMULATE;
   MOLCLR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm_f32_h3: negative size");
@@ -2775,8 +2776,20 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
   a.amax_out = amax_out;
   a.arow_parts = a_row_parts;
   a.bits_in = epilogue == MOLCLR_EPI_RELU_MASK ? mask_bits : nullptr;
+  a.bits_out = epilogue == MOLCLR_EPI_BIAS_RELU ? relu_bits : nullptr;
   a.bits_ld = M;
   return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
+}
+
+MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts,
+                                  const uint16_t* hplanes, float* C, int64_t M, int64_t N,
+                                  int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
+                                  const float* bias, const float* aux, int64_t ldaux,
+                                  const uint32_t* mask_bits, float* cmax, float* crow,
+                                  float* amax_out, molclr_stream_t stream) {
+  return molclr_gemm_f32_h3_bits(A, amax, a_row_parts, hplanes, C, M, N, K, lda, ldc,
+                                 epilogue_flags, bias, aux, ldaux, mask_bits, cmax, crow, amax_out,
+                                 nullptr, stream);
 }
 
 MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,

@@ -18,6 +18,8 @@
 // master weights and BatchNorm).
 #include "mfma.h"
 
+#include <stdlib.h>
+
 namespace {
 
 using namespace molclr;
@@ -413,7 +415,14 @@ __device__ __forceinline__ bool bf16_pos(uint32_t h) { return h - 1u < 0x7F80u; 
 // counts stores too, so a load issued among the epilogue's stores would wait
 // for them all.
 // ---------------------------------------------------------------------------
-template <int EPI, int NW, bool BITS = false>
+// SW: the MFMAs take the operands swapped (B fragment first), so a lane's
+// accumulators are one ROW of the 32 x 32 block (row li, columns in four runs
+// of four): the epilogue stores straight from registers -- no LDS transpose,
+// no wave syncs -- the bias comes from a 1 KB LDS copy of the tile's columns,
+// and a row's ReLU bits are one word from two lanes.  Same products in the
+// same k order: results identical to the unswapped form.  Needs the ReLU mask
+// (if any) as bits.
+template <int EPI, int NW, bool BITS = false, bool SW = false>
 __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ Bp, uint16_t* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
@@ -422,6 +431,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
   constexpr bool MASK_BITS = BITS && EPI == MOLCLR_EPI_RELU_MASK;
   constexpr bool OUT_BITS = BITS && EPI == MOLCLR_EPI_BIAS_RELU;
   constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
+  static_assert(!SW || EPI != MOLCLR_EPI_RELU_MASK || BITS,
+                "the swapped epilogue takes its ReLU mask as bits");
   constexpr int BM = 256, BN = 256, KT = 64;
   constexpr int SI = BM * KT * 2;       // bytes per operand image per stage (32 KB)
   constexpr int WMW = NW == 8 ? 4 : 2;  // waves along M (8 waves: 4 x 2, 4 waves: 2 x 2)
@@ -491,8 +502,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j], acc[i][j], 0,
-                                                               0, 0);
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[q & 1][j], fa[q & 1][i],
+                                                                    acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[q & 1][i], fb[q & 1][j],
+                                                                    acc[i][j], 0, 0, 0);
       if (q < 3) {
         read(q + 1, fa[(q + 1) & 1], fb[(q + 1) & 1]);
         interleave_mfma_reads<TI * TJ, TI + TJ>();
@@ -521,20 +534,32 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
   };
 
   float* tw = reinterpret_cast<float*>(lds + 4 * SI) + wave * 32 * 32;
+  // SW: the tile's bias columns, one 1 KB copy per tile parity (the epilogue
+  // region is free: no transposes)
+  float* const bias_lds = reinterpret_cast<float*>(lds + 4 * SI);
   const uint16_t* asrc[PQ];
   const uint16_t* bsrc[PQ];
   tile_src(t, asrc, bsrc);
   stage(0, asrc, bsrc, 0);
   __syncthreads();
   int buf = 0;
-  constexpr int BVJ = HAS_BIAS ? TJ : 1, MWI = MASK_BITS ? TI : 1, MWJ = MASK_BITS ? TJ : 1;
+  int parity = 0;
+  constexpr int BVJ = HAS_BIAS && !SW ? TJ : 1, MWI = MASK_BITS ? TI : 1, MWJ = MASK_BITS ? TJ : 1;
   float4 bv[BVJ];           // this lane's bias columns of the tile
   uint32_t mw[MWI][MWJ][4];  // this lane's mask words of the tile (MASK_BITS)
   for (;;) {
     const int64_t m0 = (int64_t)(t / ntn) * BM, n0 = (int64_t)(t % ntn) * BN;
     const int tn = t + P;
     const bool more = tn < hi;
-    if constexpr (HAS_BIAS) {
+    float* const bl = bias_lds + 256 * parity;
+    float4 breg = f4zero();  // SW: lanes 0..63's chunk of the tile's bias
+    if constexpr (SW && HAS_BIAS) {
+      if (tid < 64) {
+        int64_t n = n0 + 4 * tid;
+        n = n + 4 <= N ? n : N - 4;  // clamped chunks are never read (full path only)
+        breg = *reinterpret_cast<const float4*>(bias + n);
+      }
+    } else if constexpr (HAS_BIAS) {
       // unconditional loads from a clamped column (bv[j] is used only where
       // n + 4 <= N): a zero-initialised conditional load wrote its registers
       // by VALU, which made the compiler drain the previous tile's stores
@@ -563,11 +588,90 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_tp(
         tile_src(tn, an, bn);
         stage(buf ^ 1, an, bn, 0);
       }
+      if constexpr (SW && HAS_BIAS) {
+        // visible to every wave after this step's barrier; the copy of the
+        // other parity may still be read by the previous tile's epilogue
+        if (s == nt - 1 && tid < 64) *reinterpret_cast<float4*>(bl + 4 * tid) = breg;
+      }
       compute(buf);
       __syncthreads();  // step s + 1 (or the next tile's step 0) has landed; buf is free
       buf ^= 1;
     }
 
+    if constexpr (SW) {
+      // rows from registers: lane (li, lh) of block (i, j) holds row mb + li,
+      // columns nb + 8 q + 4 lh .. +3 in acc[i][j][4 q .. 4 q + 3]
+      uint32_t mws[MWI][MWJ];  // the row's mask word per block (MASK_BITS)
+      if constexpr (MASK_BITS) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            int64_t m = m0 + 32 * TI * wm + 32 * i + li;
+            m = m < M ? m : M - 1;
+            int64_t nb = n0 + 32 * TJ * wn + 32 * j;
+            nb = nb < N ? nb : 0;
+            mws[i][j] = bits_in[(nb >> 5) * bits_ld + m];
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int64_t mb = m0 + 32 * TI * wm + 32 * i, nb = n0 + 32 * TJ * wn + 32 * j;
+          if (nb >= N) continue;  // wave-uniform
+          const int64_t m = mb + li;
+          uint32_t pos = 0;  // OUT_BITS: the row's bits of C > 0 in this lane's columns
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cb = 8 * q + 4 * lh;  // column within the block
+            const int64_t n = nb + cb;
+            float4 v = make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                   acc[i][j][4 * q + 3]);
+            uint32_t mk = 15u;
+            if constexpr (MASK_BITS) mk = (mws[i][j] >> cb) & 15u;
+            if (m < M && n < N) {
+              if (n + 4 <= N) {
+                if constexpr (HAS_BIAS) {
+                  v = f4add(v, *reinterpret_cast<const float4*>(bl + (nb - n0) + cb));
+                  if (EPI == MOLCLR_EPI_BIAS_RELU)
+                    v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+                }
+                if constexpr (MASK_BITS)
+                  v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                                  mk & 8u ? v.w : 0.f);
+                const uint2 o = f4_to_bf16x4(v);
+                *reinterpret_cast<uint2*>(C + m * ldc + n) = o;
+                if constexpr (OUT_BITS)
+                  pos |= ((bf16_pos(o.x & 0xFFFFu) ? 1u : 0u) | (bf16_pos(o.x >> 16) ? 2u : 0u) |
+                          (bf16_pos(o.y & 0xFFFFu) ? 4u : 0u) | (bf16_pos(o.y >> 16) ? 8u : 0u))
+                         << cb;
+              } else {
+                const float e[4] = {v.x, v.y, v.z, v.w};
+                for (int jj = 0; jj < 4 && n + jj < N; ++jj) {
+                  float xv = e[jj];
+                  if (EPI == MOLCLR_EPI_BIAS) xv = xv + bias[n + jj];
+                  if (EPI == MOLCLR_EPI_BIAS_RELU) xv = fmaxf(xv + bias[n + jj], 0.f);
+                  if constexpr (MASK_BITS) xv = ((mk >> jj) & 1u) ? xv : 0.f;
+                  const uint16_t h = (uint16_t)(f32x2_to_bf16x2(xv, 0.f) & 0xFFFFu);
+                  C[m * ldc + n + jj] = h;
+                  if constexpr (OUT_BITS) pos |= (bf16_pos(h) ? 1u : 0u) << (cb + jj);
+                }
+              }
+            }
+          }
+          if constexpr (OUT_BITS) {
+            pos |= __shfl_xor(pos, 32, 64);  // the row's other 16 columns (lane half lh ^ 1)
+            if (lh == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = pos;
+          }
+        }
+      }
+      parity ^= 1;
+      if (!more) break;
+      t = tn;
+      tile_src(t, asrc, bsrc);
+      continue;
+    }
     if constexpr (MASK_BITS) {
       // the tile's mask words, all loaded before the first store (then one
       // latency per tile); held through the K loop they would spill
@@ -1279,6 +1383,15 @@ int launch_tb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
 // molclr::cu_count()
 using molclr::cu_count;
 
+// MOLCLR_TP_SWAP=1: k_gemm_tp's swapped-operand register epilogue (A/B switch)
+static bool tp_swap() {
+  static const bool on = [] {
+    const char* e = getenv("MOLCLR_TP_SWAP");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 template <int NW>
 int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64_t M, int64_t N,
               int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc, const float* bias,
@@ -1295,21 +1408,31 @@ int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
   if (bits_out || bits_in) {
     MOLCLR_REQUIRE(bits_out ? epi == MOLCLR_EPI_BIAS_RELU : epi == MOLCLR_EPI_RELU_MASK,
                    "gemm_bf16: ReLU bits go out of a bias+ReLU product / into a ReLU-mask one");
+    const bool sw = NW == 8 && tp_swap();  // 4 waves: 256 accumulators each, the swap spills
     if (bits_out)
-      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<MOLCLR_EPI_BIAS_RELU, NW, true>, g, b, 0, s,
-                           A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, bits_out,
-                           bits_in, M);
+      molclr::launch_timed(molclr::kTimeGemm,
+                           sw ? k_gemm_tp<MOLCLR_EPI_BIAS_RELU, NW, true, NW == 8>
+                              : k_gemm_tp<MOLCLR_EPI_BIAS_RELU, NW, true, false>,
+                           g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux,
+                           bits_out, bits_in, M);
     else
-      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true>, g, b, 0, s,
-                           A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, bits_out,
-                           bits_in, M);
+      molclr::launch_timed(molclr::kTimeGemm,
+                           sw ? k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true, NW == 8>
+                              : k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true, false>,
+                           g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux,
+                           bits_out, bits_in, M);
     return MOLCLR_OK;
   }
   uint32_t* no_out = nullptr;
   const uint32_t* no_in = nullptr;
+  const bool sw = NW == 8 && tp_swap();
 #define MOLCLR_TP(EPV)                                                                          \
-  molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<EPV, NW>, g, b, 0, s, A, Bp, C, M, N, K, lda, kp, \
-                       npad, ldc, bias, aux, ldaux, no_out, no_in, (int64_t)0)
+  molclr::launch_timed(molclr::kTimeGemm,                                                       \
+                       sw && EPV != MOLCLR_EPI_RELU_MASK                                        \
+                           ? k_gemm_tp<EPV, NW, false, NW == 8 && EPV != MOLCLR_EPI_RELU_MASK>  \
+                           : k_gemm_tp<EPV, NW, false, false>,                                  \
+                       g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, no_out, \
+                       no_in, (int64_t)0)
   switch (epi) {
     case MOLCLR_EPI_NONE: MOLCLR_TP(MOLCLR_EPI_NONE); return MOLCLR_OK;
     case MOLCLR_EPI_BIAS: MOLCLR_TP(MOLCLR_EPI_BIAS); return MOLCLR_OK;

@@ -295,20 +295,22 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_stats_final(
       const float* sm = pmean + at.part0 * D;
       const float* sq = pm2 + at.part0 * D;
       const float* sn = pn + at.part0;
-      int64_t p = sl;
-      for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
+      // four partials per lane in flight, the ragged last round included (a
+      // missing one merges as n = 0, which chan1 skips): one dependent round
+      // trip for P <= 4 kSegLanes; merge order = increasing p, as before
+      for (int64_t p = sl; p < P; p += 4 * kSegLanes) {
         float bn[4], bm[4], bq[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int64_t q = p + u * kSegLanes;
-          bn[u] = sn[q];
-          bm[u] = sm[q * D + c];
-          bq[u] = sq[q * D + c];
+          const bool in = q < P;
+          bn[u] = in ? sn[q] : 0.f;
+          bm[u] = in ? sm[q * D + c] : 0.f;
+          bq[u] = in ? sq[q * D + c] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) chan1(n, mean, m2, bn[u], bm[u], bq[u]);
       }
-      for (; p < P; p += kSegLanes) chan1(n, mean, m2, sn[p], sm[p * D + c], sq[p * D + c]);
     }
     __syncthreads();  // the previous pair's trees are done with the arrays
     rn[rl][cl] = n;
@@ -489,20 +491,23 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
       const int64_t P = at.P;
       const float* q1 = p1 + at.part0 * D;
       const float* q2 = p2 + at.part0 * D;
-      int64_t p = sl;
-      for (; p + 3 * kSegLanes < P; p += 4 * kSegLanes) {
-        a0 += q1[p * D + c];
-        a1 += q1[(p + kSegLanes) * D + c];
-        a2 += q1[(p + 2 * kSegLanes) * D + c];
-        a3 += q1[(p + 3 * kSegLanes) * D + c];
-        b0 += q2[p * D + c];
-        b1 += q2[(p + kSegLanes) * D + c];
-        b2 += q2[(p + 2 * kSegLanes) * D + c];
-        b3 += q2[(p + 3 * kSegLanes) * D + c];
-      }
-      for (; p < P; p += kSegLanes) {
-        a0 += q1[p * D + c];
-        b0 += q2[p * D + c];
+      // four partials per lane in flight, the ragged last round included
+      for (int64_t p = sl; p < P; p += 4 * kSegLanes) {
+        float x1[4], x2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t q = p + u * kSegLanes;
+          x1[u] = q < P ? q1[q * D + c] : 0.f;
+          x2[u] = q < P ? q2[q * D + c] : 0.f;
+        }
+        a0 += x1[0];
+        a1 += x1[1];
+        a2 += x1[2];
+        a3 += x1[3];
+        b0 += x2[0];
+        b1 += x2[1];
+        b2 += x2[2];
+        b3 += x2[3];
       }
     }
     float a = (a0 + a1) + (a2 + a3), b = (b0 + b1) + (b2 + b3);
@@ -576,10 +581,7 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
     int relu, Segs sg, float* __restrict__ rowparts, int nparts, float* __restrict__ slot) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (rowparts != nullptr) {  // block-uniform: every thread reaches the reductions
-    // dz's row maxima as plain stores: a row's float4s are contiguous lanes,
-    // spread over at most nparts waves; each wave's piece of a row (a
-    // segment) is reduced by a segmented shuffle and its first lane stores
-    // the piece's max as part (its wave - the row's first wave)
+    // dz's row maxima as row parts (row_max_parts) and its max
     const int64_t rows = total4 / d4;
     float m = 0.f;
     int row = -1;
@@ -589,22 +591,7 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
       m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
       row = (int)(t / d4);
     }
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float mv = __shfl_down(m, off, 64);
-      const int rv = __shfl_down(row, off, 64);
-      if (lane + off < 64 && rv == row) m = fmaxf(m, mv);
-    }
-    const int rp = __shfl_up(row, 1, 64);
-    if (row >= 0 && (lane == 0 || rp != row)) {
-      const int64_t rs = (int64_t)row * d4;  // the row's first float4
-      const int part = (int)((t >> 6) - (rs >> 6));
-      rowparts[part * rows + row] = m;
-      if (part == 0)  // parts this row does not reach
-        for (int q = (int)(((rs + d4 - 1) >> 6) - (rs >> 6)) + 1; q < nparts; ++q)
-          rowparts[q * rows + row] = 0.f;
-    }
+    row_max_parts(m, row, t, rows, d4, rowparts, nparts);
     if (slot != nullptr) absmax_publish(m, slot);
     return;
   }

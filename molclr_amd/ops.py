@@ -260,11 +260,13 @@ def _refresh_planes(gen: int) -> None:
 # fp32 GEMMs of the GIN MLP backward (data and weight gradients): "h3" = three
 # fp16 MFMAs per product with power-of-two scaling (molclr_gemm_f32_h3 with
 # row-wise scales, molclr_linear_wgrad_h3), "x6" = six split-bf16 MFMAs.
-# H3_FORWARD puts the forward products on h3 too (off: it moved the c1 3-step
-# trajectory test by 2.5e-5).  The encoder executor reads the same switches,
-# so both paths issue identical kernels.
+# H3_FORWARD puts the forward products on h3 too, A scaled row by row (the
+# default: elementwise as accurate as the reference's fp32 sgemm, no more
+# ReLU decisions flipped against fp64 -- tools/h3_forward_flips.py;
+# MOLCLR_H3_FORWARD=0 keeps them on x6).  The encoder executor reads the same
+# switches, so both paths issue identical kernels.
 FP32_GEMM = os.environ.get("MOLCLR_FP32_GEMM", "h3")
-H3_FORWARD = os.environ.get("MOLCLR_H3_FORWARD", "0") == "1"
+H3_FORWARD = os.environ.get("MOLCLR_H3_FORWARD", "1") == "1"
 
 
 MAX_SLOT = 64 * 32  # floats per max |x| slot (molclr_absmax_f32: 64 entries, 128 B apart)
@@ -287,19 +289,20 @@ def row_parts(N: int) -> int:
 
 
 def gemm_h3(A, amax, W, N, K, ldb, b_kmajor, epi=EPI_NONE, bias=None, aux=None, cmax=None,
-            rowwise=0, crow=None, amax_out=None, mask_bits=None):
-    """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3.  amax: A's
-    max slot, or (rowwise = P > 0) its row maxima as P partial arrays [P][M];
-    cmax (zeroed) receives max |C|, crow [row_parts(N)][M] C's row maxima."""
+            rowwise=0, crow=None, amax_out=None, mask_bits=None, bits_out=None):
+    """C = epilogue(A B) with B(k, n) in W, by molclr_gemm_f32_h3_bits.  amax:
+    A's max slot, or (rowwise = P > 0) its row maxima as P partial arrays [P][M];
+    cmax (zeroed) receives max |C|, crow [row_parts(N)][M] C's row maxima,
+    bits_out (BIAS_RELU) C's ReLU mask as bits."""
     _check(A, W)
     M = A.shape[0]
     planes = weight_planes(W, N, K, ldb, b_kmajor, "h3")
     out = torch.empty(M, N, dtype=torch.float32, device=A.device)
-    _lib.call("molclr_gemm_f32_h3", A.data_ptr(), amax.data_ptr(), int(rowwise),
+    _lib.call("molclr_gemm_f32_h3_bits", A.data_ptr(), amax.data_ptr(), int(rowwise),
               planes.data_ptr(),
               out.data_ptr(), M, N, K, A.stride(0), out.stride(0), epi, _lib.ptr(bias),
               _lib.ptr(aux), aux.stride(0) if aux is not None else 0, _lib.ptr(mask_bits),
-              _lib.ptr(cmax), _lib.ptr(crow), _lib.ptr(amax_out), _stream(A))
+              _lib.ptr(cmax), _lib.ptr(crow), _lib.ptr(amax_out), _lib.ptr(bits_out), _stream(A))
     if _TIMER is not None:
         _TIMER.add("gemm_f32", 2.0 * M * N * K)
     return out
@@ -545,7 +548,8 @@ class _MLP(torch.autograd.Function):
             # the products (row-wise h3 when H3_FORWARD, else x6 with max |a1| by
             # a pass); the max slots serve the h3 weight gradients
             slots = torch.zeros(2, MAX_SLOT, dtype=torch.float32, device=x.device)
-            ctx.bits = None
+            # a1's ReLU mask as bits for the dz1 product, from the first product
+            ctx.bits = torch.empty((2 * D + 31) // 32, M, dtype=torch.int32, device=x.device)
             if H3_FORWARD:
                 P = row_parts(2 * D)
                 rx = torch.empty(M, dtype=torch.float32, device=x.device)
@@ -553,13 +557,11 @@ class _MLP(torch.autograd.Function):
                 _lib.call("molclr_absmax_rows_f32", x.data_ptr(), M, D, x.stride(0),
                           rx.data_ptr(), slots[0].data_ptr(), 1, _stream(x))
                 a1 = gemm_h3(x, rx, W1, 2 * D, D, D, 0, EPI_BIAS_RELU, bias=b1,
-                             cmax=slots[1], rowwise=1, crow=ra1)
+                             cmax=slots[1], rowwise=1, crow=ra1, bits_out=ctx.bits)
                 z = gemm_h3(a1, ra1, W2, D, 2 * D, 2 * D, 0, EPI_BIAS, bias=b2, rowwise=P)
             else:
                 # the first product (q6, x6 planes) also yields max |x| and max |a1|
-                # and a1's ReLU mask as bits for the dz1 product
                 a1 = torch.empty(M, 2 * D, dtype=torch.float32, device=x.device)
-                ctx.bits = torch.empty((2 * D + 31) // 32, M, dtype=torch.int32, device=x.device)
                 ws_bytes = _wsq("molclr_gemm_f32_workspace_bytes", M, 2 * D, D)
                 ws = _ws(ws_bytes, x.device) if ws_bytes else None
                 _lib.call("molclr_gemm_f32_bplanes_max", x.data_ptr(),

@@ -187,6 +187,47 @@ def test_gine_aggregate_high_degree(dev, D):
     assert torch.equal(hd.grad.cpu(), hr.grad)
 
 
+@pytest.mark.parametrize("B,D", [(512, 300), (64, 4), (64, 128), (16, 512)])
+def test_gine_aggregate_rowmax(dev, B, D):
+    """molclr_gine_aggregate_fwd_rowmax: the plain aggregation's output bit for
+    bit, its row maxima as row parts (max over parts == max |row|, exactly) and
+    max |out| folded into the slot -- the h3 forward's row scales."""
+    from ctypes import c_void_p
+    from molclr_amd import _lib
+    b = batch(B, 2) if B != 16 else hub_batch()
+    N = b.x.shape[0]
+    g = dgraph(b, dev)
+    torch.manual_seed(4)
+    h, E1, E2 = torch.randn(N, D, device=dev), torch.randn(5, D, device=dev), torch.randn(3, D, device=dev)
+    ref = ops.gine_aggregate(h, E1, E2, g)
+    lib = _lib.load()
+    st = _lib.stream_of(dev)
+    Ec = torch.empty(15, D, device=dev)
+    arr = lambda t: (c_void_p * 1)(t.data_ptr())  # noqa: E731
+    assert lib.molclr_edge_tables_combine(1, arr(E1), arr(E2), Ec.data_ptr(), D, st) == 0
+    P = lib.molclr_bn_row_parts(D)
+    out = torch.empty(N, D, device=dev)
+    parts = torch.full((P, N), -1.0, device=dev)
+    slot = torch.zeros(ops.MAX_SLOT, device=dev)
+    assert lib.molclr_gine_aggregate_fwd_rowmax(h.data_ptr(), g.rowptr.data_ptr(), g.col.data_ptr(),
+                                                g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                                                out.data_ptr(), N, D, parts.data_ptr(),
+                                                slot.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert bool((parts >= 0).all()), "a row part was left unwritten"
+    assert torch.equal(parts.max(0).values, out.abs().max(1).values)
+    assert slot.max().item() == out.abs().max().item()
+    # no slot (the encoder's h3 forward folds max |agg| in the lin1 GEMM)
+    parts2 = torch.full((P, N), -1.0, device=dev)
+    assert lib.molclr_gine_aggregate_fwd_rowmax(h.data_ptr(), g.rowptr.data_ptr(), g.col.data_ptr(),
+                                                g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                                                out.data_ptr(), N, D, parts2.data_ptr(), None,
+                                                st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(parts2, parts)
+
+
 def test_gcn_conv(dev):
     from oracle.reference_cpu import RefGCNConv
     b = batch(64, 3)

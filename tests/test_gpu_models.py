@@ -172,6 +172,7 @@ def test_training_steps_match_oracle(dev, kind):
     opt_r = torch.optim.Adam(ref.parameters(), 5e-4, weight_decay=1e-5)
     opt_m = FusedAdam(mine.parameters(), 5e-4, weight_decay=1e-5)
     data = SyntheticPairBatches(B, seed=21)
+    errs = []
     for step in range(3):
         xi, xj = data.next()
         opt_r.zero_grad()
@@ -185,7 +186,15 @@ def test_training_steps_match_oracle(dev, kind):
         lm = crit_m(l2_normalize(zi), l2_normalize(zj))
         lm.backward()
         opt_m.step()
-        assert abs(lm.item() - lr.item()) <= TOL * abs(lr.item()), step
+        errs.append(abs(lm.item() - lr.item()) / abs(lr.item()))
+    # step 0 (identical weights): the 1e-5 bar.  Later steps follow weights
+    # that one Adam step has already moved by +-lr wherever a gradient sits
+    # within rounding of 0, so they are held to what the reference's OWN fp32
+    # path spreads by when only its summation order changes
+    # (tools/traj_fp32_spread.py, profiles/r4_traj_fp32_spread.jsonl: 4.4e-5
+    # after one step, 6.6e-4 after two), with a 2x margin.
+    bounds = [TOL, 1e-4, 1.5e-3]
+    assert all(e <= b for e, b in zip(errs, bounds)), errs
     # Adam's first steps move every element by ~lr * sign(g): an element whose
     # gradient is within fp32 rounding of 0 may legitimately step the other way
     # (a 2*lr difference) in ANY fp32 implementation, the reference's included,
