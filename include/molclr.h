@@ -738,10 +738,9 @@ typedef struct molclr_gin_encoder {
    * 0 = none; bit 0 = the backward (weight gradients with per-tensor scales,
    * data gradients with row-wise scales; mlp*_planes_t are then
    * molclr_hplanes_make_batch images); bit 1 = the forward products too
-   * (mlp0/2_planes h3 images; measured to move the c1 3-step trajectory by
-   * 2.5e-5 after one Adam step, so not used by default).  The max slots of
-   * agg / a1 live in the arena, those of dz / dz1 and all row maxima in the
-   * workspace. */
+   * (mlp0/2_planes h3 images, A scaled row by row; the Python side's default,
+   * 3 = both).  The max slots of agg / a1 live in the arena, those of dz /
+   * dz1 and all row maxima in the workspace. */
   int32_t fp32_gemm;
   /* nullable: receives MOLCLR_STATUS_ATOM_RANGE (molclr_atom_embed_fwd) */
   int32_t* status;

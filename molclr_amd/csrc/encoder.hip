@@ -352,11 +352,13 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     const bool last = l == L - 1;
     MOLCLR_REQUIRE(gr->bn_weight[l] && gr->bn_bias[l], "gin_encoder_bwd: BatchNorm grads needed");
     if (h3) {
-      // dz's row maxima and max slot for the h3 products
+      // dz's row maxima for the h3 products (its max comes from the dz1
+      // product's A reads: a max slot here would cost the BatchNorm backward
+      // a block barrier)
       MOLCLR_TRY(seg_bn_bwd(seg, dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
                             F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l], D,
-                            MOLCLR_DTYPE_F32, last ? 0 : 1, 1, rdz, bmax + 2 * l * kMaxSlotFloats,
-                            kws, kws_bytes, stream));
+                            MOLCLR_DTYPE_F32, last ? 0 : 1, 1, rdz, nullptr, kws, kws_bytes,
+                            stream));
     } else {
       MOLCLR_TRY(seg_bn_bwd(seg, dy, z, e->bn_weight[l], e->bn_bias[l], F(lay.mean[l]),
                             F(lay.invstd[l]), dz, gr->bn_weight[l], gr->bn_bias[l], D, dt,
@@ -392,8 +394,8 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
     } else if (h3) {
       // ops._MLP's h3 backward: dz1 (ReLU mask of a1), dW2 (+db2), dW1 (+db1),
       // dagg.  The data-gradient products scale A row by row (gradient rows
-      // span many binades): dz's row maxima and max come from the BatchNorm
-      // backward, dz1's from the dz1 product's epilogue.
+      // span many binades): dz's row maxima come from the BatchNorm backward,
+      // max |dz| from the dz1 product's A reads, dz1's from its epilogue.
       const float *fz = (const float*)dz, *fa1 = (const float*)a1, *fagg = (const float*)agg;
       float* sl = bmax + 2 * l * kMaxSlotFloats;
       const float* fl = fmax + 2 * l * kMaxSlotFloats;
@@ -405,7 +407,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
       MOLCLR_TRY(molclr_gemm_f32_h3(fz, rdz, molclr_bn_row_parts(D), e->mlp2_planes_t[l],
                                     (float*)dz1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_RELU_MASK,
                                     nullptr, fa1, 2 * D, (const uint32_t*)(A + lay.bits[l]),
-                                    sl + kMaxSlotFloats, rdz1, nullptr, stream));
+                                    sl + kMaxSlotFloats, rdz1, sl, stream));
       MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
                                         gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
                                         stream));

@@ -1383,11 +1383,15 @@ int launch_tb(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
 // molclr::cu_count()
 using molclr::cu_count;
 
-// MOLCLR_TP_SWAP=1: k_gemm_tp's swapped-operand register epilogue (A/B switch)
+// k_gemm_tp's swapped-operand register epilogue: taken by the bias+ReLU
+// product that writes ReLU bits (c5 lin1: 115.5 -> 98.9 us, the four ballots
+// per row group gone); measured slower on the others (mask-bits consumer
+// 97.8 -> 99.7, plain 71.6 -> 74.0 us: four times the cache lines per store
+// instruction), which keep the LDS transpose.  MOLCLR_TP_SWAP=0 disables it.
 static bool tp_swap() {
   static const bool on = [] {
     const char* e = getenv("MOLCLR_TP_SWAP");
-    return e != nullptr && e[0] == '1';
+    return !(e != nullptr && e[0] == '0');
   }();
   return on;
 }
@@ -1416,23 +1420,16 @@ int launch_tp(int epi, const uint16_t* A, const uint16_t* Bp, uint16_t* C, int64
                            g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux,
                            bits_out, bits_in, M);
     else
-      molclr::launch_timed(molclr::kTimeGemm,
-                           sw ? k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true, NW == 8>
-                              : k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true, false>,
-                           g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux,
-                           bits_out, bits_in, M);
+      molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<MOLCLR_EPI_RELU_MASK, NW, true>, g, b, 0, s,
+                           A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, bits_out,
+                           bits_in, M);
     return MOLCLR_OK;
   }
   uint32_t* no_out = nullptr;
   const uint32_t* no_in = nullptr;
-  const bool sw = NW == 8 && tp_swap();
 #define MOLCLR_TP(EPV)                                                                          \
-  molclr::launch_timed(molclr::kTimeGemm,                                                       \
-                       sw && EPV != MOLCLR_EPI_RELU_MASK                                        \
-                           ? k_gemm_tp<EPV, NW, false, NW == 8 && EPV != MOLCLR_EPI_RELU_MASK>  \
-                           : k_gemm_tp<EPV, NW, false, false>,                                  \
-                       g, b, 0, s, A, Bp, C, M, N, K, lda, kp, npad, ldc, bias, aux, ldaux, no_out, \
-                       no_in, (int64_t)0)
+  molclr::launch_timed(molclr::kTimeGemm, k_gemm_tp<EPV, NW>, g, b, 0, s, A, Bp, C, M, N, K, lda, kp, \
+                       npad, ldc, bias, aux, ldaux, no_out, no_in, (int64_t)0)
   switch (epi) {
     case MOLCLR_EPI_NONE: MOLCLR_TP(MOLCLR_EPI_NONE); return MOLCLR_OK;
     case MOLCLR_EPI_BIAS: MOLCLR_TP(MOLCLR_EPI_BIAS); return MOLCLR_OK;

@@ -189,12 +189,16 @@ def test_training_steps_match_oracle(dev, kind):
         errs.append(abs(lm.item() - lr.item()) / abs(lr.item()))
     # step 0 (identical weights): the 1e-5 bar.  Later steps follow weights
     # that one Adam step has already moved by +-lr wherever a gradient sits
-    # within rounding of 0, so they are held to what the reference's OWN fp32
-    # path spreads by when only its summation order changes
-    # (tools/traj_fp32_spread.py, profiles/r4_traj_fp32_spread.jsonl: 4.4e-5
-    # after one step, 6.6e-4 after two), with a 2x margin.
-    bounds = [TOL, 1e-4, 1.5e-3]
-    assert all(e <= b for e, b in zip(errs, bounds)), errs
+    # within rounding of 0, so they (and the parameters after 3 steps, below)
+    # are held to twice what the reference's OWN fp32 path spreads by from
+    # fp64 -- in its own order or with only its summation order changed
+    # (tools/traj_fp32_spread.py -> tests/golden/traj_fp32_spread.json, gin:
+    # loss 4.4e-5 after one step, 6.6e-4 after two; batch_norms.*.bias up to
+    # 4.3e-2 norm-wise after three).
+    spread = json.loads((GOLDEN / "traj_fp32_spread.json").read_text()) if kind == "gin" else None
+    bounds = ([max(TOL, 2 * g) for g in spread["loss_rel_per_step"]] if spread
+              else [TOL] * 3)
+    assert all(e <= b for e, b in zip(errs, bounds)), (errs, bounds)
     # Adam's first steps move every element by ~lr * sign(g): an element whose
     # gradient is within fp32 rounding of 0 may legitimately step the other way
     # (a 2*lr difference) in ANY fp32 implementation, the reference's included,
@@ -206,7 +210,8 @@ def test_training_steps_match_oracle(dev, kind):
         b = pr[name].detach()
         assert (a - b).abs().max().item() <= 3 * 2 * 5e-4 * 1.01, name
         if not pre_bn_bias(name):
-            assert rel(p, pr[name]) < 2e-3, name
+            bound = max(2e-3, 2 * spread["param_rel"][name]) if spread else 2e-3
+            assert rel(p, pr[name]) < bound, (name, rel(p, pr[name]), bound)
 
 
 @pytest.mark.parametrize("kind", ["gin", "gcn"])
