@@ -314,9 +314,10 @@ def main():
     # the scatter-add timed for the HBM roofline: GINE's, or GCN's for c3
     agg_kind = "gcn_aggregate_fwd" if cfg["model_type"] == "gcn" else "gine_aggregate_fwd"
     captured = None
-    if not args.two_pass and not args.no_hip_graph:
+    if not args.two_pass and not args.no_hip_graph and mdist.graph_capturable():
         # N > 1: the step's RCCL collectives (NT-Xent all-gathers, bucketed
-        # gradient all-reduces) are captured with it
+        # gradient all-reduces) are captured with it (a gloo group -- the
+        # two-ranks-on-one-GPU test -- stays eager)
         from molclr_amd.graph_step import CapturedTrainStep
         captured = CapturedTrainStep(model, opt, crit, reducer=reducer)
 
@@ -539,6 +540,8 @@ def main():
             "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if captured is not None:
+        captured.close()  # graphs holding RCCL collectives go before their group
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 

@@ -333,9 +333,7 @@ __device__ __forceinline__ float4 gine_agg_elem(
     const typename St::T* __restrict__ x, const int32_t* __restrict__ rowptr,
     const int32_t* __restrict__ col, const uint8_t* __restrict__ ecode,
     const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
-    int64_t t, int d4) {
-  int64_t i = t / d4;
-  int c = (int)(t - i * d4);
+    int64_t t, int64_t i, int c, int d4) {
   auto X = [&](int64_t idx) { return St::ld(x, idx); };
   auto msg = [&](uint32_t w) {
     return f4add(X((int64_t)nbr_node(w) * d4 + c), Ec[nbr_ecomb(w) * d4 + c]);
@@ -378,14 +376,25 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     const uint4* __restrict__ nbr, const float4* __restrict__ Ec, typename St::T* __restrict__ out,
     int64_t N, int d4, float* __restrict__ rowparts, int nparts, float* __restrict__ slot) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  // (row, float4 column) of this lane: 32-bit division when the grid allows
+  int64_t i;
+  int c;
+  if (N * d4 < (1ll << 32)) {
+    const uint32_t q = (uint32_t)t / (uint32_t)d4;
+    i = q;
+    c = (int)((uint32_t)t - q * (uint32_t)d4);
+  } else {
+    i = t / d4;
+    c = (int)(t - i * d4);
+  }
   if constexpr (ROWMAX) {
-    // every lane reaches the shuffles and the block barrier
+    // every lane reaches the wave reductions (and the slot's block barrier)
     float m = 0.f;
     int row = -1;
     if (t < N * d4) {
-      const float4 v = gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, d4);
+      const float4 v = gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, i, c, d4);
       m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
-      row = (int)(t / d4);
+      row = (int)i;
     }
     row_max_parts(m, row, t, N, d4, rowparts, nparts);
     // the tensor max costs a block barrier (waves of one block then retire
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
     return;
   }
   if (t >= N * d4) return;
-  gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, d4);
+  gine_agg_elem<St, NT>(x, rowptr, col, ecode, nbr, Ec, out, t, i, c, d4);
 }
 
 // dx[j] = Σ_{out-edges of j in edge order} g[dst] + g[j]  (neighbour slots of the CSC).

@@ -3,6 +3,8 @@
 
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <stdint.h>
 #include <stddef.h>
 
@@ -228,6 +230,23 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// max over the wave of v >= 0 by DPP within rows of 16 and four lane reads
+// (no LDS crossbar traffic; every lane gets the result)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value,
+                                                      0xF, 0xF, false));
+  };
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0xB1>{}));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x4E>{}));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x141>{}));  // row_half_mirror
+  v = fmaxf(v, dpp(v, std::integral_constant<int, 0x140>{}));  // row_mirror
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -245,6 +264,29 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ void row_max_parts(float m, int row, int64_t t, int64_t rows, int d4,
                                               float* __restrict__ rowparts, int nparts) {
   const int lane = threadIdx.x & 63;
+  if (d4 >= 64) {
+    // a wave holds pieces of at most two rows, r0 (its first lane's) and r0 + 1:
+    // two plain wave maxima instead of the segmented scan
+    const int64_t t0 = t - lane;
+    const int64_t r0 = rows * d4 < (1ll << 32) ? (int64_t)((uint32_t)t0 / (uint32_t)d4) : t0 / d4;
+    const bool second = row >= 0 && row != r0;
+    const float m0 = wave_max_dpp(second ? 0.f : m), m1 = wave_max_dpp(second ? m : 0.f);
+    if (lane == 0 && r0 < rows) {
+      const int64_t rs = r0 * d4;
+      const int part = (int)((t0 >> 6) - (rs >> 6));
+      rowparts[part * rows + r0] = m0;
+      if (part == 0)
+        for (int q = (int)(((rs + d4 - 1) >> 6) - (rs >> 6)) + 1; q < nparts; ++q)
+          rowparts[q * rows + r0] = 0.f;
+    }
+    const int64_t r1 = r0 + 1, rs1 = r1 * d4;
+    if (lane == 1 && r1 < rows && rs1 < t0 + 64) {  // r1 starts in this wave: part 0
+      rowparts[r1] = m1;
+      for (int q = (int)(((rs1 + d4 - 1) >> 6) - (rs1 >> 6)) + 1; q < nparts; ++q)
+        rowparts[q * rows + r1] = 0.f;
+    }
+    return;
+  }
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const float mv = __shfl_down(m, off, 64);

@@ -1187,7 +1187,13 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
 // ---------------------------------------------------------------------------
 constexpr int kPPRows = 256;
 
-template <int TN, int EPI, int H3>
+// SW (h3 only): the MFMAs take the operands swapped, so a lane's accumulators
+// are one ROW of each 32 x 32 block (row li, columns in four runs of four):
+// the epilogue unscales by the lane's own row shift, stores float4s straight
+// from registers (no LDS transpose), keeps the row max in one register (crow:
+// one shuffle per tile) and builds a row's ReLU bits from two lanes.  Same
+// products in the same order: results identical to the unswapped form.
+template <int TN, int EPI, int H3, bool SW = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_pp(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
@@ -1199,6 +1205,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   constexpr int BN = 32 * TN;
   constexpr int NP = H3 ? 2 : 3;
   constexpr int BI = NP * BN * XK;
+  static_assert(!SW || H3, "the swapped form is the h3 kernel's");
   // two B images (separate arrays: the LDS-DMA into one must not look like it
   // aliases the fragment reads of the other) and the epilogue's wave tiles
   __shared__ __attribute__((aligned(16))) uint16_t bimg0[BI];
@@ -1220,10 +1227,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 
   // epilogue operands ahead of the main loop (vmcnt counts stores too)
   constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
-  constexpr int BVN = HAS_BIAS ? TN : 1, MWN = EPI == MOLCLR_EPI_RELU_MASK ? TN : 1;
+  constexpr int BVN = HAS_BIAS && !SW ? TN : 1, MWN = EPI == MOLCLR_EPI_RELU_MASK && !SW ? TN : 1;
+  constexpr int MSN = EPI == MOLCLR_EPI_RELU_MASK && SW ? TN : 1;
   float4 bvq[BVN];
   uint32_t mwq[MWN][4];
-  {
+  uint32_t mws[MSN];  // SW: the lane's row's mask word per column block
+  float4 breg = f4zero();  // SW: lanes 0 .. BN/4-1's chunk of the tile's bias
+  if constexpr (SW) {
+    // the tile's bias columns go to the (then unused) epilogue LDS in the
+    // prologue, once the load has landed
+    if constexpr (HAS_BIAS) {
+      const int64_t n = n0 + 4 * (tid < BN / 4 ? tid : 0);
+      if (n + 4 <= N && (reinterpret_cast<uintptr_t>(bias) & 15) == 0)
+        breg = *reinterpret_cast<const float4*>(bias + n);
+    }
+    if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+      if (bits_in != nullptr) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          int64_t m = mw + li;
+          m = m < M ? m : M - 1;
+          int64_t nb = n0 + 32 * b;
+          nb = nb < N ? nb : 0;
+          mws[b] = bits_in[(nb >> 5) * bits_ld + m];
+        }
+      }
+    }
+  } else {
     const int c4l = lane & 7;
     if constexpr (HAS_BIAS) {
 #pragma unroll
@@ -1336,7 +1366,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       const int s = k / TN, b = k % TN;
       if (k + 1 < NB) rd(k + 1, q[(k + 1) & 1]);
       const u32x4* cb = q[k & 1];
-      if constexpr (H3) {
+      if constexpr (H3 && SW) {
+        acc[b] = mfma_h3_t(__builtin_bit_cast(f16x8, fr[s][0]), __builtin_bit_cast(f16x8, fr[s][1]),
+                           __builtin_bit_cast(f16x8, cb[0]), __builtin_bit_cast(f16x8, cb[1]), acc[b]);
+      } else if constexpr (H3) {
         acc[b] = mfma_h3(__builtin_bit_cast(f16x8, fr[s][0]), __builtin_bit_cast(f16x8, fr[s][1]),
                          __builtin_bit_cast(f16x8, cb[0]), __builtin_bit_cast(f16x8, cb[1]), acc[b]);
       } else {
@@ -1378,6 +1411,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   } else {
     vm_wait<0>();
   }
+  if constexpr (SW && HAS_BIAS)
+    if (tid < BN / 4) *reinterpret_cast<float4*>(ep + 4 * tid) = breg;
   __syncthreads();
   split(ar0, 0);
   if (S > 1 && grp == 1) dma_b(1, bimg1);
@@ -1406,13 +1441,87 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
   if (grp == 0) __syncthreads();  // the barrier count of both groups: 2 S
 
-  // Epilogue (q6's): per 32 x 32 block, the wave's accumulator goes through
-  // its own 4 KB of LDS so that rows leave as 16-byte pieces
   const bool vec = ((ldc & 3) == 0) && ((reinterpret_cast<uintptr_t>(C) & 15) == 0) &&
                    (EPI != MOLCLR_EPI_RELU_MASK || bits_in != nullptr ||
                     (((ldaux & 3) == 0) && (reinterpret_cast<uintptr_t>(aux) & 15) == 0)) &&
                    ((EPI != MOLCLR_EPI_BIAS && EPI != MOLCLR_EPI_BIAS_RELU) ||
                     (reinterpret_cast<uintptr_t>(bias) & 15) == 0);
+  if constexpr (SW) {
+    // rows from registers: lane (li, lh) holds row m = mw + li of block b at
+    // columns nb + 8 q + 4 lh .. +3 in acc[b][4 q .. 4 q + 3]
+    const int64_t m = mw + li;
+    const float sc = __builtin_ldexpf(1.f, -(sha + shb));  // exact: a power of two
+    float rmax = 0.f;
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int64_t nb = n0 + 32 * b;
+      if (nb >= N) break;  // block-uniform
+      uint32_t pos = 0;  // bits of C > 0 in this lane's columns of the row
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cb = 8 * q + 4 * lh;
+        const int64_t n = nb + cb;
+        if (m < M && n < N) {
+          float* o = C + m * ldc + n;
+          const float4 v4 = make_float4(acc[b][4 * q] * sc, acc[b][4 * q + 1] * sc,
+                                        acc[b][4 * q + 2] * sc, acc[b][4 * q + 3] * sc);
+          uint32_t mk = 15u;
+          if constexpr (EPI == MOLCLR_EPI_RELU_MASK)
+            if (bits_in != nullptr) mk = (mws[b] >> cb) & 15u;
+          if (vec && n + 4 <= N) {
+            float4 v = v4;
+            if constexpr (HAS_BIAS) {
+              v = f4add(v, *reinterpret_cast<const float4*>(ep + 32 * b + cb));
+              if (EPI == MOLCLR_EPI_BIAS_RELU)
+                v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            }
+            if (EPI == MOLCLR_EPI_RELU_MASK) {
+              if (bits_in != nullptr) {
+                v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                                mk & 8u ? v.w : 0.f);
+              } else {
+                const float4 x = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+                v = make_float4(x.x > 0.f ? v.x : 0.f, x.y > 0.f ? v.y : 0.f,
+                                x.z > 0.f ? v.z : 0.f, x.w > 0.f ? v.w : 0.f);
+              }
+            }
+            if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+            *reinterpret_cast<float4*>(o) = v;
+            rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            pos |= ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+                    (v.w > 0.f ? 8u : 0u)) << cb;
+          } else {
+            const float e[4] = {v4.x, v4.y, v4.z, v4.w};
+            for (int j = 0; j < 4 && n + j < N; ++j) {
+              float x = e[j];
+              if (EPI == MOLCLR_EPI_BIAS) x = x + bias[n + j];
+              if (EPI == MOLCLR_EPI_BIAS_RELU) x = fmaxf(x + bias[n + j], 0.f);
+              if (EPI == MOLCLR_EPI_RELU_MASK)
+                x = (bits_in != nullptr ? ((mk >> j) & 1u) != 0u : aux[m * ldaux + n + j] > 0.f)
+                        ? x : 0.f;
+              if (accumulate) x += o[j];
+              o[j] = x;
+              rmax = fmaxf(rmax, fabsf(x));
+              pos |= (x > 0.f ? 1u : 0u) << (cb + j);
+            }
+          }
+        }
+      }
+      if (bits_out != nullptr) {
+        pos |= __shfl_xor(pos, 32, 64);  // the row's other 16 columns
+        if (lh == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = pos;
+      }
+    }
+    if (crow != nullptr) {
+      const float v = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
+      if (lh == 0 && m < M) crow[(n0 / BN) * M + m] = v;
+    }
+    if (cmax != nullptr) absmax_publish(rmax, cmax);
+    if (amax_out != nullptr) absmax_publish(ain, amax_out);
+    return;
+  }
+  // Epilogue (q6's): per 32 x 32 block, the wave's accumulator goes through
+  // its own 4 KB of LDS so that rows leave as 16-byte pieces
   float* tw = ep + w * 32 * 32;
   float rm[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2151,11 +2260,21 @@ bool q6_pp_ok(const Args& a, int64_t npad, int tn, int kg, int h3) {
   return !off && kg == 1 && tn == 5 && a.M * a.lda * 4 < (1ll << 31) &&
          (int64_t)(h3 ? 2 : 3) * npad * kp * 2 < (1ll << 31) && a.lda % 4 == 0;
 }
+// the h3 products take k_gemm_pp's swapped register epilogue; MOLCLR_PP_SWAP=0
+// keeps the LDS-transpose epilogue
+bool pp_swap() {
+  static const bool on = [] {
+    const char* e = getenv("MOLCLR_PP_SWAP");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
 template <int TN, int EPI, int H3>
 void launch_pp(const Args& a, int64_t npad, hipStream_t s) {
   const int64_t bn = 32 * TN;
   const int64_t blocks = ((a.M + kPPRows - 1) / kPPRows) * ((a.N + bn - 1) / bn);
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_pp<TN, EPI, H3>), dim3((unsigned)blocks),
+  auto kern = (H3 != 0 && pp_swap()) ? k_gemm_pp<TN, EPI, H3, H3 != 0> : k_gemm_pp<TN, EPI, H3, false>;
+  molclr::launch_timed(molclr::kTimeGemm, kern, dim3((unsigned)blocks),
                        dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc,
                        a.bias, a.aux, a.ldaux, a.accumulate, a.amax, a.bmax, a.cmax, a.crow,
                        a.amax_out, a.arow_parts, a.bits_out, a.bits_in, a.bits_ld);

@@ -124,6 +124,13 @@ __device__ __forceinline__ f32x16 mfma_h3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl
   acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc, 0, 0, 0);
 }
+// the same three products in the same order with the operands swapped: the
+// accumulator holds the transposed 32 x 32 block (lane li = row of A)
+__device__ __forceinline__ f32x16 mfma_h3_t(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, al, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(bh, ah, acc, 0, 0, 0);
+}
 
 // K-major [k][ROWS] image planes (the dY^T / X^T operands of a weight
 // gradient), read with the gfx950 transposed LDS read.  32-element XOR of

@@ -66,6 +66,13 @@ def init(backend: str | None = None) -> tuple[int, int, torch.device]:
     return rank, world, device
 
 
+def graph_capturable() -> bool:
+    """Whether a HIP graph can hold the step's collectives: RCCL ("nccl")
+    enqueues them on the stream, gloo runs them on the host (no process group:
+    nothing to capture)."""
+    return not (dist.is_available() and dist.is_initialized()) or dist.get_backend() == "nccl"
+
+
 def _all_gather_stack(t: torch.Tensor, group=None) -> torch.Tensor:
     """[world, *t.shape]: every rank's t, in rank order.  One collective
     (all_gather_into_tensor on RCCL; the list form on backends without it)."""

@@ -158,7 +158,7 @@ class MolCLR(object):
             return None
         if not getattr(self, "paired", True) or not hasattr(model, "forward_staged"):
             return None
-        if not model._executor_ok() or model._dim_pad():
+        if not model._executor_ok() or model._dim_pad() or not mdist.graph_capturable():
             return None
         cs = getattr(self, "_captured", None)
         if cs is None or cs.model is not model or cs.optimizer is not optimizer:

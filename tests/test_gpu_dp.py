@@ -278,3 +278,4 @@ def test_captured_dp_step_rccl_world1(dev, rccl_world1, kind):
         assert abs(lc.item() - le.item()) <= 1e-6 * abs(le.item()), (i, lc.item(), le.item())
         assert rel(opts[1].flat_grad, opts[0].flat_grad) < 5e-5, i
     assert step.captures >= 2 and step.replays == len(pairs) + 2
+    step.close()  # before the fixture destroys the process group

@@ -9,6 +9,7 @@ launch touched:
 
     python tools/scatter_cold.py [sets] [reps] [warm|cold]
     python tools/scatter_cold.py [sets] [reps] exp [blocks_per_cu]
+    python tools/scatter_cold.py [sets] [reps] rowmax
 
 ``exp`` times the layout variants of tools/exp/agg_exp.hip (build with
 tools/exp/build_agg_exp.sh) on the same cold rotation, each checked
@@ -67,6 +68,8 @@ def main():
     if mode == "exp":
         return experiments(graphs, hs, outs, Ec, st, D, reps,
                            int(sys.argv[4]) if len(sys.argv) > 4 else 8)
+    if mode == "rowmax":
+        return rowmax_cost(graphs, hs, outs, Ec, st, D, reps)
     order = list(range(sets)) if mode == "cold" else [0] * sets
     # flush: a 1 GB write between the set-up and the timed loop evicts the MALL
     flush = torch.empty(256 * 2**20, device=dev)
@@ -93,6 +96,50 @@ def main():
                       "achieved_GBs": round(gbs, 1), "frac_of_8TBs": round(gbs / PEAK_GBS, 3),
                       "avg_nodes": sum(graphs[s].num_nodes for s in order) // len(order)}),
           flush=True)
+
+
+def rowmax_cost(graphs, hs, outs, Ec, st, D, reps):
+    """The product entry points cold and warm: the plain aggregation, and
+    molclr_gine_aggregate_fwd_rowmax (row maxima for the h3 forward) without
+    and with the max slot."""
+    sets = len(graphs)
+    P = _lib.load().molclr_bn_row_parts(D)
+    parts = [torch.empty(P, g.num_nodes, device=Ec.device) for g in graphs]
+    slot = torch.zeros(ops.MAX_SLOT, device=Ec.device)
+    flush = torch.empty(256 * 2**20, device=Ec.device)
+    alg = sum(ops.gine_aggregate_bytes(g.num_nodes, D, g.num_edges) for g in graphs) / sets
+
+    def plain(s):
+        g = graphs[s]
+        _lib.call("molclr_gine_aggregate_fwd", hs[s].data_ptr(), g.rowptr.data_ptr(),
+                  g.col.data_ptr(), g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                  outs[s].data_ptr(), g.num_nodes, D, st)
+
+    def rowmax(with_slot):
+        def f(s):
+            g = graphs[s]
+            _lib.call("molclr_gine_aggregate_fwd_rowmax", hs[s].data_ptr(), g.rowptr.data_ptr(),
+                      g.col.data_ptr(), g.ecode.data_ptr(), g.nbr.data_ptr(), Ec.data_ptr(),
+                      outs[s].data_ptr(), g.num_nodes, D, parts[s].data_ptr(),
+                      slot.data_ptr() if with_slot else None, st)
+        return f
+    for name, fn in (("plain", plain), ("rowmax", rowmax(False)), ("rowmax+slot", rowmax(True))):
+        for mode in ("cold", "warm"):
+            order = list(range(sets)) if mode == "cold" else [0] * sets
+            for s in order:
+                fn(s)
+            flush.fill_(1.0)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                for s in order:
+                    fn(s)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / (reps * sets)
+            print(json.dumps({"entry": name, "mode": mode, "avg_us": round(us, 2),
+                              "frac_of_8TBs": round(alg / us / 1e3 / PEAK_GBS, 3)}), flush=True)
 
 
 def experiments(graphs, hs, outs, Ec, st, D, reps, bpc):
