@@ -291,12 +291,16 @@ int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr, const int32
                               const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
                               float* out, int64_t num_nodes, int64_t dim,
                               molclr_stream_t stream);
-/* molclr_gine_aggregate_fwd that also writes the output's row maxima as
- * molclr_bn_row_parts(D) partial arrays rowparts[p][N] (plain stores; the row
- * max is the max over p) and, when `slot` is not NULL, folds max |out| into
- * it (zeroed by the caller): the row scales of the h3 product that consumes it
- * (molclr_gemm_f32_h3 with a_row_parts = molclr_bn_row_parts(D)), with no
- * pass of its own. */
+/* molclr_gine_aggregate_fwd that also writes the output's row maxima and,
+ * when `slot` is not NULL, folds max |out| into it (zeroed by the caller):
+ * the row scales of the h3 product that consumes it (molclr_gemm_f32_h3 with
+ * a_row_parts = molclr_rowmax_layout(D)), with no pass of its own.  Layout
+ * (molclr_rowmax_layout(D), molclr_rowmax_bytes(N, D) bytes): P > 0: P
+ * partial arrays rowparts[p][N] (the row max is the max over p); < 0 (D / 4
+ * >= 64): one float2 per 64 float4s of the row-major output (the maxima of
+ * the pieces of the wave's first row and of the next row). */
+int64_t molclr_rowmax_layout(int64_t D);
+size_t molclr_rowmax_bytes(int64_t N, int64_t D);
 int molclr_gine_aggregate_fwd_rowmax(const float* x, const int32_t* rowptr, const int32_t* col,
                                      const uint8_t* ecode, const uint32_t* nbr, const float* Ec,
                                      float* out, int64_t N, int64_t D, float* rowparts,
@@ -442,7 +446,8 @@ int molclr_linear_wgrad_groups(const float* dy, const float* x, float* dW, float
  *   molclr_gemm_f32_h3: C = epilogue(A B) for a row-major A [M][K] (lda) and
  *     h3 planes of B; K <= 1024, K and lda multiples of 4.  a_row_parts == 0:
  *     `amax` is A's max slot (one scale for A); P > 0: `amax` holds A's row
- *     maxima as P partial arrays [P][M] and every row is scaled by its own
+ *     maxima as P partial arrays [P][M] (P < 0: as the per-wave pairs of
+ *     molclr_rowmax_layout(K) = P) and every row is scaled by its own
  *     (a row of small values, e.g. a node with a small gradient, keeps full
  *     precision).  cmax / crow (each may be NULL): max |C| folded into the
  *     slot cmax (the caller zeroes it) / C's row maxima as

@@ -44,6 +44,8 @@ SIGNATURES = {
                                       _P]),
     "molclr_edge_tables_combine": (c_int, [c_int, _P, _P, _P, _I64, _P]),
     "molclr_gine_aggregate_fwd": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P]),
+    "molclr_rowmax_layout": (_I64, [_I64]),
+    "molclr_rowmax_bytes": (c_size_t, [_I64, _I64]),
     "molclr_gine_aggregate_fwd_rowmax": (c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, _I64, _P, _P,
                                                  _P]),
     "molclr_gine_aggregate_bwd_workspace_bytes": (c_size_t, [_I64, _I64]),

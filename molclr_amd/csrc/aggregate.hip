@@ -396,7 +396,10 @@ __global__ __launch_bounds__(kT) void k_gine_agg_fwd(
       m = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
       row = (int)i;
     }
-    row_max_parts(m, row, t, N, d4, rowparts, nparts);
+    if (nparts < 0)  // d4 >= 64: per-wave pairs (molclr_rowmax_layout)
+      row_max_waves(m, row, t, N, d4, reinterpret_cast<float2*>(rowparts));
+    else
+      row_max_parts(m, row, t, N, d4, rowparts, nparts);
     // the tensor max costs a block barrier (waves of one block then retire
     // together): callers whose consumer can fold it (a GEMM's amax_out) pass
     // no slot
@@ -867,6 +870,16 @@ MOLCLR_API int molclr_gine_aggregate_fwd(const float* x, const int32_t* rowptr,
   return MOLCLR_OK;
 }
 
+MOLCLR_API int64_t molclr_rowmax_layout(int64_t D) {
+  const int64_t d4 = D / 4;
+  return d4 >= 64 ? -d4 : (int64_t)molclr_bn_row_parts(D);
+}
+MOLCLR_API size_t molclr_rowmax_bytes(int64_t N, int64_t D) {
+  const int64_t code = molclr_rowmax_layout(D);
+  return code < 0 ? (size_t)((N * (D / 4) + 63) / 64) * 2 * sizeof(float)
+                  : (size_t)code * N * sizeof(float);
+}
+
 MOLCLR_API int molclr_gine_aggregate_fwd_rowmax(const float* x, const int32_t* rowptr,
                                                 const int32_t* col, const uint8_t* ecode,
                                                 const uint32_t* nbr, const float* Ec, float* out,
@@ -884,7 +897,7 @@ MOLCLR_API int molclr_gine_aggregate_fwd_rowmax(const float* x, const int32_t* r
                                                       : k_gine_agg_fwd<StF32, true, false>,
                        dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0, molclr::as_stream(stream),
                        x, rowptr, col, ecode, (const uint4*)nbr, (const float4*)Ec, out, N, d4,
-                       rowparts, (int)molclr_bn_row_parts(D), slot);
+                       rowparts, (int)molclr_rowmax_layout(D), slot);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -304,6 +304,32 @@ __device__ __forceinline__ void row_max_parts(float m, int row, int64_t t, int64
   }
 }
 
+// Row maxima as per-wave pairs (rows of d4 >= 64 float4s, one thread per
+// float4 as row_max_parts): a wave holds pieces of at most two rows, r0 (its
+// first lane's) and r0 + 1, and its lane 0 stores the two pieces' maxima as
+// one float2 wm[wave] -- one 8-byte store per wave, consecutive across waves
+// (row_max_parts' scattered 4-byte stores and zero fills cost the
+// aggregation ~2 us).  row_max_of_waves folds a row's pieces back.
+__device__ __forceinline__ void row_max_waves(float m, int row, int64_t t, int64_t rows, int d4,
+                                              float2* __restrict__ wm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t0 = t - lane;
+  const int64_t r0 = rows * d4 < (1ll << 32) ? (int64_t)((uint32_t)t0 / (uint32_t)d4) : t0 / d4;
+  const bool second = row >= 0 && row != r0;
+  const float m0 = wave_max_dpp(second ? 0.f : m), m1 = wave_max_dpp(second ? m : 0.f);
+  if (lane == 0 && t0 < rows * d4) wm[t0 >> 6] = make_float2(m0, m1);
+}
+__device__ __forceinline__ float row_max_of_waves(const float2* __restrict__ wm, int64_t row,
+                                                  int d4) {
+  const int64_t s = row * d4, e = s + d4 - 1;
+  float m = 0.f;
+  for (int64_t w = s >> 6; w <= (e >> 6); ++w) {
+    const float2 v = wm[w];
+    m = fmaxf(m, (w << 6) / d4 == row ? v.x : v.y);
+  }
+  return m;
+}
+
 // A tensor's max |x| "slot" (molclr_absmax_f32) is kMaxSlotParts entries, each
 // on its own 128-byte line, whose max is the value: producers spread their
 // atomics over the entries (atomics on one line serialise: thousands of them

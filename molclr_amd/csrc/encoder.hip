@@ -172,11 +172,18 @@ MOLCLR_API size_t molclr_gin_encoder_arena_bytes(int L, int64_t N, int64_t D, in
 // workspace: backward scratch | h3 max slots of dz_l / dz1_l | h3 row maxima
 // of agg / dz [N] and of a1 / dz1 [parts][N] | the entry points' workspace
 constexpr size_t kSlotBytes = MOLCLR_MAX_LAYERS * 2 * kMaxSlotFloats * sizeof(float);
-// row maxima of a [N,D] tensor (1 part) and of a [N,2D] GEMM output
+// row maxima of a [N,D] tensor and of a [N,2D] GEMM output
 // (molclr_gemm_row_parts(2D) partial arrays)
+// the first region: dz's row-max parts, or agg's in the aggregation's layout
+// (h3 forward, molclr_rowmax_layout)
+size_t rowmax_first_bytes(int64_t N, int64_t D) {
+  const size_t dz = (size_t)molclr_bn_row_parts(D) * N * sizeof(float);
+  const size_t agg = molclr_rowmax_bytes(N, D);
+  return molclr::align_up(dz > agg ? dz : agg, 256);
+}
 size_t rowmax_bytes(int64_t N, int64_t D) {
-  return molclr::align_up((size_t)(molclr_bn_row_parts(D) + molclr_gemm_row_parts(2 * D)) * N *
-                              sizeof(float), 256);
+  return molclr::align_up(
+      rowmax_first_bytes(N, D) + (size_t)molclr_gemm_row_parts(2 * D) * N * sizeof(float), 256);
 }
 
 MOLCLR_API size_t molclr_gin_encoder_workspace_bytes(int L, int64_t N, int64_t D, int dtype) {
@@ -207,7 +214,7 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   // h3: row maxima of agg and a1 (workspace row-maxima region)
   float* ragg = (float*)((char*)workspace + molclr::align_up(scratch_bytes(N, D, es), 256) +
                          kSlotBytes);
-  float* ra1 = ragg + (size_t)molclr_bn_row_parts(D) * N;  // after agg's row-max parts
+  float* ra1 = (float*)((char*)ragg + rowmax_first_bytes(N, D));  // after agg's row maxima
   void* kws = (char*)ragg + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const bool h3 = !bf && e->fp32_gemm != 0;
@@ -267,9 +274,10 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
         // the first GEMM
         const uint16_t* p0 = e->mlp0_planes[l];
         const uint16_t* p2 = e->mlp2_planes[l];
-        MOLCLR_TRY(molclr_gemm_f32_h3_bits(agg, ragg, molclr_bn_row_parts(D), p0, a1, N, 2 * D, D,
-                                           D, 2 * D, MOLCLR_EPI_BIAS_RELU, e->mlp0_bias[l], nullptr,
-                                           0, nullptr, sl + kMaxSlotFloats, ra1, sl,
+        MOLCLR_TRY(molclr_gemm_f32_h3_bits(agg, ragg, (int)molclr_rowmax_layout(D), p0, a1, N,
+                                           2 * D, D, D, 2 * D, MOLCLR_EPI_BIAS_RELU,
+                                           e->mlp0_bias[l], nullptr, 0, nullptr,
+                                           sl + kMaxSlotFloats, ra1, sl,
                                            (uint32_t*)(A + lay.bits[l]), stream));
         MOLCLR_TRY(molclr_gemm_f32_h3(a1, ra1, (int)molclr_gemm_row_parts(2 * D), p2, z, N, D,
                                       2 * D, 2 * D, D, MOLCLR_EPI_BIAS, e->mlp2_bias[l], nullptr, 0,
@@ -331,7 +339,7 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
   float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
   float* rdz = bmax + kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
-  float* rdz1 = rdz + (size_t)molclr_bn_row_parts(D) * N;  // after dz's row-max parts
+  float* rdz1 = (float*)((char*)rdz + rowmax_first_bytes(N, D));  // after dz's row maxima
   void* kws = (char*)rdz + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
   const int dt = bf ? MOLCLR_DTYPE_BF16 : MOLCLR_DTYPE_F32;

@@ -935,7 +935,10 @@ __global__ __launch_bounds__(64 * kQ6Waves * KG) __attribute__((amdgpu_waves_per
   if constexpr (H3 == 1) sha = h3_shift(amax);
   if constexpr (H3 == 2) {
     float m = 0.f;
-    for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
+    if (arow_parts < 0)  // per-wave pairs of a producer with D / 4 = -arow_parts
+      m = row_max_of_waves(reinterpret_cast<const float2*>(amax), arow_i, -arow_parts);
+    else
+      for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
     sha = h3_shift_of(m);
   }
   const int shb = H3 ? h3_shift(bmax) : 0;
@@ -1325,7 +1328,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   if constexpr (H3 == 1) sha = h3_shift(amax);
   if constexpr (H3 == 2) {
     float m = 0.f;
-    for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
+    if (arow_parts < 0)  // per-wave pairs of a producer with D / 4 = -arow_parts
+      m = row_max_of_waves(reinterpret_cast<const float2*>(amax), arow_i, -arow_parts);
+    else
+      for (int p = 0; p < arow_parts; ++p) m = fmaxf(m, amax[(int64_t)p * M + arow_i]);
     sha = h3_shift_of(m);
   }
   const int shb = H3 ? h3_shift(bmax) : 0;
@@ -2893,11 +2899,14 @@ MOLCLR_API int molclr_gemm_f32_h3_bits(const float* A, const float* amax, int a_
   a.cmax = cmax;
   a.crow = crow;
   a.amax_out = amax_out;
+  MOLCLR_REQUIRE(a_row_parts >= 0 || (-a_row_parts == K / 4 && K / 4 >= 64 && lda == K),
+                 "gemm_f32_h3: per-wave row maxima (a_row_parts %d) need a dense A of K / 4 "
+                 "= %d >= 64 float4s per row", a_row_parts, (int)(K / 4));
   a.arow_parts = a_row_parts;
   a.bits_in = epilogue == MOLCLR_EPI_RELU_MASK ? mask_bits : nullptr;
   a.bits_out = epilogue == MOLCLR_EPI_BIAS_RELU ? relu_bits : nullptr;
   a.bits_ld = M;
-  return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts > 0 ? 2 : 1);
+  return run_q6(a, npad, epilogue, molclr::as_stream(stream), a_row_parts != 0 ? 2 : 1);
 }
 
 MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts,

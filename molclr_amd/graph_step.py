@@ -277,6 +277,19 @@ class CapturedTrainStep:
         # data parallel: the process group's watchdog thread polls its events
         # while we capture; thread-local capture keeps those calls legal
         mode = "global" if self.group is None else "thread_local"
+        ops.CAPTURE_SCOPE = {id(p) for p in self.model.parameters()}
+        try:
+            self._record(g, mode, graph, opt)
+        finally:
+            ops.CAPTURE_SCOPE = None
+        self.captures += 1
+        # a capture only records: the cached images must be regenerated by
+        # the next eager use as well
+        ops.bump_param_generation()
+        return _Captured(graph, g)
+
+    def _record(self, g, mode, graph, opt):
+        """The step's work into g (the tensors it allocates live in the pool)."""
         with torch.cuda.graph(g, pool=self._pool, capture_error_mode=mode):
             graph.build()
             opt.zero_grad()
@@ -295,11 +308,6 @@ class CapturedTrainStep:
             # graph build and atom embedding write the batch's validity bits
             torch.bitwise_or(self.status, graph.status, out=self.status)
         del loss, z
-        self.captures += 1
-        # a capture only records: the cached images must be regenerated by
-        # the next eager use as well
-        ops.bump_param_generation()
-        return _Captured(graph, g)
 
     def _insert(self, ent) -> None:
         self._graphs[id(ent)] = ent

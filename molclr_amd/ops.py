@@ -210,13 +210,19 @@ def weight_planes(W, N, K, ldb, b_kmajor, kind: str = "x6") -> torch.Tensor:
     key = (W.data_ptr(), N, K, ldb, int(b_kmajor), kind)
     gen = PARAM_GENERATION[0]
     ent = _PLANES.get(key)
-    if ent is not None and ent[1]() is W and ent[0] == (W._version, gen):
-        return ent[3]
-    if ent is not None and ent[0][1] != gen and ent[1]() is W:
-        _refresh_planes(gen)
-        ent = _PLANES.get(key)
-        if ent is not None and ent[0] == (W._version, gen):
+    if ent is not None and ent[1]() is W:
+        if ent[0] == (W._version, gen):
             return ent[3]
+        if ent[0][1] != gen:
+            _refresh_planes(gen)
+            ent = _PLANES[key]
+        if ent[0] != (W._version, gen):
+            # changed in place within the generation: regenerate into the SAME
+            # image -- a captured step writes (and its replays read) this
+            # address, so it must never be freed while W lives
+            _make_planes(kind, [(W, ent[2], ent[3])])
+            ent = _PLANES[key] = ((W._version, gen), ent[1], ent[2], ent[3])
+        return ent[3]
     # drop entries of dead tensors on every insert: a padded weight (emb_dim
     # not a multiple of the kernels' width) is a new tensor each call, and its
     # planes must not stay pinned in HBM
@@ -241,13 +247,24 @@ def _make_planes(kind, jobs) -> None:
               arr([j[2].data_ptr() for j in jobs], ctypes.c_void_p), _stream(jobs[0][2]))
 
 
+# While a step is being captured (molclr_amd.graph_step): the ids of its
+# model's parameters.  The capture then regenerates only THEIR images: an image
+# of another model refreshed inside the graph would be written by every replay
+# even after that model's image was freed and its memory reused.
+CAPTURE_SCOPE: set | None = None
+
+
 def _refresh_planes(gen: int) -> None:
-    """Regenerate every live cached image of an older generation, batched."""
+    """Regenerate every live cached image of an older generation, batched
+    (while capturing: the captured model's only)."""
     jobs = {}
+    scope = CAPTURE_SCOPE
     for k, (tok, ref, shape, planes) in list(_PLANES.items()):
         W = ref()
         if W is None:
             del _PLANES[k]
+            continue
+        if scope is not None and id(W) not in scope:
             continue
         if tok[1] != gen and W.data_ptr() == k[0]:
             jobs.setdefault(k[5], []).append((k, W, shape, planes))

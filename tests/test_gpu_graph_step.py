@@ -273,7 +273,7 @@ def test_capacity_fit_lookup_and_prepare(dev):
                 continue
             r = rel(pc.grad, pr.grad)
             if r > 5e-5:
-                bad.append((name, r))
+                bad.append((name, r, pc.grad.norm().item(), pr.grad.norm().item()))
         assert not bad, bad
     assert step.captures == n_prepared  # nothing captured after prepare()
     assert step.replays == len(pairs) + 2
