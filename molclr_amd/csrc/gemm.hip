@@ -2262,7 +2262,11 @@ bool q6_pp_ok(const Args& a, int64_t npad, int tn, int kg, int h3) {
   const int64_t kp = (a.K + BK - 1) / BK * BK;
   // narrow h3 products (<= 2 column tiles: 30 MFMAs per phase over 19 steps
   // at K = 600) measured slower in the step (dagg 53.0 -> 57.9 us): q6
-  if (h3 && a.N <= 320) return false;
+  static const bool narrow = [] {
+    const char* e = getenv("MOLCLR_PP_NARROW");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (h3 && a.N <= 320 && !narrow) return false;
   return !off && kg == 1 && tn == 5 && a.M * a.lda * 4 < (1ll << 31) &&
          (int64_t)(h3 ? 2 : 3) * npad * kp * 2 < (1ll << 31) && a.lda % 4 == 0;
 }
