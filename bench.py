@@ -448,6 +448,8 @@ def main():
             roofline = {"kernel": ("molclr_gcn_aggregate_fwd (k_gcn_agg_fwd)" if agg_kind ==
                                    "gcn_aggregate_fwd" else
                                    ("molclr_gine_aggregate_fwd_bf16" if precision == "bf16" else
+                                    "molclr_gine_aggregate_fwd_rowmax (+ its row maxima for the h3 "
+                                    "forward)" if ops.H3_FORWARD else
                                     "molclr_gine_aggregate_fwd") + " (k_gine_agg_fwd)"),
                         "bound": "hbm",
                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1011,8 +1011,11 @@ class _GINEncoder(torch.autograd.Function):
                   ws.data_ptr(), ws_bytes, _stream(x_idx))
         if _TIMER is not None:
             es = 2 if dtype == _lib.DTYPE_BF16 else 4
+            # the h3 forward's aggregation also stores its row maxima
+            rmb = _wsq("molclr_rowmax_bytes", N, D) if (enc.fp32_gemm & 2) else 0
             for _ in range(L):
-                _TIMER.add("gine_aggregate_fwd", gine_aggregate_bytes(N, D, graph.num_edges, es))
+                _TIMER.add("gine_aggregate_fwd",
+                           gine_aggregate_bytes(N, D, graph.num_edges, es) + rmb)
                 _TIMER.add("gemm_f32", 2 * 2.0 * N * D * (2 * D))
         ctx.enc, ctx.graph, ctx.arena, ctx.arena_bytes = enc, graph, arena, arena_bytes
         ctx.x_idx, ctx.params, ctx.training = x_idx, params, training
