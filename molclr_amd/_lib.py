@@ -281,8 +281,24 @@ def last_error() -> str:
     return (load().molclr_last_error() or b"").decode()
 
 
+# Dry run (graph_step.CapturedTrainStep, before a capture): every call is
+# skipped, so a pass through the Python layer only allocates what it would
+# use (notably the cached weight images) and launches nothing.
+DRY_RUN = [False]
+
+
+class dry_run:
+    def __enter__(self):
+        DRY_RUN[0] = True
+
+    def __exit__(self, *exc):
+        DRY_RUN[0] = False
+
+
 def call(name: str, *args) -> None:
     """Call an int-returning entry point and raise on a non-zero status."""
+    if DRY_RUN[0]:
+        return
     rc = getattr(load(), name)(*args)
     if rc != 0:
         raise MolclrError(f"{name} failed (status {rc}): {last_error()}")

@@ -776,7 +776,7 @@ int emb_bwd(const int64_t* x, const typename St::T* dh, float* dX1, float* dX2, 
     hipLaunchKernelGGL(k_emb_hist, dim3((unsigned)e.nblk), dim3(kEmbBlock), nk * sizeof(int32_t), s,
                        x, N, n1, n2, e.hist);
   } else {
-    (void)hipMemsetAsync(e.hist, 0, (size_t)e.nblk * nk * sizeof(int32_t), s);
+    (void)molclr::zero_async(e.hist, (size_t)e.nblk * nk * sizeof(int32_t), s);
   }
   hipLaunchKernelGGL(k_emb_keyscan, dim3((unsigned)nk), dim3(64), 0, s, e.hist, (int)e.nblk,
                      e.total);

@@ -842,8 +842,7 @@ int aug_plan_impl(const int64_t* store_atom_ptr, const int64_t* store_edge_index
   }
   hipLaunchKernelGGL(k_aug_edge_offsets, dim3(1), dim3(1024), 0, s,
                      static_cast<const int64_t*>(a.cnt), batch_size, a.edge_off);
-  if (hipMemcpyAsync(num_edges_out, a.edge_off + batch_size, sizeof(int64_t),
-                     hipMemcpyDeviceToDevice, s) != hipSuccess) {
+  if (molclr::copy_async(num_edges_out, a.edge_off + batch_size, sizeof(int64_t), s) != hipSuccess) {
     molclr::set_error("aug_views_plan: copy failed");
     return MOLCLR_ERR_ARG;
   }

@@ -110,6 +110,59 @@ void launch_timed(int kind, F kernel, dim3 grid, dim3 block, uint32_t shmem,
   hipLaunchKernelGGL(kernel, grid, block, shmem, stream, args...);
 }
 
+// Zeroing and device-to-device copies as KERNELS, never hipMemsetAsync /
+// hipMemcpyAsync: the library's steps are captured into HIP graphs, and a
+// memset node that follows a kernel node in a captured graph was measured
+// not to take effect on replays (tools/capture_memset_probe3.py: the region
+// kept the value written before the replay in 299 of 300 replays, on this
+// ROCm 7.0 runtime) -- which left the h3 max slots holding stale values and,
+// on fresh pool memory, HBM garbage (zero MLP weight gradients).
+namespace detail {
+__global__ __launch_bounds__(256) static void k_fill_bytes(uint8_t* __restrict__ p, size_t n,
+                                                           uint8_t v) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t n16 = (reinterpret_cast<uintptr_t>(p) & 15) == 0 ? n / 16 : 0;
+  const uint32_t w = 0x01010101u * v;
+  for (size_t i = t; i < n16; i += stride)
+    reinterpret_cast<uint4*>(p)[i] = make_uint4(w, w, w, w);
+  for (size_t i = 16 * n16 + t; i < n; i += stride) p[i] = v;
+}
+__global__ __launch_bounds__(256) static void k_copy_bytes(uint8_t* __restrict__ d,
+                                                           const uint8_t* __restrict__ s,
+                                                           size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool al = ((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 15) == 0;
+  const size_t n16 = al ? n / 16 : 0;
+  for (size_t i = t; i < n16; i += stride)
+    reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+  for (size_t i = 16 * n16 + t; i < n; i += stride) d[i] = s[i];
+}
+inline unsigned fill_blocks(size_t n) {
+  const size_t b = (n / 16 + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : b > 2048 ? 2048 : b);
+}
+}  // namespace detail
+
+// memset(p, v, bytes) on `s` as a kernel (capturable); hipSuccess or the launch error
+inline hipError_t fill_async(void* p, int v, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  hipLaunchKernelGGL(detail::k_fill_bytes, dim3(detail::fill_blocks(bytes)), dim3(256), 0, s,
+                     static_cast<uint8_t*>(p), bytes, (uint8_t)v);
+  return hipGetLastError();
+}
+inline hipError_t zero_async(void* p, size_t bytes, hipStream_t s) {
+  return fill_async(p, 0, bytes, s);
+}
+// device-to-device memcpy on `s` as a kernel (capturable)
+inline hipError_t copy_async(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return hipSuccess;
+  hipLaunchKernelGGL(detail::k_copy_bytes, dim3(detail::fill_blocks(bytes)), dim3(256), 0, s,
+                     static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), bytes);
+  return hipGetLastError();
+}
+
 }  // namespace molclr
 
 // norm.hip: BatchNorm workspace for any split of `rows` into segments

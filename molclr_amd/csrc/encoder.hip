@@ -220,9 +220,9 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   const bool h3 = !bf && e->fp32_gemm != 0;
   const bool h3f = h3 && (e->fp32_gemm & 2);  // h3 forward products (not the default)
   float* fmax = F(lay.smax);  // h3: [l][0] = max |agg_l|, [l][1] = max |a1_l|
-  if (h3 && hipMemsetAsync(fmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && molclr::zero_async(fmax, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
-    molclr::set_error("gin_encoder_fwd: hipMemsetAsync failed");
+    molclr::set_error("gin_encoder_fwd: zeroing the max slots failed");
     return MOLCLR_ERR_ARG;
   }
 
@@ -346,9 +346,9 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   const bool h3 = !bf && e->fp32_gemm != 0;
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
-  if (h3 && hipMemsetAsync(bmax, 0, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
+  if (h3 && molclr::zero_async(bmax, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
                 hipSuccess) {
-    molclr::set_error("gin_encoder_bwd: hipMemsetAsync failed");
+    molclr::set_error("gin_encoder_bwd: zeroing the max slots failed");
     return MOLCLR_ERR_ARG;
   }
 
@@ -574,9 +574,9 @@ MOLCLR_API int molclr_gcn_encoder_fwd(const molclr_gcn_encoder* e, const int64_t
   const size_t kws_bytes = gcn_kernels_ws(N, D);
 
   const bool h3 = e->fp32_gemm == 1;
-  if (h3 && hipMemsetAsync(A + lay.hmax[0], 0, (size_t)L * kMaxSlotFloats * sizeof(float),
+  if (h3 && molclr::zero_async(A + lay.hmax[0], (size_t)L * kMaxSlotFloats * sizeof(float),
                            molclr::as_stream(stream)) != hipSuccess) {
-    molclr::set_error("gcn_encoder_fwd: hipMemsetAsync failed");
+    molclr::set_error("gcn_encoder_fwd: zeroing the max slots failed");
     return MOLCLR_ERR_ARG;
   }
   float* h = A + lay.h0;

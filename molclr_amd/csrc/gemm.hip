@@ -2710,8 +2710,7 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
       hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, s, C, M, N, ldc, rows,
                          cmax);
       for (int64_t p = 1; p < q6_col_tiles(N); ++p)
-        (void)hipMemcpyAsync(rows + p * M, rows, (size_t)M * sizeof(float),
-                             hipMemcpyDeviceToDevice, s);
+        (void)molclr::copy_async(rows + p * M, rows, (size_t)M * sizeof(float), s);
     }
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;
@@ -2769,8 +2768,8 @@ MOLCLR_API int molclr_linear_wgrad_groups(const float* dy, const float* x, float
   const int flags = accumulate ? MOLCLR_EPI_ACCUMULATE : 0;
   if (rows == 0) {  // an empty batch contributes nothing: dW = 0 (or unchanged)
     if (!accumulate) {
-      (void)hipMemsetAsync(dW, 0, (size_t)n_out * n_in * sizeof(float), molclr::as_stream(stream));
-      if (db) (void)hipMemsetAsync(db, 0, (size_t)n_out * sizeof(float), molclr::as_stream(stream));
+      (void)molclr::zero_async(dW, (size_t)n_out * n_in * sizeof(float), molclr::as_stream(stream));
+      if (db) (void)molclr::zero_async(db, (size_t)n_out * sizeof(float), molclr::as_stream(stream));
     }
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;
@@ -2808,7 +2807,7 @@ MOLCLR_API int molclr_absmax_f32(const float* x, int64_t rows, int64_t cols, int
                                  float* slot, int accumulate, molclr_stream_t stream) {
   MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && slot, "absmax_f32: bad arguments");
   hipStream_t s = molclr::as_stream(stream);
-  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotFloats * sizeof(float), s);
+  if (!accumulate) (void)molclr::zero_async(slot, kMaxSlotFloats * sizeof(float), s);
   if (rows > 0 && cols > 0) {
     MOLCLR_REQUIRE(x, "absmax_f32: null x");
     int64_t blocks = ld == cols ? molclr::ceil_div(rows * cols, 256 * 16) : rows;
@@ -2825,7 +2824,7 @@ MOLCLR_API int molclr_absmax_rows_f32(const float* x, int64_t rows, int64_t cols
   MOLCLR_REQUIRE(rows >= 0 && cols >= 0 && ld >= cols && rowmax && slot,
                  "absmax_rows_f32: bad arguments");
   hipStream_t s = molclr::as_stream(stream);
-  if (!accumulate) (void)hipMemsetAsync(slot, 0, kMaxSlotFloats * sizeof(float), s);
+  if (!accumulate) (void)molclr::zero_async(slot, kMaxSlotFloats * sizeof(float), s);
   if (rows > 0) {
     MOLCLR_REQUIRE(x || cols == 0, "absmax_rows_f32: null x");
     int64_t blocks = molclr::ceil_div(rows, 4 * 8);
@@ -2941,8 +2940,8 @@ MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax
   hipStream_t s = molclr::as_stream(stream);
   if (rows == 0) {
     if (!accumulate) {
-      (void)hipMemsetAsync(dW, 0, (size_t)n_out * n_in * sizeof(float), s);
-      if (db) (void)hipMemsetAsync(db, 0, (size_t)n_out * sizeof(float), s);
+      (void)molclr::zero_async(dW, (size_t)n_out * n_in * sizeof(float), s);
+      if (db) (void)molclr::zero_async(db, (size_t)n_out * sizeof(float), s);
     }
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;

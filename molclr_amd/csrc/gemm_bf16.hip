@@ -1645,8 +1645,8 @@ MOLCLR_API int molclr_linear_wgrad_bf16_impl(const uint16_t* dy, const uint16_t*
   hipStream_t s = molclr::as_stream(stream);
   if (rows == 0) {
     if (!accumulate) {
-      (void)hipMemsetAsync(dW, 0, (size_t)n_out * n_in * sizeof(float), s);
-      if (db) (void)hipMemsetAsync(db, 0, (size_t)n_out * sizeof(float), s);
+      (void)molclr::zero_async(dW, (size_t)n_out * n_in * sizeof(float), s);
+      if (db) (void)molclr::zero_async(db, (size_t)n_out * sizeof(float), s);
     }
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;

@@ -1099,7 +1099,7 @@ MOLCLR_API int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_p
   }
   hipStream_t s = molclr::as_stream(stream);
   // nodes outside every segment get zero gradient
-  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * sizeof(float), s) != hipSuccess) {
+  if (N > 0 && molclr::zero_async(dh, (size_t)N * D * sizeof(float), s) != hipSuccess) {
     molclr::set_error("segment_pool_bwd: memset failed");
     return MOLCLR_ERR_ARG;
   }
@@ -1130,7 +1130,7 @@ MOLCLR_API int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* gr
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_bwd_bf16: dim must be a multiple of 4");
   MOLCLR_REQUIRE(mode == 0 || mode == 1, "segment_pool_bwd_bf16: mode %d (0 mean, 1 add)", mode);
   hipStream_t s = molclr::as_stream(stream);
-  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * sizeof(uint16_t), s) != hipSuccess) {
+  if (N > 0 && molclr::zero_async(dh, (size_t)N * D * sizeof(uint16_t), s) != hipSuccess) {
     molclr::set_error("segment_pool_bwd_bf16: memset failed");
     return MOLCLR_ERR_ARG;
   }
@@ -1174,7 +1174,7 @@ MOLCLR_API int molclr_segment_max_bwd(const float* dout, const int32_t* argmax, 
   MOLCLR_REQUIRE(N >= 0 && G >= 0, "segment_max_bwd: bad sizes");
   hipStream_t s = molclr::as_stream(stream);
   const size_t esz = dtype == MOLCLR_DTYPE_BF16 ? sizeof(uint16_t) : sizeof(float);
-  if (N > 0 && hipMemsetAsync(dh, 0, (size_t)N * D * esz, s) != hipSuccess) {
+  if (N > 0 && molclr::zero_async(dh, (size_t)N * D * esz, s) != hipSuccess) {
     molclr::set_error("segment_max_bwd: memset failed");
     return MOLCLR_ERR_ARG;
   }

@@ -197,17 +197,30 @@ class OverlappedGradReducer:
         self.num_layer = model.num_layer
         self.cuda = self.flat.is_cuda
         self.works, self.calls = [], 0
+        self._begin_ev = None
+        # events of the step being captured (CapturedTrainStep keeps them with
+        # its graph); eager steps reuse self.events
+        self.capture_events: list = []
         if self.cuda:
             self.stream = torch.cuda.Stream(device=self.flat.device)
-            # the executor re-records these; a first record creates the handles
-            self.events = [torch.cuda.Event() for _ in range(self.num_layer + 1)]
-            for e in self.events:
-                e.record()
+            self.events = self._new_events()
+
+    def _new_events(self):
+        # the executor re-records these; a first record creates the handles
+        ev = [torch.cuda.Event() for _ in range(self.num_layer + 1)]
+        for e in ev:
+            e.record()
+        return ev
 
     # -- step protocol --------------------------------------------------------
     def arm(self):
         from . import ops
         self.works, self.calls = [], 0
+        if self.cuda and torch.cuda.is_current_stream_capturing():
+            # every capture records and waits on events of its own: no event
+            # handle is shared by two graphs
+            self.events = self._new_events()
+            self.capture_events = list(self.events)
         ops.set_grad_hook(self)
 
     def finish(self):
@@ -219,6 +232,10 @@ class OverlappedGradReducer:
         for w in self.works:
             w.wait()  # the current stream waits for the bucket's collective
         self.works = []
+        if self._begin_ev is not None:
+            if torch.cuda.is_current_stream_capturing():
+                self.capture_events.append(self._begin_ev)
+            self._begin_ev = None
 
     def _reduce(self, i, after=None):
         lo, hi = self.slices[i]
@@ -238,7 +255,8 @@ class OverlappedGradReducer:
             raise RuntimeError("OverlappedGradReducer: one encoder backward per step (paired views)")
         self.calls += 1
         if self.cuda:
-            ev = torch.cuda.Event()
+            # kept until finish(): the side stream's wait must not outlive it
+            self._begin_ev = ev = torch.cuda.Event()
             ev.record()
             self._reduce(0, ev)
         else:

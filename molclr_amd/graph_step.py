@@ -29,8 +29,13 @@ captured with it -- NT-Xent's two all-gathers, and the bucketed gradient
 all-reduces of OverlappedGradReducer, which wait on the encoder backward's
 per-layer events from a side stream and are joined before Adam, exactly as
 in the eager step (RCCL kernels are captured into the HIP graph like any
-other launch).  Every rank must replay the same sequence of graphs in
-lockstep, as it would issue the same collectives eagerly.
+other launch).  Every step issues the same collectives in the same order
+whatever graph a rank replays (the bucket sizes and the gathered NT-Xent
+shapes do not depend on the batch's atom count), so ranks may replay
+different buckets.  Captures themselves happen in lockstep: prepare /
+prepare_sizes capture the union of every rank's sizes on every rank, and a
+rank whose batch no captured graph holds steps eagerly (same collectives)
+instead of capturing alone.
 """
 from __future__ import annotations
 
@@ -142,9 +147,12 @@ class StagedPairGraph(DeviceGraph):
 
 
 class _Captured:
-    def __init__(self, graph: StagedPairGraph, cuda_graph):
+    def __init__(self, graph: StagedPairGraph, cuda_graph, keep=()):
         self.graph = graph
         self.cuda_graph = cuda_graph
+        # what the graph writes or reads across replays and does not own:
+        # the weight images it regenerates, the reducer events it waits on
+        self.keep = list(keep)
 
 
 def _drain_collectives(*groups) -> None:
@@ -183,14 +191,16 @@ class CapturedTrainStep:
     ``prepare(pairs)`` captures what a known set of batches needs ahead of
     time.
 
-    Memory invariant (all captures share ONE graph memory pool): every replay
-    runs on the same stream as every other replay and eager step, and no
-    tensor allocated inside a capture is read by a replay before that replay
-    has written it.  Cross-replay state lives outside the pool (parameters,
-    gradients, Adam moments, BatchNorm running statistics, the loss and status
-    buffers below, the staging buffers); pool blocks of one capture that a
-    later capture reuses are therefore only ever scratch of one replay at a
-    time.  tests/test_gpu_graph_step.py alternates buckets against eager steps.
+    Memory: every capture gets its OWN graph memory pool (a c2 bucket holds
+    ~1.5 GB of arena and workspace; a few buckets are a few percent of the
+    288 GB HBM), so no capture can hand another capture's blocks to a third
+    party, whatever order graphs replay in.  Cross-replay state lives outside
+    every pool (parameters, gradients, Adam moments, BatchNorm running
+    statistics, the loss and status buffers below, the staging buffers, the
+    weight images -- ops.weight_planes never allocates an image inside a
+    capture).  tests/test_gpu_graph_step.py alternates buckets against eager
+    steps and checks that no step reads memory it did not write
+    (test_no_uninitialised_reads).
 
     The returned loss tensor is this object's own buffer, overwritten by the
     next step.  ``status`` ORs every replayed batch's input-validity word
@@ -203,7 +213,7 @@ class CapturedTrainStep:
     collective, e.g. the initial parameter broadcast, creates it)."""
 
     def __init__(self, model, optimizer, criterion, node_quantum: int = 256,
-                 edge_quantum: int = 2048, max_graphs: int = 32, node_slack: int | None = None,
+                 edge_quantum: int = 2048, max_graphs: int = 16, node_slack: int | None = None,
                  edge_headroom: float = 0.04, reducer=None):
         from .optim import FusedAdam
         if not isinstance(optimizer, FusedAdam):
@@ -222,11 +232,11 @@ class CapturedTrainStep:
         self.max_graphs = int(max_graphs)
         self.device = optimizer.flat.device
         self._graphs: OrderedDict = OrderedDict()
-        self._pool = torch.cuda.graph_pool_handle()
         self.loss = torch.zeros((), dtype=torch.float32, device=self.device)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.captures = 0
         self.replays = 0
+        self.eager_steps = 0  # data parallel: batches no captured graph held
         self.last_graph: StagedPairGraph | None = None
 
     @staticmethod
@@ -277,20 +287,44 @@ class CapturedTrainStep:
         # data parallel: the process group's watchdog thread polls its events
         # while we capture; thread-local capture keeps those calls legal
         mode = "global" if self.group is None else "thread_local"
+        self._dry_run(graph)
         ops.CAPTURE_SCOPE = {id(p) for p in self.model.parameters()}
+        ops.CAPTURE_KEEP = keep = []
         try:
             self._record(g, mode, graph, opt)
         finally:
             ops.CAPTURE_SCOPE = None
+            ops.CAPTURE_KEEP = None
+        if self.reducer is not None:
+            keep += self.reducer.capture_events
         self.captures += 1
         # a capture only records: the cached images must be regenerated by
         # the next eager use as well
         ops.bump_param_generation()
-        return _Captured(graph, g)
+        return _Captured(graph, g, keep)
+
+    def _dry_run(self, graph):
+        """The step's forward and backward through the Python layer with every
+        library call skipped (nothing runs on the GPU; the process group's
+        NT-Xent gathers do run, on every rank alike: captures are made in
+        lockstep).  What it leaves behind is what the capture must not
+        allocate from its pool: the weight images the step reads, created
+        here from the ordinary allocator (regenerated inside the graph)."""
+        from . import _lib
+        with _lib.dry_run():
+            _, z = self.model.forward_staged(graph)
+            loss = self.criterion.forward_pair(ops.l2_normalize(z))
+            loss.backward()
+        del loss, z
+        # the images it created hold nothing yet: the capture must record
+        # their regeneration
+        ops.bump_param_generation()
+        torch.cuda.synchronize(self.device)
 
     def _record(self, g, mode, graph, opt):
         """The step's work into g (the tensors it allocates live in the pool)."""
-        with torch.cuda.graph(g, pool=self._pool, capture_error_mode=mode):
+        # a private pool per capture (see the class docstring)
+        with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle(), capture_error_mode=mode):
             graph.build()
             opt.zero_grad()
             if self.reducer is not None:
@@ -323,10 +357,44 @@ class CapturedTrainStep:
         self._graphs.move_to_end(id(ent))
         return ent, False
 
+    # -- data parallel: captures in lockstep ----------------------------------
+    def _multi_rank(self) -> bool:
+        import torch.distributed as dist
+        return (self.group is not None and dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(self.group) > 1)
+
+    def _global_sizes(self, sizes) -> list:
+        """Every rank's (nodes, edges) sizes (one all-gather of a padded list),
+        so that all ranks capture the same buckets in the same order."""
+        import torch.distributed as dist
+        loc = torch.tensor([[int(a), int(b)] for a, b in sizes] or [[0, 0]],
+                           dtype=torch.long, device=self.device)[: max(len(sizes), 1)]
+        n = torch.tensor([len(sizes)], dtype=torch.long, device=self.device)
+        ns = [torch.zeros_like(n) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(ns, n, group=self.group)
+        most = max(1, max(int(t.item()) for t in ns))
+        pad = torch.zeros(most, 2, dtype=torch.long, device=self.device)
+        pad[: loc.shape[0]] = loc
+        outs = [torch.zeros_like(pad) for _ in ns]
+        dist.all_gather(outs, pad, group=self.group)
+        return sorted({(int(a), int(b)) for o, k in zip(outs, ns)
+                       for a, b in o[: int(k.item())].tolist()}, reverse=True)
+
     def prepare(self, pairs) -> int:
         """Capture (without running) every graph the given batch pairs need;
-        returns the number of new captures."""
+        returns the number of new captures.  Data parallel over several ranks:
+        the union of every rank's sizes is captured on every rank, in the same
+        order (a collective: all ranks call it together)."""
         before = self.captures
+        pairs = list(pairs)
+        if self._multi_rank():
+            sizes = [self._need(a, b)[:2] for a, b in pairs]
+            gi = {self._need(a, b)[2] for a, b in pairs}
+            gj = {self._need(a, b)[3] for a, b in pairs}
+            if len(gi) != 1 or len(gj) != 1:
+                raise ValueError("CapturedTrainStep.prepare: data parallel batches must hold a "
+                                 "fixed number of molecules per view")
+            return self.prepare_sizes(sizes, gi.pop(), gj.pop())
         for xis, xjs in pairs:
             self._entry(xis, xjs)
         return self.captures - before
@@ -337,8 +405,11 @@ class CapturedTrainStep:
         largest first, so that each capture serves every smaller size within
         the node slack (captures spaced ~node_slack + node_quantum apart).
         Nothing is staged: the first replay stages its batch.  Returns the
-        number of new captures."""
+        number of new captures.  Data parallel over several ranks: a
+        collective (every rank captures the union of all ranks' sizes)."""
         before = self.captures
+        if self._multi_rank():
+            sizes = self._global_sizes(list(sizes))
 
         class _V:  # the shape view lookup() / bucket() read
             def __init__(self, n, e, g):
@@ -356,7 +427,35 @@ class CapturedTrainStep:
                 self._insert(self._capture(self.bucket(vi, vj)))
         return self.captures - before
 
+    def _eager(self, xis, xjs) -> torch.Tensor:
+        """The same step without a graph (a data-parallel batch no captured
+        graph holds): the same collectives in the same order as a replay, so
+        ranks replaying graphs and a rank stepping eagerly stay matched."""
+        from .data import pair_graph
+        opt = self.optimizer
+        opt.zero_grad()
+        if self.reducer is not None:
+            self.reducer.arm()
+        _, z = self.model.forward_pair(xis, xjs)
+        loss = self.criterion.forward_pair(ops.l2_normalize(z))
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        else:
+            from .distributed import allreduce_grads
+            allreduce_grads(opt.flat_grad, self.group)
+        opt.step()
+        self.loss.copy_(loss.detach())
+        torch.bitwise_or(self.status, pair_graph(xis, xjs).status, out=self.status)
+        self.eager_steps += 1
+        self.last_graph = None
+        return self.loss
+
     def __call__(self, xis, xjs) -> torch.Tensor:
+        if self._multi_rank() and self.lookup(xis, xjs) is None:
+            # capturing here would capture on this rank alone: step eagerly
+            # (prepare / prepare_sizes capture in lockstep ahead of time)
+            return self._eager(xis, xjs)
         ent, fresh = self._entry(xis, xjs)
         if not fresh:
             ent.graph.stage([xis, xjs])

@@ -15,9 +15,10 @@ rule, one kernel); optional config keys ``world_size`` (data parallel via
 torchrun), ``seed``, ``dataset.views`` ('device', the default: both views of
 every batch are built on the GPU from the resident molecules, for every
 ``aug`` mode; 'host': the reference's DataLoader, node masking only),
-``hip_graph`` (default True: one process replays the whole step from HIP
+``hip_graph`` (default True: each process replays the whole step from HIP
 graphs captured per batch-size capacity bucket, molclr_amd.graph_step, when
-the run allows it -- one process, the paired executor pass; False: eager); the
+the run allows it -- the paired executor pass, one process or data parallel
+over RCCL; False: eager); the
 scalar writer is TensorBoard when installed, otherwise a JSONL file with the
 same tags.  ``data_path`` may be the reference's SMILES text file (featurised
 once into a cached binary shard), a shard, or ``synthetic:<count>``.
@@ -152,8 +153,10 @@ class MolCLR(object):
 
     def _graph_step(self, model, optimizer):
         """The HIP-graph step (molclr_amd.graph_step) unless the config turns
-        it off (``hip_graph: False``), when the run allows it: one process,
-        the paired executor pass at an unpadded width; else None (eager)."""
+        it off (``hip_graph: False``), when the run allows it: the paired
+        executor pass at an unpadded width, one process or data parallel over
+        RCCL (the collectives are captured with the step; captures happen in
+        lockstep across ranks); else None (eager)."""
         if not self.config.get('hip_graph', True):
             return None
         if not getattr(self, "paired", True) or not hasattr(model, "forward_staged"):
@@ -206,8 +209,19 @@ class MolCLR(object):
         cs = self._graph_step(model, optimizer)
         if cs is not None and hasattr(train_loader, "on_epoch_plan"):
             # capture every graph an epoch's batches need when it is drawn
-            # (node masking: exact sizes), not in the middle of the epoch
+            # (node masking: exact sizes), not in the middle of the epoch;
+            # data parallel: every rank captures the union of all ranks' sizes
             train_loader.on_epoch_plan = cs.prepare_sizes
+        try:
+            return self._train_epochs(model, optimizer, scheduler, train_loader, valid_loader,
+                                      model_checkpoints_folder)
+        finally:
+            # graphs holding RCCL collectives go before the process group does
+            if cs is not None:
+                cs.close()  # its counters and status word stay readable
+
+    def _train_epochs(self, model, optimizer, scheduler, train_loader, valid_loader,
+                      model_checkpoints_folder):
         n_iter = 0
         valid_n_iter = 0
         best_valid_loss = np.inf
@@ -310,7 +324,11 @@ def main(config_path: str = "config.yaml"):
 
     dataset = MoleculeDatasetWrapper(config['batch_size'], **config['dataset'])
     molclr = MolCLR(dataset, config)
-    molclr.train()
+    try:
+        molclr.train()  # closes its captured graphs itself
+    finally:
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -212,7 +212,7 @@ def weight_planes(W, N, K, ldb, b_kmajor, kind: str = "x6") -> torch.Tensor:
     ent = _PLANES.get(key)
     if ent is not None and ent[1]() is W:
         if ent[0] == (W._version, gen):
-            return ent[3]
+            return _keep_image(ent[3])
         if ent[0][1] != gen:
             _refresh_planes(gen)
             ent = _PLANES[key]
@@ -222,17 +222,43 @@ def weight_planes(W, N, K, ldb, b_kmajor, kind: str = "x6") -> torch.Tensor:
             # address, so it must never be freed while W lives
             _make_planes(kind, [(W, ent[2], ent[3])])
             ent = _PLANES[key] = ((W._version, gen), ent[1], ent[2], ent[3])
-        return ent[3]
+        return _keep_image(ent[3])
     # drop entries of dead tensors on every insert: a padded weight (emb_dim
     # not a multiple of the kernels' width) is a new tensor each call, and its
     # planes must not stay pinned in HBM
     for k in [k for k, e in _PLANES.items() if e[1]() is None]:
-        del _PLANES[k]
+        _drop_image(_PLANES.pop(k)[3])
     nbytes = _wsq(_PLANE_FNS[kind][0], N, K)
-    planes = torch.empty(nbytes // 2, dtype=torch.int16, device=W.device)
+    planes = _new_image(nbytes, W.device)
     _make_planes(kind, [(W, (N, K, ldb, int(b_kmajor)), planes)])
     _PLANES[key] = ((W._version, gen), weakref.ref(W), (N, K, ldb, int(b_kmajor)), planes)
+    return _keep_image(planes)
+
+
+# Weight images are state that outlives a step: they must not come from a
+# graph's private memory pool.  CapturedTrainStep runs the step once as a dry
+# run (_lib.dry_run: every library call skipped) before capturing it, so every
+# image the step uses already exists when the capture starts and the capture
+# only records its regeneration.  The capture also keeps a reference to every
+# image its graph writes (CAPTURE_KEEP, held by the captured entry), so an
+# image a live graph regenerates can never be freed and handed to someone else.
+CAPTURE_KEEP: list | None = None
+
+
+def _new_image(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(nbytes // 2, dtype=torch.int16, device=device)
+
+
+def _keep_image(planes: torch.Tensor) -> torch.Tensor:
+    if CAPTURE_KEEP is not None:
+        CAPTURE_KEEP.append(planes)
     return planes
+
+
+def _drop_image(planes: torch.Tensor) -> None:
+    """An image of a dead weight leaves the cache (the caching allocator
+    reuses it in stream order)."""
+    del planes
 
 
 def _make_planes(kind, jobs) -> None:
@@ -262,7 +288,7 @@ def _refresh_planes(gen: int) -> None:
     for k, (tok, ref, shape, planes) in list(_PLANES.items()):
         W = ref()
         if W is None:
-            del _PLANES[k]
+            _drop_image(_PLANES.pop(k)[3])
             continue
         if scope is not None and id(W) not in scope:
             continue
@@ -271,7 +297,7 @@ def _refresh_planes(gen: int) -> None:
     for kind, js in jobs.items():
         _make_planes(kind, [(W, shape, planes) for _, W, shape, planes in js])
         for k, W, shape, planes in js:
-            _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, planes)
+            _PLANES[k] = ((W._version, gen), weakref.ref(W), shape, _keep_image(planes))
 
 
 # fp32 GEMMs of the GIN MLP backward (data and weight gradients): "h3" = three

@@ -214,3 +214,38 @@ def test_overlapped_grad_reducer_buckets_and_sums():
     for r in res:
         assert r[4] == expect and r[5] == expect
         assert r[6] == "refused"
+
+
+def _global_sizes_worker(rank, world, port, q):
+    import types
+
+    import torch.distributed as dist
+
+    from molclr_amd.graph_step import CapturedTrainStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fake = types.SimpleNamespace(group=dist.group.WORLD, device=torch.device("cpu"))
+        local = [[(3000, 9000), (2800, 8000)], [(3100, 9100)], []][rank]
+        q.put((rank, CapturedTrainStep._global_sizes(fake, local)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_capture_sizes_union_across_ranks():
+    """Data-parallel captures happen in lockstep: every rank gets the union of
+    all ranks' (nodes, edges) sizes, largest first, whatever its own list
+    (graph_step.CapturedTrainStep._global_sizes over gloo, world 3, one rank
+    with no sizes)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_sizes_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    want = [(3100, 9100), (3000, 9000), (2800, 8000)]
+    assert all(got[r] == want for r in range(3)), got

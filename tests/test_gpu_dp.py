@@ -218,6 +218,50 @@ def test_overlapped_reducer_step_rccl_world1(dev, rccl_world1, kind):
         assert torch.equal(out[0][n], out[1][n]), n
 
 
+def _param_report(model, opt_a, opt_b, names=("a", "b")):
+    """Per-parameter rel error of opt_a.flat_grad against opt_b.flat_grad with
+    both norms (which side is wrong), worst first."""
+    name_of = {id(p): n for n, p in model.named_parameters()}
+    rows = []
+    for (p, off, n) in opt_a.views:  # same bucketed layout on both sides
+        ga = opt_a.flat_grad[off:off + n].double()
+        gb = opt_b.flat_grad[off:off + n].double()
+        nb = gb.norm().item()
+        rows.append((((ga - gb).norm().item() / max(nb, 1e-30)), name_of.get(id(p), "?"),
+                     ga.norm().item(), nb))
+    rows.sort(reverse=True)
+    return "; ".join(f"{nm}: rel {r:.3g} |{names[0]}| {na:.4g} |{names[1]}| {nb:.4g}"
+                     for r, nm, na, nb in rows[:8])
+
+
+def _snapshot_buffers(opt, model):
+    """Pinned host buffers for _snapshot (allocated once, outside the loop)."""
+    ts = [opt.flat, opt.exp_avg, opt.exp_avg_sq, opt._step_dev]
+    for bn in model.batch_norms:
+        ts += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    return [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ts]
+
+
+def _snapshot(opt, model, bufs):
+    """Asynchronous host copies (no device allocation and no synchronisation:
+    the failure this test guards against depended on both)."""
+    ts = [opt.flat, opt.exp_avg, opt.exp_avg_sq, opt._step_dev]
+    for bn in model.batch_norms:
+        ts += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    for b, t in zip(bufs, ts):
+        b.copy_(t, non_blocking=True)
+    return bufs
+
+
+def _restore(opt, model, bufs):
+    ts = [opt.flat, opt.exp_avg, opt.exp_avg_sq, opt._step_dev]
+    for bn in model.batch_norms:
+        ts += [bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    with torch.no_grad():
+        for t, b in zip(ts, bufs):
+            t.copy_(b)
+
+
 @pytest.mark.parametrize("kind", ["gin", "gcn"])
 def test_captured_dp_step_rccl_world1(dev, rccl_world1, kind):
     """The data-parallel step captured as HIP graphs (CapturedTrainStep with
@@ -227,7 +271,14 @@ def test_captured_dp_step_rccl_world1(dev, rccl_world1, kind):
     buckets: loss to 1e-6, gradients to 5e-5 norm-wise (the padded rows only
     change the weight gradients' split-K partition, i.e. the fp32 summation
     order of dW over ~2k rows: measured 2.3e-5 at this B = 32 size, against
-    ~1e-3 for the reference's own fp32 vs fp64)."""
+    ~1e-3 for the reference's own fp32 vs fp64).  On a mismatch the message
+    names every step's capture / replay, the worst parameters with both
+    sides' norms, and a third (eager, no process group) gradient from the
+    same state, so the failing side is identified."""
+    _captured_dp_case(dev, rccl_world1, kind)
+
+
+def _captured_dp_case(dev, group, kind, seed=6, n_pairs=5):
     import copy
 
     from molclr_amd.dataset import SyntheticPairBatches
@@ -237,45 +288,120 @@ def test_captured_dp_step_rccl_world1(dev, rccl_world1, kind):
     from molclr_amd.nt_xent import NTXentLoss
     from molclr_amd.ops import bump_param_generation, l2_normalize
     from molclr_amd.optim import FusedAdam
-    torch.manual_seed(6)
+    torch.manual_seed(seed)
     ref = (GINet if kind == "gin" else GCN)(3, 64, 128).to(dev)
     cap = copy.deepcopy(ref)
     B = 32
-    pairs = [tuple(b.to(dev) for b in p) for p in SyntheticPairBatches(B, seed=31).take(5)]
+    pairs = [tuple(b.to(dev) for b in p) for p in SyntheticPairBatches(B, seed=31).take(n_pairs)]
     opts, reds = [], []
     for m in (ref, cap):
         opt = FusedAdam(mdist.bucketed_parameters(m), 5e-4, weight_decay=1e-5)
         mdist.broadcast_params(opt.flat)
         opts.append(opt)
-        reds.append(mdist.OverlappedGradReducer(m, opt, rccl_world1))
-    crit = NTXentLoss(dev, B, 0.1, True, group=rccl_world1)
+        reds.append(mdist.OverlappedGradReducer(m, opt, group))
+    crit = NTXentLoss(dev, B, 0.1, True, group=group)
     step = CapturedTrainStep(cap, opts[1], crit, node_quantum=128, edge_quantum=512, node_slack=0,
                              reducer=reds[1])
 
     def rel(a, b):
         return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
-    for i, (xi, xj) in enumerate(pairs + pairs[:2]):
-        with torch.no_grad():  # ref := cap's state
-            for a, b in ((opts[0].flat, opts[1].flat), (opts[0].exp_avg, opts[1].exp_avg),
-                         (opts[0].exp_avg_sq, opts[1].exp_avg_sq),
-                         (opts[0]._step_dev, opts[1]._step_dev)):
-                a.copy_(b)
-            for br, bc in zip(ref.batch_norms, cap.batch_norms):
-                br.running_mean.copy_(bc.running_mean)
-                br.running_var.copy_(bc.running_var)
-                br.num_batches_tracked.copy_(bc.num_batches_tracked)
-        bump_param_generation()
-        opts[0].zero_grad()
-        reds[0].arm()
-        _, z = ref.forward_pair(xi, xj)
-        le = crit.forward_pair(l2_normalize(z))
-        le.backward()
-        reds[0].finish()
-        opts[0].step()
-        lc = step(xi, xj).clone()
-        torch.cuda.synchronize()
-        assert abs(lc.item() - le.item()) <= 1e-6 * abs(le.item()), (i, lc.item(), le.item())
-        assert rel(opts[1].flat_grad, opts[0].flat_grad) < 5e-5, i
-    assert step.captures >= 2 and step.replays == len(pairs) + 2
-    step.close()  # before the fixture destroys the process group
+    history = []
+    bufs = _snapshot_buffers(opts[0], ref)
+    try:
+        for i, (xi, xj) in enumerate(pairs + pairs[:2]):
+            with torch.no_grad():  # ref := cap's state
+                for a, b in ((opts[0].flat, opts[1].flat), (opts[0].exp_avg, opts[1].exp_avg),
+                             (opts[0].exp_avg_sq, opts[1].exp_avg_sq),
+                             (opts[0]._step_dev, opts[1]._step_dev)):
+                    a.copy_(b)
+                for br, bc in zip(ref.batch_norms, cap.batch_norms):
+                    br.running_mean.copy_(bc.running_mean)
+                    br.running_var.copy_(bc.running_var)
+                    br.num_batches_tracked.copy_(bc.num_batches_tracked)
+            snap = _snapshot(opts[0], ref, bufs)
+            bump_param_generation()
+            opts[0].zero_grad()
+            reds[0].arm()
+            _, z = ref.forward_pair(xi, xj)
+            le = crit.forward_pair(l2_normalize(z))
+            le.backward()
+            reds[0].finish()
+            opts[0].step()
+            before = step.captures
+            lc = step(xi, xj).clone()
+            torch.cuda.synchronize()
+            history.append("capture" if step.captures > before else "replay")
+            assert abs(lc.item() - le.item()) <= 1e-6 * abs(le.item()), (i, lc.item(), le.item())
+            r = rel(opts[1].flat_grad, opts[0].flat_grad)
+            if r >= 5e-5:
+                eager_grad = opts[0].flat_grad.clone()
+                # a third gradient from the same state: eager, no group, no reducer
+                _restore(opts[0], ref, snap)
+                bump_param_generation()
+                opts[0].zero_grad()
+                _, z = ref.forward_pair(xi, xj)
+                NTXentLoss(dev, B, 0.1, True).forward_pair(l2_normalize(z)).backward()
+                torch.cuda.synchronize()
+                third = opts[0].flat_grad.clone()
+                opts[0].flat_grad.copy_(eager_grad)
+                # the same replay again from the same state: persistent damage
+                # to the graph's own state, or a transient race?
+                _restore(opts[1], cap, snap)
+                bump_param_generation()
+                step(xi, xj)
+                torch.cuda.synchronize()
+                again = rel(opts[1].flat_grad, eager_grad)
+                msg = (f"step {i} ({history}): again {again:.3g}; rel(captured, eager DP) = {r:.3g}; "
+                       f"rel(eager DP, eager local) = {rel(eager_grad, third):.3g}; "
+                       f"rel(captured, eager local) = {rel(opts[1].flat_grad, third):.3g}; "
+                       f"captured vs eager DP: {_param_report(cap, opts[1], opts[0], ('cap', 'eager'))}")
+                raise AssertionError(msg)
+        assert step.captures >= 2 and step.replays == len(pairs) + 2
+    finally:
+        step.close()  # before the fixture destroys the process group
+
+
+def _churn(dev, kind, seed):
+    """Create, step (eager, then captured over two buckets) and drop a model,
+    leaving what such a model leaves in the process: cached weight images of
+    dead weights, freed graph pools, collected autograd state."""
+    import gc
+
+    from molclr_amd.dataset import SyntheticPairBatches
+    from molclr_amd.gcn_molclr import GCN
+    from molclr_amd.ginet_molclr import GINet
+    from molclr_amd.graph_step import CapturedTrainStep
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import l2_normalize
+    from molclr_amd.optim import FusedAdam
+    torch.manual_seed(seed)
+    m = (GINet if kind == "gin" else GCN)(3, 64, 128).to(dev)
+    opt = FusedAdam(m.parameters(), 5e-4, weight_decay=1e-5)
+    crit = NTXentLoss(dev, 32, 0.1, True)
+    pairs = [tuple(b.to(dev) for b in p) for p in SyntheticPairBatches(32, seed=seed).take(3)]
+    for xi, xj in pairs[:2]:
+        opt.zero_grad()
+        _, z = m.forward_pair(xi, xj)
+        crit.forward_pair(l2_normalize(z)).backward()
+        opt.step()
+    step = CapturedTrainStep(m, opt, crit, node_quantum=128, edge_quantum=512, node_slack=0)
+    for xi, xj in pairs + pairs[:1]:
+        step(xi, xj)
+    torch.cuda.synchronize()
+    del step, m, opt, crit, pairs
+    gc.collect()
+
+
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_captured_dp_step_after_other_models(dev, rccl_world1, kind):
+    """The captured data-parallel step in a process where other models were
+    built, stepped eagerly and as HIP graphs, and dropped first -- the state the
+    round-4 driver run left before its one failure of
+    test_captured_dp_step_rccl_world1 (MLP weight gradients of the captured
+    side exactly zero).  Then the same case twice more with fresh models, each
+    after more churn, all against the eager data-parallel step."""
+    for rep in range(3):
+        _churn(dev, "gin", 100 + rep)
+        _churn(dev, "gcn", 200 + rep)
+        _captured_dp_case(dev, rccl_world1, kind, seed=7 + rep)

@@ -194,7 +194,13 @@ def test_captured_step_follows_eager(dev, kind):
         lc = step(xi, xj).clone()
         torch.cuda.synchronize()
         assert abs(lc.item() - lr_.item()) <= 1e-6 * abs(lr_.item()), (i, lc.item(), lr_.item())
-        assert rel(opt_c.flat_grad, opt_r.flat_grad) < tol_grad, i
+        r = rel(opt_c.flat_grad, opt_r.flat_grad)
+        if r >= tol_grad:
+            per = sorted(((rel(pc.grad, pr.grad), n, pc.grad.norm().item(), pr.grad.norm().item())
+                          for (n, pc), pr in zip(cap.named_parameters(), ref.parameters())),
+                         reverse=True)[:8]
+            raise AssertionError(f"step {i}: rel {r:.3g}, captures {step.captures}, replays "
+                                 f"{step.replays}; worst (rel, name, |cap|, |eager|): {per}")
         for bc, br in zip(cap.batch_norms, ref.batch_norms):
             assert rel(bc.running_mean, br.running_mean) < 1e-6, i
             assert rel(bc.running_var, br.running_var) < 1e-6, i
@@ -284,3 +290,109 @@ def test_capacity_fit_lookup_and_prepare(dev):
     assert tight.lookup(*small) is None
     tight.prepare([small])
     assert tight.captures == 2 and tight.lookup(*small) is not None
+
+
+class _Poison:
+    """Every floating-point torch.empty / empty_like of the library's Python
+    code (executor arenas, GEMM / BatchNorm outputs, NT-Xent buffers, graph
+    capacities) comes back filled with ``value`` -- inside a capture too, as a
+    fill node that runs on every replay.  A kernel that reads memory it was
+    never given a value for then sees 0, a huge finite number or NaN
+    depending on the poison, and the step's results change with it."""
+
+    def __init__(self, value):
+        self.value = value
+
+    def __enter__(self):
+        self._empty, self._like = torch.empty, torch.empty_like
+        value, real_empty, real_like = self.value, self._empty, self._like
+
+        def empty(*a, **k):
+            t = real_empty(*a, **k)
+            if t.is_cuda and t.is_floating_point():
+                t.fill_(value)
+            return t
+
+        def empty_like(x, *a, **k):
+            t = real_like(x, *a, **k)
+            if t.is_cuda and t.is_floating_point():
+                t.fill_(value)
+            return t
+        torch.empty, torch.empty_like = empty, empty_like
+        return self
+
+    def __exit__(self, *exc):
+        torch.empty, torch.empty_like = self._empty, self._like
+
+
+def _poisoned_run(dev, kind, value, batches, captured):
+    with _Poison(value):
+        model = _make(kind, 9).to(dev)
+        opt = FusedAdam(model.parameters(), 5e-4, weight_decay=1e-5)
+        crit = NTXentLoss(dev, 32, 0.1, True)
+        losses = []
+        if captured:
+            step = CapturedTrainStep(model, opt, crit, node_quantum=128, edge_quantum=512,
+                                     node_slack=0)
+            for xi, xj in batches:
+                losses.append(step(xi, xj).clone())
+            grads = opt.flat_grad.clone()
+            step.close()
+        else:
+            for xi, xj in batches:
+                losses.append(_eager_step(model, opt, crit, xi, xj))
+            grads = opt.flat_grad.clone()
+        torch.cuda.synchronize()
+        bn = [(b.running_mean.clone(), b.running_var.clone()) for b in model.batch_norms]
+        return torch.stack(losses), grads, opt.flat.clone(), bn
+
+
+@pytest.mark.parametrize("captured", [False, True], ids=["eager", "captured"])
+@pytest.mark.parametrize("kind", ["gin", "bf16", "gcn"])
+def test_no_uninitialised_reads(dev, kind, captured):
+    """The step's results do not depend on what its buffers held before:
+    with every fresh floating-point buffer pre-filled with 0, 3e38 or NaN,
+    the losses, the last step's gradients, the parameters after Adam and the
+    BatchNorm running statistics are bit-identical.  Captured: several
+    capacity buckets, replays of smaller batches on a graph whose padding rows
+    then lie between the batch and the capacity (the captured data-parallel
+    step once lost its MLP weight gradients after other tests had run in the
+    same process: a read of stale memory is the class of fault that depends on
+    process history)."""
+    batches = [_to(p, dev) for p in SyntheticPairBatches(32, seed=41).take(4)]
+    order = batches + [batches[0], batches[2], batches[1]]
+    runs = {v: _poisoned_run(dev, kind, v, order, captured) for v in (0.0, 3e38, float("nan"))}
+    base = runs[0.0]
+    for v, r in runs.items():
+        assert torch.equal(r[0], base[0]), (v, r[0], base[0])
+        assert torch.equal(r[1], base[1]), (v, rel(r[1], base[1]))
+        assert torch.equal(r[2], base[2]), v
+        for (m, s), (m0, s0) in zip(r[3], base[3]):
+            assert torch.equal(m, m0) and torch.equal(s, s0), v
+
+
+def test_captured_zeroing_takes_effect(dev):
+    """The library zeroes buffers (h3 max slots, pooled-gradient rows, edge
+    histograms) with kernels (common.h zero_async), not hipMemsetAsync: a
+    memset node that follows a kernel node in a captured graph did not take
+    effect on replays on this runtime (profiles/r5_capture_memset_probe.txt:
+    299 of 300 replays), which left the h3 max slots stale -- the round-4
+    captured data-parallel failure.  Region poisoned before each replay; the
+    zeroing and a kernel reading the zeroed region after it must see 0."""
+    lib = _lib.load()
+    x = torch.randn(16, device=dev)
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        slot = torch.empty(ops.MAX_SLOT, device=dev)
+        y = x * 2  # a kernel node first: the memset node then follows it
+        # rows = 0: the call only zeroes its max slot
+        assert lib.molclr_absmax_f32(y.data_ptr(), 0, 0, 1, slot.data_ptr(), 0,
+                                     ops._stream(y)) == 0
+        copy = slot * 1.0
+    for _ in range(20):
+        slot.fill_(3e38)
+        copy.fill_(3e38)
+        g.replay()
+        torch.cuda.synchronize()
+        assert int((slot != 0).sum()) == 0 and int((copy != 0).sum()) == 0
