@@ -157,6 +157,12 @@ def cpu_baseline(cfg, batches_cpu, steps):
             crit(zi, zj).backward()
             nt.append(time.perf_counter() - t0)
         ntx = min(nt)
+        band = {"c2": [1.19, 1.62], "c3": [0.91, 1.38]}.get(cfg["desc"][:2])
+        ratio = med / ntx
+        # the restatement stands in for the reference's CPU path only while it
+        # costs what the reference's modules do, relative to the reference's
+        # own NT-Xent on the same host (say so in the line)
+        out["calibrated"] = bool(band and band[0] <= ratio <= band[1])
         out["calibration"] = {
             "ntxent_fwd_bwd_ms": round(ntx * 1e3, 1),
             "step_over_ntxent": round(med / ntx, 3),
@@ -395,6 +401,7 @@ def main():
     torch.cuda.synchronize()
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     captures_before = captured.captures if captured is not None else 0
+    eager_before = captured.eager_steps if captured is not None else 0
     t0 = time.perf_counter()
     marks[0].record()
     for i in range(args.steps):
@@ -405,7 +412,21 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     captures_timed = (captured.captures - captures_before) if captured is not None else 0
+    eager_timed = (captured.eager_steps - eager_before) if captured is not None else 0
     ops.set_kernel_timer(None)
+    # every rank's view of the run (the first multi-GPU line must be readable
+    # on its own): world size, graphs captured, captures and eager fallbacks
+    # inside the timed region
+    mine = torch.tensor([rank, world, captured.captures if captured is not None else 0,
+                         captures_timed, eager_timed], dtype=torch.long, device=dev)
+    if world > 1:
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        torch.distributed.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    per_rank = [dict(zip(("rank", "world_size", "captures", "captures_in_timed_region",
+                          "eager_steps_in_timed_region"), (int(v) for v in t.tolist())))
+                for t in allr]
     elapsed = mdist.max_over_ranks(elapsed, dev)
     final_loss = float(loss.item())
 
@@ -538,6 +559,7 @@ def main():
             "host_enqueue_ms_per_step": round(statistics.median(host) * 1e3, 3),
             "captures": captured.captures if captured is not None else 0,
             "captures_in_timed_region": captures_timed,
+            "ranks": per_rank,
             "roofline": roofline, "roofline_mfma": roofline_mfma,
             "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
         }

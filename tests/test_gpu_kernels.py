@@ -851,7 +851,7 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
-@pytest.mark.parametrize("spread", ["uniform", "rows", "cols"])
+@pytest.mark.parametrize("spread", ["uniform", "rows", "cols", "binades30"])
 def test_linear_wgrad_h3(dev, rows, n_out, n_in, spread):
     """h3 weight gradient dW = dy^T x (+ db) against fp64.  ``rows``: dy's rows
     (nodes) span 12 decades, as gradient rows do; ``cols``: dy's columns (the
@@ -864,7 +864,13 @@ def test_linear_wgrad_h3(dev, rows, n_out, n_in, spread):
     the max (below that the lo part is an fp16 subnormal, absolute precision
     2^-38 max |dy|), so the ``cols`` case -- whole features 10^-6 below the
     largest -- is held to the path's fp32 tolerance 1e-5 per row and element
-    (measured 4.0e-6 / 2.2e-6 per row), every other case to 2e-6."""
+    (measured 4.0e-6 / 2.2e-6 per row), every other case to 2e-6.
+    ``binades30``: dy's rows spread over 30 binades (the per-tensor scale's
+    flush region starts 17 below the max) and the result is also held to the
+    reference's own arithmetic -- torch's fp32 CPU matmul of the same
+    operands, measured against fp64 here: no further from fp64 than twice
+    that, norm-wise and per row of dW ("f32" must not be narrower
+    than the reference's fp32)."""
     from molclr_amd import _lib
     lib = _lib.load()
     g = torch.Generator().manual_seed(rows + len(spread))
@@ -873,6 +879,8 @@ def test_linear_wgrad_h3(dev, rows, n_out, n_in, spread):
         dy *= torch.pow(10.0, -12 * torch.rand(rows, 1, generator=g, dtype=torch.float64))
     if spread == "cols":
         dy *= torch.pow(10.0, -6 * torch.rand(1, n_out, generator=g, dtype=torch.float64))
+    if spread == "binades30":
+        dy *= torch.pow(2.0, -30 * torch.rand(rows, 1, generator=g, dtype=torch.float64))
     x = torch.randn(rows, n_in, generator=g, dtype=torch.float64)
     dyd, xd = dy.float().to(dev), x.float().to(dev)
     dW, db = wgrad_h3(lib, dyd, xd, dev)
@@ -886,6 +894,12 @@ def test_linear_wgrad_h3(dev, rows, n_out, n_in, spread):
     bound = dy.abs().t() @ x.abs()
     elem = ((Wc - ref).abs() / bound).max().item()
     assert elem < tol, elem
+    if spread == "binades30":  # against the reference's fp32 (torch CPU sgemm)
+        r32 = (dy.float().t() @ x.float()).double()
+        e32 = rel(r32, ref)
+        row32 = ((r32 - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+        assert rel(dW, ref) <= max(2 * e32, 1e-7), (rel(dW, ref), e32)
+        assert row_err <= max(2 * row32, 1e-7), (row_err, row32)
 
 
 def wgrad_h3(lib, dyd, xd, dev):

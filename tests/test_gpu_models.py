@@ -157,13 +157,19 @@ def test_max_pool_encoder(dev, kind, L, D, B):
         assert rel(p.grad, g64[name].grad) < 1e-4, name
 
 
+@pytest.mark.parametrize("h3_forward", [True, False], ids=["h3fwd", "x6fwd"])
 @pytest.mark.parametrize("kind", ["gin", "gcn"])
-def test_training_steps_match_oracle(dev, kind):
+def test_training_steps_match_oracle(dev, kind, h3_forward, monkeypatch):
     """Three full steps (2 encoder forwards, F.normalize, NT-Xent, backward,
-    Adam with coupled L2) on the c1 shape (3 x 128, batch 64)."""
+    Adam with coupled L2) on the c1 shape (3 x 128, batch 64).  With the x6
+    forward products (MOLCLR_H3_FORWARD=0) every step's loss is held to 1e-5;
+    the trajectory bounds derived from the reference's own fp32 spread apply
+    to the h3 forward (the default) only."""
+    from molclr_amd import ops
     from molclr_amd.nt_xent import NTXentLoss
     from molclr_amd.ops import l2_normalize
     from molclr_amd.optim import FusedAdam
+    monkeypatch.setattr(ops, "H3_FORWARD", h3_forward)
     _, ref, mine = pair_models(kind, 3, 128, 512, seed=1)  # oracle in fp64
     mine = mine.to(dev)
     B = 64
@@ -195,7 +201,8 @@ def test_training_steps_match_oracle(dev, kind):
     # (tools/traj_fp32_spread.py -> tests/golden/traj_fp32_spread.json, gin:
     # loss 4.4e-5 after one step, 6.6e-4 after two; batch_norms.*.bias up to
     # 4.3e-2 norm-wise after three).
-    spread = json.loads((GOLDEN / "traj_fp32_spread.json").read_text()) if kind == "gin" else None
+    spread = (json.loads((GOLDEN / "traj_fp32_spread.json").read_text())
+              if kind == "gin" and h3_forward else None)
     bounds = ([max(TOL, 2 * g) for g in spread["loss_rel_per_step"]] if spread
               else [TOL] * 3)
     assert all(e <= b for e, b in zip(errs, bounds)), (errs, bounds)
@@ -496,3 +503,30 @@ def test_any_emb_dim(dev, kind, L, D, B, pool):
     h1, o1 = b(bi.to(dev))
     h2, o2 = b(bj.to(dev))
     assert rel(hp, torch.cat([h1, h2])) < TOL and rel(op, torch.cat([o1, o2])) < TOL
+
+
+def test_gcn_pretrained_checkpoint_eval_matches_oracle(dev):
+    """SURVEY §8(c) golden (3): the reference's own trained GCN
+    (ckpt/pretrained_gcn, 5 x 300, feat 512; tests/golden/gcn_pretrained_b16.npz,
+    made by tests/golden/make_gcn_pretrained.py and pinned to the shipped file
+    by tests/test_oracle_golden.py) loaded strictly into the HIP GCN, eval mode
+    (the checkpoint's running BatchNorm statistics), one fixed 16-molecule
+    batch: h and out within 1e-5 norm-wise of the fp64 oracle
+    (models/gcn_molclr.py:94-158)."""
+    import numpy as np
+
+    from molclr_amd.data import Batch
+    from molclr_amd.gcn_molclr import GCN
+    d = np.load(GOLDEN / "gcn_pretrained_b16.npz")
+    sd = {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w/")}
+    model = GCN(5, 300, 512)
+    model.load_state_dict(sd, strict=True)
+    model = model.to(dev).eval()
+    b = Batch(x=torch.from_numpy(d["x"]), edge_index=torch.from_numpy(d["edge_index"]),
+              edge_attr=torch.from_numpy(d["edge_attr"]), batch=torch.from_numpy(d["batch"]))
+    with torch.no_grad():
+        h, out = model(b.to(dev))
+    torch.cuda.synchronize()
+    h64, out64 = torch.from_numpy(d["h"]), torch.from_numpy(d["out"])
+    assert rel(h, h64) < TOL, rel(h, h64)
+    assert rel(out, out64) < TOL, rel(out, out64)

@@ -94,3 +94,37 @@ def test_trainable_param_counts():
     assert n(GINet(5, 300, 512)) == 2_404_196
     assert n(GINet(5, 512, 512)) == 5_995_264
     assert n(GCN(5, 300, 512)) == 1_039_236
+
+
+def _gcn_fixture():
+    import numpy as np
+    d = np.load(GOLDEN / "gcn_pretrained_b16.npz")  # allow_pickle=False (default)
+    sd = {k[2:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("w/")}
+    return d, sd
+
+
+def test_gcn_pretrained_fixture_is_the_shipped_checkpoint():
+    """tests/golden/gcn_pretrained_b16.npz carries the reference's shipped
+    pretrained_gcn weights (ckpt/pretrained_gcn/checkpoints/model.pth):
+    every key / shape of the manifest, the manifest's sha256 of five tensors."""
+    import hashlib
+    d, sd = _gcn_fixture()
+    m = json.loads((GOLDEN / "pretrained_gcn_manifest.json").read_text())
+    assert {k: list(v.shape) for k, v in sd.items()} == m["keys"]
+    for k, c in m["checksums"].items():
+        assert hashlib.sha256(sd[k].numpy().tobytes()).hexdigest() == c["sha256"], k
+
+
+def test_gcn_pretrained_fixture_oracle_outputs():
+    """The fixture's h / out are the fp64 oracle's (eval mode) on its batch."""
+    from molclr_amd.data import Batch
+    from oracle.reference_cpu import RefGCN
+    d, sd = _gcn_fixture()
+    ref = RefGCN(5, 300, 512).double()
+    ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in sd.items()})
+    ref.eval()
+    b = Batch(x=torch.from_numpy(d["x"]), edge_index=torch.from_numpy(d["edge_index"]),
+              edge_attr=torch.from_numpy(d["edge_attr"]), batch=torch.from_numpy(d["batch"]))
+    with torch.no_grad():
+        h, out = ref(b)
+    assert torch.equal(h, torch.from_numpy(d["h"])) and torch.equal(out, torch.from_numpy(d["out"]))
