@@ -1915,8 +1915,21 @@ __global__ __launch_bounds__(256) void k_hplanes_max_batch(PlanesJobs jobs) {
   // B stored [rows][cols]: rows = N (kmajor 0) or K (kmajor 1)
   const int64_t rows = jb.kmajor ? jb.K : jb.N, cols = jb.kmajor ? jb.N : jb.K;
   float m = 0.f;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
-    for (int64_t c = threadIdx.x; c < cols; c += blockDim.x) m = fmaxf(m, fabsf(jb.B[r * jb.ldb + c]));
+  if (jb.ldb == cols && cols % 4 == 0 && (reinterpret_cast<uintptr_t>(jb.B) & 15) == 0) {
+    // dense: one flat float4 range (a large image -- e.g. NT-Xent's gathered
+    // columns, 8192 x 256 -- is not 64 blocks of row-serial loops)
+    const int64_t n4 = rows * cols / 4;
+    const float4* b4 = reinterpret_cast<const float4*>(jb.B);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const float4 v = b4[t];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
+      for (int64_t c = threadIdx.x; c < cols; c += blockDim.x)
+        m = fmaxf(m, fabsf(jb.B[r * jb.ldb + c]));
+  }
   __shared__ float red[4];
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;

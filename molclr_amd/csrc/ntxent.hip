@@ -362,6 +362,94 @@ __global__ __launch_bounds__(256) void k_ntxent_weights(const float* S, float* W
   *reinterpret_cast<float4*>(W + r * ncols + c0) = make_float4(e[0], e[1], e[2], e[3]);
 }
 
+// ---- h3 formulation (impl 2) ----------------------------------------------------
+// S = R_rows R_cols^T by the h3 GEMM (three fp16 MFMAs per product,
+// per-tensor power-of-two scales; the rows are unit vectors after
+// F.normalize / the cosine's own normalisation), the row logsumexp as in
+// impl 1; in the backward W^T = f(S) through an LDS transpose, and
+// dR = W R_cols as the h3 weight-gradient product (dR = (W^T)^T R_cols:
+// K = ncols, a long K split into ordered partials).
+
+// max |x| of a dense [rows][cols] matrix into a max slot with plain stores
+// (block b writes entry b of kMaxSlotParts: no zeroing, no atomics); block 0
+// also zeroes `zero_slot` (the atomic slot the next kernel folds into)
+__global__ __launch_bounds__(256) void k_ntxent_absmax_plain(const float* __restrict__ x,
+                                                             int64_t n4, float* __restrict__ slot,
+                                                             float* __restrict__ zero_slot) {
+  float m = 0.f;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[t];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  __shared__ float red[4];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    slot[blockIdx.x * kMaxSlotStride] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (zero_slot != nullptr && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < kMaxSlotFloats; i += blockDim.x) zero_slot[i] = 0.f;
+}
+
+// W^T[c][r] = g/(2B T) (exp(S_rc/T - lse_r) + exp(S_rc/T - lse_c) - 2 [c = p(r)]),
+// 0 at c = r, from the row-major S through an LDS transpose: a block of 256
+// threads takes a 64 (r) x 64 (c) tile, reads S rows as float4 runs along c and
+// writes W^T rows as float4 runs along r; max |W| into `wmax` (zeroed before)
+constexpr int kWT = 64;
+__global__ __launch_bounds__(256) void k_ntxent_weights_tt(
+    const float* __restrict__ S, float* __restrict__ Wt, int64_t nrows, int64_t ncols,
+    const int32_t* __restrict__ gidx, const float* __restrict__ lse_cols,
+    const float* __restrict__ grad_loss, int64_t B, float inv_t, float* __restrict__ wmax) {
+  __shared__ float tile[kWT][kWT + 1];  // [c][r]
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * kWT, c0 = (int64_t)blockIdx.x * kWT;
+  const float coef = (*grad_loss) * inv_t / (float)(2 * B);
+  float mx = 0.f;
+  // read: 64 rows x 16 float4 = 1024 float4, 4 per thread (16 threads per row)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + 256 * q;
+    const int rr = idx >> 4, cc = 4 * (idx & 15);
+    const int64_t r = r0 + rr, c = c0 + cc;
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    if (r < nrows && c < ncols) {  // ncols % 4 == 0 (host)
+      const float4 v = *reinterpret_cast<const float4*>(S + r * ncols + c);
+      const int64_t rg = gidx[r];
+      const int64_t pg = rg + B < 2 * B ? rg + B : rg - B;
+      const float lr = lse_cols[rg];
+      const float4 lc = *reinterpret_cast<const float4*>(lse_cols + c);
+      const float sv[4] = {v.x, v.y, v.z, v.w}, lcv[4] = {lc.x, lc.y, lc.z, lc.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float w = 0.f;
+        if (c + j != rg) {
+          const float lg = sv[j] * inv_t;
+          w = expf(lg - lr) + expf(lg - lcv[j]);
+          if (c + j == pg) w -= 2.f;
+          w *= coef;
+        }
+        e[j] = w;
+        mx = fmaxf(mx, fabsf(w));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[cc + j][rr] = e[j];
+  }
+  __syncthreads();
+  // write: 64 W^T rows (c) x 16 float4 along r
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + 256 * q;
+    const int cc = idx >> 4, rr = 4 * (idx & 15);
+    const int64_t c = c0 + cc, r = r0 + rr;
+    if (c < ncols && r < nrows)  // nrows % 4 == 0 (host)
+      *reinterpret_cast<float4*>(Wt + c * nrows + r) =
+          make_float4(tile[cc][rr], tile[cc][rr + 1], tile[cc][rr + 2], tile[cc][rr + 3]);
+  }
+  absmax_publish(mx, wmax);
+}
+
 // rhat = r / max(||r||, 1e-8) (cosine) or r (dot); norm saved for the backward
 __global__ __launch_bounds__(256) void k_ntxent_prep(const float* __restrict__ r,
                                                      float* __restrict__ rhat,
@@ -453,11 +541,28 @@ size_t ntx_gemm_ws(int64_t nrows, int64_t ncols, int64_t C) {
   return molclr_bplanes_bytes(ncols, C) + (size_t)nrows * ncols * sizeof(float) + g1 + g2 +
          4 * 256;
 }
-// automatic choice: the GEMM formulation once S has >= 2^20 elements (c2's
-// 1024 x 1024 and up), the fused kernels below that
+// shapes the h3 transposed formulation takes: the h3 GEMM's K = C <= 1024,
+// float4 rows of S^T, the weight-gradient kernel's long K (ncols >= 1024)
+bool ntx_h3_ok(int64_t nrows, int64_t ncols, int64_t C) {
+  return nrows % 4 == 0 && ncols % 4 == 0 && C % 4 == 0 && C <= 1024 && ncols >= 1024;
+}
+// workspace of the h3 formulation: S^T / W^T, the rows' h3 image, the max
+// slots of the columns and of W, the lse partials, the weight-gradient space
+size_t ntx_h3_ws(int64_t nrows, int64_t ncols, int64_t C) {
+  // W^T, and S when the backward recomputes it
+  return 2 * (size_t)nrows * ncols * sizeof(float) + molclr_hplanes_bytes(ncols, C) +
+         3 * (size_t)kMaxSlotFloats * sizeof(float) +
+         molclr_linear_wgrad_workspace_bytes(ncols, nrows, C) + 8 * 256;
+}
+// automatic choice: the fused kernels below 2^20 elements of S; the x6 GEMM
+// formulation up to 2^22 (c2's 1024 x 1024: 41 us per step against 52 for
+// h3, whose fixed costs -- max slots, the columns' image -- dominate there);
+// the h3 formulation from 2^22 where its shapes allow (the c4 rank shard
+// 1024 x 8192 x 256: 117.6 us against 128.6, tools/ntxent_c4.py)
 int ntx_impl(int64_t nrows, int64_t ncols, int64_t C, int impl) {
   if (impl >= 0) return impl;
-  return (nrows * ncols >= (1 << 20) && ncols % 4 == 0 && C % 4 == 0) ? 1 : 0;
+  if (nrows * ncols < (1 << 20) || ncols % 4 || C % 4) return 0;
+  return nrows * ncols >= (1 << 22) && ntx_h3_ok(nrows, ncols, C) ? 2 : 1;
 }
 
 // S = rows cols^T into `sim` (or, when null, the workspace; planes of the
@@ -482,6 +587,24 @@ int ntx_similarity(const float* rows, const float* cols, int64_t nrows, int64_t 
   return rc;
 }
 
+// S = rows cols^T into S (h3, row-major [nrows][ncols]): the rows' max slot
+// (plain stores), the columns' h3 image (its own max slot included)
+int ntx_similarity_h3(const float* rows, const float* cols, int64_t nrows, int64_t ncols, int64_t C,
+                      float* S, uint16_t* planes, float* rmax, hipStream_t s) {
+  molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+  hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(256), 0, s, rows,
+                     nrows * C / 4, rmax, nullptr);
+  const float* bl[1] = {cols};
+  const int64_t nn[1] = {ncols}, kk[1] = {C}, ld[1] = {C};
+  const int km[1] = {0};
+  uint16_t* pl[1] = {planes};
+  int rc = molclr_hplanes_make_batch(1, bl, nn, kk, ld, km, pl, s);
+  if (rc) return rc;
+  return molclr_gemm_f32_h3(rows, rmax, 0, planes, S, nrows, ncols, C, C, ncols,
+                            MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                            nullptr, s);
+}
+
 }  // namespace
 
 MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C) {
@@ -490,12 +613,14 @@ MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, in
   size_t bwd = (size_t)ntx_splits(nrows, ncols, kBwdWaves) * nrows * C * sizeof(float);
   size_t fused = (fwd > bwd ? fwd : bwd) + 256;
   size_t gemm = ntx_gemm_ws(nrows, ncols, C);
-  return fused > gemm ? fused : gemm;
+  size_t h3 = ntx_h3_ok(nrows, ncols, C) ? ntx_h3_ws(nrows, ncols, C) : 0;
+  size_t m = fused > gemm ? fused : gemm;
+  return m > h3 ? m : h3;
 }
 
 MOLCLR_API size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl) {
-  if (nrows <= 0 || ncols <= 0 || C <= 0 || ntx_impl(nrows, ncols, C, impl) != 1) return 0;
-  return (size_t)nrows * ncols * sizeof(float);
+  if (nrows <= 0 || ncols <= 0 || C <= 0 || ntx_impl(nrows, ncols, C, impl) == 0) return 0;
+  return (size_t)nrows * ncols * sizeof(float);  // S (impl 1) or S^T (impl 2)
 }
 
 MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, const float* cols,
@@ -506,12 +631,33 @@ MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, co
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_fwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_fwd: bad nrows");
   MOLCLR_REQUIRE(T > 0, "ntxent_fwd: temperature must be > 0");
-  MOLCLR_REQUIRE(impl >= -1 && impl <= 1, "ntxent_fwd: bad impl %d", impl);
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 2, "ntxent_fwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
   const float inv_t = (float)(1.0 / T);
   molclr::Workspace w(workspace, ws_bytes);
-  if (ntx_impl(nrows, ncols, C, impl) == 1) {
+  const int which = ntx_impl(nrows, ncols, C, impl);
+  if (which == 2) {
+    MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
+                   "ntxent_fwd: the h3 formulation needs nrows, ncols, C multiples of 4, "
+                   "C <= 1024, ncols >= 1024");
+    float* S = w.take<float>((size_t)nrows * ncols);
+    if (sim) S = sim;
+    uint16_t* planes = reinterpret_cast<uint16_t*>(w.take<char>(molclr_hplanes_bytes(ncols, C)));
+    float* rmax = w.take<float>(kMaxSlotFloats);
+    if (!w.ok()) {
+      molclr::set_error("ntxent_fwd: workspace too small");
+      return MOLCLR_ERR_WORKSPACE;
+    }
+    const int rc = ntx_similarity_h3(rows, cols, nrows, ncols, C, S, planes, rmax, s);
+    if (rc) return rc;
+    molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_row_lse,
+                         dim3((unsigned)molclr::ceil_div(nrows * 64, 256)), dim3(256), 0, s, S,
+                         nrows, ncols, gidx, B, inv_t, (float)(1.0 / (2.0 * B)), lse, loss);
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  if (which == 1) {
     MOLCLR_REQUIRE(ncols % 4 == 0, "ntxent_fwd: the GEMM formulation needs ncols %% 4 == 0");
     float* S = nullptr;
     const int rc = ntx_similarity(rows, cols, nrows, ncols, C, w, sim, &S, s);
@@ -559,11 +705,54 @@ MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, co
   MOLCLR_REQUIRE(C > 0 && C % 32 == 0, "ntxent_bwd: C=%lld must be a multiple of 32", (long long)C);
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_bwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_bwd: bad nrows");
-  MOLCLR_REQUIRE(impl >= -1 && impl <= 1, "ntxent_bwd: bad impl %d", impl);
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 2, "ntxent_bwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
   const float inv_t = (float)(1.0 / T);
-  if (ntx_impl(nrows, ncols, C, impl) == 1) {
+  const int which = ntx_impl(nrows, ncols, C, impl);
+  if (which == 2) {
+    MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
+                   "ntxent_bwd: the h3 formulation needs nrows, ncols, C multiples of 4, "
+                   "C <= 1024, ncols >= 1024");
+    molclr::Workspace w(workspace, ws_bytes);
+    float* Wt = w.take<float>((size_t)nrows * ncols);
+    uint16_t* planes = reinterpret_cast<uint16_t*>(w.take<char>(molclr_hplanes_bytes(ncols, C)));
+    float* cmax = w.take<float>(kMaxSlotFloats);
+    float* wmax = w.take<float>(kMaxSlotFloats);
+    float* rmax = w.take<float>(kMaxSlotFloats);
+    float* Sw = sim ? nullptr : w.take<float>((size_t)nrows * ncols);
+    const size_t gws = molclr_linear_wgrad_workspace_bytes(ncols, nrows, C);
+    void* g = w.take<char>(gws);
+    if (!w.ok()) {
+      molclr::set_error("ntxent_bwd: workspace too small");
+      return MOLCLR_ERR_WORKSPACE;
+    }
+    int rc = 0;
+    const float* S = sim;  // the forward's S, or recomputed here
+    if (!sim) {
+      rc = ntx_similarity_h3(rows, cols, nrows, ncols, C, Sw, planes, rmax, s);
+      if (rc) return rc;
+      S = Sw;
+    }
+    {
+      molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+      // the columns' max slot and W's zeroed slot in one launch
+      hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(256), 0, s, cols,
+                         ncols * C / 4, cmax, wmax);
+      molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_weights_tt,
+                           dim3((unsigned)molclr::ceil_div(ncols, kWT),
+                                (unsigned)molclr::ceil_div(nrows, kWT)),
+                           dim3(256), 0, s, S, Wt, nrows, ncols, gidx, lse_cols, grad_loss, B,
+                           inv_t, wmax);
+      // dR[r][k] = Σ_c W^T[c][r] cols[c][k]: the weight-gradient product
+      rc = molclr_linear_wgrad_h3(Wt, wmax, cols, cmax, drows, nullptr, ncols, nrows, C, nrows, C,
+                                  0, g, gws, s);
+    }
+    if (rc) return rc;
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  if (which == 1) {
     MOLCLR_REQUIRE(ncols % 4 == 0, "ntxent_bwd: the GEMM formulation needs ncols %% 4 == 0");
     molclr::Workspace w(workspace, ws_bytes);
     int rc;

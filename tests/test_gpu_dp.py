@@ -44,10 +44,13 @@ def _prep(lib, R, cosine, dev):
 
 
 @pytest.mark.parametrize("W,Bl,C,cosine,impl", [(8, 512, 256, True, 0), (8, 512, 256, True, 1),
-                                                (8, 512, 256, True, -1), (3, 37, 64, False, 0),
+                                                (8, 512, 256, True, 2), (8, 512, 256, True, -1),
+                                                (2, 512, 256, False, 2), (3, 37, 64, False, 0),
                                                 (3, 36, 64, False, 1), (3, 37, 64, False, -1)])
 def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine, impl):
-    """impl: 0 fused kernels, 1 GEMM formulation, -1 automatic."""
+    """impl: 0 fused kernels, 1 x6 GEMM formulation, 2 h3 transposed GEMM
+    formulation (S^T by the h3 GEMM, dR by the h3 weight-gradient product),
+    -1 automatic."""
     lib = _lib.load()
     B = W * Bl
     T = 0.1
