@@ -345,7 +345,7 @@ def main():
             loss = crit(ops.l2_normalize(zi), ops.l2_normalize(zj))
         else:  # both views in one pass (MolCLR._step's default)
             _, z = model.forward_pair(xi, xj)
-            loss = crit.forward_pair(ops.l2_normalize(z))
+            loss = crit.forward_pair_normalized(z)
         loss.backward()
         if reducer is not None:  # bucketed, overlapped with the encoder backward
             reducer.finish()

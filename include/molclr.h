@@ -641,6 +641,19 @@ int molclr_ntxent_prep(const float* r, float* rhat, float* norm, int64_t n, int6
 int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, const float* norm,
                            float* dr, int64_t n, int64_t C, int cosine,
                            molclr_stream_t stream);
+/* The paired step's F.normalize (molclr.py:63-64, eps) and ntxent_prep in one
+ * launch, replacing l2norm_fwd + torch.cat([zjs, zis]) + ntxent_prep
+ * (GINet.forward_pair's z = [zis; zjs], 2 * batch_local rows):
+ *   rhat [2Bl,C] = scaled rows of R = [zjs; zis], y [2Bl,C] the normalised R,
+ *   n1 [2Bl] = |R row| (unclamped, as l2norm_fwd's norm), n2 [2Bl] the clamped
+ *   cosine denominator (1 for dot similarity).  Bit-identical to the three ops.
+ * ntxent_prep_pair_bwd: dz [2Bl,C] in z's row order from drhat. */
+int molclr_ntxent_prep_pair(const float* z, float* y, float* rhat, float* n1, float* n2,
+                            int64_t batch_local, int64_t C, double eps, int cosine,
+                            molclr_stream_t stream);
+int molclr_ntxent_prep_pair_bwd(const float* drhat, const float* rhat, const float* n2,
+                                const float* y, const float* n1, float* dz, int64_t batch_local,
+                                int64_t C, double eps, int cosine, molclr_stream_t stream);
 size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C);
 int molclr_ntxent_fwd(const float* rhat_rows, const int32_t* row_gidx, const float* rhat_cols,
                       int64_t nrows, int64_t ncols, int64_t C, int64_t batch_size,
@@ -686,6 +699,15 @@ int molclr_sum_f32(const float* x, float* out, int64_t n, molclr_stream_t stream
 int molclr_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                      int64_t n, const float* lr, int32_t* step, double beta1, double beta2,
                      double eps, double weight_decay, molclr_stream_t stream);
+/* molclr_adam_step with tick = 0 leaves the step counter alone (the update
+ * uses *step + 1 as always): molclr_step_tail then advances it, and also
+ * copies the loss scalar and ORs the batch's status word into a sticky word
+ * (either may be NULL) -- the HIP-graph step's single closing launch. */
+int molclr_adam_step_ex(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        int64_t n, const float* lr, int32_t* step, double beta1, double beta2,
+                        double eps, double weight_decay, int tick, molclr_stream_t stream);
+int molclr_step_tail(int32_t* step, const float* loss_src, float* loss_dst,
+                     const int32_t* status_src, int32_t* status_acc, molclr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * GIN encoder executor (models/ginet_molclr.py:98-111 as ONE call).

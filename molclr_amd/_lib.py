@@ -114,6 +114,9 @@ SIGNATURES = {
     "molclr_l2norm_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, c_double, _P]),
     "molclr_ntxent_prep": (c_int, [_P, _P, _P, _I64, _I64, c_int, _P]),
     "molclr_ntxent_prep_bwd": (c_int, [_P, _P, _P, _P, _I64, _I64, c_int, _P]),
+    "molclr_ntxent_prep_pair": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, c_double, c_int, _P]),
+    "molclr_ntxent_prep_pair_bwd": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, c_double, c_int,
+                                            _P]),
     "molclr_ntxent_workspace_bytes": (c_size_t, [_I64, _I64, _I64]),
     "molclr_ntxent_fwd": (c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P, _P, _P,
                                   c_size_t, _P]),
@@ -127,6 +130,9 @@ SIGNATURES = {
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
+    "molclr_adam_step_ex": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
+                                    c_double, c_int, _P]),
+    "molclr_step_tail": (c_int, [_P, _P, _P, _P, _P, _P]),
     "molclr_gin_encoder_arena_bytes": (c_size_t, [c_int, _I64, _I64, c_int]),
     "molclr_gin_encoder_workspace_bytes": (c_size_t, [c_int, _I64, _I64, c_int]),
     "molclr_gin_encoder_fwd": (c_int, [_P, _P, _P, _P, _P, c_size_t, _P, c_size_t, _P]),

@@ -83,6 +83,15 @@ __global__ void k_adam_step(float4* __restrict__ p, const float4* __restrict__ g
 
 __global__ void k_adam_tick(int32_t* step) { *step += 1; }
 
+// the captured step's last launch: Adam's step counter, the loss copied to
+// the caller's buffer, the batch's status word ORed into the sticky word
+__global__ void k_step_tail(int32_t* step, const float* loss_src, float* loss_dst,
+                            const int32_t* status_src, int32_t* status_acc) {
+  *step += 1;
+  if (loss_dst) *loss_dst = *loss_src;
+  if (status_acc) *status_acc |= *status_src;
+}
+
 }  // namespace
 
 MOLCLR_API const char* molclr_version(void) { return "molclr_amd 0.1.0 gfx950"; }
@@ -92,6 +101,25 @@ MOLCLR_API int molclr_adam_step(float* param, const float* grad, float* exp_avg,
                                 float* exp_avg_sq, int64_t n, const float* lr, int32_t* step,
                                 double beta1, double beta2, double eps, double weight_decay,
                                 molclr_stream_t stream) {
+  return molclr_adam_step_ex(param, grad, exp_avg, exp_avg_sq, n, lr, step, beta1, beta2, eps,
+                             weight_decay, 1, stream);
+}
+
+MOLCLR_API int molclr_step_tail(int32_t* step, const float* loss_src, float* loss_dst,
+                                const int32_t* status_src, int32_t* status_acc,
+                                molclr_stream_t stream) {
+  MOLCLR_REQUIRE(step && (!loss_dst || loss_src) && (!status_acc || status_src),
+                 "step_tail: null pointer");
+  hipLaunchKernelGGL(k_step_tail, dim3(1), dim3(1), 0, molclr::as_stream(stream), step, loss_src,
+                     loss_dst, status_src, status_acc);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_adam_step_ex(float* param, const float* grad, float* exp_avg,
+                                   float* exp_avg_sq, int64_t n, const float* lr, int32_t* step,
+                                   double beta1, double beta2, double eps, double weight_decay,
+                                   int tick, molclr_stream_t stream) {
   MOLCLR_REQUIRE(n % 4 == 0, "adam_step: flat buffer length %lld must be a multiple of 4",
                  (long long)n);
   MOLCLR_REQUIRE(lr && step, "adam_step: lr and step must be device pointers");
@@ -101,7 +129,7 @@ MOLCLR_API int molclr_adam_step(float* param, const float* grad, float* exp_avg,
     hipLaunchKernelGGL(k_adam_step, dim3(molclr::ceil_div(n4, 256)), dim3(256), 0, s,
                        (float4*)param, (const float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
                        n4, lr, step, beta1, beta2, (float)eps, (float)weight_decay);
-  hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);
+  if (tick) hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

@@ -494,6 +494,82 @@ __global__ __launch_bounds__(256) void k_ntxent_prep_bwd(const float* __restrict
     dr[row * C + c] = clamped ? g[c] / den : (g[c] - dot * y[c]) / den;
 }
 
+// The paired step's two row scalings in one pass (molclr.py:63-64 then
+// nt_xent.py:40-45): z = [zis; zjs] ([2 Bl, C], GINet.forward_pair), R =
+// [zjs; zis] (nt_xent.py:48) by a row swap, y = F.normalize(R row) (eps1), rhat =
+// y / max(|y|, 1e-8) (cosine) or y.  Same per-lane loops and wave sums as
+// k_l2norm_fwd followed by k_ntxent_prep: bit-identical results, one launch,
+// no torch.cat.  y, |z| (n1) and the clamped |y| (n2) are kept for the backward.
+__device__ __forceinline__ int64_t pair_src(int64_t r, int64_t Bl) { return r < Bl ? r + Bl : r - Bl; }
+
+__global__ __launch_bounds__(256) void k_ntxent_prep_pair(const float* __restrict__ z,
+                                                          float* __restrict__ y,
+                                                          float* __restrict__ rhat,
+                                                          float* __restrict__ n1,
+                                                          float* __restrict__ n2, int64_t Bl,
+                                                          int64_t C, float eps1, int cosine) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= 2 * Bl) return;
+  const float* zr = z + pair_src(r, Bl) * C;
+  float ss = 0.f;
+  for (int64_t c = lane; c < C; c += 64) ss += zr[c] * zr[c];
+  ss = wave_sum(ss);
+  const float nrm = sqrtf(ss);
+  const float d1 = fmaxf(nrm, eps1);
+  float* yr = y + r * C;
+  float ss2 = 0.f;
+  for (int64_t c = lane; c < C; c += 64) {
+    const float v = zr[c] / d1;
+    yr[c] = v;
+    ss2 += v * v;
+  }
+  float d2 = 1.f;
+  if (cosine) {
+    ss2 = wave_sum(ss2);
+    d2 = fmaxf(sqrtf(ss2), 1e-8f);
+  }
+  if (lane == 0) {
+    n1[r] = nrm;
+    n2[r] = d2;
+  }
+  for (int64_t c = lane; c < C; c += 64) rhat[r * C + c] = cosine ? yr[c] / d2 : yr[c];
+}
+
+// dz (rows of z, un-swapped) from drhat: k_ntxent_prep_bwd then k_l2norm_bwd,
+// the same arithmetic per element (dy staged in dz's row)
+__global__ __launch_bounds__(256) void k_ntxent_prep_pair_bwd(
+    const float* __restrict__ drhat, const float* __restrict__ rhat, const float* __restrict__ n2,
+    const float* __restrict__ y, const float* __restrict__ n1, float* __restrict__ dz, int64_t Bl,
+    int64_t C, float eps1, int cosine) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= 2 * Bl) return;
+  const float* g = drhat + r * C;
+  float* out = dz + pair_src(r, Bl) * C;
+  if (!cosine) {
+    for (int64_t c = lane; c < C; c += 64) out[c] = g[c];
+  } else {
+    const float den = n2[r];
+    const float* rh = rhat + r * C;
+    float dot = 0.f;
+    for (int64_t c = lane; c < C; c += 64) dot += g[c] * rh[c];
+    dot = wave_sum(dot);
+    const bool clamped = !(den > 1e-8f);
+    for (int64_t c = lane; c < C; c += 64) out[c] = clamped ? g[c] / den : (g[c] - dot * rh[c]) / den;
+  }
+  const float nrm = n1[r];
+  const float* yr = y + r * C;
+  if (nrm > eps1) {
+    float dot = 0.f;
+    for (int64_t c = lane; c < C; c += 64) dot += out[c] * yr[c];
+    dot = wave_sum(dot);
+    for (int64_t c = lane; c < C; c += 64) out[c] = (out[c] - dot * yr[c]) / nrm;
+  } else {
+    for (int64_t c = lane; c < C; c += 64) out[c] = out[c] / eps1;
+  }
+}
+
 // column splits: single-wave workgroups per (32-row block, split); measured
 // best at ~512 waves for the forward and ~1024 for the backward
 // (tools/ntxent_scale.py; the backward's partials are [nrows][C] each)
@@ -524,6 +600,32 @@ MOLCLR_API int molclr_ntxent_prep_bwd(const float* drhat, const float* rhat, con
   if (n == 0) return MOLCLR_OK;
   hipLaunchKernelGGL(k_ntxent_prep_bwd, dim3(molclr::ceil_div(n * 64, 256)), dim3(256), 0,
                      molclr::as_stream(stream), drhat, rhat, norm, dr, n, C, cosine);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ntxent_prep_pair(const float* z, float* y, float* rhat, float* n1, float* n2,
+                                       int64_t batch_local, int64_t C, double eps, int cosine,
+                                       molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && batch_local >= 0 && (batch_local == 0 || (z && y && rhat && n1 && n2)),
+                 "ntxent_prep_pair: bad arguments");
+  if (batch_local == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_ntxent_prep_pair, dim3(molclr::ceil_div(2 * batch_local * 64, 256)),
+                     dim3(256), 0, molclr::as_stream(stream), z, y, rhat, n1, n2, batch_local, C,
+                     (float)eps, cosine);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+
+MOLCLR_API int molclr_ntxent_prep_pair_bwd(const float* drhat, const float* rhat, const float* n2,
+                                           const float* y, const float* n1, float* dz,
+                                           int64_t batch_local, int64_t C, double eps, int cosine,
+                                           molclr_stream_t stream) {
+  MOLCLR_REQUIRE(C > 0 && batch_local >= 0, "ntxent_prep_pair_bwd: bad arguments");
+  if (batch_local == 0) return MOLCLR_OK;
+  hipLaunchKernelGGL(k_ntxent_prep_pair_bwd, dim3(molclr::ceil_div(2 * batch_local * 64, 256)),
+                     dim3(256), 0, molclr::as_stream(stream), drhat, rhat, n2, y, n1, dz,
+                     batch_local, C, (float)eps, cosine);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

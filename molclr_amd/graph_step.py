@@ -313,7 +313,7 @@ class CapturedTrainStep:
         from . import _lib
         with _lib.dry_run():
             _, z = self.model.forward_staged(graph)
-            loss = self.criterion.forward_pair(ops.l2_normalize(z))
+            loss = self.criterion.forward_pair_normalized(z)
             loss.backward()
         del loss, z
         # the images it created hold nothing yet: the capture must record
@@ -330,17 +330,20 @@ class CapturedTrainStep:
             if self.reducer is not None:
                 self.reducer.arm()
             _, z = self.model.forward_staged(graph)
-            loss = self.criterion.forward_pair(ops.l2_normalize(z))
+            loss = self.criterion.forward_pair_normalized(z)
             loss.backward()
             if self.reducer is not None:  # bucketed, overlapped with the backward
                 self.reducer.finish()
             elif self.group is not None:
                 from .distributed import allreduce_grads
                 allreduce_grads(opt.flat_grad, self.group)
-            opt.step(sync_lr=False)
-            self.loss.copy_(loss)
-            # graph build and atom embedding write the batch's validity bits
-            torch.bitwise_or(self.status, graph.status, out=self.status)
+            opt.step(sync_lr=False, tick=False)
+            # one closing launch: Adam's step counter, the loss into this
+            # object's buffer, the batch's validity bits (written by the graph
+            # build and the atom embedding) into the sticky status word
+            _lib.call("molclr_step_tail", opt._step_dev.data_ptr(), loss.data_ptr(),
+                      self.loss.data_ptr(), graph.status.data_ptr(), self.status.data_ptr(),
+                      _lib.stream_of(self.device))
         del loss, z
 
     def _insert(self, ent) -> None:
@@ -437,7 +440,7 @@ class CapturedTrainStep:
         if self.reducer is not None:
             self.reducer.arm()
         _, z = self.model.forward_pair(xis, xjs)
-        loss = self.criterion.forward_pair(ops.l2_normalize(z))
+        loss = self.criterion.forward_pair_normalized(z)
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()

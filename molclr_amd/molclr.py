@@ -107,7 +107,7 @@ class MolCLR(object):
         two-call semantics); F.normalize and NT-Xent on the stacked [zis; zjs]."""
         if getattr(self, "paired", True) and hasattr(model, "forward_pair"):
             _, z = model.forward_pair(xis, xjs)
-            return self.nt_xent_criterion.forward_pair(l2_normalize(z))
+            return self.nt_xent_criterion.forward_pair_normalized(z)
         ris, zis = model(xis)  # [N,C]
         rjs, zjs = model(xjs)  # [N,C]
         zis = l2_normalize(zis)

@@ -49,3 +49,9 @@ class NTXentLoss(torch.nn.Module):
         (GINet.forward_pair): the same value as forward(z[:B], z[B:])."""
         return ops.nt_xent_pair(z, self.batch_size, self.temperature,
                                 self.use_cosine_similarity, self.group)
+
+    def forward_pair_normalized(self, z):
+        """forward_pair(F.normalize(z, dim=1)) (molclr.py:63-66) as one fused
+        node: bit-identical to the two calls, fewer launches."""
+        return ops.nt_xent_pair_normalized(z, self.batch_size, self.temperature,
+                                           self.use_cosine_similarity, self.group)

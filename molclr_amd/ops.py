@@ -897,6 +897,97 @@ class _L2Normalize(torch.autograd.Function):
         return dz, None
 
 
+# gidx (each local row's global R row) per (n, rank, world, device): built once
+# outside any capture (CapturedTrainStep's dry run populates it first)
+_GIDX: dict = {}
+
+
+def _row_index(n, dev, group):
+    if group is None:
+        key, rank, world = (n, dev.index, 0, 1), 0, 1
+    else:
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        key = (n, dev.index, rank, world)
+    g = _GIDX.get(key)
+    if g is not None:
+        return g
+    if group is None:
+        g = torch.arange(n, dtype=torch.int32, device=dev)
+    else:
+        from . import distributed as mdist
+        g = mdist.global_row_index(n // 2, rank, world, dev)
+    if not torch.cuda.is_current_stream_capturing():
+        _GIDX[key] = g
+    return g
+
+
+def _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group):
+    """NT-Xent over this process's prepared rows rhat (utils/nt_xent.py:47-65
+    after the row scaling): the columns (gathered with a group), the row
+    logsumexp, the loss; saves what _ntxent_rows_backward needs."""
+    dev = rhat.device
+    n, C = rhat.shape
+    Bl = n // 2
+    st = _lib.stream_of(dev)
+    if group is None:
+        B = Bl
+        if batch_size != B:
+            raise ValueError(f"NTXentLoss built for batch_size={batch_size} got {B} rows "
+                             "(the reference requires full batches, dataset.py:179)")
+        cols = rhat
+    else:
+        import torch.distributed as dist
+
+        from . import distributed as mdist
+        B = Bl * dist.get_world_size(group)
+        if batch_size != B:
+            raise ValueError(f"global batch {B} != NTXentLoss batch_size {batch_size}")
+        cols = mdist.gather_rows(rhat, group)
+    gidx = _row_index(n, dev, group)
+    lse = torch.empty(n, dtype=torch.float32, device=dev)
+    loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
+    ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+    ws = _ws(ws_bytes, dev)
+    # the GEMM formulations keep S for the backward
+    sim_bytes = _wsq("molclr_ntxent_sim_bytes", n, 2 * B, C, -1)
+    sim = (torch.empty(sim_bytes // 4, dtype=torch.float32, device=dev) if sim_bytes
+           else torch.empty(0, dtype=torch.float32, device=dev))
+    _lib.call("molclr_ntxent_fwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n,
+              2 * B, C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(),
+              sim.data_ptr() if sim_bytes else None, ws.data_ptr(), ws_bytes, st, -1)
+    if _TIMER is not None:
+        _TIMER.add("ntxent", 2.0 * n * 2 * B * C)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    _lib.call("molclr_sum_f32", loss_rows.data_ptr(), loss.data_ptr(), n, st)
+    if group is None:
+        lse_cols = lse
+    else:  # one all-gather carries the row lse and the rank's loss share
+        from . import distributed as mdist
+        lse_cols, loss = mdist.gather_lse_and_sum(lse, loss, group)
+    ctx.ntx = (cols, gidx, lse_cols, sim, B, C, float(temperature))
+    return loss
+
+
+def _ntxent_rows_backward(ctx, rhat, gloss):
+    """drhat (this process's rows) from the upstream scalar gradient."""
+    cols, gidx, lse_cols, sim, B, C, T = ctx.ntx
+    dev = rhat.device
+    n = rhat.shape[0]
+    gloss = gloss.to(torch.float32).contiguous()
+    drhat = torch.empty_like(rhat)
+    ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
+    ws = _ws(ws_bytes, dev)
+    _lib.call("molclr_ntxent_bwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+              lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T,
+              sim.data_ptr() if sim.numel() else None, drhat.data_ptr(), ws.data_ptr(),
+              ws_bytes, _lib.stream_of(dev), -1)
+    if _TIMER is not None:  # dR = W R (and S again when the forward kept none)
+        _TIMER.add("ntxent", (2.0 if sim.numel() else 4.0) * n * 2 * B * C)
+    ctx.ntx = None
+    return drhat
+
+
 class _NTXent(torch.autograd.Function):
     """NT-Xent over this process's rows R = [zj; zi] (utils/nt_xent.py:48).
     With a ``group`` (torch.distributed) the batch is the global one: rows
@@ -905,77 +996,64 @@ class _NTXent(torch.autograd.Function):
     @staticmethod
     def forward(ctx, R, batch_size, temperature, cosine, group):
         _check(R)
-        dev = R.device
         R = _c(R)
         n, C = R.shape
-        Bl = n // 2
         rhat = torch.empty_like(R)
-        norm = torch.empty(n, dtype=torch.float32, device=dev)
-        st = _lib.stream_of(dev)
+        norm = torch.empty(n, dtype=torch.float32, device=R.device)
         _lib.call("molclr_ntxent_prep", R.data_ptr(), rhat.data_ptr(), norm.data_ptr(), n, C,
-                  int(cosine), st)
-        if group is None:
-            B = Bl
-            if batch_size != B:
-                raise ValueError(f"NTXentLoss built for batch_size={batch_size} got {B} rows "
-                                 "(the reference requires full batches, dataset.py:179)")
-            cols = rhat
-            gidx = torch.arange(n, dtype=torch.int32, device=dev)
-        else:
-            import torch.distributed as dist
-
-            from . import distributed as mdist
-            world = dist.get_world_size(group)
-            rank = dist.get_rank(group)
-            B = Bl * world
-            if batch_size != B:
-                raise ValueError(f"global batch {B} != NTXentLoss batch_size {batch_size}")
-            cols = mdist.gather_rows(rhat, group)
-            gidx = mdist.global_row_index(Bl, rank, world, dev)
-        lse = torch.empty(n, dtype=torch.float32, device=dev)
-        loss_rows = torch.empty(n, dtype=torch.float32, device=dev)
-        ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
-        ws = _ws(ws_bytes, dev)
-        # the GEMM formulation keeps S = rows cols^T for the backward
-        sim_bytes = _lib.query("molclr_ntxent_sim_bytes", n, 2 * B, C, -1)
-        sim = (torch.empty(sim_bytes // 4, dtype=torch.float32, device=dev) if sim_bytes
-               else torch.empty(0, dtype=torch.float32, device=dev))
-        _lib.call("molclr_ntxent_fwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n,
-                  2 * B, C, B, float(temperature), lse.data_ptr(), loss_rows.data_ptr(),
-                  sim.data_ptr() if sim_bytes else None, ws.data_ptr(), ws_bytes, st, -1)
-        if _TIMER is not None:
-            _TIMER.add("ntxent", 2.0 * n * 2 * B * C)
-        loss = torch.empty((), dtype=torch.float32, device=dev)
-        _lib.call("molclr_sum_f32", loss_rows.data_ptr(), loss.data_ptr(), n, st)
-        if group is None:
-            lse_cols = lse
-        else:  # one all-gather carries the row lse and the rank's loss share
-            lse_cols, loss = mdist.gather_lse_and_sum(lse, loss, group)
-        ctx.save_for_backward(rhat, norm, cols, gidx, lse_cols, sim)
-        ctx.meta = (B, C, float(temperature), int(cosine))
+                  int(cosine), _lib.stream_of(R.device))
+        loss = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
+        ctx.save_for_backward(rhat, norm)
+        ctx.cosine = int(cosine)
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        rhat, norm, cols, gidx, lse_cols, sim = ctx.saved_tensors
-        B, C, T, cosine = ctx.meta
-        dev = rhat.device
-        n = rhat.shape[0]
-        gloss = gloss.to(torch.float32).contiguous()
-        st = _lib.stream_of(dev)
-        drhat = torch.empty_like(rhat)
-        ws_bytes = _wsq("molclr_ntxent_workspace_bytes", n, 2 * B, C)
-        ws = _ws(ws_bytes, dev)
-        _lib.call("molclr_ntxent_bwd_impl", rhat.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
-                  lse_cols.data_ptr(), gloss.data_ptr(), n, 2 * B, C, B, T,
-                  sim.data_ptr() if sim.numel() else None, drhat.data_ptr(), ws.data_ptr(),
-                  ws_bytes, st, -1)
-        if _TIMER is not None:  # dR = W R (and S again when the forward kept none)
-            _TIMER.add("ntxent", (2.0 if sim.numel() else 4.0) * n * 2 * B * C)
+        rhat, norm = ctx.saved_tensors
+        n, C = rhat.shape
+        drhat = _ntxent_rows_backward(ctx, rhat, gloss)
         dR = torch.empty_like(rhat)
         _lib.call("molclr_ntxent_prep_bwd", drhat.data_ptr(), rhat.data_ptr(), norm.data_ptr(),
-                  dR.data_ptr(), n, C, cosine, st)
+                  dR.data_ptr(), n, C, ctx.cosine, _lib.stream_of(rhat.device))
         return dR, None, None, None, None
+
+
+class _NTXentPairNormalized(torch.autograd.Function):
+    """F.normalize (molclr.py:63-64) and NT-Xent (utils/nt_xent.py:47-65) of a
+    paired forward's projections z = [zis; zjs] as one node:
+    molclr_ntxent_prep_pair does the row swap to R = [zjs; zis], F.normalize
+    and the cosine scaling in one launch (bit-identical to l2_normalize +
+    torch.cat + _NTXent's prep), and its backward puts dz straight into z's
+    row order."""
+
+    @staticmethod
+    def forward(ctx, z, batch_size, temperature, cosine, group, eps):
+        _check(z)
+        z = _c(z)
+        n, C = z.shape
+        dev = z.device
+        y = torch.empty_like(z)
+        rhat = torch.empty_like(z)
+        n1 = torch.empty(n, dtype=torch.float32, device=dev)
+        n2 = torch.empty(n, dtype=torch.float32, device=dev)
+        _lib.call("molclr_ntxent_prep_pair", z.data_ptr(), y.data_ptr(), rhat.data_ptr(),
+                  n1.data_ptr(), n2.data_ptr(), n // 2, C, float(eps), int(cosine),
+                  _lib.stream_of(dev))
+        loss = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
+        ctx.save_for_backward(y, rhat, n1, n2)
+        ctx.cosine, ctx.eps = int(cosine), float(eps)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        y, rhat, n1, n2 = ctx.saved_tensors
+        n, C = rhat.shape
+        drhat = _ntxent_rows_backward(ctx, rhat, gloss)
+        dz = torch.empty_like(rhat)
+        _lib.call("molclr_ntxent_prep_pair_bwd", drhat.data_ptr(), rhat.data_ptr(), n2.data_ptr(),
+                  y.data_ptr(), n1.data_ptr(), dz.data_ptr(), n // 2, C, ctx.eps, ctx.cosine,
+                  _lib.stream_of(rhat.device))
+        return dz, None, None, None, None, None
 
 
 GIN_PARAMS_PER_LAYER = 8  # mlp0.W, mlp0.b, mlp2.W, mlp2.b, edge_emb1, edge_emb2, bn.W, bn.b
@@ -1271,3 +1349,13 @@ def nt_xent_pair(z, batch_size, temperature, use_cosine_similarity=True, group=N
     B = z.shape[0] // 2
     return _NTXent.apply(torch.cat([z[B:], z[:B]], 0), batch_size, temperature,
                          bool(use_cosine_similarity), group)
+
+
+def nt_xent_pair_normalized(z, batch_size, temperature, use_cosine_similarity=True, group=None,
+                            eps: float = 1e-12):
+    """nt_xent_pair(l2_normalize(z)) as one autograd node (one prep launch
+    each way instead of l2norm + cat + prep and their backwards; the same
+    values bit for bit)."""
+    _check(z)
+    return _NTXentPairNormalized.apply(z, batch_size, temperature, bool(use_cosine_similarity),
+                                       group, eps)

@@ -82,18 +82,21 @@ class FusedAdam(torch.optim.Optimizer):
             self._lr_host = lr
 
     @torch.no_grad()
-    def step(self, closure=None, sync_lr: bool = True):
+    def step(self, closure=None, sync_lr: bool = True, tick: bool = True):
         """``sync_lr=False`` while capturing a HIP graph: the replays read the
-        device learning rate, which the caller syncs before each replay."""
+        device learning rate, which the caller syncs before each replay.
+        ``tick=False``: the caller advances the device step counter itself
+        (molclr_step_tail, the captured step's closing launch)."""
         loss = closure() if closure is not None else None
         g = self.param_groups[0]
         if sync_lr:
             self.sync_lr()
         b1, b2 = g["betas"]
-        _lib.call("molclr_adam_step", self.flat.data_ptr(), self.flat_grad.data_ptr(),
+        _lib.call("molclr_adam_step_ex", self.flat.data_ptr(), self.flat_grad.data_ptr(),
                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.numel,
                   self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(b1), float(b2),
-                  float(g["eps"]), float(g["weight_decay"]), _lib.stream_of(self.flat.device))
+                  float(g["eps"]), float(g["weight_decay"]), int(tick),
+                  _lib.stream_of(self.flat.device))
         ops.bump_param_generation()  # cached weight planes are stale now
         return loss
 

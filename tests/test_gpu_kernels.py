@@ -1010,3 +1010,23 @@ def test_batchnorm_seg_bwd_max(dev, rows, D, relu):
     dz, rmax, slot = outs[1][0], outs[1][3], outs[1][4]
     assert torch.equal(rmax.amax(0), dz.abs().amax(1))
     assert slot.max().item() == dz.abs().max().item()
+
+
+@pytest.mark.parametrize("B,C,cosine", [(512, 256, True), (37, 64, True), (40, 128, False)])
+def test_ntxent_pair_normalized_bit_identical(dev, B, C, cosine):
+    """NTXentLoss.forward_pair_normalized(z) -- F.normalize, the [zjs; zis]
+    row swap and the cosine scaling in one molclr_ntxent_prep_pair launch each
+    way -- equals forward_pair(l2_normalize(z)) bit for bit: loss and dz."""
+    from molclr_amd.nt_xent import NTXentLoss
+    torch.manual_seed(B + C)
+    z0 = torch.randn(2 * B, C, device=dev) * 3
+    z0[1] = 0.0  # a zero row: the F.normalize eps branch
+    crit = NTXentLoss(dev, B, 0.1, cosine)
+    za = z0.clone().requires_grad_(True)
+    zb = z0.clone().requires_grad_(True)
+    la = crit.forward_pair(ops.l2_normalize(za))
+    la.backward()
+    lb = crit.forward_pair_normalized(zb)
+    lb.backward()
+    assert torch.equal(la, lb)
+    assert torch.equal(za.grad, zb.grad)
