@@ -506,6 +506,19 @@ int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,
                            const float* xmax, float* dW, float* db, int64_t rows, int64_t n_out,
                            int64_t n_in, int64_t ld_dy, int64_t ld_x, int accumulate,
                            void* workspace, size_t workspace_bytes, molclr_stream_t stream);
+/* Two h3 weight gradients (a: dW_a = dy_a^T x_a, b likewise) over the same
+ * row count, their ordered split-K reductions in ONE launch: the same results
+ * as two molclr_linear_wgrad_h3 calls (rows >= 1024; sizes multiples of 4). */
+size_t molclr_linear_wgrad_h3_pair_workspace_bytes(int64_t rows, int64_t n_out_a, int64_t n_in_a,
+                                                   int64_t n_out_b, int64_t n_in_b);
+int molclr_linear_wgrad_h3_pair(const float* dy_a, const float* dymax_a, const float* x_a,
+                                const float* xmax_a, float* dW_a, float* db_a, int64_t n_out_a,
+                                int64_t n_in_a, int64_t ld_dy_a, int64_t ld_x_a,
+                                const float* dy_b, const float* dymax_b, const float* x_b,
+                                const float* xmax_b, float* dW_b, float* db_b, int64_t n_out_b,
+                                int64_t n_in_b, int64_t ld_dy_b, int64_t ld_x_b, int64_t rows,
+                                int accumulate, void* workspace, size_t workspace_bytes,
+                                molclr_stream_t stream);
 
 /* out[n] = Σ_m X[m*ld + n]  (bias gradients), deterministic. */
 size_t molclr_colsum_f32_workspace_bytes(int64_t rows, int64_t cols);

@@ -128,6 +128,10 @@ SIGNATURES = {
     "molclr_ntxent_bwd_impl": (c_int, [_P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, c_double, _P,
                                        _P, _P, c_size_t, _P, c_int]),
     "molclr_sum_f32": (c_int, [_P, _P, _I64, _P]),
+    "molclr_linear_wgrad_h3_pair_workspace_bytes": (c_size_t, [_I64, _I64, _I64, _I64, _I64]),
+    "molclr_linear_wgrad_h3_pair": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
+                                            _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64,
+                                            _I64, c_int, _P, c_size_t, _P]),
     "molclr_adam_step": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,
                                  c_double, _P]),
     "molclr_adam_step_ex": (c_int, [_P, _P, _P, _P, _I64, _P, _P, c_double, c_double, c_double,

@@ -301,9 +301,11 @@ struct TablePtrs {
   const float* e1[MOLCLR_MAX_LAYERS];
   const float* e2[MOLCLR_MAX_LAYERS];
 };
-__global__ void k_edge_tables_combine(TablePtrs p, float* __restrict__ Ec, int layers, int64_t D) {
+__global__ void k_edge_tables_combine(TablePtrs p, float* __restrict__ Ec, int layers, int64_t D,
+                                      float* __restrict__ zero, int64_t n_zero) {
   const int64_t per = (int64_t)MOLCLR_NUM_ECOMB * D;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n_zero) zero[t] = 0.f;  // a caller's slots, zeroed by the same launch
   if (t >= layers * per) return;
   const int l = (int)(t / per);
   const int64_t rc = t - l * per;
@@ -826,6 +828,12 @@ MOLCLR_API int molclr_atom_embed_bwd(const int64_t* x, const float* dh, float* d
 MOLCLR_API int molclr_edge_tables_combine(int layers, const float* const* E1s,
                                           const float* const* E2s, float* Ec, int64_t D,
                                           molclr_stream_t stream) {
+  return molclr::edge_tables_combine_zero(layers, E1s, E2s, Ec, D, nullptr, 0, stream);
+}
+
+int molclr::edge_tables_combine_zero(int layers, const float* const* E1s, const float* const* E2s,
+                                     float* Ec, int64_t D, float* zero, int64_t n_zero,
+                                     molclr_stream_t stream) {
   MOLCLR_REQUIRE(layers >= 0 && layers <= MOLCLR_MAX_LAYERS && D > 0,
                  "edge_tables_combine: %d layers (max %d), dim %lld", layers, MOLCLR_MAX_LAYERS,
                  (long long)D);
@@ -838,8 +846,9 @@ MOLCLR_API int molclr_edge_tables_combine(int layers, const float* const* E1s,
     p.e2[l] = E2s[l];
   }
   const int64_t n = (int64_t)layers * MOLCLR_NUM_ECOMB * D;
-  hipLaunchKernelGGL(k_edge_tables_combine, dim3(molclr::ceil_div(n, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), p, Ec, layers, D);
+  const int64_t work = n > n_zero ? n : n_zero;
+  hipLaunchKernelGGL(k_edge_tables_combine, dim3(molclr::ceil_div(work, kT)), dim3(kT), 0,
+                     molclr::as_stream(stream), p, Ec, layers, D, zero, n_zero);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

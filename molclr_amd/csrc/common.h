@@ -19,6 +19,12 @@ void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 
 inline hipStream_t as_stream(molclr_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// molclr_edge_tables_combine that also zeroes n_zero floats at `zero` in the
+// same launch (the encoder executor's h3 max slots)
+int edge_tables_combine_zero(int layers, const float* const* E1s, const float* const* E2s,
+                             float* Ec, int64_t D, float* zero, int64_t n_zero,
+                             molclr_stream_t stream);
+
 // Compute units of the current device (cached per device): the grid of a
 // persistent kernel.
 inline int cu_count() {

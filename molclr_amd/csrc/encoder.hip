@@ -23,7 +23,7 @@ struct ArenaLayout {
   size_t agg[MOLCLR_MAX_LAYERS], a1[MOLCLR_MAX_LAYERS], z[MOLCLR_MAX_LAYERS],
       h[MOLCLR_MAX_LAYERS], mean[MOLCLR_MAX_LAYERS], invstd[MOLCLR_MAX_LAYERS];
   size_t bits[MOLCLR_MAX_LAYERS];  // h3: ReLU mask of a1_l as bits [ceil(2D / 32)][N]
-  size_t h0, ec, smax, total;
+  size_t h0, ec, smax, bmax, total;
   ArenaLayout(int L, int64_t N, int64_t D, size_t es) {
     size_t used = 0;
     auto off = [&](size_t bytes) {
@@ -43,6 +43,8 @@ struct ArenaLayout {
     h0 = off(N * D * es);
     ec = off((size_t)L * MOLCLR_NUM_ECOMB * D * sizeof(float));
     smax = off((size_t)MOLCLR_MAX_LAYERS * 2 * kMaxSlotFloats * sizeof(float));  // h3: max |agg_l|, |a1_l|
+    // h3: the backward's max |dz_l|, |dz1_l| (zeroed by the forward with smax)
+    bmax = off((size_t)MOLCLR_MAX_LAYERS * 2 * kMaxSlotFloats * sizeof(float));
     total = used;
   }
 };
@@ -59,6 +61,7 @@ size_t kernels_ws(int64_t N, int64_t D) {
   mx(molclr_colsum_f32_workspace_bytes(N, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, D, 2 * D));
   mx(molclr_linear_wgrad_workspace_bytes(N, 2 * D, D));
+  if (N >= 1024 && D % 4 == 0) mx(molclr_linear_wgrad_h3_pair_workspace_bytes(N, D, 2 * D, 2 * D, D));
   mx(molclr_linear_wgrad_bf16_workspace_bytes(N, D, 2 * D));
   mx(molclr_linear_wgrad_bf16_workspace_bytes(N, 2 * D, D));
   mx(molclr_batchnorm_ws_bound(N, D));
@@ -220,11 +223,6 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
   const bool h3 = !bf && e->fp32_gemm != 0;
   const bool h3f = h3 && (e->fp32_gemm & 2);  // h3 forward products (not the default)
   float* fmax = F(lay.smax);  // h3: [l][0] = max |agg_l|, [l][1] = max |a1_l|
-  if (h3 && molclr::zero_async(fmax, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
-                hipSuccess) {
-    molclr::set_error("gin_encoder_fwd: zeroing the max slots failed");
-    return MOLCLR_ERR_ARG;
-  }
 
   void* h = A + lay.h0;
   if (bf)
@@ -234,7 +232,11 @@ MOLCLR_API int molclr_gin_encoder_fwd(const molclr_gin_encoder* e, const int64_t
     MOLCLR_TRY(molclr_atom_embed_fwd(x, e->x_embedding1, e->x_embedding2, (float*)h, N, D,
                                      e->n_atom, e->n_chiral, e->status, stream));
   float* Ec = F(lay.ec);
-  MOLCLR_TRY(molclr_edge_tables_combine(L, e->edge_embedding1, e->edge_embedding2, Ec, D, stream));
+  // h3: the forward's and the backward's max slots (smax, bmax: adjacent)
+  // zeroed by the same launch
+  const int64_t nz = h3 ? (int64_t)(lay.bmax - lay.smax) / 4 + (int64_t)L * 2 * kMaxSlotFloats : 0;
+  MOLCLR_TRY(molclr::edge_tables_combine_zero(L, e->edge_embedding1, e->edge_embedding2, Ec, D,
+                                              h3 ? fmax : nullptr, nz, stream));
   for (int l = 0; l < L; ++l) {
     const bool last = l == L - 1;
     void* y = last ? h_out : A + lay.h[l];
@@ -337,8 +339,11 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   void* dz = S + (size_t)N * D * es;         // w.r.t. the BatchNorm input z
   void* dagg = S + 2 * (size_t)N * D * es;   // w.r.t. the aggregation output
   void* dz1 = S + 3 * (size_t)N * D * es;    // w.r.t. the first Linear's pre-activation [N,2D]
-  float* bmax = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256));
-  float* rdz = bmax + kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
+  // h3: the arena's backward slots, zeroed by the forward (a second backward
+  // of the same forward folds the same maxima again: the same values)
+  float* bmax = const_cast<float*>(F(lay.bmax));
+  float* rdz = (float*)(S + molclr::align_up(scratch_bytes(N, D, es), 256)) +
+               kSlotBytes / sizeof(float);  // h3: row maxima of dz, then of dz1
   float* rdz1 = (float*)((char*)rdz + rowmax_first_bytes(N, D));  // after dz's row maxima
   void* kws = (char*)rdz + rowmax_bytes(N, D);
   const size_t kws_bytes = kernels_ws(N, D);
@@ -346,11 +351,6 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
   const bool h3 = !bf && e->fp32_gemm != 0;
   const float* fmax = F(lay.smax);  // the forward's max |agg_l|, max |a1_l|
   // h3: bmax[l][0] = max |dz_l|, [l][1] = max |dz1_l|
-  if (h3 && molclr::zero_async(bmax, (size_t)L * 2 * kMaxSlotFloats * sizeof(float), molclr::as_stream(stream)) !=
-                hipSuccess) {
-    molclr::set_error("gin_encoder_bwd: zeroing the max slots failed");
-    return MOLCLR_ERR_ARG;
-  }
 
   const void* dy = dh_out;
   for (int l = L - 1; l >= 0; --l) {
@@ -416,12 +416,19 @@ MOLCLR_API int molclr_gin_encoder_bwd(const molclr_gin_encoder* e,
                                     (float*)dz1, N, 2 * D, D, D, 2 * D, MOLCLR_EPI_RELU_MASK,
                                     nullptr, fa1, 2 * D, (const uint32_t*)(A + lay.bits[l]),
                                     sl + kMaxSlotFloats, rdz1, sl, stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
-                                        gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws, kws_bytes,
-                                        stream));
-      MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotFloats, fagg, fl,
-                                        gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D, 2 * D,
-                                        D, 1, kws, kws_bytes, stream));
+      if (N >= 1024) {  // both weight gradients, one reduction launch
+        MOLCLR_TRY(molclr_linear_wgrad_h3_pair(
+            fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l], gr->mlp2_bias[l], D, 2 * D, D,
+            2 * D, (const float*)dz1, sl + kMaxSlotFloats, fagg, fl, gr->mlp0_weight[l],
+            gr->mlp0_bias[l], 2 * D, D, 2 * D, D, N, 1, kws, kws_bytes, stream));
+      } else {
+        MOLCLR_TRY(molclr_linear_wgrad_h3(fz, sl, fa1, fl + kMaxSlotFloats, gr->mlp2_weight[l],
+                                          gr->mlp2_bias[l], N, D, 2 * D, D, 2 * D, 1, kws,
+                                          kws_bytes, stream));
+        MOLCLR_TRY(molclr_linear_wgrad_h3((const float*)dz1, sl + kMaxSlotFloats, fagg, fl,
+                                          gr->mlp0_weight[l], gr->mlp0_bias[l], N, 2 * D, D, 2 * D,
+                                          D, 1, kws, kws_bytes, stream));
+      }
       MOLCLR_TRY(molclr_gemm_f32_h3((const float*)dz1, rdz1, (int)molclr_gemm_row_parts(2 * D),
                                     e->mlp0_planes_t[l], (float*)dagg, N, D, 2 * D, 2 * D, D,
                                     MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr,

@@ -2070,6 +2070,52 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
   C[m * ldc + n] = v;
 }
 
+// Two weight gradients' ordered split-K reductions in ONE launch (the GIN
+// layer's dW2 and dW1: molclr_linear_wgrad_h3_pair).  Threads [0, M_a N_a)
+// reduce job a, the rest job b, each exactly as k_splitk_reduce<EPI_NONE>.
+struct ReduceJob {
+  const float* partial;
+  int splits;
+  int64_t M, N;
+  float* C;
+  int64_t ldc;
+  const float* cs_partial;
+  float* colsum;
+};
+__global__ void k_splitk_reduce_pair(ReduceJob ja, ReduceJob jb, int accumulate) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool second = t >= ja.M * ja.N;
+  const ReduceJob& j = second ? jb : ja;
+  if (second) t -= ja.M * ja.N;
+  auto ordered_sum = [](const float* __restrict__ p, int64_t stride, int splits) {
+    float v = 0.f;
+    int z = 0;
+    for (; z + 16 <= splits; z += 16) {
+      float buf[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) buf[q] = p[(int64_t)(z + q) * stride];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v += buf[q];
+    }
+    float buf[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) buf[q] = z + q < splits ? p[(int64_t)(z + q) * stride] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (z + q < splits) v += buf[q];
+    return v;
+  };
+  if (j.cs_partial && t < j.M) {
+    const float c = ordered_sum(j.cs_partial + t, j.M, j.splits);
+    j.colsum[t] = accumulate ? j.colsum[t] + c : c;
+  }
+  if (t >= j.M * j.N) return;
+  const int64_t m = t / j.N, n = t - m * j.N;
+  float v = ordered_sum(j.partial + t, j.M * j.N, j.splits);
+  if (accumulate) v += j.C[m * j.ldc + n];
+  j.C[m * j.ldc + n] = v;
+}
+
 // Implementations of molclr_gemm_f32 (per call, molclr_gemm_f32_impl):
 // 0 = f32-input MFMA, 64 x 64 tiles; 5 (automatic) / 6 = split-bf16 "p6",
 // 64 x 64 / 128 x 64.  The split-bf16 kernels stage K-major operands 4 rows
@@ -2962,6 +3008,72 @@ MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax
   MOLCLR_REQUIRE_WS(workspace_bytes, w6_ws_bytes(n_out, n_in, rows, db != nullptr));
   return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
                 workspace_bytes, s, groups, dymax, xmax);
+}
+
+namespace {
+// the w6 launch of run_w6 without its reduction: partials (and the bias
+// partials) into `part`; returns the plan
+W6Plan launch_w6_h3(const float* A, const float* B, float* part, bool colsum, int64_t M, int64_t N,
+                    int64_t K, int64_t lda, int64_t ldb, hipStream_t s, const float* amax,
+                    const float* bmax) {
+  const W6Plan p = w6_plan(M, N, K, 2);
+  float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
+  if (p.tn == 5) launch_w6<5, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  else if (p.tn == 4) launch_w6<4, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  else launch_w6<2, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+  return p;
+}
+size_t w6_part_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
+  const W6Plan p = w6_plan(M, N, K, 2);
+  return molclr::align_up((size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float), 256);
+}
+}  // namespace
+
+MOLCLR_API size_t molclr_linear_wgrad_h3_pair_workspace_bytes(int64_t rows, int64_t n_out_a,
+                                                              int64_t n_in_a, int64_t n_out_b,
+                                                              int64_t n_in_b) {
+  return w6_part_bytes(n_out_a, n_in_a, rows, true) + w6_part_bytes(n_out_b, n_in_b, rows, true) +
+         256;
+}
+
+MOLCLR_API int molclr_linear_wgrad_h3_pair(
+    const float* dy_a, const float* dymax_a, const float* x_a, const float* xmax_a, float* dW_a,
+    float* db_a, int64_t n_out_a, int64_t n_in_a, int64_t ld_dy_a, int64_t ld_x_a,
+    const float* dy_b, const float* dymax_b, const float* x_b, const float* xmax_b, float* dW_b,
+    float* db_b, int64_t n_out_b, int64_t n_in_b, int64_t ld_dy_b, int64_t ld_x_b, int64_t rows,
+    int accumulate, void* workspace, size_t workspace_bytes, molclr_stream_t stream) {
+  MOLCLR_REQUIRE(rows >= 1024, "linear_wgrad_h3_pair: rows %lld < 1024 (use linear_wgrad_h3)",
+                 (long long)rows);
+  MOLCLR_REQUIRE(dy_a && dymax_a && x_a && xmax_a && dW_a && dy_b && dymax_b && x_b && xmax_b &&
+                     dW_b,
+                 "linear_wgrad_h3_pair: null pointer");
+  for (int q = 0; q < 2; ++q) {
+    const int64_t no = q ? n_out_b : n_out_a, ni = q ? n_in_b : n_in_a;
+    const int64_t ld1 = q ? ld_dy_b : ld_dy_a, ld2 = q ? ld_x_b : ld_x_a;
+    MOLCLR_REQUIRE(no > 0 && ni > 0 && no % 4 == 0 && ni % 4 == 0 && ld1 % 4 == 0 &&
+                       ld2 % 4 == 0 && ld1 >= no && ld2 >= ni && no * ni < (1ll << 28),
+                   "linear_wgrad_h3_pair: job %d sizes must be multiples of 4", q);
+  }
+  MOLCLR_REQUIRE_WS(workspace_bytes, molclr_linear_wgrad_h3_pair_workspace_bytes(
+                                         rows, n_out_a, n_in_a, n_out_b, n_in_b));
+  hipStream_t s = molclr::as_stream(stream);
+  float* pa = static_cast<float*>(workspace);
+  float* pb = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                       w6_part_bytes(n_out_a, n_in_a, rows, true));
+  const W6Plan qa = launch_w6_h3(dy_a, x_a, pa, db_a != nullptr, n_out_a, n_in_a, rows, ld_dy_a,
+                                 ld_x_a, s, dymax_a, xmax_a);
+  const W6Plan qb = launch_w6_h3(dy_b, x_b, pb, db_b != nullptr, n_out_b, n_in_b, rows, ld_dy_b,
+                                 ld_x_b, s, dymax_b, xmax_b);
+  ReduceJob ja{pa, qa.splits, n_out_a, n_in_a, dW_a, n_in_a,
+               db_a ? pa + (size_t)qa.splits * n_out_a * n_in_a : nullptr, db_a};
+  ReduceJob jb{pb, qb.splits, n_out_b, n_in_b, dW_b, n_in_b,
+               db_b ? pb + (size_t)qb.splits * n_out_b * n_in_b : nullptr, db_b};
+  const int64_t total = n_out_a * n_in_a + n_out_b * n_in_b;
+  molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce_pair,
+                       dim3((unsigned)molclr::ceil_div(total, 256)), dim3(256), 0, s, ja, jb,
+                       accumulate);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
 }
 
 MOLCLR_API int molclr_linear_wgrad_h3(const float* dy, const float* dymax, const float* x,

@@ -76,11 +76,21 @@ __global__ void k_graph_init(int32_t* __restrict__ ecount, int32_t* __restrict__
   }
 }
 
+__device__ void graph_ptr_item(const GSegs& sg, int64_t t, int64_t N, int64_t G,
+                               int32_t* __restrict__ graph_ptr, int32_t* __restrict__ status);
+
+// blockIdx.y == 0: the edges (below); == 1: graph_ptr and the batch checks
+// (independent work, one launch)
 __global__ void k_graph_count(GSegs sg, int64_t E, int32_t* __restrict__ src32,
                               int32_t* __restrict__ dst32, uint8_t* __restrict__ code8,
                               int32_t* __restrict__ indeg, int32_t* __restrict__ outdeg,
-                              int32_t* __restrict__ ecount, int32_t* __restrict__ status) {
+                              int32_t* __restrict__ ecount, int32_t* __restrict__ status, int64_t N,
+                              int64_t G, int32_t* __restrict__ graph_ptr) {
   int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.y == 1) {
+    if (k < (N > G + 1 ? N : G + 1)) graph_ptr_item(sg, k, N, G, graph_ptr, status);
+    return;
+  }
   if (k >= E) return;
   const GLoc le = glocate(sg, 1, k);
   if (le.s < 0) return;  // past the real edges of a device-sized build
@@ -245,9 +255,8 @@ __global__ void k_graph_rows(int64_t N, const int32_t* __restrict__ src32,
   (csc ? nbr_t : nbr)[i] = make_uint4(slot[0], slot[1], slot[2], slot[3]);
 }
 
-__global__ void k_graph_ptr(GSegs sg, int64_t N, int64_t G, int32_t* __restrict__ graph_ptr,
-                            int32_t* __restrict__ status) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void graph_ptr_item(const GSegs& sg, int64_t t, int64_t N, int64_t G,
+                               int32_t* __restrict__ graph_ptr, int32_t* __restrict__ status) {
   if (t < N) {
     const GLoc ln = glocate(sg, 0, t);
     if (ln.s >= 0) {  // (padding rows of a device-sized build have no batch entry)
@@ -305,10 +314,10 @@ int build_launch(const GSegs& sg, int64_t N, int64_t E, int64_t G, int32_t* rowp
   if (n_init < 1) n_init = 1;
   hipLaunchKernelGGL(k_graph_init, dim3(molclr::ceil_div(n_init, T)), dim3(T), 0, s, ecount,
                      counters, 4 * N, N, status);
-  if (E > 0) {
-    hipLaunchKernelGGL(k_graph_count, dim3(molclr::ceil_div(E, T)), dim3(T), 0, s, sg, E, src32,
-                       dst32, code8, indeg, outdeg, ecount, status);
-  }
+  const int64_t n_ptr = N > G + 1 ? N : G + 1;
+  const int64_t bx = molclr::ceil_div(E > n_ptr ? E : n_ptr, T);
+  hipLaunchKernelGGL(k_graph_count, dim3((unsigned)bx, 2), dim3(T), 0, s, sg, E, src32, dst32,
+                     code8, indeg, outdeg, ecount, status, N, G, graph_ptr);
   hipLaunchKernelGGL(k_scan2, dim3(2), dim3(kScanThreads), 0, s, indeg, rowptr, outdeg, rowptr_t,
                      N);
   if (E > 0) {
@@ -320,9 +329,6 @@ int build_launch(const GSegs& sg, int64_t N, int64_t E, int64_t G, int32_t* rowp
                        dst32, code8, rowptr, rowptr_t, perm, perm_t, col, ecode, col_t,
                        (uint4*)nbr, (uint4*)nbr_t);
   }
-  int64_t n_ptr = N > G + 1 ? N : G + 1;
-  hipLaunchKernelGGL(k_graph_ptr, dim3(molclr::ceil_div(n_ptr, T)), dim3(T), 0, s, sg, N, G,
-                     graph_ptr, status);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

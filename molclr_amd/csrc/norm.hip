@@ -630,10 +630,20 @@ __global__ void k_pool_fwd(const typename St::T* __restrict__ h, const int32_t* 
   out[t] = acc;
 }
 
+// Rows outside every segment ([0, ptr[0]) and [ptr[G], N): the padding rows
+// of a captured step's capacity) get zero gradient from the same grid, no
+// separate memset of all N rows.
 template <typename St = StF32>
 __global__ void k_pool_bwd(const float4* __restrict__ dout, const int32_t* __restrict__ ptr,
-                           typename St::T* __restrict__ dh, int64_t G, int d4, int mode) {
+                           typename St::T* __restrict__ dh, int64_t G, int d4, int mode, int64_t N) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t lo = (int64_t)ptr[0] * d4, hi0 = (int64_t)ptr[G] * d4, n4 = N * d4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t q = t; q < lo; q += stride) St::st(dh, q, z);
+    for (int64_t q = hi0 + t; q < n4; q += stride) St::st(dh, q, z);
+  }
   if (t >= G * d4) return;
   int64_t g = t / d4;
   int c = (int)(t - g * d4);
@@ -1098,15 +1108,12 @@ MOLCLR_API int molclr_segment_pool_bwd(const float* dout, const int32_t* graph_p
     return MOLCLR_ERR_UNSUPPORTED;
   }
   hipStream_t s = molclr::as_stream(stream);
-  // nodes outside every segment get zero gradient
-  if (N > 0 && molclr::zero_async(dh, (size_t)N * D * sizeof(float), s) != hipSuccess) {
-    molclr::set_error("segment_pool_bwd: memset failed");
-    return MOLCLR_ERR_ARG;
-  }
-  if (G == 0) return MOLCLR_OK;
+  if (N == 0) return MOLCLR_OK;
   int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_pool_bwd<StF32>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
-                     (const float4*)dout, graph_ptr, dh, G, d4, mode);
+  // nodes outside every segment get zero gradient (inside the kernel)
+  const int64_t work = G * d4 > 0 ? G * d4 : 1;
+  hipLaunchKernelGGL(k_pool_bwd<StF32>, dim3(molclr::ceil_div(work, kT)), dim3(kT), 0, s,
+                     (const float4*)dout, graph_ptr, dh, G, d4, mode, N);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -1130,14 +1137,11 @@ MOLCLR_API int molclr_segment_pool_bwd_bf16(const float* dout, const int32_t* gr
   MOLCLR_REQUIRE(D > 0 && D % 4 == 0, "segment_pool_bwd_bf16: dim must be a multiple of 4");
   MOLCLR_REQUIRE(mode == 0 || mode == 1, "segment_pool_bwd_bf16: mode %d (0 mean, 1 add)", mode);
   hipStream_t s = molclr::as_stream(stream);
-  if (N > 0 && molclr::zero_async(dh, (size_t)N * D * sizeof(uint16_t), s) != hipSuccess) {
-    molclr::set_error("segment_pool_bwd_bf16: memset failed");
-    return MOLCLR_ERR_ARG;
-  }
-  if (G == 0) return MOLCLR_OK;
+  if (N == 0) return MOLCLR_OK;
   const int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_pool_bwd<StBF16>, dim3(molclr::ceil_div(G * d4, kT)), dim3(kT), 0, s,
-                     (const float4*)dout, graph_ptr, dh, G, d4, mode);
+  const int64_t work = G * d4 > 0 ? G * d4 : 1;  // rows outside every segment: zeroed inside
+  hipLaunchKernelGGL(k_pool_bwd<StBF16>, dim3(molclr::ceil_div(work, kT)), dim3(kT), 0, s,
+                     (const float4*)dout, graph_ptr, dh, G, d4, mode, N);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

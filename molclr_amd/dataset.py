@@ -132,7 +132,9 @@ def collate_views(views) -> Batch:
     sizes = np.array([v[0].shape[0] for v in views], dtype=np.int64)
     offs = np.concatenate([[0], np.cumsum(sizes)])
     x = np.concatenate([v[0] for v in views], 0)
-    ei = np.concatenate([v[1] + offs[g] for g, v in enumerate(views)], 1)
+    # C order, as PyG's collate yields it (a strided edge_index would cost
+    # every consumer a copy)
+    ei = np.ascontiguousarray(np.concatenate([v[1] + offs[g] for g, v in enumerate(views)], 1))
     ea = np.concatenate([v[2] for v in views], 0)
     batch = np.repeat(np.arange(len(views), dtype=np.int64), sizes)
     b = Batch(x=torch.from_numpy(x), edge_index=torch.from_numpy(ei),

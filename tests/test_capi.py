@@ -68,3 +68,15 @@ def test_product_path_has_no_cpu_fallback():
     for p in (ROOT / "molclr_amd").rglob("*.py"):
         assert "oracle" not in re.sub(r'""".*?"""', "", p.read_text(), flags=re.S).replace(
             "# oracle", ""), p
+
+
+def test_torch_ops_registered():
+    """import molclr_amd.torch_ops registers the operator seam
+    in the torch.ops.molclr namespace (no device needed to register)."""
+    import torch
+
+    import molclr_amd.torch_ops as tops
+    for name in tops.OPS:
+        assert hasattr(torch.ops.molclr, name), name
+    schema = str(torch.ops.molclr.gine_aggregate.default._schema)
+    assert schema.startswith("molclr::gine_aggregate(Tensor h, Tensor E1, Tensor E2")

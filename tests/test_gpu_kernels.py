@@ -1030,3 +1030,43 @@ def test_ntxent_pair_normalized_bit_identical(dev, B, C, cosine):
     lb.backward()
     assert torch.equal(la, lb)
     assert torch.equal(za.grad, zb.grad)
+
+
+@pytest.mark.parametrize("rows,D", [(30556, 300), (2048, 64)])
+def test_linear_wgrad_h3_pair_matches_two_calls(dev, rows, D):
+    """molclr_linear_wgrad_h3_pair (the GIN layer's dW2 = dz^T a1 and
+    dW1 = dz1^T agg, one reduction launch) equals two molclr_linear_wgrad_h3
+    calls bit for bit, weights and biases, accumulating into non-zero grads."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(rows)
+    dz, a1 = torch.randn(rows, D, generator=g) * 1e-3, torch.randn(rows, 2 * D, generator=g)
+    dz1, agg = torch.randn(rows, 2 * D, generator=g) * 1e-3, torch.randn(rows, D, generator=g)
+    dz, a1, dz1, agg = (t.to(dev) for t in (dz, a1, dz1, agg))
+    slots = torch.zeros(4, 2048, device=dev)
+    for t, sl in zip((dz, a1, dz1, agg), slots):
+        assert lib.molclr_absmax_f32(t.data_ptr(), t.shape[0], t.shape[1], t.shape[1],
+                                     sl.data_ptr(), 0, ops._stream(t)) == 0
+    init = [torch.randn(s, generator=g).to(dev) for s in ((D, 2 * D), (D,), (2 * D, D), (2 * D,))]
+    one = [t.clone() for t in init]
+    two = [t.clone() for t in init]
+    st = ops._stream(dz)
+    for (dy, sdy, x, sx, W, b) in ((dz, slots[0], a1, slots[1], one[0], one[1]),
+                                   (dz1, slots[2], agg, slots[3], one[2], one[3])):
+        wsb = lib.molclr_linear_wgrad_workspace_bytes(rows, dy.shape[1], x.shape[1])
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        assert lib.molclr_linear_wgrad_h3(dy.data_ptr(), sdy.data_ptr(), x.data_ptr(),
+                                          sx.data_ptr(), W.data_ptr(), b.data_ptr(), rows,
+                                          dy.shape[1], x.shape[1], dy.shape[1], x.shape[1], 1,
+                                          ws.data_ptr(), wsb, st) == 0
+    wsb = lib.molclr_linear_wgrad_h3_pair_workspace_bytes(rows, D, 2 * D, 2 * D, D)
+    ws = torch.full((wsb + 1024,), 0x5A, dtype=torch.uint8, device=dev)
+    assert lib.molclr_linear_wgrad_h3_pair(
+        dz.data_ptr(), slots[0].data_ptr(), a1.data_ptr(), slots[1].data_ptr(), two[0].data_ptr(),
+        two[1].data_ptr(), D, 2 * D, D, 2 * D, dz1.data_ptr(), slots[2].data_ptr(),
+        agg.data_ptr(), slots[3].data_ptr(), two[2].data_ptr(), two[3].data_ptr(), 2 * D, D,
+        2 * D, D, rows, 1, ws.data_ptr(), wsb, st) == 0, lib.molclr_last_error()
+    torch.cuda.synchronize()
+    assert bool((ws[wsb:] == 0x5A).all()), "wrote past the workspace"
+    for a, b in zip(one, two):
+        assert torch.equal(a, b)
