@@ -89,18 +89,33 @@ def _(edge_index, edge_attr, batch, num_nodes, num_graphs):
 # ---------------------------------------------------------------------------
 # GINE aggregation
 # ---------------------------------------------------------------------------
+def _check_graph(N, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount):
+    """Host-side shape / dtype checks of graph_build's tensors against N rows
+    (a mismatched tensor would send the kernels' index reads out of bounds)."""
+    i32 = torch.int32
+    E = col.shape[0]
+    want = ((rowptr, (N + 1,), i32), (rowptr_t, (N + 1,), i32), (col, (E,), i32),
+            (col_t, (E,), i32), (ecode, (E,), torch.uint8), (nbr, (4 * max(N, 1),), i32),
+            (nbr_t, (4 * max(N, 1),), i32), (ecount, (8 * max(N, 1),), i32))
+    for k, (t, shape, dt) in enumerate(want):
+        if tuple(t.shape) != shape or t.dtype != dt or not t.is_cuda:
+            raise ValueError(f"molclr graph tensor {k}: {tuple(t.shape)} {t.dtype}, expected "
+                             f"{shape} {dt} on the GPU (graph_build's outputs 0..7, in order)")
+
+
 @custom_op("molclr::gine_aggregate", mutates_args=(), device_types="cuda")
 def gine_aggregate(h: torch.Tensor, E1: torch.Tensor, E2: torch.Tensor, rowptr: torch.Tensor,
-                   col: torch.Tensor, ecode: torch.Tensor, nbr: torch.Tensor,
-                   rowptr_t: torch.Tensor, col_t: torch.Tensor, nbr_t: torch.Tensor,
+                   col: torch.Tensor, ecode: torch.Tensor, rowptr_t: torch.Tensor,
+                   col_t: torch.Tensor, nbr: torch.Tensor, nbr_t: torch.Tensor,
                    ecount: torch.Tensor) -> torch.Tensor:
     """agg_i = Σ_{in-edges k of i, self loop last} (h[src_k] + E1[bt_k] + E2[bd_k]) in PyG's
-    order (molclr_edge_tables_combine + molclr_gine_aggregate_fwd).  The source-CSC
-    tensors (rowptr_t, col_t, nbr_t, ecount) are the backward's: pass graph_build's
-    outputs 0..7 in order."""
+    order (molclr_edge_tables_combine + molclr_gine_aggregate_fwd).  The graph
+    tensors are graph_build's outputs 0..7 in its order (rowptr, col, ecode,
+    rowptr_t, col_t, nbr, nbr_t, ecount); the source-CSC half is the backward's."""
     _cuda(h, E1, E2)
     h = h.contiguous()
     N, D = h.shape
+    _check_graph(N, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount)
     Ec = ops.edge_tables_combine([E1], [E2])[0]
     out = torch.empty_like(h)
     _lib.call("molclr_gine_aggregate_fwd", h.data_ptr(), rowptr.data_ptr(), col.data_ptr(),
@@ -109,7 +124,7 @@ def gine_aggregate(h: torch.Tensor, E1: torch.Tensor, E2: torch.Tensor, rowptr: 
 
 
 @gine_aggregate.register_fake
-def _(h, E1, E2, rowptr, col, ecode, nbr, rowptr_t, col_t, nbr_t, ecount):
+def _(h, E1, E2, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount):
     return torch.empty_like(h)
 
 
@@ -121,6 +136,14 @@ def gine_aggregate_bwd(g: torch.Tensor, rowptr_t: torch.Tensor, col_t: torch.Ten
     transposed gather in index_select order, count-weighted table sums)."""
     g = g.contiguous()
     N, D = g.shape
+    i32 = torch.int32
+    for k, (t, shape) in enumerate(((rowptr_t, (N + 1,)), (nbr_t, (4 * max(N, 1),)),
+                                    (ecount, (8 * max(N, 1),)))):
+        if tuple(t.shape) != shape or t.dtype != i32:
+            raise ValueError(f"gine_aggregate_bwd: graph tensor {k} {tuple(t.shape)} {t.dtype}, "
+                             f"expected {shape} int32")
+    if col_t.dtype != i32 or col_t.dim() != 1:
+        raise ValueError("gine_aggregate_bwd: col_t must be int32 [E]")
     dh = torch.empty_like(g)
     dE1 = torch.zeros(n_e1, D, dtype=torch.float32, device=g.device)
     dE2 = torch.zeros(n_e2, D, dtype=torch.float32, device=g.device)
@@ -272,7 +295,7 @@ def _(grad, zis, zjs, batch_size, temperature, use_cosine_similarity):
 # autograd
 # ---------------------------------------------------------------------------
 def _agg_setup(ctx, inputs, output):
-    h, E1, E2, rowptr, col, ecode, nbr, rowptr_t, col_t, nbr_t, ecount = inputs
+    h, E1, E2, rowptr, col, ecode, rowptr_t, col_t, nbr, nbr_t, ecount = inputs
     ctx.save_for_backward(rowptr_t, col_t, nbr_t, ecount)
     ctx.n = (E1.shape[0], E2.shape[0])
 
