@@ -401,6 +401,37 @@ constexpr int kMaxSlotFloats = kMaxSlotParts * kMaxSlotStride;
 // global atomic max on the float's bits (ordered like the values for v >= 0)
 // into entry blockIdx.x % 64.  Every thread of the block must call it (a
 // block barrier inside).
+// max |x| over float4 elements t, t + stride, ... < n4 with eight independent
+// loads in flight per lane (a dependent one-load loop over a few blocks is
+// latency-bound: 8 MB took 48 us)
+__device__ __forceinline__ float absmax4_range(const float4* __restrict__ x, int64_t t, int64_t n4,
+                                               int64_t stride) {
+  auto amax4 = [](float4 v) {
+    return fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+  };
+  float m = 0.f;
+  for (; t + 7 * stride < n4; t += 8 * stride) {
+    float4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[t + j * stride];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, amax4(v[j]));
+  }
+  for (; t < n4; t += stride) m = fmaxf(m, amax4(x[t]));
+  return m;
+}
+
+// block max of v (blockDim a multiple of 64, <= 1024), valid in thread 0
+__device__ __forceinline__ float block_max(float v) {
+  __shared__ float red_b[16];
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red_b[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = fmaxf(v, red_b[w]);
+  return v;
+}
+
 __device__ __forceinline__ void absmax_publish(float v, float* slot) {
   __shared__ float red_[16];
   v = wave_max(v);

@@ -1910,7 +1910,7 @@ __global__ void k_bplanes_make_batch(PlanesJobs jobs) {
 // gives each job one block per slot entry, each storing its partial (plain
 // stores: no zeroing, no atomics).
 constexpr int kHMaxParts = kMaxSlotParts;
-__global__ __launch_bounds__(256) void k_hplanes_max_batch(PlanesJobs jobs) {
+__global__ __launch_bounds__(1024) void k_hplanes_max_batch(PlanesJobs jobs) {
   const PlanesJob& jb = jobs.j[blockIdx.y];
   // B stored [rows][cols]: rows = N (kmajor 0) or K (kmajor 1)
   const int64_t rows = jb.kmajor ? jb.K : jb.N, cols = jb.kmajor ? jb.N : jb.K;
@@ -1918,25 +1918,17 @@ __global__ __launch_bounds__(256) void k_hplanes_max_batch(PlanesJobs jobs) {
   if (jb.ldb == cols && cols % 4 == 0 && (reinterpret_cast<uintptr_t>(jb.B) & 15) == 0) {
     // dense: one flat float4 range (a large image -- e.g. NT-Xent's gathered
     // columns, 8192 x 256 -- is not 64 blocks of row-serial loops)
-    const int64_t n4 = rows * cols / 4;
-    const float4* b4 = reinterpret_cast<const float4*>(jb.B);
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
-         t += (int64_t)gridDim.x * blockDim.x) {
-      const float4 v = b4[t];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
+    m = absmax4_range(reinterpret_cast<const float4*>(jb.B),
+                      (int64_t)blockIdx.x * blockDim.x + threadIdx.x, rows * cols / 4,
+                      (int64_t)gridDim.x * blockDim.x);
   } else {
     for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
       for (int64_t c = threadIdx.x; c < cols; c += blockDim.x)
         m = fmaxf(m, fabsf(jb.B[r * jb.ldb + c]));
   }
-  __shared__ float red[4];
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
+  m = block_max(m);
   if (threadIdx.x == 0)
-    reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x * kMaxSlotStride] =
-        fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x * kMaxSlotStride] = m;
 }
 // one thread per (n, 8 k) of the padded grid: two 16-byte plane stores
 __global__ __launch_bounds__(256) void k_hplanes_make_batch(PlanesJobs jobs) {
@@ -1971,12 +1963,8 @@ __global__ __launch_bounds__(256) void k_absmax(const float* __restrict__ x, int
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-      const float4* x4 = reinterpret_cast<const float4*>(x);
       const int64_t n4 = n >> 2;
-      for (; t < n4; t += stride) {
-        const float4 v = x4[t];
-        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-      }
+      m = absmax4_range(reinterpret_cast<const float4*>(x), t, n4, stride);
       for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         m = fmaxf(m, fabsf(x[i]));
     } else {
@@ -2921,7 +2909,7 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
       most = e > most ? e : most;
     }
     hipStream_t s = molclr::as_stream(stream);
-    hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)n), dim3(256), 0, s, jobs);
+    hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)n), dim3(1024), 0, s, jobs);
     hipLaunchKernelGGL(k_hplanes_make_batch, dim3((unsigned)molclr::ceil_div(most / 8, 256), (unsigned)n),
                        dim3(256), 0, s, jobs);
   }

@@ -305,12 +305,14 @@ __global__ __launch_bounds__(256) void k_ntxent_row_lse(const float* __restrict_
     }
   };
   int64_t c0 = 4 * lane;  // ncols % 4 == 0 (host)
-  for (; c0 + 768 < ncols; c0 += 1024) {  // four loads in flight
-    float4 v[4];
+  // eight loads in flight: one wave per row leaves few waves per CU, so the
+  // row loop is latency-bound with fewer (c4's 1024 x 8192: 12.7 us at four)
+  for (; c0 + 1792 < ncols; c0 += 2048) {
+    float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(row + c0 + 256 * u);
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(row + c0 + 256 * u);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) take(v[u], c0 + 256 * u);
+    for (int u = 0; u < 8; ++u) take(v[u], c0 + 256 * u);
   }
   for (; c0 < ncols; c0 += 256) take(*reinterpret_cast<const float4*>(row + c0), c0);
 #pragma unroll
@@ -373,21 +375,14 @@ __global__ __launch_bounds__(256) void k_ntxent_weights(const float* S, float* W
 // max |x| of a dense [rows][cols] matrix into a max slot with plain stores
 // (block b writes entry b of kMaxSlotParts: no zeroing, no atomics); block 0
 // also zeroes `zero_slot` (the atomic slot the next kernel folds into)
-__global__ __launch_bounds__(256) void k_ntxent_absmax_plain(const float* __restrict__ x,
-                                                             int64_t n4, float* __restrict__ slot,
-                                                             float* __restrict__ zero_slot) {
-  float m = 0.f;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const float4 v = reinterpret_cast<const float4*>(x)[t];
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-  __shared__ float red[4];
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    slot[blockIdx.x * kMaxSlotStride] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+__global__ __launch_bounds__(1024) void k_ntxent_absmax_plain(const float* __restrict__ x,
+                                                              int64_t n4, float* __restrict__ slot,
+                                                              float* __restrict__ zero_slot) {
+  float m = absmax4_range(reinterpret_cast<const float4*>(x),
+                          (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n4,
+                          (int64_t)gridDim.x * blockDim.x);
+  m = block_max(m);
+  if (threadIdx.x == 0) slot[blockIdx.x * kMaxSlotStride] = m;
   if (zero_slot != nullptr && blockIdx.x == 0)
     for (int i = threadIdx.x; i < kMaxSlotFloats; i += blockDim.x) zero_slot[i] = 0.f;
 }
@@ -406,35 +401,46 @@ __global__ __launch_bounds__(256) void k_ntxent_weights_tt(
   const int64_t r0 = (int64_t)blockIdx.y * kWT, c0 = (int64_t)blockIdx.x * kWT;
   const float coef = (*grad_loss) * inv_t / (float)(2 * B);
   float mx = 0.f;
-  // read: 64 rows x 16 float4 = 1024 float4, 4 per thread (16 threads per row)
+  // read: 64 rows x 16 float4 = 1024 float4, 4 per thread (16 threads per
+  // row; a thread's column run cc is the same for its four rows).  All loads
+  // are issued before any use (clamped indices, masked after): the chain
+  // gidx -> lse_cols[rg] and the four S loads overlap instead of serialising.
+  const int cc = 4 * (tid & 15), rr0 = tid >> 4;
+  const int64_t c = c0 + cc;
+  const bool cv = c < ncols;  // ncols % 4 == 0 (host)
+  const int64_t cl = cv ? c : 0;
+  const float4 lc = *reinterpret_cast<const float4*>(lse_cols + cl);
+  float4 v[4];
+  int64_t rg[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int idx = tid + 256 * q;
-    const int rr = idx >> 4, cc = 4 * (idx & 15);
-    const int64_t r = r0 + rr, c = c0 + cc;
-    float e[4] = {0.f, 0.f, 0.f, 0.f};
-    if (r < nrows && c < ncols) {  // ncols % 4 == 0 (host)
-      const float4 v = *reinterpret_cast<const float4*>(S + r * ncols + c);
-      const int64_t rg = gidx[r];
-      const int64_t pg = rg + B < 2 * B ? rg + B : rg - B;
-      const float lr = lse_cols[rg];
-      const float4 lc = *reinterpret_cast<const float4*>(lse_cols + c);
-      const float sv[4] = {v.x, v.y, v.z, v.w}, lcv[4] = {lc.x, lc.y, lc.z, lc.w};
+    const int64_t r = r0 + rr0 + 16 * q;
+    const int64_t rl = r < nrows ? r : nrows - 1;
+    v[q] = *reinterpret_cast<const float4*>(S + rl * ncols + cl);
+    rg[q] = gidx[rl];
+  }
+  float lr[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float w = 0.f;
-        if (c + j != rg) {
-          const float lg = sv[j] * inv_t;
-          w = expf(lg - lr) + expf(lg - lcv[j]);
-          if (c + j == pg) w -= 2.f;
-          w *= coef;
-        }
-        e[j] = w;
-        mx = fmaxf(mx, fabsf(w));
+  for (int q = 0; q < 4; ++q) lr[q] = lse_cols[rg[q]];
+  const float lcv[4] = {lc.x, lc.y, lc.z, lc.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int rr = rr0 + 16 * q;
+    const bool ok = cv && r0 + rr < nrows;
+    const int64_t pg = rg[q] + B < 2 * B ? rg[q] + B : rg[q] - B;
+    const float sv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float w = 0.f;
+      if (ok && c + j != rg[q]) {
+        const float lg = sv[j] * inv_t;
+        w = expf(lg - lr[q]) + expf(lg - lcv[j]);
+        if (c + j == pg) w -= 2.f;
+        w *= coef;
       }
+      mx = fmaxf(mx, fabsf(w));
+      tile[cc + j][rr] = w;
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) tile[cc + j][rr] = e[j];
   }
   __syncthreads();
   // write: 64 W^T rows (c) x 16 float4 along r
@@ -694,7 +700,7 @@ int ntx_similarity(const float* rows, const float* cols, int64_t nrows, int64_t 
 int ntx_similarity_h3(const float* rows, const float* cols, int64_t nrows, int64_t ncols, int64_t C,
                       float* S, uint16_t* planes, float* rmax, hipStream_t s) {
   molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
-  hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(256), 0, s, rows,
+  hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(1024), 0, s, rows,
                      nrows * C / 4, rmax, nullptr);
   const float* bl[1] = {cols};
   const int64_t nn[1] = {ncols}, kk[1] = {C}, ld[1] = {C};
@@ -839,7 +845,7 @@ MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, co
     {
       molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
       // the columns' max slot and W's zeroed slot in one launch
-      hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(256), 0, s, cols,
+      hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(1024), 0, s, cols,
                          ncols * C / 4, cmax, wmax);
       molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_weights_tt,
                            dim3((unsigned)molclr::ceil_div(ncols, kWT),

@@ -124,6 +124,8 @@ def global_row_index(b_local: int, rank: int, world: int, device) -> torch.Tenso
 def allreduce_grads(flat_grad: torch.Tensor, group=None) -> None:
     """SUM the flat gradient buffer over ranks (the loss already carries the
     global 1/2B normalisation, so the sum is the exact global gradient)."""
+    from . import ops
+    ops.join_side()  # side-stream weight gradients land in flat_grad
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
 
@@ -226,6 +228,7 @@ class OverlappedGradReducer:
     def finish(self):
         from . import ops
         ops.set_grad_hook(None)
+        ops.join_side()
         if self.calls == 0:  # no executor backward ran (per-op path): one collective
             allreduce_grads(self.flat, self.group)
             return

@@ -187,9 +187,9 @@ class GINet(nn.Module):
         W = self.feat_lin.weight
         if h.shape[1] != W.shape[1]:  # padded width: zero weight columns for the pads
             W = F.pad(W, (0, h.shape[1] - W.shape[1]))
-        h = ops.linear(h, W, self.feat_lin.bias)
+        h = ops.linear(h, W, self.feat_lin.bias, side=True)
         out = ops.projection_head(h, self.out_lin[0].weight, self.out_lin[0].bias,
-                                  self.out_lin[2].weight, self.out_lin[2].bias)
+                                  self.out_lin[2].weight, self.out_lin[2].bias, side=True)
         return h, out
 
     def forward(self, data):

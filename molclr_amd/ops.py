@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import torch
 
+import contextlib
 import ctypes
 import os
 import functools
@@ -61,6 +62,9 @@ def _check(*ts):
             continue
         if t.device.type != "cuda":
             raise RuntimeError("molclr_amd kernels run on the GPU only; got a %s tensor" % t.device)
+
+
+_NULL_CTX = contextlib.nullcontext()
 
 
 def _ws(nbytes: int, device) -> torch.Tensor:
@@ -145,8 +149,35 @@ def set_grad_hook(hook) -> None:
     _GRAD_HOOK = hook
 
 
+# Weight gradients of the readout heads on a second stream.  The heads'
+# products (feat_lin, out_lin: 2B rows, ginet_molclr.py:90-96,114-115) are
+# small GEMMs that leave most CUs idle, so with ``side=True`` (the models'
+# _readout) a FusedAdam-owned weight's dW / db run on a side stream beside the
+# data-gradient chain.  join_side() makes the current stream wait for them; the
+# encoder backward (before the reducer's heads bucket), FusedAdam.step and the
+# reducer's finish() call it.  MOLCLR_SIDE_WGRAD=0 keeps them on one stream.
+SIDE_WGRAD = os.environ.get("MOLCLR_SIDE_WGRAD", "1") != "0"
+_SIDE_STREAMS = {}
+_SIDE_PENDING = []
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
+    return s
+
+
+def join_side() -> None:
+    """The current stream waits for every pending side-stream weight gradient."""
+    while _SIDE_PENDING:
+        dev, ev = _SIDE_PENDING.pop()
+        torch.cuda.current_stream(dev).wait_event(ev)
+
+
 def _grad_events(grads_struct, L, owned):
     """Start the hook's heads bucket and fill the executor's done-events."""
+    join_side()  # the heads' gradients are final before their bucket starts
     hook = _GRAD_HOOK
     if hook is None or not owned:
         return None
@@ -425,9 +456,10 @@ def colsum(x, out=None, accumulate=0):
 
 
 def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=None,
-               W_param=None, b_param=None):
+               W_param=None, b_param=None, side=False):
     """Backward of y = x W^T + b.  Returns (dx, dW, db); dW / db are None when
-    they were accumulated straight into a FusedAdam-owned .grad."""
+    they were accumulated straight into a FusedAdam-owned .grad (``side``: on
+    the side stream then, see join_side)."""
     M, K = x.shape
     N = W.shape[0]
     dx = dW = db = None
@@ -438,11 +470,22 @@ def linear_bwd(dy, x, W, need_x=True, need_w=True, need_b=True, relu_mask_src=No
         if wacc != bacc:  # mixed ownership: fresh buffers for both
             wbuf, wacc, dW = _grad_sink(None, (N, K), dy.device)
             bbuf, bacc, db = _grad_sink(None, (N,), dy.device)
-        ws_bytes = _wsq("molclr_linear_wgrad_workspace_bytes", M, N, K)
-        ws = _ws(ws_bytes, dy.device)
-        _lib.call("molclr_linear_wgrad", dy.data_ptr(), x.data_ptr(), wbuf.data_ptr(),
-                  bbuf.data_ptr(), M, N, K, dy.stride(0), x.stride(0), wacc, ws.data_ptr(),
-                  ws_bytes, _stream(dy))
+        side = side and SIDE_WGRAD and wacc == 1 and _TIMER is None
+        ss = _side_stream(dy.device) if side else None
+        if side:
+            ss.wait_stream(torch.cuda.current_stream(dy.device))
+        with torch.cuda.stream(ss) if side else _NULL_CTX:
+            ws_bytes = _wsq("molclr_linear_wgrad_workspace_bytes", M, N, K)
+            ws = _ws(ws_bytes, dy.device)  # allocated on (and freed to) the side stream
+            _lib.call("molclr_linear_wgrad", dy.data_ptr(), x.data_ptr(), wbuf.data_ptr(),
+                      bbuf.data_ptr(), M, N, K, dy.stride(0), x.stride(0), wacc, ws.data_ptr(),
+                      ws_bytes, _stream(dy))
+        if side:
+            dy.record_stream(ss)
+            x.record_stream(ss)
+            ev = torch.cuda.Event()
+            ev.record(ss)
+            _SIDE_PENDING.append((dy.device, ev))
         if _TIMER is not None:
             _TIMER.add("gemm_f32", 2.0 * M * N * K)
     elif need_w:
@@ -581,9 +624,10 @@ class _MLP(torch.autograd.Function):
     epilogue (forward) and into the dZ1 GEMM's epilogue (backward)."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2):
+    def forward(ctx, x, W1, b1, W2, b2, side=False):
         _check(x, W1, b1, W2, b2)
         x = _c(x)
+        ctx.side = side
         M, D = x.shape
         ctx.h3 = h3_ok(M, D) and W1.shape == (2 * D, D) and W2.shape == (D, 2 * D)
         if ctx.h3:
@@ -646,22 +690,23 @@ class _MLP(torch.autograd.Function):
             dW2, db2 = linear_wgrad_h3(dz, bslots[0], a1, slots[1], pW2, pb2)
             dW1, db1 = linear_wgrad_h3(dz1, bslots[1], x, slots[0], pW1, pb1)
             dx = (gemm_h3(dz1, rdz1, W1, D, 2 * D, D, 1, rowwise=P) if need[0] else None)
-            return dx, dW1, db1, dW2, db2
+            return dx, dW1, db1, dW2, db2, None
         # through the second Linear; ReLU mask of a1 fused into dz1's epilogue
         dz1, dW2, db2 = linear_bwd(dz, a1, W2, need_x=True, need_w=need[3], need_b=need[4],
-                                   relu_mask_src=a1, W_param=pW2, b_param=pb2)
+                                   relu_mask_src=a1, W_param=pW2, b_param=pb2, side=ctx.side)
         dx, dW1, db1 = linear_bwd(dz1, x, W1, need_x=need[0], need_w=need[1], need_b=need[2],
-                                  W_param=pW1, b_param=pb1)
-        return dx, dW1, db1, dW2, db2
+                                  W_param=pW1, b_param=pb1, side=ctx.side)
+        return dx, dW1, db1, dW2, db2, None
 
 
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, W, b):
+    def forward(ctx, x, W, b, side=False):
         _check(x, W, b)
         x = _c(x)
         ctx.save_for_backward(x, W)
         ctx.params = (W, b)
+        ctx.side = side
         return linear_fwd(x, W, b)
 
     @staticmethod
@@ -669,8 +714,8 @@ class _Linear(torch.autograd.Function):
         x, W = ctx.saved_tensors
         need = ctx.needs_input_grad
         dx, dW, db = linear_bwd(_c(dy), x, W, need[0], need[1], need[2],
-                                W_param=ctx.params[0], b_param=ctx.params[1])
-        return dx, dW, db
+                                W_param=ctx.params[0], b_param=ctx.params[1], side=ctx.side)
+        return dx, dW, db, None
 
 
 class _BatchNorm(torch.autograd.Function):
@@ -1289,15 +1334,17 @@ def gine_aggregate(h, E1, E2, graph, Ec=None):
     return _GINEAggregate.apply(h, E1, E2, graph, Ec)
 
 
-def gin_mlp(x, W1, b1, W2, b2):
-    return _MLP.apply(x, W1, b1, W2, b2)
+def gin_mlp(x, W1, b1, W2, b2, side=False):
+    return _MLP.apply(x, W1, b1, W2, b2, side)
 
 
-projection_head = gin_mlp
+def projection_head(x, W1, b1, W2, b2, side=False):
+    """out_lin; ``side``: weight gradients on the side stream (join_side)."""
+    return _MLP.apply(x, W1, b1, W2, b2, side)
 
 
-def linear(x, W, b):
-    return _Linear.apply(x, W, b)
+def linear(x, W, b, side=False):
+    return _Linear.apply(x, W, b, side)
 
 
 def batch_norm(z, bn: torch.nn.BatchNorm1d, relu: bool):

@@ -88,6 +88,7 @@ class FusedAdam(torch.optim.Optimizer):
         ``tick=False``: the caller advances the device step counter itself
         (molclr_step_tail, the captured step's closing launch)."""
         loss = closure() if closure is not None else None
+        ops.join_side()  # side-stream weight gradients (ops.linear_bwd) are final
         g = self.param_groups[0]
         if sync_lr:
             self.sync_lr()

@@ -371,6 +371,29 @@ def test_no_uninitialised_reads(dev, kind, captured):
             assert torch.equal(m, m0) and torch.equal(s, s0), v
 
 
+@pytest.mark.parametrize("captured", [False, True], ids=["eager", "captured"])
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_side_stream_head_gradients_bit_identical(dev, kind, captured, monkeypatch):
+    """The readout heads' weight gradients run on a side stream
+    (ops.linear_bwd side=True, joined by the encoder backward and Adam): the
+    same kernels in the same per-stream order, so losses, gradients, parameters
+    and running statistics equal the one-stream step's bit for bit, eager and
+    as a captured graph (fork / join inside the capture)."""
+    from molclr_amd import ops
+    batches = [_to(p, dev) for p in SyntheticPairBatches(32, seed=43).take(3)]
+    order = batches + [batches[0]]
+    monkeypatch.setattr(ops, "SIDE_WGRAD", False)
+    one = _poisoned_run(dev, kind, 0.0, order, captured)
+    monkeypatch.setattr(ops, "SIDE_WGRAD", True)
+    two = _poisoned_run(dev, kind, 0.0, order, captured)
+    assert not ops._SIDE_PENDING
+    assert torch.equal(one[0], two[0]), (one[0], two[0])
+    assert torch.equal(one[1], two[1]), rel(one[1], two[1])
+    assert torch.equal(one[2], two[2])
+    for (m, s), (m0, s0) in zip(one[3], two[3]):
+        assert torch.equal(m, m0) and torch.equal(s, s0)
+
+
 def test_captured_zeroing_takes_effect(dev):
     """The library zeroes buffers (h3 max slots, pooled-gradient rows, edge
     histograms) with kernels (common.h zero_async), not hipMemsetAsync: a
