@@ -50,35 +50,62 @@ namespace {
 // with bc1 = 1 - b1^t, bc2 = 1 - b2^t, step_size and sqrt(bc2) evaluated in
 // double (torch does them in Python floats on the host) and rounded to fp32
 // once, as torch's scalar arguments are.  The step count t lives on the device.
-__global__ void k_adam_step(float4* __restrict__ p, const float4* __restrict__ g,
-                            float4* __restrict__ m, float4* __restrict__ v, int64_t n4,
-                            const float* __restrict__ lr_ptr, const int32_t* __restrict__ step_ptr,
-                            double b1, double b2, float eps, float wd) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n4) return;
-  const int step = *step_ptr + 1;  // the counter is advanced by k_adam_tick afterwards
-  const double bc1 = 1.0 - pow(b1, (double)step);
-  const double bc2 = 1.0 - pow(b2, (double)step);
-  const float neg_step_size = (float)(-((double)*lr_ptr / bc1));
-  const float bc2s = (float)sqrt(bc2);
+// A block of 256 threads takes kAdamPer x 256 float4 (a thread's float4s
+// 256 apart: coalesced), all loads issued before the math; thread 0 evaluates
+// the step's scalars (two double pow) once for the block and shares them
+// through LDS -- per thread, the fp64 pows cost the kernel ~3 us at c2.
+constexpr int kAdamPer = 4;
+__global__ __launch_bounds__(256) void k_adam_step(float4* __restrict__ p,
+                                                   const float4* __restrict__ g,
+                                                   float4* __restrict__ m, float4* __restrict__ v,
+                                                   int64_t n4, const float* __restrict__ lr_ptr,
+                                                   const int32_t* __restrict__ step_ptr, double b1,
+                                                   double b2, float eps, float wd) {
+  __shared__ float sc[2];
+  const int64_t base = (int64_t)blockIdx.x * (256 * kAdamPer) + threadIdx.x;
+  float4 pp[kAdamPer], gg[kAdamPer], mm[kAdamPer], vv[kAdamPer];
+#pragma unroll
+  for (int j = 0; j < kAdamPer; ++j) {
+    const int64_t t = base + 256 * j;
+    if (t < n4) {
+      pp[j] = p[t];
+      gg[j] = g[t];
+      mm[j] = m[t];
+      vv[j] = v[t];
+    }
+  }
+  if (threadIdx.x == 0) {
+    const int step = *step_ptr + 1;  // the counter is advanced by k_adam_tick afterwards
+    const double bc1 = 1.0 - pow(b1, (double)step);
+    const double bc2 = 1.0 - pow(b2, (double)step);
+    sc[0] = (float)(-((double)*lr_ptr / bc1));
+    sc[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float neg_step_size = sc[0], bc2s = sc[1];
   const float w1 = (float)(1.0 - b1), fb2 = (float)b2, w2 = (float)(1.0 - b2);
-  float4 pp = p[t], gg = g[t], mm = m[t], vv = v[t];
+#pragma unroll
+  for (int j = 0; j < kAdamPer; ++j) {
+    const int64_t t = base + 256 * j;
+    if (t >= n4) continue;
+    float4 P = pp[j], G = gg[j], M = mm[j], V = vv[j];
 #define MOLCLR_ADAM_LANE(c)                                                   \
   {                                                                           \
-    const float gr = gg.c + wd * pp.c;                                        \
-    mm.c = fabsf(w1) < 0.5f ? mm.c + w1 * (gr - mm.c) : gr - (gr - mm.c) * (1.f - w1); \
-    vv.c = vv.c * fb2 + w2 * gr * gr;                                         \
-    const float den = sqrtf(vv.c) / bc2s + eps;                               \
-    pp.c = pp.c + neg_step_size * (mm.c / den);                               \
+    const float gr = G.c + wd * P.c;                                          \
+    M.c = fabsf(w1) < 0.5f ? M.c + w1 * (gr - M.c) : gr - (gr - M.c) * (1.f - w1); \
+    V.c = V.c * fb2 + w2 * gr * gr;                                           \
+    const float den = sqrtf(V.c) / bc2s + eps;                                \
+    P.c = P.c + neg_step_size * (M.c / den);                                  \
   }
-  MOLCLR_ADAM_LANE(x)
-  MOLCLR_ADAM_LANE(y)
-  MOLCLR_ADAM_LANE(z)
-  MOLCLR_ADAM_LANE(w)
+    MOLCLR_ADAM_LANE(x)
+    MOLCLR_ADAM_LANE(y)
+    MOLCLR_ADAM_LANE(z)
+    MOLCLR_ADAM_LANE(w)
 #undef MOLCLR_ADAM_LANE
-  p[t] = pp;
-  m[t] = mm;
-  v[t] = vv;
+    p[t] = P;
+    m[t] = M;
+    v[t] = V;
+  }
 }
 
 __global__ void k_adam_tick(int32_t* step) { *step += 1; }
@@ -126,7 +153,7 @@ MOLCLR_API int molclr_adam_step_ex(float* param, const float* grad, float* exp_a
   hipStream_t s = molclr::as_stream(stream);
   int64_t n4 = n / 4;
   if (n4 > 0)
-    hipLaunchKernelGGL(k_adam_step, dim3(molclr::ceil_div(n4, 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_adam_step, dim3(molclr::ceil_div(n4, 256 * kAdamPer)), dim3(256), 0, s,
                        (float4*)param, (const float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq,
                        n4, lr, step, beta1, beta2, (float)eps, (float)weight_decay);
   if (tick) hipLaunchKernelGGL(k_adam_tick, dim3(1), dim3(1), 0, s, step);

@@ -83,9 +83,16 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 // Scale exponent for values of max |x| = m: 0 for a zero / NaN / infinite m
 // (NaN and inf then propagate as in fp32).
+// Capped at 127 (m < 2^-112: such a tensor / row keeps fewer lo bits) so that
+// 2^sh is an fp32 normal and the split scales by a multiply (h3_scale).
 __device__ __forceinline__ int h3_shift_of(float m) {
   if (!(m > 0.f) || !(m <= 3.402823466e38f)) return 0;
-  return 15 - __builtin_amdgcn_frexp_expf(m);  // m = f 2^e, f in [0.5, 1)
+  const int sh = 15 - __builtin_amdgcn_frexp_expf(m);  // m = f 2^e, f in [0.5, 1)
+  return sh < 127 ? sh : 127;
+}
+// 2^sh for sh in [-126, 127] (h3_shift_of's range: e <= 128 gives sh >= -113)
+__device__ __forceinline__ float h3_scale(int sh) {
+  return __builtin_bit_cast(float, (uint32_t)(sh + 127) << 23);
 }
 // ... of a tensor from its max slot (kMaxSlotParts entries, molclr_absmax_f32).
 // Every lane of the wave must call it.
@@ -93,13 +100,32 @@ __device__ __forceinline__ int h3_shift(const float* __restrict__ slot) {
   return h3_shift_of(wave_max(slot[(threadIdx.x & (kMaxSlotParts - 1)) * kMaxSlotStride]));
 }
 
+// x 2^sh as a multiply by the exact power of two (the same value as ldexp),
+// hi by the packed conversion, and lo = fp16(x 2^sh - hi) by one fma_mix per
+// element reading hi's f16 half straight from the packed word (op_sel): the
+// fma forms x 2^sh - hi exactly (a power-of-two product, an f32-exact
+// difference) and rounds once to fp16 -- the value of the C expression
+// (_Float16)(x 2^sh - (float)hi).  Written out because the compiler re-derives
+// hi per element instead of reading the packed word: 4-5 VALU per pair
+// against 7 (multiply form) and 10 (ldexp form).
 __device__ __forceinline__ void hsplit2(float a, float b, int sh, uint32_t& h, uint32_t& l) {
+#ifdef MOLCLR_HSPLIT_LDEXP  // the previous form, for A/B checks
   a = __builtin_ldexpf(a, sh);
   b = __builtin_ldexpf(b, sh);
-  const f16x2 hh = {(_Float16)a, (_Float16)b};
-  const f16x2 ll = {(_Float16)(a - (float)hh[0]), (_Float16)(b - (float)hh[1])};
+  const f16x2 h2 = {(_Float16)a, (_Float16)b};
+  const f16x2 l2 = {(_Float16)(a - (float)h2[0]), (_Float16)(b - (float)h2[1])};
+  h = __builtin_bit_cast(uint32_t, h2);
+  l = __builtin_bit_cast(uint32_t, l2);
+  return;
+#endif
+  const float s = h3_scale(sh);
+  const f16x2 hh = {(_Float16)(a * s), (_Float16)(b * s)};
   h = __builtin_bit_cast(uint32_t, hh);
-  l = __builtin_bit_cast(uint32_t, ll);
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(lo) : "v"(a), "v"(s), "v"(h));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(lo) : "v"(b), "v"(s), "v"(h));
+  l = lo;
 }
 
 __device__ __forceinline__ void hsplit4(float4 v, int sh, uint2& hi, uint2& lo) {

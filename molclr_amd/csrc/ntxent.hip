@@ -274,47 +274,62 @@ __global__ void k_reduce_splits(const float* __restrict__ partial, int64_t split
 // dR = W R_cols a second GEMM.  At the c4 row shard (1024 x 8192 x 256) the
 // buffer is 32 MB.
 
-// one wave per row: lse_r = log Σ_{c != r} exp(S_rc / T), loss_r =
-// (lse_r - S_{r,p(r)} / T) / 2B
-__global__ __launch_bounds__(256) void k_ntxent_row_lse(const float* __restrict__ S, int64_t nrows,
-                                                        int64_t ncols, const int32_t* __restrict__ gidx,
-                                                        int64_t B, float inv_t, float inv_2b,
-                                                        float* __restrict__ lse, float* __restrict__ loss) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (r >= nrows) return;
+// four waves per row: lse_r = log Σ_{c != r} exp(S_rc / T), loss_r =
+// (lse_r - S_{r,p(r)} / T) / 2B.  Wave w takes the float4 columns
+// 4 lane + 256 w + 1024 j; each lane folds eight float4 loads (issued together)
+// at a time into its running (max, sum) with one rescale per batch; the lanes
+// and then the four waves merge in a fixed order.  (One wave per row with a
+// rescale per float4 left one wave per SIMD in a serial exp chain: 12.1 us on
+// c4's 1024 x 8192.)
+constexpr int kLseWaves = 4;
+__global__ __launch_bounds__(64 * kLseWaves) void k_ntxent_row_lse(
+    const float* __restrict__ S, int64_t nrows, int64_t ncols, const int32_t* __restrict__ gidx,
+    int64_t B, float inv_t, float inv_2b, float* __restrict__ lse, float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r = blockIdx.x;  // block-uniform: no early exit inside the block
   const int64_t rg = gidx[r];
   const float* row = S + r * ncols;
   float m = -INFINITY, s = 0.f;
-  // one float4 of logits into the running (max, sum)
-  auto take = [&](float4 v, int64_t c0) {
-    const float e[4] = {v.x, v.y, v.z, v.w};
-    float x[4], bm = -INFINITY;
+  // n float4 of logits (columns c[u] .. c[u] + 3) into the running (max, sum)
+  auto fold = [&](const float4* v, const int64_t* c, int n) {
+    float x[32], bm = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      x[j] = c0 + j != rg ? e[j] * inv_t : -INFINITY;
-      bm = fmaxf(bm, x[j]);
+    for (int u = 0; u < 8; ++u) {
+      const float e[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[4 * u + j] = (u < n && c[u] + j != rg) ? e[j] * inv_t : -INFINITY;
+        bm = fmaxf(bm, x[4 * u + j]);
+      }
     }
     if (bm > -INFINITY) {
       const float nm = fmaxf(m, bm);
       float acc = s * expf(m - nm);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc += expf(x[j] - nm);
+      for (int i = 0; i < 32; ++i) acc += expf(x[i] - nm);
       m = nm;
       s = acc;
     }
   };
-  int64_t c0 = 4 * lane;  // ncols % 4 == 0 (host)
-  // eight loads in flight: one wave per row leaves few waves per CU, so the
-  // row loop is latency-bound with fewer (c4's 1024 x 8192: 12.7 us at four)
-  for (; c0 + 1792 < ncols; c0 += 2048) {
+  constexpr int64_t kStep = 256 * kLseWaves;  // columns per float4 round of the block
+  int64_t c0 = 4 * lane + 256 * wave;         // ncols % 4 == 0 (host)
+  while (c0 < ncols) {
     float4 v[8];
+    int64_t c[8];
+    int n = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(row + c0 + 256 * u);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) take(v[u], c0 + 256 * u);
+    for (int u = 0; u < 8; ++u) {
+      c[u] = c0 + kStep * u;
+      if (c[u] < ncols) {
+        v[u] = *reinterpret_cast<const float4*>(row + c[u]);
+        n = u + 1;
+      } else {
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    fold(v, c, n);
+    c0 += 8 * kStep;
   }
-  for (; c0 < ncols; c0 += 256) take(*reinterpret_cast<const float4*>(row + c0), c0);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float mo = __shfl_xor(m, o, 64), so = __shfl_xor(s, o, 64);
@@ -322,7 +337,20 @@ __global__ __launch_bounds__(256) void k_ntxent_row_lse(const float* __restrict_
     s = nm == -INFINITY ? 0.f : s * expf(m - nm) + so * expf(mo - nm);
     m = nm;
   }
+  __shared__ float wm[kLseWaves], ws[kLseWaves];
   if (lane == 0) {
+    wm[wave] = m;
+    ws[wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = wm[0];
+    s = ws[0];
+    for (int w = 1; w < kLseWaves; ++w) {
+      const float nm = fmaxf(m, wm[w]);
+      s = nm == -INFINITY ? 0.f : s * expf(m - nm) + ws[w] * expf(wm[w] - nm);
+      m = nm;
+    }
     const float l = m + logf(s);
     const int64_t pg = (rg + B) % (2 * B);
     lse[r] = l;
@@ -760,7 +788,7 @@ MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, co
     const int rc = ntx_similarity_h3(rows, cols, nrows, ncols, C, S, planes, rmax, s);
     if (rc) return rc;
     molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_row_lse,
-                         dim3((unsigned)molclr::ceil_div(nrows * 64, 256)), dim3(256), 0, s, S,
+                         dim3((unsigned)nrows), dim3(64 * kLseWaves), 0, s, S,
                          nrows, ncols, gidx, B, inv_t, (float)(1.0 / (2.0 * B)), lse, loss);
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;
@@ -771,7 +799,7 @@ MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, co
     const int rc = ntx_similarity(rows, cols, nrows, ncols, C, w, sim, &S, s);
     if (rc) return rc;
     molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_row_lse,
-                         dim3((unsigned)molclr::ceil_div(nrows * 64, 256)), dim3(256), 0, s, S,
+                         dim3((unsigned)nrows), dim3(64 * kLseWaves), 0, s, S,
                          nrows, ncols, gidx, B, inv_t, (float)(1.0 / (2.0 * B)), lse, loss);
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;

@@ -155,8 +155,11 @@ def set_grad_hook(hook) -> None:
 # _readout) a FusedAdam-owned weight's dW / db run on a side stream beside the
 # data-gradient chain.  join_side() makes the current stream wait for them; the
 # encoder backward (before the reducer's heads bucket), FusedAdam.step and the
-# reducer's finish() call it.  MOLCLR_SIDE_WGRAD=0 keeps them on one stream.
-SIDE_WGRAD = os.environ.get("MOLCLR_SIDE_WGRAD", "1") != "0"
+# reducer's finish() call it.  Opt-in (MOLCLR_SIDE_WGRAD=1): bit-identical, but
+# the captured c2 step measured slower with the fork than without (171.5k vs
+# 176.0k molecules/s, two runs each on one box) -- the same finding as the
+# encoder's per-layer second stream.
+SIDE_WGRAD = os.environ.get("MOLCLR_SIDE_WGRAD", "0") == "1"
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 
@@ -673,7 +676,7 @@ class _MLP(torch.autograd.Function):
         pW1, pb1, pW2, pb2 = ctx.params
         dz = _c(dz)
         need = ctx.needs_input_grad
-        if ctx.h3 and all(need[1:]):
+        if ctx.h3 and all(need[1:5]):
             # the executor's h3 order: dz1 (relu mask of a1; max |dz1| and its row
             # maxima from its epilogue), dW2 (+db2), dW1 (+db1), dx
             D = x.shape[1]
