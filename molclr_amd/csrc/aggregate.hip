@@ -38,7 +38,7 @@ __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __
                                  int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
-  int64_t i = t / d4;
+  int64_t i = N * d4 < (1ll << 32) ? (int64_t)((uint32_t)t / (uint32_t)d4) : t / d4;
   int c = (int)(t - i * d4);
   const int64_t a = x[2 * i], b = x[2 * i + 1];
   if (a < 0 || a >= n1 || b < 0 || b >= n2) {
@@ -425,7 +425,8 @@ __global__ __launch_bounds__(kT) void k_transpose_gather(const typename St::T* _
                                                          int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
-  int64_t j = t / d4;
+  // 32-bit division when the grid allows (uniform branch)
+  int64_t j = N * d4 < (1ll << 32) ? (int64_t)((uint32_t)t / (uint32_t)d4) : t / d4;
   int c = (int)(t - j * d4);
   const uint4 s = nbr_t[j];
   const uint32_t deg = nbr_degree(s.x);
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(kT) void k_gcn_agg_fwd(
     const float4* __restrict__ bias, float4* __restrict__ out, int64_t N, int d4) {
   int64_t t = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (t >= N * d4) return;
-  int64_t i = t / d4;
+  int64_t i = N * d4 < (1ll << 32) ? (int64_t)((uint32_t)t / (uint32_t)d4) : t / d4;
   int c = (int)(t - i * d4);
   const uint4 s = nbr[i];
   const float4 self = xw[t];

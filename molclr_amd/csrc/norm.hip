@@ -165,6 +165,10 @@ __device__ __forceinline__ SegAt seg_of_part(const Segs& sg, int64_t b) {
   }
   return {-1, r, r, p, 0, 1};
 }
+// t / d4 in 32 bits when the whole index range fits (uniform branch)
+__device__ __forceinline__ int64_t row_of(int64_t t, int d4, int64_t total4) {
+  return total4 <= 0x7FFFFFFF ? (int64_t)((uint32_t)t / (uint32_t)d4) : t / d4;
+}
 __device__ __forceinline__ int seg_of_row(const Segs& sg, int64_t i) {
   int64_t r = 0;
   for (int s = 0; s < sg.n; ++s) {
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(kT) void k_bn_apply(const typename St::T* __restric
                                                  int d4, int relu, Segs sg) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total4) return;
-  const int64_t i = t / d4;
+  const int64_t i = row_of(t, d4, total4);
   const int c = (int)(t - i * d4);
   const int s = seg_of_row(sg, i);
   if (s < 0) {  // padding row of a device-sized plan
@@ -545,8 +549,8 @@ __device__ __forceinline__ float4 bn_bwd_elem(
     const float4* __restrict__ mean, const float4* __restrict__ invstd,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
     const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t t, int d4, int relu,
-    Segs sg) {
-  const int64_t i = t / d4;
+    Segs sg, int64_t total4) {
+  const int64_t i = row_of(t, d4, total4);
   const int c = (int)(t - i * d4);
   const int s = seg_of_row(sg, i);
   if (s < 0) {  // padding row of a device-sized plan: no gradient
@@ -587,16 +591,16 @@ __global__ __launch_bounds__(kT) void k_bn_bwd_apply(
     int row = -1;
     if (t < total4) {
       const float4 o = bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu,
-                                       sg);
+                                       sg, total4);
       m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-      row = (int)(t / d4);
+      row = (int)row_of(t, d4, total4);
     }
     row_max_parts(m, row, t, rows, d4, rowparts, nparts);
     if (slot != nullptr) absmax_publish(m, slot);
     return;
   }
   if (t >= total4) return;
-  bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu, sg);
+  bn_bwd_elem<St>(dy, z, mean, invstd, gamma, beta, k1, k2, dz, t, d4, relu, sg, total4);
 }
 
 
