@@ -35,6 +35,12 @@ The JSON line adds:
                   kept S and dR = W R), work = the two products' flops, against
                   157.3 TF/s (fp32 MFMA) and 417 TF/s (the six-product split-bf16
                   ceiling, 2.5 PF / 6); rows x cols x dim of this rank's share.
+  roofline_ntxent_c4 — the same NT-Xent calls on one data-parallel rank's
+                  share at c4 (BASELINE config 4: 8 ranks x 512 molecules ->
+                  1024 rows x 8192 gathered columns x 256), standalone HIP
+                  events over 20 fwd+bwd pairs on synthetic unit rows; the
+                  automatic formulation there is h3 (three fp16 MFMAs per
+                  product): frac against its ceiling 2.5 PF / 3.
   cpu_baseline  — the oracle (CPU restatement of the reference step, incl.
                   the broadcast-cosine NT-Xent) on this host, rank 0, N=1 only,
                   a bounded sample of the same workload.
@@ -522,6 +528,10 @@ def main():
                                "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                          f"after the timed region"}
 
+    roofline_ntxent_c4 = None
+    if rank == 0 and not args.no_kernel_timing and precision != "bf16":
+        roofline_ntxent_c4 = ntxent_c4_roofline(dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log(rank, "timing the CPU baseline (oracle) ...")
@@ -561,13 +571,76 @@ def main():
             "captures_in_timed_region": captures_timed,
             "ranks": per_rank,
             "roofline": roofline, "roofline_mfma": roofline_mfma,
-            "roofline_ntxent": roofline_ntxent, "cpu_baseline": cpu,
+            "roofline_ntxent": roofline_ntxent, "roofline_ntxent_c4": roofline_ntxent_c4,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if captured is not None:
         captured.close()  # graphs holding RCCL collectives go before their group
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
+
+
+def ntxent_c4_roofline(dev, reps: int = 20) -> dict:
+    """NT-Xent of one c4 data-parallel rank (rows [zj; zi] of 512 molecules,
+    columns gathered from 8 ranks: 1024 x 8192 x 256) through the C ABI as the
+    training step calls it: molclr_ntxent_prep, _fwd_impl (S kept), _bwd_impl,
+    _prep_bwd.  Work = the two products S = R C^T and dR = W C."""
+    import torch
+    from molclr_amd import _lib
+    from molclr_amd import distributed as mdist
+    lib = _lib.load()
+    st = _lib.stream_of(dev)
+    W, Bl, C, T = 8, 512, 256, 0.1
+    B, n = W * Bl, 2 * Bl
+    g = torch.Generator(device=dev).manual_seed(4)
+    R = torch.randn(n, C, device=dev, generator=g)
+    cols = torch.nn.functional.normalize(torch.randn(2 * B, C, device=dev, generator=g), dim=1)
+    gidx = mdist.global_row_index(Bl, 0, W, dev)
+    rh, nrm = torch.empty_like(R), torch.empty(n, device=dev)
+    lse, lr = torch.empty(n, device=dev), torch.empty(n, device=dev)
+    lse_cols = torch.rand(2 * B, device=dev, generator=g) + 5
+    gl = torch.ones((), device=dev)
+    drh, dR = torch.empty_like(R), torch.empty_like(R)
+    wsb = lib.molclr_ntxent_workspace_bytes(n, 2 * B, C)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    sb = lib.molclr_ntxent_sim_bytes(n, 2 * B, C, -1)
+    sim = torch.empty(max(sb, 4), dtype=torch.uint8, device=dev) if sb else None
+
+    def pair():
+        for rc in (lib.molclr_ntxent_prep(R.data_ptr(), rh.data_ptr(), nrm.data_ptr(), n, C, 1, st),
+                   lib.molclr_ntxent_fwd_impl(rh.data_ptr(), gidx.data_ptr(), cols.data_ptr(), n,
+                                              2 * B, C, B, T, lse.data_ptr(), lr.data_ptr(),
+                                              _lib.ptr(sim), ws.data_ptr(), wsb, st, -1),
+                   lib.molclr_ntxent_bwd_impl(rh.data_ptr(), gidx.data_ptr(), cols.data_ptr(),
+                                              lse_cols.data_ptr(), gl.data_ptr(), n, 2 * B, C, B,
+                                              T, _lib.ptr(sim), drh.data_ptr(), ws.data_ptr(), wsb,
+                                              st, -1),
+                   lib.molclr_ntxent_prep_bwd(drh.data_ptr(), rh.data_ptr(), nrm.data_ptr(),
+                                              dR.data_ptr(), n, C, 1, st)):
+            if rc != 0:
+                raise RuntimeError(_lib.last_error())
+
+    for _ in range(3):
+        pair()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        pair()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / reps * 1e3
+    work = (2 if sb else 3) * 2.0 * n * 2 * B * C  # S (again in the backward when not kept), dR
+    tfs = work / (us / 1e6) / 1e12
+    ceiling = BF16_MFMA_PEAK_TFS / 3
+    return {"kernel": "molclr_ntxent_prep + _fwd_impl + _bwd_impl + _prep_bwd (automatic "
+                      "formulation: h3 at this shape)", "bound": "mfma",
+            "achieved": round(tfs, 2), "peak": round(ceiling, 1),
+            "unit": "TFLOP/s (fp32-equivalent)", "frac": round(tfs / ceiling, 4),
+            "frac_of_fp32_mfma_peak": round(tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None,
+            "rows": n, "cols": 2 * B, "dim": C, "us_per_step": round(us, 1),
+            "timing": f"HIP events around {reps} fwd+bwd pairs, standalone, after the timed region"}
 
 
 def load_pmc_traffic(config: str, two_pass: bool):

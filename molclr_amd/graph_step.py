@@ -237,6 +237,7 @@ class CapturedTrainStep:
         self.captures = 0
         self.replays = 0
         self.eager_steps = 0  # data parallel: batches no captured graph held
+        self._one = None
         self.last_graph: StagedPairGraph | None = None
 
     @staticmethod
@@ -311,10 +312,12 @@ class CapturedTrainStep:
         allocate from its pool: the weight images the step reads, created
         here from the ordinary allocator (regenerated inside the graph)."""
         from . import _lib
+        if self._one is None:  # d loss / d loss, outside every pool
+            self._one = torch.ones((), dtype=torch.float32, device=self.device)
         with _lib.dry_run():
             _, z = self.model.forward_staged(graph)
             loss = self.criterion.forward_pair_normalized(z)
-            loss.backward()
+            loss.backward(self._one)
         del loss, z
         # the images it created hold nothing yet: the capture must record
         # their regeneration
@@ -331,7 +334,9 @@ class CapturedTrainStep:
                 self.reducer.arm()
             _, z = self.model.forward_staged(graph)
             loss = self.criterion.forward_pair_normalized(z)
-            loss.backward()
+            # the seed gradient from a tensor made before the capture: no
+            # fill kernel in the graph for autograd's ones_like(loss)
+            loss.backward(self._one)
             if self.reducer is not None:  # bucketed, overlapped with the backward
                 self.reducer.finish()
             elif self.group is not None:
