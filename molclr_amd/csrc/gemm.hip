@@ -1879,7 +1879,7 @@ __global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K
   planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
 }
 
-// Batched form: blockIdx.y = job (one weight image per job).
+// Batched images (k_planes_make_tiled below): blockIdx.y = job.
 struct PlanesJob {
   const float* B;
   uint16_t* planes;
@@ -1890,21 +1890,6 @@ constexpr int kPlanesBatch = 32;
 struct PlanesJobs {
   PlanesJob j[kPlanesBatch];
 };
-__global__ void k_bplanes_make_batch(PlanesJobs jobs) {
-  const PlanesJob& jb = jobs.j[blockIdx.y];
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= jb.npad * jb.kp) return;
-  const int64_t n = t / jb.kp, k = t - n * jb.kp;
-  float v = 0.f;
-  if (n < jb.N && k < jb.K) v = jb.kmajor ? jb.B[k * jb.ldb + n] : jb.B[n * jb.ldb + k];
-  uint32_t h, m, l;
-  split2(v, 0.f, h, m, l);
-  const int64_t ps = jb.npad * jb.kp;
-  jb.planes[t] = (uint16_t)(h & 0xFFFFu);
-  jb.planes[ps + t] = (uint16_t)(m & 0xFFFFu);
-  jb.planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
-}
-
 // h3 planes: [2][Npad][Kp] fp16 (hi, lo of B(k, n) 2^sh), zero beyond (N, K),
 // then the max |B| slot (kMaxSlotParts floats), which sets sh.  The max kernel
 // gives each job one block per slot entry, each storing its partial (plain
@@ -1930,26 +1915,101 @@ __global__ __launch_bounds__(1024) void k_hplanes_max_batch(PlanesJobs jobs) {
   if (threadIdx.x == 0)
     reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x * kMaxSlotStride] = m;
 }
-// one thread per (n, 8 k) of the padded grid: two 16-byte plane stores
-__global__ __launch_bounds__(256) void k_hplanes_make_batch(PlanesJobs jobs) {
-  const PlanesJob& jb = jobs.j[blockIdx.y];
+// Weight images of both kinds in one launch per batch, 8 consecutive k of one
+// n per item (16-byte stores per plane).  A K-major job (B stored [K][N]: the
+// data-gradient orientation) goes through a 64 (k) x 64 (n) LDS tile, read
+// as float4 runs along n and written as runs along k; a row-major one reads
+// its 8 k directly.  The per-job work is block-uniform (blockIdx.y = job).
+// Same split per element as k_bplanes_make (molclr_bplanes_make): bit-identical
+// images (tests/test_gpu_kernels.py::test_weight_images_bit_exact).  The
+// per-element batch kernels this replaces read K-major weights one cache line
+// per lane: c5's images took 44.9 us a step, c2's 7.3 + 15.1.
+constexpr int kPT = 64;  // tile edge
+template <bool H3>
+__device__ __forceinline__ void planes_store8(const PlanesJob& jb, int sh, int64_t n, int64_t k0,
+                                              const float v[8]) {
   const int64_t ps = jb.npad * jb.kp;
-  const int sh = h3_shift(reinterpret_cast<const float*>(jb.planes + 2 * ps));
-  const int kc = (int)(jb.kp >> 3);  // 8-k chunks per row
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= jb.npad * kc) return;
-  const int64_t n = t / kc;
-  const int64_t k0 = 8 * (t - n * kc);
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int64_t k = k0 + j;
-    v[j] = (n < jb.N && k < jb.K) ? (jb.kmajor ? jb.B[k * jb.ldb + n] : jb.B[n * jb.ldb + k]) : 0.f;
+  const float4 a = make_float4(v[0], v[1], v[2], v[3]), b = make_float4(v[4], v[5], v[6], v[7]);
+  if constexpr (H3) {
+    u32x4 h, l;
+    hsplit8(a, b, sh, h, l);
+    *reinterpret_cast<u32x4*>(jb.planes + n * jb.kp + k0) = h;
+    *reinterpret_cast<u32x4*>(jb.planes + ps + n * jb.kp + k0) = l;
+  } else {
+    u32x4 h, m, l;
+    split8(a, b, h, m, l);
+    *reinterpret_cast<u32x4*>(jb.planes + n * jb.kp + k0) = h;
+    *reinterpret_cast<u32x4*>(jb.planes + ps + n * jb.kp + k0) = m;
+    *reinterpret_cast<u32x4*>(jb.planes + 2 * ps + n * jb.kp + k0) = l;
   }
-  u32x4 h, l;
-  hsplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), sh, h, l);
-  *reinterpret_cast<u32x4*>(jb.planes + n * jb.kp + k0) = h;
-  *reinterpret_cast<u32x4*>(jb.planes + ps + n * jb.kp + k0) = l;
+}
+template <bool H3>
+__global__ __launch_bounds__(256) void k_planes_make_tiled(PlanesJobs jobs) {
+  const PlanesJob& jb = jobs.j[blockIdx.y];
+  // every lane reads the slot (a wave reduction) before any lane returns
+  const int sh = H3 ? h3_shift(reinterpret_cast<const float*>(jb.planes + 2 * jb.npad * jb.kp)) : 0;
+  const int tid = threadIdx.x;
+  const int kc = (int)(jb.kp >> 3);  // 8-k chunks per row
+  if (!jb.kmajor) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + tid;
+    if (t >= jb.npad * kc) return;
+    const int64_t n = t / kc, k0 = 8 * (t - n * kc);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t k = k0 + j;
+      v[j] = (n < jb.N && k < jb.K) ? jb.B[n * jb.ldb + k] : 0.f;
+    }
+    planes_store8<H3>(jb, sh, n, k0, v);
+    return;
+  }
+  const int64_t tn = (jb.npad + kPT - 1) / kPT, tk = (jb.kp + kPT - 1) / kPT;
+  if ((int64_t)blockIdx.x >= tn * tk) return;  // block-uniform
+  const int64_t n0 = ((int64_t)blockIdx.x % tn) * kPT, k0t = ((int64_t)blockIdx.x / tn) * kPT;
+  __shared__ float tile[kPT][kPT + 1];  // [k][n]
+  // load: 64 k-rows x 16 float4 along n, 4 per thread
+  const bool vec = (jb.ldb & 3) == 0 && (reinterpret_cast<uintptr_t>(jb.B) & 15) == 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int idx = tid + 256 * q;
+    const int kr = idx >> 4, nc = 4 * (idx & 15);
+    const int64_t k = k0t + kr, n = n0 + nc;
+    float e[4] = {0.f, 0.f, 0.f, 0.f};
+    if (k < jb.K) {
+      if (vec && n + 3 < jb.N) {
+        const float4 x = *reinterpret_cast<const float4*>(jb.B + k * jb.ldb + n);
+        e[0] = x.x;
+        e[1] = x.y;
+        e[2] = x.z;
+        e[3] = x.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (n + j < jb.N) e[j] = jb.B[k * jb.ldb + n + j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tile[kr][nc + j] = e[j];
+  }
+  __syncthreads();
+  // store: 64 n x 8 chunks of 8 k, 2 per thread
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = tid + 256 * q;
+    const int nr = idx >> 3, kq = 8 * (idx & 7);
+    const int64_t n = n0 + nr, k0 = k0t + kq;
+    if (n >= jb.npad || k0 >= jb.kp) continue;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[kq + j][nr];
+    planes_store8<H3>(jb, sh, n, k0, v);
+  }
+}
+
+// blocks one launch needs for a job of k_planes_make_tiled
+int64_t planes_tiled_blocks(const PlanesJob& j) {
+  return j.kmajor ? ((j.npad + kPT - 1) / kPT) * ((j.kp + kPT - 1) / kPT)
+                  : molclr::ceil_div(j.npad * (j.kp >> 3), 256);
 }
 
 // max |x| over a [rows][cols] (ld) fp32 matrix, folded into *slot.  A dense
@@ -2659,11 +2719,11 @@ MOLCLR_API int molclr_bplanes_make_batch(int count, const float* const* B, const
                      "bplanes_make_batch: job %d leading dimension too small", q);
       jobs.j[i] = PlanesJob{B[q], planes[q], N[q], K[q], ldb[q], planes_npad(N[q]), planes_kp(K[q]),
                             b_kmajor[q]};
-      const int64_t e = jobs.j[i].npad * jobs.j[i].kp;
+      const int64_t e = planes_tiled_blocks(jobs.j[i]);
       most = e > most ? e : most;
     }
-    hipLaunchKernelGGL(k_bplanes_make_batch, dim3((unsigned)molclr::ceil_div(most, 256), (unsigned)n),
-                       dim3(256), 0, molclr::as_stream(stream), jobs);
+    hipLaunchKernelGGL(k_planes_make_tiled<false>, dim3((unsigned)most, (unsigned)n), dim3(256), 0,
+                       molclr::as_stream(stream), jobs);
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
@@ -2905,13 +2965,13 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
                      "hplanes_make_batch: job %d leading dimension too small", q);
       jobs.j[i] = PlanesJob{B[q], planes[q], N[q], K[q], ldb[q], planes_npad(N[q]), planes_kp(K[q]),
                             b_kmajor[q]};
-      const int64_t e = jobs.j[i].npad * jobs.j[i].kp;
+      const int64_t e = planes_tiled_blocks(jobs.j[i]);
       most = e > most ? e : most;
     }
     hipStream_t s = molclr::as_stream(stream);
     hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)n), dim3(1024), 0, s, jobs);
-    hipLaunchKernelGGL(k_hplanes_make_batch, dim3((unsigned)molclr::ceil_div(most / 8, 256), (unsigned)n),
-                       dim3(256), 0, s, jobs);
+    hipLaunchKernelGGL(k_planes_make_tiled<true>, dim3((unsigned)most, (unsigned)n), dim3(256), 0, s,
+                       jobs);
   }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;

@@ -785,6 +785,56 @@ def _h3_planes(lib, W, N, K, kmajor, dev):
     return buf
 
 
+@pytest.mark.parametrize("N,K", [(600, 300), (300, 600), (37, 45), (256, 512), (8, 1000)])
+@pytest.mark.parametrize("kmajor", [0, 1])
+def test_weight_images_bit_exact(dev, N, K, kmajor):
+    """The batched weight-image kernel (k_planes_make_tiled: an LDS tile for
+    K-major weights) writes exactly the per-element images: split-bf16 planes
+    equal molclr_bplanes_make's byte for byte; h3 planes equal fp16(B 2^sh)
+    and fp16(B 2^sh - hi) computed by torch with sh from max |B|, zero padding
+    included, for both orientations and ragged sizes."""
+    import ctypes
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(N * 7 + K + kmajor)
+    ld = (N if kmajor else K) + 4  # a padded leading dimension
+    rows = K if kmajor else N
+    Wfull = (torch.randn(rows, ld, generator=g) * torch.exp2(torch.randint(-8, 8, (rows, 1),
+                                                                           generator=g).float()))
+    W = Wfull.to(dev)
+    B = (Wfull[:, :N] if kmajor else Wfull[:, :K].T)  # B(k, n) as [K][N]
+    i64 = lambda v: (ctypes.c_int64 * 1)(v)  # noqa: E731
+    st = ops._stream(W)
+    # split-bf16: batched (tiled) against the single per-element kernel
+    nb = lib.molclr_bplanes_bytes(N, K)
+    one = torch.full((nb,), 0x5A, dtype=torch.uint8, device=dev)
+    bat = torch.full((nb,), 0xA5, dtype=torch.uint8, device=dev)
+    assert lib.molclr_bplanes_make(W.data_ptr(), N, K, ld, kmajor, one.data_ptr(), st) == 0
+    assert lib.molclr_bplanes_make_batch(1, (ctypes.c_void_p * 1)(W.data_ptr()), i64(N), i64(K),
+                                         i64(ld), (ctypes.c_int * 1)(kmajor),
+                                         (ctypes.c_void_p * 1)(bat.data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(one, bat)
+    # h3: against torch's fp16 rounding of the scaled values
+    nb = lib.molclr_hplanes_bytes(N, K)
+    buf = torch.full((nb,), 0x5A, dtype=torch.uint8, device=dev)
+    assert lib.molclr_hplanes_make_batch(1, (ctypes.c_void_p * 1)(W.data_ptr()), i64(N), i64(K),
+                                         i64(ld), (ctypes.c_int * 1)(kmajor),
+                                         (ctypes.c_void_p * 1)(buf.data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    kp = (K + 31) // 32 * 32
+    npad = (nb - 2048 * 4) // (4 * kp)
+    planes = buf[: 4 * npad * kp].view(torch.float16).view(2, npad, kp).cpu()
+    m = B.abs().max()
+    sh = min(15 - int(torch.frexp(m).exponent), 127)
+    x = torch.zeros(npad, kp)
+    x[:N, :K] = B.T * 2.0 ** sh
+    hi = x.half()
+    lo = (x - hi.float()).half()
+    assert torch.equal(planes[0].view(torch.int16), hi.view(torch.int16))
+    assert torch.equal(planes[1].view(torch.int16), lo.view(torch.int16))
+
+
 @pytest.mark.parametrize("M,N,K", H3_SHAPES)
 @pytest.mark.parametrize("rowwise", [0, 1])
 @pytest.mark.parametrize("epi", [0, 2, 3])
