@@ -251,6 +251,15 @@ struct StF32 {
   __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
     reinterpret_cast<float4*>(p)[unit] = v;
   }
+  __device__ __forceinline__ static void ld2(const T* __restrict__ p, int64_t u2, float4& a,
+                                             float4& b) {
+    a = reinterpret_cast<const float4*>(p)[2 * u2];
+    b = reinterpret_cast<const float4*>(p)[2 * u2 + 1];
+  }
+  __device__ __forceinline__ static void st2(T* __restrict__ p, int64_t u2, float4 a, float4 b) {
+    reinterpret_cast<float4*>(p)[2 * u2] = a;
+    reinterpret_cast<float4*>(p)[2 * u2 + 1] = b;
+  }
   __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) { return p[i]; }
   __device__ __forceinline__ static void st1(T* __restrict__ p, int64_t i, float v) { p[i] = v; }
 };
@@ -275,6 +284,19 @@ struct StBF16 {
   }
   __device__ __forceinline__ static void st(T* __restrict__ p, int64_t unit, float4 v) {
     reinterpret_cast<uint2*>(p)[unit] = make_uint2(f32x2_to_bf16x2(v.x, v.y), f32x2_to_bf16x2(v.z, v.w));
+  }
+  // units 2 u2 and 2 u2 + 1 as one 16-byte access
+  __device__ __forceinline__ static void ld2(const T* __restrict__ p, int64_t u2, float4& a,
+                                             float4& b) {
+    const uint4 q = reinterpret_cast<const uint4*>(p)[u2];
+    a = make_float4(bf16_to_f32(q.x & 0xFFFFu), bf16_to_f32(q.x >> 16), bf16_to_f32(q.y & 0xFFFFu),
+                    bf16_to_f32(q.y >> 16));
+    b = make_float4(bf16_to_f32(q.z & 0xFFFFu), bf16_to_f32(q.z >> 16), bf16_to_f32(q.w & 0xFFFFu),
+                    bf16_to_f32(q.w >> 16));
+  }
+  __device__ __forceinline__ static void st2(T* __restrict__ p, int64_t u2, float4 a, float4 b) {
+    reinterpret_cast<uint4*>(p)[u2] = make_uint4(f32x2_to_bf16x2(a.x, a.y), f32x2_to_bf16x2(a.z, a.w),
+                                                 f32x2_to_bf16x2(b.x, b.y), f32x2_to_bf16x2(b.z, b.w));
   }
   __device__ __forceinline__ static float ld1(const T* __restrict__ p, int64_t i) {
     return bf16_to_f32(p[i]);

@@ -377,26 +377,39 @@ __global__ void k_bn_eval_coeffs(const float* __restrict__ gamma, const float* _
 
 __device__ __forceinline__ float bn_apply1(float z, float sc, float sh) { return __fmaf_rn(z, sc, sh); }
 
-template <typename St>
+// U = 2 (bf16 storage): two column units per thread, one 16-byte access each
+// way (8-byte bf16 accesses ran at half the HBM rate of the fp32 form); the
+// same per-element arithmetic.  d4 % U == 0 (host).
+template <typename St, int U = 1>
 __global__ __launch_bounds__(kT) void k_bn_apply(const typename St::T* __restrict__ z,
                                                  const float4* __restrict__ scale,
                                                  const float4* __restrict__ shift,
                                                  typename St::T* __restrict__ y, int64_t total4,
                                                  int d4, int relu, Segs sg) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total4) return;
-  const int64_t i = row_of(t, d4, total4);
-  const int c = (int)(t - i * d4);
+  if (t >= total4 / U) return;
+  const int64_t u0 = t * U;
+  const int64_t i = row_of(u0, d4, total4);
+  const int c = (int)(u0 - i * d4);
   const int s = seg_of_row(sg, i);
+  float4 v[U];
   if (s < 0) {  // padding row of a device-sized plan
-    St::st(y, t, f4zero());
+    if constexpr (U == 2) St::st2(y, t, f4zero(), f4zero());
+    else St::st(y, t, f4zero());
     return;
   }
-  float4 v = St::ld(z, t), sc = scale[s * d4 + c], sh = shift[s * d4 + c];
-  float4 o = make_float4(bn_apply1(v.x, sc.x, sh.x), bn_apply1(v.y, sc.y, sh.y),
-                         bn_apply1(v.z, sc.z, sh.z), bn_apply1(v.w, sc.w, sh.w));
-  if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
-  St::st(y, t, o);
+  if constexpr (U == 2) St::ld2(z, t, v[0], v[1]);
+  else v[0] = St::ld(z, t);
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const float4 sc = scale[s * d4 + c + j], sh = shift[s * d4 + c + j];
+    float4 o = make_float4(bn_apply1(v[j].x, sc.x, sh.x), bn_apply1(v[j].y, sc.y, sh.y),
+                           bn_apply1(v[j].z, sc.z, sh.z), bn_apply1(v[j].w, sc.w, sh.w));
+    if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+    v[j] = o;
+  }
+  if constexpr (U == 2) St::st2(y, t, v[0], v[1]);
+  else St::st(y, t, v[0]);
 }
 
 // BN backward pass 1: per-column Σ dyr and Σ dyr * xhat (fixed order).
@@ -542,6 +555,32 @@ __global__ __launch_bounds__(kRedCols* kRedLanes) void k_bn_bwd_final(
   }
 }
 
+// one float4 of dz from its dy / z units (segment s, column unit c)
+__device__ __forceinline__ float4 bn_bwd_math(float4 g, float4 x, const float4* __restrict__ mean,
+                                              const float4* __restrict__ invstd,
+                                              const float* __restrict__ gamma,
+                                              const float* __restrict__ beta,
+                                              const float4* __restrict__ k1,
+                                              const float4* __restrict__ k2, int s, int c, int d4,
+                                              int relu) {
+  float4 mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
+  bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
+  float4 a = k1[s * d4 + c], b = k2[s * d4 + c];
+  if (relu) {
+    g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
+    g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
+    g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
+    g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
+  }
+  // dz = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat))  (torch CPU BN backward)
+  float4 o;
+  o.x = (g.x - a.x - ((x.x - mu.x) * is.x) * b.x) * sc.x;
+  o.y = (g.y - a.y - ((x.y - mu.y) * is.y) * b.y) * sc.y;
+  o.z = (g.z - a.z - ((x.z - mu.z) * is.z) * b.z) * sc.z;
+  o.w = (g.w - a.w - ((x.w - mu.w) * is.w) * b.w) * sc.w;
+  return o;
+}
+
 // one float4 of dz (k_bn_bwd_apply), stored and returned
 template <typename St>
 __device__ __forceinline__ float4 bn_bwd_elem(
@@ -557,23 +596,35 @@ __device__ __forceinline__ float4 bn_bwd_elem(
     St::st(dz, t, f4zero());
     return f4zero();
   }
-  float4 g = St::ld(dy, t), x = St::ld(z, t), mu = mean[s * d4 + c], is = invstd[s * d4 + c], sc, sh;
-  bn_coeffs4(gamma, beta, mu, is, c, sc, sh);
-  float4 a = k1[s * d4 + c], b = k2[s * d4 + c];
-  if (relu) {
-    g.x = bn_apply1(x.x, sc.x, sh.x) > 0.f ? g.x : 0.f;
-    g.y = bn_apply1(x.y, sc.y, sh.y) > 0.f ? g.y : 0.f;
-    g.z = bn_apply1(x.z, sc.z, sh.z) > 0.f ? g.z : 0.f;
-    g.w = bn_apply1(x.w, sc.w, sh.w) > 0.f ? g.w : 0.f;
-  }
-  // dz = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat))  (torch CPU BN backward)
-  float4 o;
-  o.x = (g.x - a.x - ((x.x - mu.x) * is.x) * b.x) * sc.x;
-  o.y = (g.y - a.y - ((x.y - mu.y) * is.y) * b.y) * sc.y;
-  o.z = (g.z - a.z - ((x.z - mu.z) * is.z) * b.z) * sc.z;
-  o.w = (g.w - a.w - ((x.w - mu.w) * is.w) * b.w) * sc.w;
+  const float4 o = bn_bwd_math(St::ld(dy, t), St::ld(z, t), mean, invstd, gamma, beta, k1, k2, s,
+                               c, d4, relu);
   St::st(dz, t, o);
   return o;
+}
+
+// two column units per thread, 16-byte accesses (bf16 storage, no row maxima)
+template <typename St>
+__global__ __launch_bounds__(kT) void k_bn_bwd_apply2(
+    const typename St::T* __restrict__ dy, const typename St::T* __restrict__ z,
+    const float4* __restrict__ mean, const float4* __restrict__ invstd,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float4* __restrict__ k1,
+    const float4* __restrict__ k2, typename St::T* __restrict__ dz, int64_t total4, int d4,
+    int relu, Segs sg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total4 / 2) return;
+  const int64_t u0 = 2 * t;
+  const int64_t i = row_of(u0, d4, total4);
+  const int c = (int)(u0 - i * d4);
+  const int s = seg_of_row(sg, i);
+  if (s < 0) {
+    St::st2(dz, t, f4zero(), f4zero());
+    return;
+  }
+  float4 g0, g1, x0, x1;
+  St::ld2(dy, t, g0, g1);
+  St::ld2(z, t, x0, x1);
+  St::st2(dz, t, bn_bwd_math(g0, x0, mean, invstd, gamma, beta, k1, k2, s, c, d4, relu),
+          bn_bwd_math(g1, x1, mean, invstd, gamma, beta, k1, k2, s, c + 1, d4, relu));
 }
 
 template <typename St>
@@ -889,10 +940,16 @@ int bn_fwd(const void* zv, const float* gamma, const float* beta, float* running
                        save_invstd, scale, shift);
   }
   const int64_t total4 = rows * (D / 4);
-  if (total4 > 0 && y)  // y == NULL: statistics only (the consumer applies them)
-    hipLaunchKernelGGL(k_bn_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, z,
-                       (const float4*)scale, (const float4*)shift, y, total4, (int)(D / 4), relu,
-                       sg);
+  if (total4 > 0 && y) {  // y == NULL: statistics only (the consumer applies them)
+    if (St::kBytes == 2 && D % 8 == 0)
+      hipLaunchKernelGGL((k_bn_apply<St, 2>), dim3(molclr::ceil_div(total4 / 2, kT)), dim3(kT), 0,
+                         s, z, (const float4*)scale, (const float4*)shift, y, total4, (int)(D / 4),
+                         relu, sg);
+    else
+      hipLaunchKernelGGL((k_bn_apply<St, 1>), dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s,
+                         z, (const float4*)scale, (const float4*)shift, y, total4, (int)(D / 4),
+                         relu, sg);
+  }
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
@@ -936,10 +993,15 @@ int bn_bwd(const void* dyv, const void* zv, const float* gamma, const float* bet
   const int64_t total4 = rows * (D / 4);
   static_assert(kT % 64 == 0, "row parts follow the waves");
   MOLCLR_REQUIRE(!rowparts || rows < (1ll << 31), "batchnorm_seg_bwd_max: too many rows");
-  hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy, z,
-                     (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
-                     (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg,
-                     rowparts, bn_row_parts(D), slot);
+  if (St::kBytes == 2 && D % 8 == 0 && !rowparts && !slot)
+    hipLaunchKernelGGL(k_bn_bwd_apply2<St>, dim3(molclr::ceil_div(total4 / 2, kT)), dim3(kT), 0, s,
+                       dy, z, (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
+                       (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<St>, dim3(molclr::ceil_div(total4, kT)), dim3(kT), 0, s, dy,
+                       z, (const float4*)save_mean, (const float4*)save_invstd, gamma, beta,
+                       (const float4*)k1, (const float4*)k2, dz, total4, (int)(D / 4), relu, sg,
+                       rowparts, bn_row_parts(D), slot);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
