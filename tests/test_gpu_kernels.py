@@ -900,7 +900,8 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
         assert torch.equal(C2, C)
 
 
-@pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12)])
+@pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12),
+                                             (777, 36, 200)])
 @pytest.mark.parametrize("spread", ["uniform", "rows", "cols", "binades30"])
 def test_linear_wgrad_h3(dev, rows, n_out, n_in, spread):
     """h3 weight gradient dW = dy^T x (+ db) against fp64.  ``rows``: dy's rows
