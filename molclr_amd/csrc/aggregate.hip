@@ -31,23 +31,31 @@ constexpr int kT = 256;
 // An atom type or chirality outside the tables (the reference's
 // nn.Embedding raises an IndexError on it) makes the row NaN and sets bit 3 of
 // *status (MOLCLR_STATUS_ATOM_RANGE) instead of being clamped to a valid row.
-template <typename St>
+// U = 2 (bf16 storage, d4 even): two column units per thread, one 16-byte
+// store (as k_bn_apply<StBF16, 2>).
+template <typename St, int U = 1>
 __global__ void k_atom_embed_fwd(const int64_t* __restrict__ x, const float4* __restrict__ X1,
                                  const float4* __restrict__ X2, typename St::T* __restrict__ h,
                                  int64_t N, int d4, int64_t n1, int64_t n2,
                                  int32_t* __restrict__ status) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N * d4) return;
-  int64_t i = N * d4 < (1ll << 32) ? (int64_t)((uint32_t)t / (uint32_t)d4) : t / d4;
-  int c = (int)(t - i * d4);
+  if (t >= N * d4 / U) return;
+  const int64_t u0 = t * U;
+  int64_t i = N * d4 < (1ll << 32) ? (int64_t)((uint32_t)u0 / (uint32_t)d4) : u0 / d4;
+  int c = (int)(u0 - i * d4);
   const int64_t a = x[2 * i], b = x[2 * i + 1];
+  float4 v[U];
   if (a < 0 || a >= n1 || b < 0 || b >= n2) {
     const float q = __builtin_nanf("");
-    St::st(h, t, make_float4(q, q, q, q));
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = make_float4(q, q, q, q);
     if (c == 0 && status != nullptr) atomicOr(status, MOLCLR_STATUS_ATOM_RANGE);
-    return;
+  } else {
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = f4add(X1[a * d4 + c + j], X2[b * d4 + c + j]);
   }
-  St::st(h, t, f4add(X1[a * d4 + c], X2[b * d4 + c]));
+  if constexpr (U == 2) St::st2(h, t, v[0], v[1]);
+  else St::st(h, t, v[0]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1013,9 +1021,14 @@ MOLCLR_API int molclr_atom_embed_fwd_bf16(const int64_t* x, const float* X1, con
   if (N == 0) return MOLCLR_OK;
   MOLCLR_REQUIRE(x && X1 && X2 && h, "atom_embed_fwd_bf16: null pointer");
   const int d4 = (int)(D / 4);
-  hipLaunchKernelGGL(k_atom_embed_fwd<StBF16>, dim3(molclr::ceil_div(N * d4, kT)), dim3(kT), 0,
-                     molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N, d4,
-                     n1, n2, status);
+  if (d4 % 2 == 0)
+    hipLaunchKernelGGL((k_atom_embed_fwd<StBF16, 2>), dim3(molclr::ceil_div(N * d4 / 2, kT)),
+                       dim3(kT), 0, molclr::as_stream(stream), x, (const float4*)X1,
+                       (const float4*)X2, h, N, d4, n1, n2, status);
+  else
+    hipLaunchKernelGGL((k_atom_embed_fwd<StBF16, 1>), dim3(molclr::ceil_div(N * d4, kT)), dim3(kT),
+                       0, molclr::as_stream(stream), x, (const float4*)X1, (const float4*)X2, h, N,
+                       d4, n1, n2, status);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
