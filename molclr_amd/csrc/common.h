@@ -25,6 +25,12 @@ int edge_tables_combine_zero(int layers, const float* const* E1s, const float* c
                              float* Ec, int64_t D, float* zero, int64_t n_zero,
                              molclr_stream_t stream);
 
+// molclr_hplanes_make_batch of one image (B: N x K row-major, ldb = K) whose
+// max launch also writes the per-tensor max slot of a second dense fp32
+// matrix x (n4 float4s) into `x_slot` (NT-Xent's rows and columns, one launch)
+int hplanes_make_and_max(const float* B, int64_t N, int64_t K, uint16_t* planes, const float* x,
+                         int64_t x_rows, int64_t x_cols, float* x_slot, hipStream_t stream);
+
 // Compute units of the current device (cached per device): the grid of a
 // persistent kernel.
 inline int cu_count() {

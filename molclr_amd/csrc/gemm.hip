@@ -1955,10 +1955,18 @@ __global__ __launch_bounds__(256) void k_planes_make_tiled(PlanesJobs jobs) {
     if (t >= jb.npad * kc) return;
     const int64_t n = t / kc, k0 = 8 * (t - n * kc);
     float v[8];
+    const float* src = jb.B + n * jb.ldb + k0;
+    if (n < jb.N && k0 + 8 <= jb.K && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+      const float4 a = reinterpret_cast<const float4*>(src)[0];
+      const float4 b = reinterpret_cast<const float4*>(src)[1];
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+      v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t k = k0 + j;
-      v[j] = (n < jb.N && k < jb.K) ? jb.B[n * jb.ldb + k] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int64_t k = k0 + j;
+        v[j] = (n < jb.N && k < jb.K) ? jb.B[n * jb.ldb + k] : 0.f;
+      }
     }
     planes_store8<H3>(jb, sh, n, k0, v);
     return;
@@ -2976,6 +2984,23 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }
+
+namespace molclr {
+int hplanes_make_and_max(const float* B, int64_t N, int64_t K, uint16_t* planes, const float* x,
+                         int64_t x_rows, int64_t x_cols, float* x_slot, hipStream_t s) {
+  MOLCLR_REQUIRE(N > 0 && K > 0 && B && planes && x && x_slot && x_rows > 0 && x_cols > 0,
+                 "hplanes_make_and_max: empty or null operand");
+  PlanesJobs jobs{};
+  jobs.j[0] = PlanesJob{B, planes, N, K, K, planes_npad(N), planes_kp(K), 0};
+  // job 1: x's max only -- no image (npad = kp = 0 puts its slot at x_slot)
+  jobs.j[1] = PlanesJob{x, reinterpret_cast<uint16_t*>(x_slot), x_rows, x_cols, x_cols, 0, 0, 0};
+  hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, 2), dim3(1024), 0, s, jobs);
+  hipLaunchKernelGGL(k_planes_make_tiled<true>, dim3((unsigned)planes_tiled_blocks(jobs.j[0]), 1),
+                     dim3(256), 0, s, jobs);
+  MOLCLR_LAUNCHED();
+  return MOLCLR_OK;
+}
+}  // namespace molclr
 
 MOLCLR_API int molclr_gemm_f32_h3_bits(const float* A, const float* amax, int a_row_parts,
                                        const uint16_t* hplanes, float* C, int64_t M, int64_t N,

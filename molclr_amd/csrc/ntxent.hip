@@ -728,13 +728,8 @@ int ntx_similarity(const float* rows, const float* cols, int64_t nrows, int64_t 
 int ntx_similarity_h3(const float* rows, const float* cols, int64_t nrows, int64_t ncols, int64_t C,
                       float* S, uint16_t* planes, float* rmax, hipStream_t s) {
   molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
-  hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(1024), 0, s, rows,
-                     nrows * C / 4, rmax, nullptr);
-  const float* bl[1] = {cols};
-  const int64_t nn[1] = {ncols}, kk[1] = {C}, ld[1] = {C};
-  const int km[1] = {0};
-  uint16_t* pl[1] = {planes};
-  int rc = molclr_hplanes_make_batch(1, bl, nn, kk, ld, km, pl, s);
+  // the columns' image and both max slots (rows', columns') in two launches
+  int rc = molclr::hplanes_make_and_max(cols, ncols, C, planes, rows, nrows, C, rmax, s);
   if (rc) return rc;
   return molclr_gemm_f32_h3(rows, rmax, 0, planes, S, nrows, ncols, C, C, ncols,
                             MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
