@@ -1861,24 +1861,6 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
   }
 }
 
-// planes[p][n][k] (p = hi, mid, lo) of B(k, n), zero beyond (N, K); one
-// thread per (n, k) of the padded [Npad][Kp] grid.
-__global__ void k_bplanes_make(const float* __restrict__ B, int64_t N, int64_t K, int64_t ldb,
-                               int kmajor, uint16_t* __restrict__ planes, int64_t npad,
-                               int64_t kp) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= npad * kp) return;
-  const int64_t n = t / kp, k = t - n * kp;
-  float v = 0.f;
-  if (n < N && k < K) v = kmajor ? B[k * ldb + n] : B[n * ldb + k];
-  uint32_t h, m, l;
-  split2(v, 0.f, h, m, l);
-  const int64_t ps = npad * kp;
-  planes[t] = (uint16_t)(h & 0xFFFFu);
-  planes[ps + t] = (uint16_t)(m & 0xFFFFu);
-  planes[2 * ps + t] = (uint16_t)(l & 0xFFFFu);
-}
-
 // Batched images (k_planes_make_tiled below): blockIdx.y = job.
 struct PlanesJob {
   const float* B;
@@ -1920,10 +1902,10 @@ __global__ __launch_bounds__(1024) void k_hplanes_max_batch(PlanesJobs jobs) {
 // data-gradient orientation) goes through a 64 (k) x 64 (n) LDS tile, read
 // as float4 runs along n and written as runs along k; a row-major one reads
 // its 8 k directly.  The per-job work is block-uniform (blockIdx.y = job).
-// Same split per element as k_bplanes_make (molclr_bplanes_make): bit-identical
-// images (tests/test_gpu_kernels.py::test_weight_images_bit_exact).  The
-// per-element batch kernels this replaces read K-major weights one cache line
-// per lane: c5's images took 44.9 us a step, c2's 7.3 + 15.1.
+// The per-element kernels this replaces read K-major weights one cache line
+// per lane (c5's images took 44.9 us a step, c2's 7.3 + 15.1); the images are
+// bit-identical to torch's round-to-nearest splits of the same values
+// (tests/test_gpu_kernels.py::test_weight_images_bit_exact).
 constexpr int kPT = 64;  // tile edge
 template <bool H3>
 __device__ __forceinline__ void planes_store8(const PlanesJob& jb, int sh, int64_t n, int64_t k0,
@@ -2702,9 +2684,10 @@ MOLCLR_API int molclr_bplanes_make(const float* B, int64_t N, int64_t K, int64_t
                                    uint16_t* planes, molclr_stream_t stream) {
   MOLCLR_REQUIRE(N > 0 && K > 0 && B && planes, "bplanes_make: empty or null operand");
   MOLCLR_REQUIRE(b_kmajor ? ldb >= N : ldb >= K, "bplanes_make: leading dimension too small");
-  const int64_t npad = planes_npad(N), kp = planes_kp(K);
-  hipLaunchKernelGGL(k_bplanes_make, dim3((unsigned)molclr::ceil_div(npad * kp, 256)), dim3(256), 0,
-                     molclr::as_stream(stream), B, N, K, ldb, b_kmajor, planes, npad, kp);
+  PlanesJobs jobs{};
+  jobs.j[0] = PlanesJob{B, planes, N, K, ldb, planes_npad(N), planes_kp(K), b_kmajor};
+  hipLaunchKernelGGL(k_planes_make_tiled<false>, dim3((unsigned)planes_tiled_blocks(jobs.j[0]), 1),
+                     dim3(256), 0, molclr::as_stream(stream), jobs);
   MOLCLR_LAUNCHED();
   return MOLCLR_OK;
 }

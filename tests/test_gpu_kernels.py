@@ -788,10 +788,11 @@ def _h3_planes(lib, W, N, K, kmajor, dev):
 @pytest.mark.parametrize("N,K", [(600, 300), (300, 600), (37, 45), (256, 512), (8, 1000)])
 @pytest.mark.parametrize("kmajor", [0, 1])
 def test_weight_images_bit_exact(dev, N, K, kmajor):
-    """The batched weight-image kernel (k_planes_make_tiled: an LDS tile for
-    K-major weights) writes exactly the per-element images: split-bf16 planes
-    equal molclr_bplanes_make's byte for byte; h3 planes equal fp16(B 2^sh)
-    and fp16(B 2^sh - hi) computed by torch with sh from max |B|, zero padding
+    """The weight-image kernel (k_planes_make_tiled: an LDS tile for K-major
+    weights) writes exactly the round-to-nearest splits torch computes from
+    the same values: split-bf16 planes hi = bf16(B), mid = bf16(B - hi),
+    lo = bf16(B - hi - mid), single and batched entry points alike; h3 planes
+    fp16(B 2^sh) and fp16(B 2^sh - hi) with sh from max |B|; zero padding
     included, for both orientations and ragged sizes."""
     import ctypes
     from molclr_amd import _lib
@@ -815,6 +816,17 @@ def test_weight_images_bit_exact(dev, N, K, kmajor):
                                          (ctypes.c_void_p * 1)(bat.data_ptr()), st) == 0
     torch.cuda.synchronize()
     assert torch.equal(one, bat)
+    kp = (K + 31) // 32 * 32
+    npad = nb // (6 * kp)
+    x = torch.zeros(npad, kp)
+    x[:N, :K] = B.T
+    hi = x.bfloat16()
+    r = x - hi.float()
+    mid = r.bfloat16()
+    lo = (r - mid.float()).bfloat16()
+    planes = one.view(torch.int16).view(3, npad, kp).cpu()
+    for q, ref in enumerate((hi, mid, lo)):
+        assert torch.equal(planes[q], ref.view(torch.int16)), q
     # h3: against torch's fp16 rounding of the scaled values
     nb = lib.molclr_hplanes_bytes(N, K)
     buf = torch.full((nb,), 0x5A, dtype=torch.uint8, device=dev)
