@@ -1867,6 +1867,7 @@ struct PlanesJob {
   uint16_t* planes;
   int64_t N, K, ldb, npad, kp;
   int kmajor;
+  float* slot2 = nullptr;  // max pass: a second image of the same matrix takes the same slot
 };
 constexpr int kPlanesBatch = 32;
 struct PlanesJobs {
@@ -1894,8 +1895,10 @@ __global__ __launch_bounds__(1024) void k_hplanes_max_batch(PlanesJobs jobs) {
         m = fmaxf(m, fabsf(jb.B[r * jb.ldb + c]));
   }
   m = block_max(m);
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     reinterpret_cast<float*>(jb.planes + 2 * jb.npad * jb.kp)[blockIdx.x * kMaxSlotStride] = m;
+    if (jb.slot2 != nullptr) jb.slot2[blockIdx.x * kMaxSlotStride] = m;
+  }
 }
 // Weight images of both kinds in one launch per batch, 8 consecutive k of one
 // n per item (16-byte stores per plane).  A K-major job (B stored [K][N]: the
@@ -2960,7 +2963,26 @@ MOLCLR_API int molclr_hplanes_make_batch(int count, const float* const* B, const
       most = e > most ? e : most;
     }
     hipStream_t s = molclr::as_stream(stream);
-    hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)n), dim3(1024), 0, s, jobs);
+    // the max pass once per matrix: both orientations of one weight (the
+    // forward's and the data gradient's image) read the same values, so the
+    // second takes the first's max (its slot written by the same block)
+    PlanesJobs mj{};
+    int nm = 0;
+    for (int i = 0; i < n; ++i) {
+      const PlanesJob& a = jobs.j[i];
+      const int64_t ra = a.kmajor ? a.K : a.N, ca = a.kmajor ? a.N : a.K;
+      int twin = -1;
+      for (int q = 0; q < nm && twin < 0; ++q) {
+        const PlanesJob& b = mj.j[q];
+        const int64_t rb = b.kmajor ? b.K : b.N, cb = b.kmajor ? b.N : b.K;
+        if (b.B == a.B && b.ldb == a.ldb && rb == ra && cb == ca && b.slot2 == nullptr) twin = q;
+      }
+      if (twin >= 0)
+        mj.j[twin].slot2 = reinterpret_cast<float*>(a.planes + 2 * a.npad * a.kp);
+      else
+        mj.j[nm++] = a;
+    }
+    hipLaunchKernelGGL(k_hplanes_max_batch, dim3(kHMaxParts, (unsigned)nm), dim3(1024), 0, s, mj);
     hipLaunchKernelGGL(k_planes_make_tiled<true>, dim3((unsigned)most, (unsigned)n), dim3(256), 0, s,
                        jobs);
   }

@@ -847,6 +847,38 @@ def test_weight_images_bit_exact(dev, N, K, kmajor):
     assert torch.equal(planes[1].view(torch.int16), lo.view(torch.int16))
 
 
+def test_h3_images_both_orientations_one_batch(dev):
+    """A batch holding both orientations of one weight (the forward's and the
+    data gradient's h3 image) runs the max pass once for the pair: every
+    image, max slot included, equals the one a single-image call writes."""
+    import ctypes
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(5)
+    W = (torch.randn(600, 300, generator=g) * 3).to(dev)  # [n_out][n_in], ld 300
+    V = torch.randn(64, 300, generator=g).to(dev)
+    # (matrix, N, K, kmajor): W as B(k = in, n = out), W as B(k = out, n = in), another weight
+    jobs = [(W, 600, 300, 0), (V, 64, 300, 0), (W, 300, 600, 1)]
+    bufs = [torch.full((lib.molclr_hplanes_bytes(n, k),), 0x5A, dtype=torch.uint8, device=dev)
+            for _, n, k, _ in jobs]
+    c = len(jobs)
+    st = ops._stream(W)
+    assert lib.molclr_hplanes_make_batch(
+        c, (ctypes.c_void_p * c)(*[m.data_ptr() for m, *_ in jobs]),
+        (ctypes.c_int64 * c)(*[n for _, n, _, _ in jobs]),
+        (ctypes.c_int64 * c)(*[k for _, _, k, _ in jobs]),
+        (ctypes.c_int64 * c)(*[m.shape[1] for m, *_ in jobs]),
+        (ctypes.c_int * c)(*[km for *_, km in jobs]),
+        (ctypes.c_void_p * c)(*[b.data_ptr() for b in bufs]), st) == 0
+    torch.cuda.synchronize()
+    for (m, n, k, km), b in zip(jobs, bufs):
+        one = _h3_planes(lib, m, n, k, km, dev)
+        torch.cuda.synchronize()
+        img = b.numel() - 2048 * 4  # the fp16 planes, then the max slot (64 entries, 32 floats apart)
+        assert torch.equal(one[:img], b[:img]), (n, k, km)
+        assert torch.equal(one[img:].view(torch.float32)[::32], b[img:].view(torch.float32)[::32])
+
+
 @pytest.mark.parametrize("M,N,K", H3_SHAPES)
 @pytest.mark.parametrize("rowwise", [0, 1])
 @pytest.mark.parametrize("epi", [0, 2, 3])
