@@ -528,6 +528,22 @@ def main():
                                "timing": f"dispatch events over {args.mfma_steps} extra steps "
                                          f"after the timed region"}
 
+    # the timed path against the eager step from the same state, on one of
+    # the run's batches (outside the timed region): the replay
+    # over its capacity bucket (padding rows) vs the batch at its own size
+    parity = None
+    if captured is not None:
+        parity = captured.replay_vs_eager(*views_of(args.warmup))  # a prepared batch
+        parity = {kk: (round(v, 9) if isinstance(v, float) else
+                       [v[0], round(v[1], 9)] if isinstance(v, list) else v)
+                  for kk, v in parity.items()}
+        parity["check"] = ("CapturedTrainStep.replay_vs_eager: one step from the same state, "
+                           "eager (own size) vs replayed (capacity bucket); "
+                           "tests/test_gpu_bench_parity.py holds loss <= 1e-6, gradients "
+                           "<= 1e-5 (bf16 1e-4) at this config")
+        parity["ok"] = bool(parity["loss_rel"] <= 1e-6 and parity["grad_rel"] <= (
+            1e-4 if precision == "bf16" else 1e-5) and parity["running_stats_rel"] <= 1e-6)
+
     roofline_ntxent_c4 = None
     if rank == 0 and not args.no_kernel_timing and precision != "bf16":
         roofline_ntxent_c4 = ntxent_c4_roofline(dev)
@@ -570,6 +586,7 @@ def main():
             "captures": captured.captures if captured is not None else 0,
             "captures_in_timed_region": captures_timed,
             "ranks": per_rank,
+            "parity": parity,
             "roofline": roofline, "roofline_mfma": roofline_mfma,
             "roofline_ntxent": roofline_ntxent, "roofline_ntxent_c4": roofline_ntxent_c4,
             "cpu_baseline": cpu,

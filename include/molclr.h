@@ -682,11 +682,14 @@ int molclr_ntxent_bwd(const float* rhat_rows, const int32_t* row_gidx, const flo
  * (similarity tiles recomputed in registers, online logsumexp, no S buffer);
  * 1 = S = rows cols^T as one split-bf16 GEMM (fp32 accuracy), then the row
  * logsumexp / the symmetric weights W as elementwise passes and dR = W cols as
- * a second GEMM (ncols % 4 == 0).  Automatic: 1 from nrows * ncols >= 2^20.
- * sim (formulation 1 only; may be NULL): the forward writes S [nrows][ncols]
- * there, and a backward given the same buffer uses it instead of recomputing
- * S.  molclr_ntxent_sim_bytes: its size, 0 when the formulation chosen for
- * (nrows, ncols, C, impl) keeps no S. */
+ * a second GEMM (ncols % 4 == 0); 2 = the h3 form of 1 (S by three fp16
+ * MFMAs per product, W^T through an LDS transpose, dR as an h3 weight-gradient
+ * product; nrows, ncols, C % 4 == 0, C <= 1024, ncols >= 1024).  Automatic: 0
+ * below 2^20 elements of S, 1 up to 2^22, 2 from there where its shapes allow.
+ * sim (formulations 1 and 2; may be NULL): the forward writes row-major S
+ * [nrows][ncols] there (both formulations), and a backward given the same
+ * buffer uses it instead of recomputing S.  molclr_ntxent_sim_bytes: its
+ * size, 0 when the formulation chosen for (nrows, ncols, C, impl) keeps no S. */
 size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl);
 int molclr_ntxent_fwd_impl(const float* rhat_rows, const int32_t* row_gidx,
                            const float* rhat_cols, int64_t nrows, int64_t ncols, int64_t C,

@@ -677,12 +677,12 @@ size_t ntx_gemm_ws(int64_t nrows, int64_t ncols, int64_t C) {
   return molclr_bplanes_bytes(ncols, C) + (size_t)nrows * ncols * sizeof(float) + g1 + g2 +
          4 * 256;
 }
-// shapes the h3 transposed formulation takes: the h3 GEMM's K = C <= 1024,
-// float4 rows of S^T, the weight-gradient kernel's long K (ncols >= 1024)
+// shapes the h3 formulation takes: the h3 GEMM's K = C <= 1024, float4 rows
+// of the row-major S, the weight-gradient kernel's long K (ncols >= 1024)
 bool ntx_h3_ok(int64_t nrows, int64_t ncols, int64_t C) {
   return nrows % 4 == 0 && ncols % 4 == 0 && C % 4 == 0 && C <= 1024 && ncols >= 1024;
 }
-// workspace of the h3 formulation: S^T / W^T, the rows' h3 image, the max
+// workspace of the h3 formulation: W^T (and S when not kept), the rows' h3 image, the max
 // slots of the columns and of W, the lse partials, the weight-gradient space
 size_t ntx_h3_ws(int64_t nrows, int64_t ncols, int64_t C) {
   // W^T, and S when the backward recomputes it
@@ -751,7 +751,9 @@ MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, in
 
 MOLCLR_API size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl) {
   if (nrows <= 0 || ncols <= 0 || C <= 0 || ntx_impl(nrows, ncols, C, impl) == 0) return 0;
-  return (size_t)nrows * ncols * sizeof(float);  // S (impl 1) or S^T (impl 2)
+  // row-major S [nrows][ncols] for both GEMM formulations (impl 1 and 2): the
+  // forward writes it, the backward reads it back
+  return (size_t)nrows * ncols * sizeof(float);
 }
 
 MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, const float* cols,

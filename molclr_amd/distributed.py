@@ -205,7 +205,9 @@ class OverlappedGradReducer:
         self.capture_events: list = []
         if self.cuda:
             self.stream = torch.cuda.Stream(device=self.flat.device)
-            self.events = self._new_events()
+            # eager steps' events: never handed to a graph
+            self.eager_events = self._new_events()
+            self.events = self.eager_events
 
     def _new_events(self):
         # the executor re-records these; a first record creates the handles
@@ -223,6 +225,10 @@ class OverlappedGradReducer:
             # handle is shared by two graphs
             self.events = self._new_events()
             self.capture_events = list(self.events)
+        elif self.cuda:
+            # an eager step (CapturedTrainStep._eager included) never
+            # re-records the handles the last captured graph holds
+            self.events = self.eager_events
         ops.set_grad_hook(self)
 
     def finish(self):

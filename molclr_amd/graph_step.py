@@ -362,7 +362,13 @@ class CapturedTrainStep:
             ent = self._capture(self.bucket(xis, xjs), (xis, xjs))  # stages this batch too
             self._insert(ent)
             return ent, True
-        self._graphs.move_to_end(id(ent))
+        if not self._multi_rank():
+            # one process: least-recently-replayed eviction.  Several ranks
+            # replay different buckets, so a replay must not reorder the set:
+            # captures (prepare / prepare_sizes) are inserted in lockstep and
+            # evicted in capture order, leaving every rank the same graphs
+            # and the same lookup() decisions
+            self._graphs.move_to_end(id(ent))
         return ent, False
 
     # -- data parallel: captures in lockstep ----------------------------------
@@ -474,6 +480,78 @@ class CapturedTrainStep:
         ops.bump_param_generation()
         self.last_graph = ent.graph
         return self.loss
+
+    # -- parity of the replayed step against the eager one ---------------------
+    def _state(self):
+        opt = self.optimizer
+        bns = [b for b in getattr(self.model, "batch_norms", [])]
+        return ([t.clone() for t in (opt.flat, opt.exp_avg, opt.exp_avg_sq, opt._step_dev)],
+                [(b.running_mean.clone(), b.running_var.clone(), b.num_batches_tracked.clone())
+                 for b in bns])
+
+    def _restore(self, state):
+        opt = self.optimizer
+        flat, bn = state
+        with torch.no_grad():
+            for dst, src in zip((opt.flat, opt.exp_avg, opt.exp_avg_sq, opt._step_dev), flat):
+                dst.copy_(src)
+            for b, (m, v, n) in zip(self.model.batch_norms, bn):
+                b.running_mean.copy_(m)
+                b.running_var.copy_(v)
+                b.num_batches_tracked.copy_(n)
+        ops.bump_param_generation()
+
+    def replay_vs_eager(self, xis, xjs) -> dict:
+        """One training step on (xis, xjs) run twice from the same state: the
+        eager step (the library's launches issued from the host, the batch at
+        its own size) and the replay of the captured graph that holds the
+        batch (capacity buckets: padding rows past the batch).  Returns the
+        differences -- loss, flat gradient and per parameter (norm-wise), the
+        BatchNorm running statistics and the parameters after Adam -- and
+        leaves the model where the replay took it.  molclr.py:107-128 is the
+        step; tests/test_gpu_bench_parity.py holds these to 1e-6 (loss) /
+        1e-5 (fp32 gradients) and bench.py records one in its line."""
+        def rel(a, b):
+            d = (a.double() - b.double()).norm().item()
+            n = b.double().norm().item()
+            return d / n if n > 0 else d
+
+        opt = self.optimizer
+        if self.lookup(xis, xjs) is None and self._multi_rank():
+            raise RuntimeError("replay_vs_eager: no captured graph holds this batch")
+        start = self._state()
+        eager_before = self.eager_steps
+        loss_e = self._eager(xis, xjs).clone()
+        self.eager_steps = eager_before
+        grad_e = opt.flat_grad.clone()
+        after_e = self._state()
+        self._restore(start)
+        ent = self.lookup(xis, xjs)
+        loss_r = self(xis, xjs).clone()
+        ent = ent or self.lookup(xis, xjs)
+        grad_r = opt.flat_grad.clone()
+        after_r = self._state()
+        torch.cuda.synchronize(self.device)
+        names = {id(q): k for k, q in self.model.named_parameters()}
+        per = {names[id(p)]: rel(grad_r[off:off + n], grad_e[off:off + n])
+               for p, off, n in opt.views}
+        # the bias feeding each BatchNorm has an exact gradient of 0 (the
+        # BatchNorm removes the column mean): rounding noise in either path
+        real = {k: v for k, v in per.items()
+                if not (k.endswith("mlp.2.bias")
+                        or (k.startswith("gnns.") and k.count(".") == 2 and k.endswith(".bias")))}
+        worst = max(real, key=real.get)
+        bn_rel = max([rel(a[0], b[0]) for a, b in zip(after_r[1], after_e[1])] +
+                     [rel(a[1], b[1]) for a, b in zip(after_r[1], after_e[1])] or [0.0])
+        n_nodes = int(xis.x.shape[0]) + int(xjs.x.shape[0])
+        return {"loss_eager": float(loss_e.item()), "loss_replay": float(loss_r.item()),
+                "loss_rel": abs(loss_r.item() - loss_e.item()) / max(abs(loss_e.item()), 1e-30),
+                "grad_rel": rel(grad_r, grad_e),
+                "grad_rel_worst_param": [worst, real[worst]],
+                "running_stats_rel": bn_rel,
+                "params_rel": rel(after_r[0][0], after_e[0][0]),
+                "nodes": n_nodes, "node_capacity": int(ent.graph.num_nodes),
+                "padding_rows": int(ent.graph.num_nodes) - n_nodes}
 
     @property
     def buckets(self) -> list:

@@ -32,6 +32,7 @@ import json
 import os
 import shutil
 import sys
+import warnings
 from datetime import datetime
 
 import numpy as np
@@ -124,11 +125,15 @@ class MolCLR(object):
         elif self.config['model_type'] == 'gcn':
             from .gcn_molclr import GCN
             if self.config.get('fp16_precision', False):
-                # the reference's apex O2 switch wraps whichever model is built
-                # (molclr.py:93-96); the GCN kernels have no bf16 storage path
-                raise NotImplementedError(
-                    "fp16_precision: True with model_type: gcn -- the GCN encoder runs in fp32 "
-                    "only (set fp16_precision: False)")
+                # The reference's switch only takes effect with apex installed
+                # (molclr.py:14-22,93-96,121-125); without it the reference
+                # prints a notice and trains in fp32.  The GCN kernels have no
+                # reduced-precision storage path, so this is the reference's
+                # no-apex behaviour: a warning, then fp32
+                warnings.warn("fp16_precision: True with model_type: gcn -- the GCN encoder has "
+                              "no reduced-precision path; training in fp32 (the reference's "
+                              "behaviour without apex, molclr.py:14-22,93-96)", RuntimeWarning,
+                              stacklevel=2)
             model = GCN(**self.config["model"]).to(self.device)
         else:
             raise ValueError('Undefined GNN model.')

@@ -1013,13 +1013,15 @@ def _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group):
     else:  # one all-gather carries the row lse and the rank's loss share
         from . import distributed as mdist
         lse_cols, loss = mdist.gather_lse_and_sum(lse, loss, group)
-    ctx.ntx = (cols, gidx, lse_cols, sim, B, C, float(temperature))
-    return loss
+    # tensors through save_for_backward by the caller (autograd's version
+    # checks; a retained graph can run backward twice), scalars on ctx
+    ctx.ntx = (B, C, float(temperature))
+    return loss, (cols, gidx, lse_cols, sim)
 
 
-def _ntxent_rows_backward(ctx, rhat, gloss):
+def _ntxent_rows_backward(ctx, rhat, gloss, cols, gidx, lse_cols, sim):
     """drhat (this process's rows) from the upstream scalar gradient."""
-    cols, gidx, lse_cols, sim, B, C, T = ctx.ntx
+    B, C, T = ctx.ntx
     dev = rhat.device
     n = rhat.shape[0]
     gloss = gloss.to(torch.float32).contiguous()
@@ -1032,7 +1034,6 @@ def _ntxent_rows_backward(ctx, rhat, gloss):
               ws_bytes, _lib.stream_of(dev), -1)
     if _TIMER is not None:  # dR = W R (and S again when the forward kept none)
         _TIMER.add("ntxent", (2.0 if sim.numel() else 4.0) * n * 2 * B * C)
-    ctx.ntx = None
     return drhat
 
 
@@ -1050,16 +1051,16 @@ class _NTXent(torch.autograd.Function):
         norm = torch.empty(n, dtype=torch.float32, device=R.device)
         _lib.call("molclr_ntxent_prep", R.data_ptr(), rhat.data_ptr(), norm.data_ptr(), n, C,
                   int(cosine), _lib.stream_of(R.device))
-        loss = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
-        ctx.save_for_backward(rhat, norm)
+        loss, kept = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
+        ctx.save_for_backward(rhat, norm, *kept)
         ctx.cosine = int(cosine)
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        rhat, norm = ctx.saved_tensors
+        rhat, norm, *kept = ctx.saved_tensors
         n, C = rhat.shape
-        drhat = _ntxent_rows_backward(ctx, rhat, gloss)
+        drhat = _ntxent_rows_backward(ctx, rhat, gloss, *kept)
         dR = torch.empty_like(rhat)
         _lib.call("molclr_ntxent_prep_bwd", drhat.data_ptr(), rhat.data_ptr(), norm.data_ptr(),
                   dR.data_ptr(), n, C, ctx.cosine, _lib.stream_of(rhat.device))
@@ -1087,16 +1088,16 @@ class _NTXentPairNormalized(torch.autograd.Function):
         _lib.call("molclr_ntxent_prep_pair", z.data_ptr(), y.data_ptr(), rhat.data_ptr(),
                   n1.data_ptr(), n2.data_ptr(), n // 2, C, float(eps), int(cosine),
                   _lib.stream_of(dev))
-        loss = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
-        ctx.save_for_backward(y, rhat, n1, n2)
+        loss, kept = _ntxent_rows_forward(ctx, rhat, batch_size, temperature, group)
+        ctx.save_for_backward(y, rhat, n1, n2, *kept)
         ctx.cosine, ctx.eps = int(cosine), float(eps)
         return loss
 
     @staticmethod
     def backward(ctx, gloss):
-        y, rhat, n1, n2 = ctx.saved_tensors
+        y, rhat, n1, n2, *kept = ctx.saved_tensors
         n, C = rhat.shape
-        drhat = _ntxent_rows_backward(ctx, rhat, gloss)
+        drhat = _ntxent_rows_backward(ctx, rhat, gloss, *kept)
         dz = torch.empty_like(rhat)
         _lib.call("molclr_ntxent_prep_pair_bwd", drhat.data_ptr(), rhat.data_ptr(), n2.data_ptr(),
                   y.data_ptr(), n1.data_ptr(), dz.data_ptr(), n // 2, C, ctx.eps, ctx.cosine,

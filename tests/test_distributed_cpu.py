@@ -249,3 +249,92 @@ def test_capture_sizes_union_across_ranks():
         p.join(timeout=60)
     want = [(3100, 9100), (3000, 9000), (2800, 8000)]
     assert all(got[r] == want for r in range(3)), got
+
+
+def _plan_worker(rank, world, port, q):
+    """CapturedTrainStep's capture planning (lookup / prepare_sizes / replay /
+    eviction) on a stub whose captures record nothing (no GPU): what each
+    rank decides, step by step."""
+    import types
+    from collections import OrderedDict
+
+    import torch.distributed as dist
+
+    from molclr_amd.graph_step import CapturedTrainStep, _Captured
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = object.__new__(CapturedTrainStep)
+        st.group = dist.group.WORLD
+        st.device = torch.device("cpu")
+        st.node_quantum, st.edge_quantum, st.node_slack, st.edge_headroom = 256, 2048, 512, 0.04
+        st.max_graphs = 2
+        st._graphs = OrderedDict()
+        st.captures = st.replays = st.eager_steps = 0
+        st.loss, st.last_graph = torch.zeros(()), None
+        st.optimizer = types.SimpleNamespace(sync_lr=lambda: None)
+        log = []
+
+        def capture(key, pair=None):
+            st.captures += 1
+            log.append(("capture", key[:2]))
+            g = types.SimpleNamespace(num_nodes=key[0], num_edges=key[1],
+                                      graphs_per_segment=list(key[2:]), stage=lambda v: None)
+            return _Captured(g, types.SimpleNamespace(replay=lambda: None))
+
+        def eager(xis, xjs):
+            st.eager_steps += 1
+            log.append(("eager",))
+            return None
+
+        st._capture, st._eager = capture, eager
+
+        class _View:
+            def __init__(self, n, e):
+                self.x = torch.empty(n, 0)
+                self.edge_index = torch.empty(2, e)
+                self.num_graphs = 4
+
+        # three size classes 1024 nodes apart (each needs its own capture)
+        sizes = [(1000, 3000), (2000, 6000), (3000, 9000)]
+        st.prepare_sizes(sizes[:2], 4, 4)            # captures 2000, then 1000
+        # ranks replay DIFFERENT buckets (rank 0 the large one, rank 1 the small)
+        mine = sizes[1] if rank == 0 else sizes[0]
+        for _ in range(3):
+            st(_View(*mine), _View(0, 0))
+        st.prepare_sizes([sizes[2]], 4, 4)           # a third capture: one eviction
+        after = [(g.graph.num_nodes, g.graph.num_edges) for g in st._graphs.values()]
+        # a batch of every class on every rank: replay or (lockstep-safe) eager
+        for n, e in sizes:
+            st(_View(n, e), _View(0, 0))
+        st.prepare_sizes(sizes, 4, 4)                # the union again
+        final = [(g.graph.num_nodes, g.graph.num_edges) for g in st._graphs.values()]
+        q.put((rank, after, final, st.captures, log))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_capture_plan_stays_in_lockstep_when_ranks_replay_different_buckets():
+    """replays used to reorder the LRU, so after an eviction ranks
+    could hold different graph sets and one rank would capture (recording
+    collectives) while another did not.  With several ranks, eviction now
+    follows capture order: every rank keeps the same graphs and makes the
+    same capture decisions, whatever buckets it replayed (gloo, world 2,
+    max_graphs 2)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a0, f0, c0, log0 = got[0]
+    a1, f1, c1, log1 = got[1]
+    assert a0 == a1 and f0 == f1 and c0 == c1
+    caps = lambda log: [e for e in log if e[0] == "capture"]  # noqa: E731
+    assert caps(log0) == caps(log1)
+    assert len(a0) == 2  # max_graphs

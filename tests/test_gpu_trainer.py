@@ -131,12 +131,34 @@ def test_out_of_vocabulary_atoms_raise(dev, tmp_path, monkeypatch):
         device_graph(bad2).check()
 
 
-def test_gcn_fp16_precision_is_refused(dev, tmp_path, monkeypatch):
+def test_gcn_fp16_precision_trains_in_fp32(dev, tmp_path, monkeypatch):
+    """model_type gcn + fp16_precision True: the reference trains it in fp32
+    when apex is absent (molclr.py:14-22,93-96,121-125: a printed notice, then
+    the plain backward).  Here: a RuntimeWarning, then the same fp32 training
+    as fp16_precision False -- the first logged loss is bit-identical."""
+    import json
     from molclr_amd.molclr import MolCLR
     monkeypatch.chdir(tmp_path)
-    config = _config("node", "synthetic:64", tmp_path, model_type="gcn", fp16=True)
-    with pytest.raises(NotImplementedError):
-        MolCLR(_wrapper(config), config).build_model()
+    losses = {}
+    for fp16 in (True, False):
+        config = _config("node", "synthetic:64", tmp_path / str(fp16), model_type="gcn", fp16=fp16)
+        torch.manual_seed(0)
+        trainer = MolCLR(_wrapper(config), config)
+        if fp16:
+            with pytest.warns(RuntimeWarning, match="fp32"):
+                model = trainer.build_model()
+        else:
+            model = trainer.build_model()
+        assert all(p.dtype == torch.float32 for p in model.parameters())
+        torch.manual_seed(0)
+        out = MolCLR(_wrapper(config), config).train()
+        assert all(torch.isfinite(p).all() for p in out.parameters())
+        logs = list((tmp_path / str(fp16) / "ckpt").glob("*/scalars.jsonl"))
+        if logs:
+            losses[fp16] = [json.loads(x)["value"] for x in logs[0].read_text().splitlines()
+                            if json.loads(x)["tag"] == "train_loss"]
+    if losses:
+        assert losses[True][0] == losses[False][0]
 
 
 @pytest.mark.parametrize("aug", ["node", "subgraph"])
