@@ -486,6 +486,17 @@ int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const
                        int epilogue_flags, const float* bias, const float* aux, int64_t ldaux,
                        const uint32_t* mask_bits, float* cmax, float* crow, float* amax_out,
                        molclr_stream_t stream);
+/* molclr_gemm_f32_h3_bits with the kernel chosen per call (tests): impl 0 =
+ * automatic, 1 = k_gemm_pp / k_gemm_q6, 2 = k_gemm_bs (K in (288, 304],
+ * N > 320, C float4-aligned, ReLU mask as bits; MOLCLR_ERR_UNSUPPORTED
+ * otherwise).  Every kernel gives bit-identical C, bits and maxima; the row
+ * maxima (crow) are molclr_gemm_row_parts(N) arrays whatever the kernel. */
+int molclr_gemm_f32_h3_impl(const float* A, const float* amax, int a_row_parts,
+                            const uint16_t* hplanes, float* C, int64_t M, int64_t N, int64_t K,
+                            int64_t lda, int64_t ldc, int epilogue_flags, const float* bias,
+                            const float* aux, int64_t ldaux, const uint32_t* mask_bits, float* cmax,
+                            float* crow, float* amax_out, uint32_t* relu_bits,
+                            molclr_stream_t stream, int impl);
 /* molclr_gemm_f32_h3 whose BIAS_RELU product also writes C's ReLU mask as
  * bits (relu_bits: molclr_gemm_f32_bplanes_max's layout, may be NULL): the h3
  * forward's first GIN-MLP product, whose mask the dz1 product reads back. */
@@ -684,10 +695,13 @@ int molclr_ntxent_bwd(const float* rhat_rows, const int32_t* row_gidx, const flo
  * logsumexp / the symmetric weights W as elementwise passes and dR = W cols as
  * a second GEMM (ncols % 4 == 0); 2 = the h3 form of 1 (S by three fp16
  * MFMAs per product, W^T through an LDS transpose, dR as an h3 weight-gradient
- * product; nrows, ncols, C % 4 == 0, C <= 1024, ncols >= 1024).  Automatic: 0
+ * product; nrows, ncols, C % 4 == 0, C <= 1024, ncols >= 1024); 3 = the
+ * transposed form of 2 (S^T = cols rows^T kept [ncols][nrows], the row
+ * logsumexp down its columns, W^T elementwise in S^T's layout: no transpose
+ * pass; same shapes as 2).  Automatic: 0
  * below 2^20 elements of S, 1 up to 2^22, 2 from there where its shapes allow.
- * sim (formulations 1 and 2; may be NULL): the forward writes row-major S
- * [nrows][ncols] there (both formulations), and a backward given the same
+ * sim (formulations 1, 2, 3; may be NULL): the forward writes row-major S
+ * [nrows][ncols] there (1 and 2) or S^T [ncols][nrows] (3), and a backward given the same
  * buffer uses it instead of recomputing S.  molclr_ntxent_sim_bytes: its
  * size, 0 when the formulation chosen for (nrows, ncols, C, impl) keeps no S. */
 size_t molclr_ntxent_sim_bytes(int64_t nrows, int64_t ncols, int64_t C, int impl);

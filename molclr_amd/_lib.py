@@ -86,6 +86,8 @@ SIGNATURES = {
                                    _P, _I64, _P, _P, _P, _P, _P]),
     "molclr_gemm_f32_h3_bits": (c_int, [_P, _P, c_int, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
                                         _P, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "molclr_gemm_f32_h3_impl": (c_int, [_P, _P, c_int, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,
+                                        _P, _P, _I64, _P, _P, _P, _P, _P, _P, c_int]),
     "molclr_linear_wgrad_h3_groups": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64,
                                               c_int, _P, c_size_t, _P, c_int]),
     "molclr_linear_wgrad_h3": (c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _I64, _I64, c_int,

@@ -1626,6 +1626,325 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 }
 
 // ---------------------------------------------------------------------------
+// "bs": B-stationary h3 product for K in (288, 304] (the c2 / c3 width 300:
+// lin1 = agg W1^T and dz1 = dz W2, 600 columns).  A 128-column tile of the
+// weight's fp16 planes for the WHOLE K (9 full 32-deep steps and the first 16
+// k of the last: 152 KB) is copied into LDS once per block by LDS-DMA; the
+// block (one per CU, 8 waves) then streams its row slabs of A through
+// registers -- load two steps ahead, split, MFMA against B fragments read from
+// LDS -- with no barrier after the prologue (k_gemm_pp stages B per K step
+// behind two barriers and its waves stalled half their lifetime,
+// profiles/r5_pmc_h3_lin1).  Same fragments, the same three products in the
+// same order as k_gemm_pp's swapped form: C, the ReLU bits, max |C|, max |A|
+// and the row maxima are bit-identical to it (tests/test_gpu_kernels.py);
+// the row maxima come as ceil(N / 128) partial arrays (molclr_gemm_row_parts).
+// Blocks: ceil(N / 128) column tiles x (CUs / tiles) row groups, the tiles of
+// a row group adjacent on one XCD (they read the same A rows).
+// ---------------------------------------------------------------------------
+constexpr int kBN = 128;  // columns per tile (TN = 4)
+constexpr int kTN = 4;
+constexpr int kFullImg = 2 * kBN * XK;  // fp16 elements of one full K step (both planes)
+constexpr int kHalfImg = 2 * kBN * 16;  // ... of a last step holding k0 .. k0+15 only
+
+// offset (fp16 units) of chunk c (0 or 1) of row `row` in a half-step plane:
+// 32 B per row, the two chunks swapped on alternate row quads
+__device__ __forceinline__ int hoff(int row, int c) { return row * 16 + ((c ^ ((row >> 2) & 1)) << 3); }
+
+// Pipelined across slabs:  A wave's next slab --
+// its row maxima, ReLU-mask words and first two A steps -- is issued during
+// the current slab's last two steps and waited for BEFORE the current
+// slab's C stores, so the next slab's first two steps run without a memory
+// wait; the stores then drain under those steps' MFMAs (any wait for a load
+// while stores are pending is a full drain on this target).  The first
+// slab's loads go out with the B image's LDS-DMA: one latency for both.
+template <int EPI, int H3, int S, bool HALF, int W = 8>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4))) void k_gemm_bs(
+    const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux, int accumulate,
+    const float* __restrict__ amax, const float* __restrict__ bmax, float* __restrict__ cmax,
+    float* __restrict__ crow, float* __restrict__ amax_out, int arow_parts,
+    uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in, int64_t bits_ld,
+    int ntn, int groups) {
+  static_assert(S % 2 == 0 && S >= 4, "two A register sets, steps in pairs");
+  constexpr int NFULL = HALF ? S - 1 : S;
+  constexpr int IMG = NFULL * kFullImg + (HALF ? kHalfImg : 0);
+  __shared__ __attribute__((aligned(16))) uint16_t img[IMG];
+  __shared__ __attribute__((aligned(16))) float bsh[kBN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 31, lh = lane >> 5;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = L % ntn, grp = L / ntn;
+  const int64_t n0 = (int64_t)tile * kBN;
+  const int64_t slabs = (M + 31) / 32;
+  const int64_t s_beg = slabs * grp / groups, s_end = slabs * (grp + 1) / groups;
+  constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
+
+  const __amdgpu_buffer_rsrc_t brsrc = make_rsrc(Bp, (int64_t)2 * npad * kp * 2);
+  {
+    constexpr int CHF = NFULL * 2 * (kBN / 16);
+    for (int q = w; q < CHF; q += W) {
+      const int st = q / (2 * (kBN / 16)), rem = q % (2 * (kBN / 16));
+      const int pl = rem / (kBN / 16), r0 = (rem % (kBN / 16)) * 16;
+      const int row = r0 + (lane >> 2), c = lane & 3;
+      int64_t gr = n0 + row;
+      gr = gr < npad ? gr : npad - 1;
+      const uint32_t voff = (uint32_t)(((pl * npad + gr) * kp + 32 * st + 8 * (c ^ ((row >> 2) & 3))) * 2);
+      buf_lds16(brsrc, img + st * kFullImg + pl * kBN * XK + r0 * XK, voff, 0);
+    }
+    if constexpr (HALF) {
+      constexpr int CHH = 2 * (kBN / 32);
+      for (int q = w; q < CHH; q += W) {
+        const int pl = q / (kBN / 32), r0 = (q % (kBN / 32)) * 32;
+        const int row = r0 + (lane >> 1), c = lane & 1;
+        int64_t gr = n0 + row;
+        gr = gr < npad ? gr : npad - 1;
+        const uint32_t voff =
+            (uint32_t)(((pl * npad + gr) * kp + 32 * (S - 1) + 8 * (c ^ ((row >> 2) & 1))) * 2);
+        buf_lds16(brsrc, img + NFULL * kFullImg + pl * kBN * 16 + r0 * 16, voff, 0);
+      }
+    }
+    if constexpr (HAS_BIAS) {
+      if (tid < kBN) bsh[tid] = n0 + tid < N ? bias[n0 + tid] : 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = make_rsrc(A, M * lda * 4);
+  float cm = 0.f, ain = 0.f;
+
+  // per-slab state: the lane's A row, its raw row-maximum words (folded when
+  // the slab starts), the ReLU-mask words
+  int64_t arow = 0;
+  uint32_t avoff = 0;
+  float rw[8];
+  uint32_t mws[kTN];
+  auto meta_issue = [&](int64_t slab) {
+    arow = slab * 32 + li;
+    arow = arow < M ? arow : M - 1;
+    avoff = (uint32_t)((arow * lda + 16 * lh) * 4);
+    if constexpr (H3 == 2) {
+      if (arow_parts < 0) {  // per-wave pairs: <= 3 float2 words of the producer
+        const int d4 = -arow_parts;
+        const int64_t s0 = arow * d4, e0 = s0 + d4 - 1;
+        const float2* wm = reinterpret_cast<const float2*>(amax);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int64_t wi = (s0 >> 6) + q;
+          const float2 v = wm[wi <= (e0 >> 6) ? wi : (s0 >> 6)];
+          rw[2 * q] = v.x;
+          rw[2 * q + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) rw[p] = amax[(int64_t)(p < arow_parts ? p : 0) * M + arow];
+      }
+    }
+    if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+#pragma unroll
+      for (int b = 0; b < kTN; ++b) {
+        int64_t nb = n0 + 32 * b;
+        nb = nb < N ? nb : 0;
+        mws[b] = bits_in[(nb >> 5) * bits_ld + arow];
+      }
+    }
+  };
+  auto row_shift = [&]() -> int {
+    if constexpr (H3 == 1) return h3_shift(amax);
+    float m = 0.f;
+    if (arow_parts < 0) {
+      const int d4 = -arow_parts;
+      const int64_t s0 = arow * d4, e0 = s0 + d4 - 1;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t wi = (s0 >> 6) + q;
+        if (wi <= (e0 >> 6)) m = fmaxf(m, (wi << 6) / d4 == arow ? rw[2 * q] : rw[2 * q + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (p < arow_parts) m = fmaxf(m, rw[p]);
+    }
+    return h3_shift_of(m);
+  };
+  auto load_a = [&](int r, float4(&v)[4]) {
+    const uint32_t soff = (uint32_t)(r * BK * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = buf_ld4(arsrc, avoff + 16 * j, soff);
+  };
+
+  float4 ar0[4], ar1[4];
+  u32x4 fr[2][2];
+  f32x16 acc[kTN];
+  auto compute = [&](const uint16_t* base) {
+    constexpr int NB = 2 * kTN;
+    auto rd = [&](int k, u32x4(&f)[2]) {
+      const int s1 = k / kTN, b1 = k % kTN;
+      const int row = 32 * b1 + li;
+      f[0] = *reinterpret_cast<const u32x4*>(base + xoff(row, 2 * lh + s1));
+      f[1] = *reinterpret_cast<const u32x4*>(base + kBN * XK + xoff(row, 2 * lh + s1));
+    };
+    u32x4 q[2][2];
+    rd(0, q[0]);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int s = k / kTN, b = k % kTN;
+      if (k + 1 < NB) rd(k + 1, q[(k + 1) & 1]);
+      acc[b] = mfma_h3_t(__builtin_bit_cast(f16x8, fr[s][0]), __builtin_bit_cast(f16x8, fr[s][1]),
+                         __builtin_bit_cast(f16x8, q[k & 1][0]), __builtin_bit_cast(f16x8, q[k & 1][1]),
+                         acc[b]);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+#pragma unroll
+      for (int mm = 0; mm < 3; ++mm) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (k + 1 < NB && mm < 2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+  };
+  auto compute_half = [&]() {
+    const uint16_t* base = img + NFULL * kFullImg;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 2 * kTN; ++k) {
+      const int s = k / kTN, b = k % kTN;
+      const int row = 32 * b + li;
+      const u32x4 h = *reinterpret_cast<const u32x4*>(base + hoff(row, s));
+      const u32x4 l = *reinterpret_cast<const u32x4*>(base + kBN * 16 + hoff(row, s));
+      acc[b] = mfma_h3_t(__builtin_bit_cast(f16x8, fr[s][0]), __builtin_bit_cast(f16x8, fr[s][1]),
+                         __builtin_bit_cast(f16x8, lh ? z : h), __builtin_bit_cast(f16x8, lh ? z : l),
+                         acc[b]);
+    }
+  };
+  auto split = [&](float4(&a)[4], int r, int sha) {
+    if (amax_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        ain = fmaxf(ain, fmaxf(fmaxf(fabsf(a[j].x), fabsf(a[j].y)), fmaxf(fabsf(a[j].z), fabsf(a[j].w))));
+    }
+    if (r == S - 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((int64_t)r * BK + 16 * lh + 4 * j >= K) a[j] = f4zero();
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) hsplit8(a[2 * s], a[2 * s + 1], sha, fr[s][0], fr[s][1]);
+  };
+
+  int64_t slab = s_beg + w;
+  if (slab < s_end) {
+    meta_issue(slab);
+    load_a(0, ar0);
+    load_a(1, ar1);
+  }
+  vm_wait<0>();  // B image, the first slab's row maxima and two A steps
+  __syncthreads();
+  const int shb = h3_shift(bmax);
+  int sha = slab < s_end ? row_shift() : 0;
+  int64_t mw = slab * 32;
+
+  for (; slab < s_end; slab += W) {
+    const int64_t next = slab + W;
+    const bool more = next < s_end;
+#pragma unroll
+    for (int b = 0; b < kTN; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+    uint32_t mcur[kTN];
+#pragma unroll
+    for (int b = 0; b < kTN; ++b) mcur[b] = mws[b];
+    // steps 0 .. S-3: A(r) waited for (steps 0 and 1: already landed), A(r+2) issued
+#pragma unroll 1
+    for (int r = 0; r < S - 2; r += 2) {
+      if (r > 0) vm_wait<4>();
+      split(ar0, r, sha);
+      load_a(r + 2, ar0);
+      compute(img + r * kFullImg);
+      if (r > 0) vm_wait<4>();
+      split(ar1, r + 1, sha);
+      load_a(r + 3, ar1);
+      compute(img + (r + 1) * kFullImg);
+    }
+    // steps S-2, S-1: the next slab's state and first two A steps go out
+    const int sha_cur = sha;
+    const int64_t mw_cur = mw;
+    {
+      float4(&a8)[4] = ar0;
+      float4(&a9)[4] = ar1;
+      vm_wait<4>();
+      split(a8, S - 2, sha_cur);
+      if (more) {
+        meta_issue(next);
+        load_a(0, ar0);
+      }
+      compute(img + (S - 2) * kFullImg);
+      if (more) vm_wait<8>();  // A(S-1) landed; the next slab's loads may be in flight
+      else vm_wait<0>();
+      split(a9, S - 1, sha_cur);
+      if (more) load_a(1, ar1);
+      if (HALF) compute_half();
+      else compute(img + (S - 1) * kFullImg);
+    }
+    // the next slab's loads landed before any store is issued
+    vm_wait<0>();
+    if (more) {
+      sha = row_shift();
+      mw = next * 32;
+    }
+
+    // ---- epilogue of this slab
+    const int64_t m = mw_cur + li;
+    const float sc = __builtin_ldexpf(1.f, -(sha_cur + shb));
+    float rmax = 0.f;
+#pragma unroll
+    for (int b = 0; b < kTN; ++b) {
+      const int64_t nb = n0 + 32 * b;
+      if (nb >= N) break;
+      uint32_t pos = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cb = 8 * q + 4 * lh;
+        const int64_t n = nb + cb;
+        if (m < M && n < N) {
+          float* o = C + m * ldc + n;
+          float4 v = make_float4(acc[b][4 * q] * sc, acc[b][4 * q + 1] * sc, acc[b][4 * q + 2] * sc,
+                                 acc[b][4 * q + 3] * sc);
+          if constexpr (HAS_BIAS) {
+            v = f4add(v, *reinterpret_cast<const float4*>(bsh + 32 * b + cb));
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+            const uint32_t mk = (mcur[b] >> cb) & 15u;
+            v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                            mk & 8u ? v.w : 0.f);
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+          *reinterpret_cast<float4*>(o) = v;
+          rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          pos |= ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+                  (v.w > 0.f ? 8u : 0u)) << cb;
+        }
+      }
+      if (bits_out != nullptr) {
+        pos |= __shfl_xor(pos, 32, 64);
+        if (lh == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = pos;
+      }
+    }
+    if (crow != nullptr) {
+      const float v = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
+      if (lh == 0 && m < M) crow[(int64_t)tile * M + m] = v;
+    }
+    cm = fmaxf(cm, rmax);
+  }
+  if (cmax != nullptr) absmax_publish(cm, cmax);
+  if (amax_out != nullptr) absmax_publish(ain, amax_out);
+}
+
+// ---------------------------------------------------------------------------
 // "w6": the weight gradient of a Linear, C[m][n] = Σ_k A[k][m] B[k][n] with
 // both operands K-major (K = rows: dW = dY^T X), optionally with the column
 // sums Σ_k A[k][m] (the bias gradient, A = dY) taken from the staged tiles.
@@ -2431,7 +2750,72 @@ int dispatch_q6_tn(int epi, const Args& a, int64_t npad, hipStream_t s) {
          : tn == 4 ? dispatch_q6<4, H3>(epi, a, npad, s)
                    : dispatch_q6<2, H3>(epi, a, npad, s);
 }
+// The h3 products k_gemm_bs takes: K in (288, 304] (its LDS image), wide
+// (> 320 columns), float4-aligned C, ReLU masks as bits, row maxima as a slot,
+// <= 8 partial arrays or per-wave pairs.  MOLCLR_GEMM_BS=0 keeps pp / q6;
+// g_bs_force (molclr_gemm_f32_h3_impl): 1 never, 2 only bs.
+int g_bs_force = 0;
+bool bs_shape_ok(const Args& a, int64_t npad, int epi, int h3) {
+  if (h3 == 0 || a.N <= 320 || a.K <= 288 || a.K > 304 || a.ldb != 320) return false;
+  if (a.lda % 4 || a.ldc % 4 || a.N % 4 || (reinterpret_cast<uintptr_t>(a.C) & 15)) return false;
+  if (a.M * a.lda * 4 >= (1ll << 31) || 2 * npad * a.ldb * 2 >= (1ll << 31)) return false;
+  if (epi == MOLCLR_EPI_RELU_MASK && a.bits_in == nullptr) return false;
+  if (h3 == 2 && (a.arow_parts > 8 || (a.arow_parts < 0 && -a.arow_parts < 64))) return false;
+  return true;
+}
+bool use_bs(const Args& a, int64_t npad, int epi, int h3) {
+  static const bool off = [] {
+    const char* e = getenv("MOLCLR_GEMM_BS");
+    return e != nullptr && e[0] == '0';
+  }();
+  if (g_bs_force == 1 || (off && g_bs_force != 2)) return false;
+  return bs_shape_ok(a, npad, epi, h3);
+}
+template <int EPI, int H3>
+void launch_bs(const Args& a, int64_t npad, hipStream_t s) {
+  const int ntn = (int)((a.N + kBN - 1) / kBN);
+  int groups = molclr::cu_count() / ntn;
+  groups = groups < 1 ? 1 : groups;
+  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs<EPI, H3, 10, true>), dim3((unsigned)(ntn * groups)),
+                       dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc,
+                       a.bias, a.aux, a.ldaux, a.accumulate, a.amax, a.bmax, a.cmax, a.crow,
+                       a.amax_out, a.arow_parts, a.bits_out, a.bits_in, a.bits_ld, ntn, groups);
+}
+template <int H3>
+int dispatch_bs(int epi, const Args& a, int64_t npad, hipStream_t s) {
+  switch (epi) {
+    case MOLCLR_EPI_NONE: launch_bs<MOLCLR_EPI_NONE, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS: launch_bs<MOLCLR_EPI_BIAS, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS_RELU: launch_bs<MOLCLR_EPI_BIAS_RELU, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_RELU_MASK: launch_bs<MOLCLR_EPI_RELU_MASK, H3>(a, npad, s); return 0;
+    default: return -1;
+  }
+}
+// partial row-max arrays of an h3 product's C (crow): one per 128 columns for
+// the wide products (k_gemm_bs's tiles); pp / q6, whose tiles may be 160
+// wide, zero the arrays they do not write
+int64_t crow_parts(int64_t N) { return N > 320 ? (N + kBN - 1) / kBN : q6_col_tiles(N); }
+
 int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, int h3 = 0) {
+  if (h3 != 0 && use_bs(a, npad, epi, h3)) {
+    const int rc = h3 == 2 ? dispatch_bs<2>(epi, a, npad, s) : dispatch_bs<1>(epi, a, npad, s);
+    if (rc) {
+      molclr::set_error("gemm_f32_h3: no bs kernel for epilogue %d", epi);
+      return MOLCLR_ERR_UNSUPPORTED;
+    }
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  if (g_bs_force == 2) {
+    molclr::set_error("gemm_f32_h3_impl: the bs kernel does not take this product");
+    return MOLCLR_ERR_UNSUPPORTED;
+  }
+  if (a.crow != nullptr && crow_parts(a.N) > q6_col_tiles(a.N)) {
+    const int64_t w = q6_col_tiles(a.N);
+    const hipError_t e = molclr::zero_async(a.crow + w * a.M,
+                                            (size_t)(crow_parts(a.N) - w) * a.M * sizeof(float), s);
+    if (e != hipSuccess) return (int)e;
+  }
   const int rc = h3 == 2   ? dispatch_q6_tn<2>(epi, a, npad, s)
                  : h3 == 1 ? dispatch_q6_tn<1>(epi, a, npad, s)
                            : dispatch_q6_tn<0>(epi, a, npad, s);
@@ -2810,7 +3194,7 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
       blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
       hipLaunchKernelGGL(k_absmax_rows, dim3((unsigned)blocks), dim3(256), 0, s, C, M, N, ldc, rows,
                          cmax);
-      for (int64_t p = 1; p < q6_col_tiles(N); ++p)
+      for (int64_t p = 1; p < crow_parts(N); ++p)
         (void)molclr::copy_async(rows + p * M, rows, (size_t)M * sizeof(float), s);
     }
     MOLCLR_LAUNCHED();
@@ -2827,7 +3211,7 @@ MOLCLR_API int molclr_gemm_f32_bplanes_max(const float* A, const uint16_t* plane
   return run_q6(a, npad, epilogue, s, 0);
 }
 
-MOLCLR_API int64_t molclr_gemm_row_parts(int64_t N) { return q6_col_tiles(N); }
+MOLCLR_API int64_t molclr_gemm_row_parts(int64_t N) { return crow_parts(N); }
 
 MOLCLR_API int molclr_gemm_f32_bplanes(const float* A, const uint16_t* planes, float* C, int64_t M,
                                        int64_t N, int64_t K, int64_t lda, int64_t ldc,
@@ -3058,6 +3442,22 @@ MOLCLR_API int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_p
   return molclr_gemm_f32_h3_bits(A, amax, a_row_parts, hplanes, C, M, N, K, lda, ldc,
                                  epilogue_flags, bias, aux, ldaux, mask_bits, cmax, crow, amax_out,
                                  nullptr, stream);
+}
+
+MOLCLR_API int molclr_gemm_f32_h3_impl(const float* A, const float* amax, int a_row_parts,
+                                       const uint16_t* hplanes, float* C, int64_t M, int64_t N,
+                                       int64_t K, int64_t lda, int64_t ldc, int epilogue_flags,
+                                       const float* bias, const float* aux, int64_t ldaux,
+                                       const uint32_t* mask_bits, float* cmax, float* crow,
+                                       float* amax_out, uint32_t* relu_bits,
+                                       molclr_stream_t stream, int impl) {
+  MOLCLR_REQUIRE(impl >= 0 && impl <= 2, "gemm_f32_h3_impl: impl %d (0 auto, 1 pp / q6, 2 bs)", impl);
+  g_bs_force = impl;
+  const int rc = molclr_gemm_f32_h3_bits(A, amax, a_row_parts, hplanes, C, M, N, K, lda, ldc,
+                                         epilogue_flags, bias, aux, ldaux, mask_bits, cmax, crow,
+                                         amax_out, relu_bits, stream);
+  g_bs_force = 0;
+  return rc;
 }
 
 MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,

@@ -484,6 +484,128 @@ __global__ __launch_bounds__(256) void k_ntxent_weights_tt(
   absmax_publish(mx, wmax);
 }
 
+// ---- transposed h3 formulation (impl 3) ------------------------------------------
+// S^T = R_cols R_rows^T [ncols][nrows] by the h3 GEMM (the columns as its A
+// operand, split in registers with their per-tensor scale; the rows' h3
+// image as B), so that the backward's W^T is elementwise in S^T's own layout
+// (no LDS transpose) and feeds the h3 weight-gradient product dR = (W^T)^T
+// R_cols directly.  The row logsumexp becomes a reduction down S^T's columns:
+// partial (max, sum) per block of kColLseC columns of S (rows of S^T), merged
+// in a fixed order by a second launch.
+constexpr int64_t kColLseC = 256;  // S columns (S^T rows) per partial
+__global__ __launch_bounds__(256) void k_ntxent_col_lse_partial(
+    const float* __restrict__ St, int64_t nrows, int64_t ncols, const int32_t* __restrict__ gidx,
+    float inv_t, float2* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t rr = r < nrows ? r : nrows - 1;
+  const int64_t rg = gidx[rr];
+  const int64_t c0 = (int64_t)blockIdx.y * kColLseC;
+  const int64_t c1 = c0 + kColLseC < ncols ? c0 + kColLseC : ncols;
+  float m = -INFINITY, sum = 0.f;
+  // wave w takes S^T rows c0 + w, + 4, ...: 64 consecutive r (256 B) per load,
+  // eight loads in flight per lane
+  for (int64_t c = c0 + wave; c < c1; c += 32) {
+    float x[8];
+    float bm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t cc = c + 4 * u;
+      const float v = St[(cc < c1 ? cc : c0) * nrows + rr];
+      x[u] = (cc < c1 && cc != rg) ? v * inv_t : -INFINITY;
+      bm = fmaxf(bm, x[u]);
+    }
+    if (bm > -INFINITY) {
+      const float nm = fmaxf(m, bm);
+      float acc = sum * expf(m - nm);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += expf(x[u] - nm);
+      m = nm;
+      sum = acc;
+    }
+  }
+  __shared__ float wm[4][64], ws[4][64];
+  wm[wave][lane] = m;
+  ws[wave][lane] = sum;
+  __syncthreads();
+  if (wave != 0 || r >= nrows) return;
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    const float mo = wm[w][lane], so = ws[w][lane];
+    const float nm = fmaxf(m, mo);
+    sum = nm == -INFINITY ? 0.f : sum * expf(m - nm) + so * expf(mo - nm);
+    m = nm;
+  }
+  part[(int64_t)blockIdx.y * nrows + r] = make_float2(m, sum);
+}
+
+// lse_r over the splits in order; the loss row (lse_r - S_{r,p(r)} / T) / 2B
+__global__ __launch_bounds__(256) void k_ntxent_col_lse_final(
+    const float2* __restrict__ part, int64_t splits, const float* __restrict__ St, int64_t nrows,
+    const int32_t* __restrict__ gidx, int64_t B, float inv_t, float inv_2b, float* __restrict__ lse,
+    float* __restrict__ loss) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  const int64_t rg = gidx[r];
+  const int64_t pg = (rg + B) % (2 * B);
+  const float pos = St[pg * nrows + r];
+  float m = -INFINITY, sum = 0.f;
+  for (int64_t q = 0; q < splits; q += 8) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = q + u < splits ? part[(q + u) * nrows + r] : make_float2(-INFINITY, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float nm = fmaxf(m, v[u].x);
+      sum = nm == -INFINITY ? 0.f : sum * expf(m - nm) + v[u].y * expf(v[u].x - nm);
+      m = nm;
+    }
+  }
+  const float l = m + logf(sum);
+  lse[r] = l;
+  loss[r] = (l - pos * inv_t) * inv_2b;
+}
+
+// W^T[c][r] = g/(2B T) (exp(S_rc/T - lse_r) + exp(S_rc/T - lse_c) - 2 [c = p(r)]),
+// 0 at c = r, elementwise from S^T (float4 runs along r); max |W| into `wmax`
+// (zeroed before)
+__global__ __launch_bounds__(256) void k_ntxent_weights_t(
+    const float* __restrict__ St, float* __restrict__ Wt, int64_t nrows, int64_t ncols,
+    const int32_t* __restrict__ gidx, const float* __restrict__ lse_cols,
+    const float* __restrict__ grad_loss, int64_t B, float inv_t, float* __restrict__ wmax) {
+  const int64_t per = nrows / 4;  // nrows % 4 == 0 (host)
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float mx = 0.f;
+  if (q < ncols * per) {
+    const int64_t c = q / per, r0 = 4 * (q - c * per);
+    const float coef = (*grad_loss) * inv_t / (float)(2 * B);
+    const float4 v = *reinterpret_cast<const float4*>(St + c * nrows + r0);
+    const int4 g4 = *reinterpret_cast<const int4*>(gidx + r0);
+    const int64_t rg[4] = {g4.x, g4.y, g4.z, g4.w};
+    const float lc = lse_cols[c];
+    float lr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lr[j] = lse_cols[rg[j]];
+    const float sv[4] = {v.x, v.y, v.z, v.w};
+    float w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = 0.f;
+      if (c != rg[j]) {
+        const float lg = sv[j] * inv_t;
+        float e = expf(lg - lr[j]) + expf(lg - lc);
+        const int64_t pg = rg[j] + B < 2 * B ? rg[j] + B : rg[j] - B;
+        if (c == pg) e -= 2.f;
+        w[j] = e * coef;
+      }
+      mx = fmaxf(mx, fabsf(w[j]));
+    }
+    *reinterpret_cast<float4*>(Wt + c * nrows + r0) = make_float4(w[0], w[1], w[2], w[3]);
+  }
+  absmax_publish(mx, wmax);
+}
+
 // rhat = r / max(||r||, 1e-8) (cosine) or r (dot); norm saved for the backward
 __global__ __launch_bounds__(256) void k_ntxent_prep(const float* __restrict__ r,
                                                      float* __restrict__ rhat,
@@ -685,10 +807,13 @@ bool ntx_h3_ok(int64_t nrows, int64_t ncols, int64_t C) {
 // workspace of the h3 formulation: W^T (and S when not kept), the rows' h3 image, the max
 // slots of the columns and of W, the lse partials, the weight-gradient space
 size_t ntx_h3_ws(int64_t nrows, int64_t ncols, int64_t C) {
-  // W^T, and S when the backward recomputes it
+  // W^T, and S when the backward recomputes it; the columns' image (impl 2)
+  // or the rows' (impl 3) and impl 3's logsumexp partials
+  const int64_t splits = (ncols + kColLseC - 1) / kColLseC;
   return 2 * (size_t)nrows * ncols * sizeof(float) + molclr_hplanes_bytes(ncols, C) +
+         molclr_hplanes_bytes(nrows, C) + (size_t)splits * nrows * sizeof(float2) +
          3 * (size_t)kMaxSlotFloats * sizeof(float) +
-         molclr_linear_wgrad_workspace_bytes(ncols, nrows, C) + 8 * 256;
+         molclr_linear_wgrad_workspace_bytes(ncols, nrows, C) + 10 * 256;
 }
 // automatic choice: the fused kernels below 2^20 elements of S; the x6 GEMM
 // formulation up to 2^22 (c2's 1024 x 1024: 41 us per step against 52 for
@@ -736,6 +861,18 @@ int ntx_similarity_h3(const float* rows, const float* cols, int64_t nrows, int64
                             nullptr, s);
 }
 
+// S^T = cols rows^T into St (h3, row-major [ncols][nrows]): the rows' h3
+// image with its max slot and the columns' max slot (cmax) in two launches
+int ntx_similarity_t(const float* rows, const float* cols, int64_t nrows, int64_t ncols, int64_t C,
+                     float* St, uint16_t* rplanes, float* cmax, hipStream_t s) {
+  molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+  int rc = molclr::hplanes_make_and_max(rows, nrows, C, rplanes, cols, ncols, C, cmax, s);
+  if (rc) return rc;
+  return molclr_gemm_f32_h3(cols, cmax, 0, rplanes, St, ncols, nrows, C, C, nrows,
+                            MOLCLR_EPI_NONE, nullptr, nullptr, 0, nullptr, nullptr, nullptr,
+                            nullptr, s);
+}
+
 }  // namespace
 
 MOLCLR_API size_t molclr_ntxent_workspace_bytes(int64_t nrows, int64_t ncols, int64_t C) {
@@ -764,12 +901,37 @@ MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, co
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_fwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_fwd: bad nrows");
   MOLCLR_REQUIRE(T > 0, "ntxent_fwd: temperature must be > 0");
-  MOLCLR_REQUIRE(impl >= -1 && impl <= 2, "ntxent_fwd: bad impl %d", impl);
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 3, "ntxent_fwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
   const float inv_t = (float)(1.0 / T);
   molclr::Workspace w(workspace, ws_bytes);
   const int which = ntx_impl(nrows, ncols, C, impl);
+  if (which == 3) {
+    MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
+                   "ntxent_fwd: the h3 formulations need nrows, ncols, C multiples of 4, "
+                   "C <= 1024, ncols >= 1024");
+    float* St = w.take<float>((size_t)nrows * ncols);
+    if (sim) St = sim;
+    uint16_t* rplanes = reinterpret_cast<uint16_t*>(w.take<char>(molclr_hplanes_bytes(nrows, C)));
+    float* cmax = w.take<float>(kMaxSlotFloats);
+    const int64_t splits = (ncols + kColLseC - 1) / kColLseC;
+    float2* part = w.take<float2>((size_t)splits * nrows);
+    if (!w.ok()) {
+      molclr::set_error("ntxent_fwd: workspace too small");
+      return MOLCLR_ERR_WORKSPACE;
+    }
+    const int rc = ntx_similarity_t(rows, cols, nrows, ncols, C, St, rplanes, cmax, s);
+    if (rc) return rc;
+    molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_col_lse_partial,
+                         dim3((unsigned)molclr::ceil_div(nrows, 64), (unsigned)splits), dim3(256), 0,
+                         s, St, nrows, ncols, gidx, inv_t, part);
+    molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_col_lse_final,
+                         dim3((unsigned)molclr::ceil_div(nrows, 256)), dim3(256), 0, s, part, splits,
+                         St, nrows, gidx, B, inv_t, (float)(1.0 / (2.0 * B)), lse, loss);
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   if (which == 2) {
     MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
                    "ntxent_fwd: the h3 formulation needs nrows, ncols, C multiples of 4, "
@@ -838,11 +1000,50 @@ MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, co
   MOLCLR_REQUIRE(C > 0 && C % 32 == 0, "ntxent_bwd: C=%lld must be a multiple of 32", (long long)C);
   MOLCLR_REQUIRE(B > 0 && ncols == 2 * B, "ntxent_bwd: ncols must equal 2*batch_size");
   MOLCLR_REQUIRE(nrows > 0 && nrows <= ncols, "ntxent_bwd: bad nrows");
-  MOLCLR_REQUIRE(impl >= -1 && impl <= 2, "ntxent_bwd: bad impl %d", impl);
+  MOLCLR_REQUIRE(impl >= -1 && impl <= 3, "ntxent_bwd: bad impl %d", impl);
   MOLCLR_REQUIRE_WS(ws_bytes, molclr_ntxent_workspace_bytes(nrows, ncols, C));
   hipStream_t s = molclr::as_stream(stream);
   const float inv_t = (float)(1.0 / T);
   const int which = ntx_impl(nrows, ncols, C, impl);
+  if (which == 3) {
+    MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
+                   "ntxent_bwd: the h3 formulations need nrows, ncols, C multiples of 4, "
+                   "C <= 1024, ncols >= 1024");
+    molclr::Workspace w(workspace, ws_bytes);
+    float* Wt = w.take<float>((size_t)nrows * ncols);
+    uint16_t* rplanes = reinterpret_cast<uint16_t*>(w.take<char>(molclr_hplanes_bytes(nrows, C)));
+    float* cmax = w.take<float>(kMaxSlotFloats);
+    float* wmax = w.take<float>(kMaxSlotFloats);
+    float* Sw = sim ? nullptr : w.take<float>((size_t)nrows * ncols);
+    const size_t gws = molclr_linear_wgrad_workspace_bytes(ncols, nrows, C);
+    void* g = w.take<char>(gws);
+    if (!w.ok()) {
+      molclr::set_error("ntxent_bwd: workspace too small");
+      return MOLCLR_ERR_WORKSPACE;
+    }
+    int rc = 0;
+    const float* St = sim;  // the forward's S^T, or recomputed here
+    if (!sim) {
+      rc = ntx_similarity_t(rows, cols, nrows, ncols, C, Sw, rplanes, cmax, s);
+      if (rc) return rc;
+      St = Sw;
+    }
+    {
+      molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
+      // the columns' max slot and W's zeroed slot in one launch
+      hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(1024), 0, s, cols,
+                         ncols * C / 4, cmax, wmax);
+      molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_weights_t,
+                           dim3((unsigned)molclr::ceil_div(ncols * nrows / 4, 256)), dim3(256), 0, s,
+                           St, Wt, nrows, ncols, gidx, lse_cols, grad_loss, B, inv_t, wmax);
+      // dR[r][k] = Σ_c W^T[c][r] cols[c][k]: the weight-gradient product
+      rc = molclr_linear_wgrad_h3(Wt, wmax, cols, cmax, drows, nullptr, ncols, nrows, C, nrows, C,
+                                  0, g, gws, s);
+    }
+    if (rc) return rc;
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   if (which == 2) {
     MOLCLR_REQUIRE(ntx_h3_ok(nrows, ncols, C),
                    "ntxent_bwd: the h3 formulation needs nrows, ncols, C multiples of 4, "

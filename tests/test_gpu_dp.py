@@ -44,8 +44,9 @@ def _prep(lib, R, cosine, dev):
 
 
 @pytest.mark.parametrize("W,Bl,C,cosine,impl", [(8, 512, 256, True, 0), (8, 512, 256, True, 1),
-                                                (8, 512, 256, True, 2), (8, 512, 256, True, -1),
-                                                (2, 512, 256, False, 2), (3, 37, 64, False, 0),
+                                                (8, 512, 256, True, 2), (8, 512, 256, True, 3),
+                                                (8, 512, 256, True, -1), (2, 512, 256, False, 2),
+                                                (2, 512, 256, False, 3), (3, 37, 64, False, 0),
                                                 (3, 36, 64, False, 1), (3, 37, 64, False, -1)])
 def test_row_sharded_ntxent_simulated_ranks(dev, W, Bl, C, cosine, impl):
     """impl: 0 fused kernels, 1 x6 GEMM formulation, 2 h3 transposed GEMM
@@ -409,3 +410,90 @@ def test_captured_dp_step_after_other_models(dev, rccl_world1, kind):
         _churn(dev, "gcn", 200 + rep)
         # 8 pairs: three capacity buckets (1792, 1920, 2048 nodes)
         _captured_dp_case(dev, rccl_world1, kind, seed=7 + rep, n_pairs=8, min_captures=3)
+
+
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_captured_dp_multi_rank_paths_world1(dev, rccl_world1, monkeypatch, kind):
+    """The code a multi-rank run takes, reached on one GPU by
+    forcing CapturedTrainStep._multi_rank() true under a real RCCL group of
+    one: prepare() goes through prepare_sizes and the _global_sizes
+    all-gathers; a batch no captured graph holds takes the lockstep eager
+    path (CapturedTrainStep._eager: the same collectives as a replay, no
+    capture); replays and eager steps alternate.  Every step is held to the
+    eager data-parallel step from the same state (loss 1e-6, gradients 5e-5,
+    running statistics 1e-6), and the counters say which path ran."""
+    import copy
+
+    from molclr_amd.dataset import SyntheticPairBatches
+    from molclr_amd.gcn_molclr import GCN
+    from molclr_amd.ginet_molclr import GINet
+    from molclr_amd.graph_step import CapturedTrainStep
+    from molclr_amd.nt_xent import NTXentLoss
+    from molclr_amd.ops import bump_param_generation, l2_normalize
+    from molclr_amd.optim import FusedAdam
+    monkeypatch.setattr(CapturedTrainStep, "_multi_rank", lambda self: True)
+    calls = []
+    real_gs = CapturedTrainStep._global_sizes
+    monkeypatch.setattr(CapturedTrainStep, "_global_sizes",
+                        lambda self, sizes: calls.append(len(sizes)) or real_gs(self, sizes))
+    torch.manual_seed(11)
+    ref = (GINet if kind == "gin" else GCN)(3, 64, 128).to(dev)
+    cap = copy.deepcopy(ref)
+    B = 32
+    pairs = [tuple(b.to(dev) for b in p) for p in SyntheticPairBatches(B, seed=41).take(6)]
+    pairs.sort(key=lambda p: p[0].x.shape[0] + p[1].x.shape[0])
+    opts, reds = [], []
+    for m in (ref, cap):
+        opt = FusedAdam(mdist.bucketed_parameters(m), 5e-4, weight_decay=1e-5)
+        mdist.broadcast_params(opt.flat)
+        opts.append(opt)
+        reds.append(mdist.OverlappedGradReducer(m, opt, rccl_world1))
+    crit = NTXentLoss(dev, B, 0.1, True, group=rccl_world1)
+    step = CapturedTrainStep(cap, opts[1], crit, node_quantum=128, edge_quantum=512, node_slack=0,
+                             reducer=reds[1])
+    held, big = pairs[:2], pairs[-1]
+    try:
+        assert step.prepare(held) >= 1 and calls == [2]
+        assert step.lookup(*big) is None
+        order = [held[0], big, held[1], big, held[0]]
+        want = ["replay", "eager", "replay", "eager", "replay"]
+        got = []
+        for i, (xi, xj) in enumerate(order):
+            with torch.no_grad():  # ref := cap's state
+                for a, b in ((opts[0].flat, opts[1].flat), (opts[0].exp_avg, opts[1].exp_avg),
+                             (opts[0].exp_avg_sq, opts[1].exp_avg_sq),
+                             (opts[0]._step_dev, opts[1]._step_dev)):
+                    a.copy_(b)
+                for br, bc in zip(ref.batch_norms, cap.batch_norms):
+                    br.running_mean.copy_(bc.running_mean)
+                    br.running_var.copy_(bc.running_var)
+                    br.num_batches_tracked.copy_(bc.num_batches_tracked)
+            bump_param_generation()
+            opts[0].zero_grad()
+            reds[0].arm()
+            _, z = ref.forward_pair(xi, xj)
+            le = crit.forward_pair(l2_normalize(z))
+            le.backward()
+            reds[0].finish()
+            opts[0].step()
+            r0, e0, c0 = step.replays, step.eager_steps, step.captures
+            lc = step(xi, xj).clone()
+            torch.cuda.synchronize()
+            assert step.captures == c0, "a multi-rank step must never capture on its own"
+            got.append("replay" if step.replays == r0 + 1 else
+                       "eager" if step.eager_steps == e0 + 1 else "?")
+            assert abs(lc.item() - le.item()) <= 1e-6 * abs(le.item()), (i, got, lc.item(), le.item())
+            g_rel = ((opts[1].flat_grad.double() - opts[0].flat_grad.double()).norm()
+                     / opts[0].flat_grad.double().norm()).item()
+            assert g_rel < 5e-5, (i, got, g_rel)
+            for bc, br in zip(cap.batch_norms, ref.batch_norms):
+                assert ((bc.running_var - br.running_var).norm() / br.running_var.norm()).item() < 1e-6
+        assert got == want, got
+        assert step.eager_steps == 2 and step.replays == 3
+        # the union again (every rank's sizes): captures the big bucket, then replays it
+        assert step.prepare([big]) == 1 and calls == [2, 1]
+        r0 = step.replays
+        step(*big)
+        assert step.replays == r0 + 1
+    finally:
+        step.close()  # before the fixture destroys the process group

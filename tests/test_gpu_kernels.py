@@ -1165,3 +1165,106 @@ def test_linear_wgrad_h3_pair_matches_two_calls(dev, rows, D):
     assert bool((ws[wsb:] == 0x5A).all()), "wrote past the workspace"
     for a, b in zip(one, two):
         assert torch.equal(a, b)
+
+
+def _wave_pairs(A):
+    """The per-wave row-maximum pairs an aggregation producer writes
+    (common.h row_max_waves): for every 64 consecutive float4 units of the
+    row-major A, (max |.| of the wave's first row's units, of the next row's)."""
+    M, K = A.shape
+    d4 = K // 4
+    u = A.abs().view(M * d4, 4).amax(1)
+    nw = (M * d4 + 63) // 64
+    out = torch.zeros(nw, 2, dtype=torch.float32)
+    rows = torch.arange(M * d4) // d4
+    for w in range(nw):
+        lo, hi = 64 * w, min(64 * w + 64, M * d4)
+        r0 = rows[lo].item()
+        seg, rr = u[lo:hi], rows[lo:hi]
+        out[w, 0] = seg[rr == r0].max()
+        if (rr != r0).any():
+            out[w, 1] = seg[rr != r0].max()
+    return out
+
+
+@pytest.mark.parametrize("M,N,K", [(30556, 600, 300), (1000, 400, 292), (70, 600, 300),
+                                   (4099, 512, 300)])
+@pytest.mark.parametrize("scales", ["tensor", "rows", "pairs"])
+@pytest.mark.parametrize("epi,acc", [(0, 0), (1, 1), (2, 0), (3, 0)])
+def test_gemm_h3_bs_matches_pp(dev, M, N, K, scales, epi, acc):
+    """k_gemm_bs (the B-stationary h3 product of the K = 300 GIN products)
+    against k_gemm_pp / k_gemm_q6 on the same inputs (molclr_gemm_f32_h3_impl
+    1 vs 2): C, the ReLU bits, max |C|, max |A| and the row maxima bit for
+    bit, for every epilogue, per-tensor / per-row / per-wave-pair A scales,
+    accumulation, partial tiles and a row count leaving most blocks idle."""
+    from molclr_amd import _lib
+    if scales == "pairs" and (K // 4 < 64 or M * (K // 4) > 400_000):
+        pytest.skip("pairs: a dense A of >= 64 float4s per row; host-built for small M")
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, generator=g) * torch.pow(10.0, -6 * torch.rand(M, 1, generator=g))
+    W = (torch.rand(N, K, generator=g) * 2 - 1) / K ** 0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    mask = torch.rand(M, N, generator=g) > 0.4
+    words = (N + 31) // 32
+    pos = torch.zeros(M, words * 32, dtype=torch.bool)
+    pos[:, :N] = mask
+    mb = ((pos.view(M, words, 32).long() << torch.arange(32)).sum(-1).remainder(1 << 32).t()
+          .contiguous())
+    mb = torch.where(mb >= (1 << 31), mb - (1 << 32), mb).to(torch.int32).to(dev)
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    planes = _h3_planes(lib, Wd, N, K, 0, dev)
+    P = int(lib.molclr_gemm_row_parts(N))
+    assert P == (N + 127) // 128
+    if scales == "tensor":
+        amax, parts = torch.zeros(2048, device=dev), 0
+        assert lib.molclr_absmax_f32(Ad.data_ptr(), M, K, K, amax.data_ptr(), 0,
+                                     ops._stream(Ad)) == 0
+    elif scales == "rows":
+        amax, parts = Ad.abs().amax(1).contiguous(), 1
+    else:
+        amax, parts = _wave_pairs(A).to(dev), -(K // 4)
+    C0 = torch.randn(M, N, generator=g).to(dev)
+    outs = []
+    for impl in (1, 2):
+        C = C0.clone()
+        crow = torch.full((P, M), 7.0, device=dev)
+        cmax = torch.zeros(2048, device=dev)
+        aout = torch.zeros(2048, device=dev)
+        bits = torch.zeros(words, M, dtype=torch.int32, device=dev)
+        rc = lib.molclr_gemm_f32_h3_impl(
+            Ad.data_ptr(), amax.data_ptr(), parts, planes.data_ptr(), C.data_ptr(), M, N, K, K, N,
+            epi | (_lib.EPI_ACCUMULATE if acc else 0), bd.data_ptr(), None, 0,
+            mb.data_ptr() if epi == 3 else None, cmax.data_ptr(), crow.data_ptr(),
+            aout.data_ptr(), bits.data_ptr() if epi == 2 else None, ops._stream(Ad), impl)
+        assert rc == 0, lib.molclr_last_error()
+        torch.cuda.synchronize()
+        outs.append((C, crow.amax(0), cmax.max(), aout.max(), bits))
+    C, rmax, cmx, amx, bits = outs[1]
+    # internal consistency of the bs outputs: row maxima, max |C|, max |A|, bits
+    assert torch.equal(rmax, C.abs().amax(1))
+    assert cmx.item() == C.abs().max().item() and amx.item() == Ad.abs().max().item()
+    if epi == 2:
+        pos = torch.zeros(M, words * 32, dtype=torch.bool, device=dev)
+        pos[:, :N] = C > 0
+        want = ((pos.view(M, words, 32).long() << torch.arange(32, device=dev)).sum(-1)
+                .remainder(1 << 32).t())
+        want = torch.where(want >= (1 << 31), want - (1 << 32), want).to(torch.int32)
+        assert torch.equal(bits, want)
+    if M >= 30556:
+        # where the automatic choice is k_gemm_pp (one K group, >= 384 blocks),
+        # k_gemm_bs is the same products in the same order: bit for bit
+        for k, (a, b) in enumerate(zip(*outs)):
+            assert torch.equal(a, b), k
+    else:
+        # q6 with two K groups sums in another order: both at fp32 accuracy
+        ref = C0.double().cpu() * acc + A.double() @ W.double().t()
+        if epi in (1, 2):
+            ref = ref + bias.double()
+        if epi == 2:
+            ref = ref.clamp_min(0)
+        if epi == 3:
+            ref = ref * mask
+        Cc = C.double().cpu()
+        err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))[ref.norm(dim=1) > 0]
+        assert err.max().item() < 2e-6 if scales != "tensor" else rel(Cc, ref) < 2e-6

@@ -253,3 +253,67 @@ def test_pool_op_refuses_pyg_int64_ptr(dev):
                                           10, 0)
     out = torch.ops.molclr.segment_pool(h, torch.tensor([0, 4, 10], dtype=torch.int32, device=dev), 1)
     assert torch.allclose(out, torch.stack([h[:4].sum(0), h[4:].sum(0)]))
+
+
+# the reference's layers rebuilt on torch.ops.molclr alone
+def _gine_layer(conv, bn, h, G, seg, relu):
+    from molclr_amd.torch_ops import batch_norm_seg_module
+    agg = torch.ops.molclr.gine_aggregate(h, conv.edge_embedding1.weight,
+                                          conv.edge_embedding2.weight, *G)
+    z = torch.ops.molclr.mlp(agg, conv.mlp[0].weight, conv.mlp[0].bias, conv.mlp[2].weight,
+                             conv.mlp[2].bias)[0]
+    return batch_norm_seg_module(z, bn, seg, relu)
+
+
+def _gcn_layer(conv, bn, h, G, seg, relu):
+    from molclr_amd.torch_ops import batch_norm_seg_module
+    z = torch.ops.molclr.gcn_conv(h, conv.weight, conv.bias, conv.edge_embedding1.weight,
+                                  conv.edge_embedding2.weight, *G)[0]
+    return batch_norm_seg_module(z, bn, seg, relu)
+
+
+def _readout(model, h, graph_ptr):
+    pooled = torch.ops.molclr.segment_pool(h, graph_ptr, 0)
+    feat = torch.ops.molclr.linear(pooled, model.feat_lin.weight, model.feat_lin.bias)
+    out = torch.ops.molclr.mlp(feat, model.out_lin[0].weight, model.out_lin[0].bias,
+                               model.out_lin[2].weight, model.out_lin[2].bias)[0]
+    return feat, out
+
+
+@pytest.mark.parametrize("kind", ["gin", "gcn"])
+def test_reference_layers_rebuilt_on_torch_ops(dev, kind):
+    """GINet / GCN's forward (ginet_molclr.py:98-117, gcn_molclr.py:139-158)
+    composed from torch.ops.molclr alone -- graph_build, gine_aggregate + mlp
+    or gcn_conv, batch_norm_seg, segment_pool, linear, mlp -- equals the
+    product model on the same batch: outputs, running statistics and every
+    parameter gradient (the same kernels in the same order)."""
+    import copy
+
+    from molclr_amd.gcn_molclr import GCN
+    from molclr_amd.ginet_molclr import GINet
+    torch.manual_seed(8)
+    model = (GINet if kind == "gin" else GCN)(3, 64, 128).to(dev)
+    twin = copy.deepcopy(model)
+    b = _batch(dev, B=40, seed=9)
+    # product
+    h_ref, out_ref = model(b)
+    (h_ref.sum() + (out_ref * out_ref).sum()).backward()
+    # rebuilt
+    g = _graph_tensors(b)
+    G, graph_ptr = g[:8], g[8]
+    h = twin.x_embedding1(b.x[:, 0]) + twin.x_embedding2(b.x[:, 1])  # ginet_molclr.py:103
+    layer = _gine_layer if kind == "gin" else _gcn_layer
+    L = len(twin.gnns)
+    for i in range(L):
+        h = layer(twin.gnns[i], twin.batch_norms[i], h, G, [b.x.shape[0]], relu=i < L - 1)
+    feat, out = _readout(twin, h, graph_ptr)
+    (feat.sum() + (out * out).sum()).backward()
+    rel = lambda a, c: ((a.double() - c.double()).norm() / c.double().norm().clamp_min(1e-30)).item()  # noqa: E731
+    assert rel(feat, h_ref) < 1e-6 and rel(out, out_ref) < 1e-6
+    for (n, p), q in zip(model.named_parameters(), twin.parameters()):
+        if n.endswith("mlp.2.bias") or (kind == "gcn" and n.startswith("gnns.") and n.count(".") == 2
+                                          and n.endswith(".bias")):
+            continue  # feeds a BatchNorm: exact gradient 0, rounding noise only
+        assert rel(q.grad, p.grad) < 1e-5, n
+    for a, c in zip(model.buffers(), twin.buffers()):
+        assert torch.equal(a, c) if not a.is_floating_point() else rel(a, c) < 1e-6
