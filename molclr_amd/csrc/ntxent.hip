@@ -492,51 +492,73 @@ __global__ __launch_bounds__(256) void k_ntxent_weights_tt(
 // R_cols directly.  The row logsumexp becomes a reduction down S^T's columns:
 // partial (max, sum) per block of kColLseC columns of S (rows of S^T), merged
 // in a fixed order by a second launch.
-constexpr int64_t kColLseC = 256;  // S columns (S^T rows) per partial
+constexpr int64_t kColLseC = 128;  // S columns (S^T rows) per partial
+// block: 256 consecutive r (a lane holds 4, one float4 per S^T row) x kColLseC
+// S^T rows, the 4 waves striding them; partial[split][r] = (max, sum)
 __global__ __launch_bounds__(256) void k_ntxent_col_lse_partial(
     const float* __restrict__ St, int64_t nrows, int64_t ncols, const int32_t* __restrict__ gidx,
     float inv_t, float2* __restrict__ part) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t r = (int64_t)blockIdx.x * 64 + lane;
-  const int64_t rr = r < nrows ? r : nrows - 1;
-  const int64_t rg = gidx[rr];
+  const int64_t r0 = (int64_t)blockIdx.x * 256 + 4 * lane;  // nrows % 4 == 0 (host)
+  const bool live = r0 < nrows;
+  const int64_t rl = live ? r0 : 0;
+  const int4 g4 = *reinterpret_cast<const int4*>(gidx + rl);
+  const int64_t rg[4] = {g4.x, g4.y, g4.z, g4.w};
   const int64_t c0 = (int64_t)blockIdx.y * kColLseC;
   const int64_t c1 = c0 + kColLseC < ncols ? c0 + kColLseC : ncols;
-  float m = -INFINITY, sum = 0.f;
-  // wave w takes S^T rows c0 + w, + 4, ...: 64 consecutive r (256 B) per load,
-  // eight loads in flight per lane
+  float m[4], sum[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m[j] = -INFINITY;
+    sum[j] = 0.f;
+  }
+  // eight S^T rows per round in flight, each one float4 per lane
   for (int64_t c = c0 + wave; c < c1; c += 32) {
-    float x[8];
-    float bm = -INFINITY;
+    float4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int64_t cc = c + 4 * u;
-      const float v = St[(cc < c1 ? cc : c0) * nrows + rr];
-      x[u] = (cc < c1 && cc != rg) ? v * inv_t : -INFINITY;
-      bm = fmaxf(bm, x[u]);
+      v[u] = *reinterpret_cast<const float4*>(St + (cc < c1 ? cc : c0) * nrows + rl);
     }
-    if (bm > -INFINITY) {
-      const float nm = fmaxf(m, bm);
-      float acc = sum * expf(m - nm);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += expf(x[u] - nm);
-      m = nm;
-      sum = acc;
+    for (int j = 0; j < 4; ++j) {
+      float x[8], bm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t cc = c + 4 * u;
+        const float e = j == 0 ? v[u].x : j == 1 ? v[u].y : j == 2 ? v[u].z : v[u].w;
+        x[u] = (cc < c1 && cc != rg[j]) ? e * inv_t : -INFINITY;
+        bm = fmaxf(bm, x[u]);
+      }
+      if (bm > -INFINITY) {
+        const float nm = fmaxf(m[j], bm);
+        float acc = sum[j] * expf(m[j] - nm);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += expf(x[u] - nm);
+        m[j] = nm;
+        sum[j] = acc;
+      }
     }
   }
-  __shared__ float wm[4][64], ws[4][64];
-  wm[wave][lane] = m;
-  ws[wave][lane] = sum;
+  __shared__ float4 wm[4][64], ws[4][64];
+  wm[wave][lane] = make_float4(m[0], m[1], m[2], m[3]);
+  ws[wave][lane] = make_float4(sum[0], sum[1], sum[2], sum[3]);
   __syncthreads();
-  if (wave != 0 || r >= nrows) return;
+  if (wave != 0 || !live) return;
 #pragma unroll
   for (int w = 1; w < 4; ++w) {
-    const float mo = wm[w][lane], so = ws[w][lane];
-    const float nm = fmaxf(m, mo);
-    sum = nm == -INFINITY ? 0.f : sum * expf(m - nm) + so * expf(mo - nm);
-    m = nm;
+    const float4 mo4 = wm[w][lane], so4 = ws[w][lane];
+    const float mo[4] = {mo4.x, mo4.y, mo4.z, mo4.w}, so[4] = {so4.x, so4.y, so4.z, so4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float nm = fmaxf(m[j], mo[j]);
+      sum[j] = nm == -INFINITY ? 0.f : sum[j] * expf(m[j] - nm) + so[j] * expf(mo[j] - nm);
+      m[j] = nm;
+    }
   }
-  part[(int64_t)blockIdx.y * nrows + r] = make_float2(m, sum);
+  float2* o = part + (int64_t)blockIdx.y * nrows + r0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = make_float2(m[j], sum[j]);
 }
 
 // lse_r over the splits in order; the loss row (lse_r - S_{r,p(r)} / T) / 2B
@@ -568,15 +590,13 @@ __global__ __launch_bounds__(256) void k_ntxent_col_lse_final(
 }
 
 // W^T[c][r] = g/(2B T) (exp(S_rc/T - lse_r) + exp(S_rc/T - lse_c) - 2 [c = p(r)]),
-// 0 at c = r, elementwise from S^T (float4 runs along r); max |W| into `wmax`
-// (zeroed before)
+// 0 at c = r, elementwise from S^T (float4 runs along r)
 __global__ __launch_bounds__(256) void k_ntxent_weights_t(
     const float* __restrict__ St, float* __restrict__ Wt, int64_t nrows, int64_t ncols,
     const int32_t* __restrict__ gidx, const float* __restrict__ lse_cols,
-    const float* __restrict__ grad_loss, int64_t B, float inv_t, float* __restrict__ wmax) {
+    const float* __restrict__ grad_loss, int64_t B, float inv_t) {
   const int64_t per = nrows / 4;  // nrows % 4 == 0 (host)
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float mx = 0.f;
   if (q < ncols * per) {
     const int64_t c = q / per, r0 = 4 * (q - c * per);
     const float coef = (*grad_loss) * inv_t / (float)(2 * B);
@@ -599,11 +619,29 @@ __global__ __launch_bounds__(256) void k_ntxent_weights_t(
         if (c == pg) e -= 2.f;
         w[j] = e * coef;
       }
-      mx = fmaxf(mx, fabsf(w[j]));
     }
     *reinterpret_cast<float4*>(Wt + c * nrows + r0) = make_float4(w[0], w[1], w[2], w[3]);
   }
-  absmax_publish(mx, wmax);
+}
+
+// impl 3's scales: the columns' max slot (plain stores, as k_ntxent_absmax_plain)
+// and W's slot set to its bound, |W| <= 2 |g| / (2B T): the positive pair's
+// -2 dominates every row, so max |W| is within a factor (1 - P) of the bound
+// and the h3 scale (a power of two) is the one the measured max would give
+// but for rows whose positive probability P exceeds 1/2
+__global__ __launch_bounds__(1024) void k_ntxent_absmax_bound(const float* __restrict__ x,
+                                                             int64_t n4, float* __restrict__ slot,
+                                                             float* __restrict__ wslot,
+                                                             const float* __restrict__ grad_loss,
+                                                             int64_t B, float inv_t) {
+  float m = absmax4_range(reinterpret_cast<const float4*>(x),
+                          (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n4,
+                          (int64_t)gridDim.x * blockDim.x);
+  m = block_max(m);
+  if (threadIdx.x == 0) {
+    slot[blockIdx.x * kMaxSlotStride] = m;
+    wslot[blockIdx.x * kMaxSlotStride] = 2.f * fabsf(*grad_loss) * inv_t / (float)(2 * B);
+  }
 }
 
 // rhat = r / max(||r||, 1e-8) (cosine) or r (dot); norm saved for the backward
@@ -924,7 +962,7 @@ MOLCLR_API int molclr_ntxent_fwd_impl(const float* rows, const int32_t* gidx, co
     const int rc = ntx_similarity_t(rows, cols, nrows, ncols, C, St, rplanes, cmax, s);
     if (rc) return rc;
     molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_col_lse_partial,
-                         dim3((unsigned)molclr::ceil_div(nrows, 64), (unsigned)splits), dim3(256), 0,
+                         dim3((unsigned)molclr::ceil_div(nrows, 256), (unsigned)splits), dim3(256), 0,
                          s, St, nrows, ncols, gidx, inv_t, part);
     molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_col_lse_final,
                          dim3((unsigned)molclr::ceil_div(nrows, 256)), dim3(256), 0, s, part, splits,
@@ -1030,12 +1068,12 @@ MOLCLR_API int molclr_ntxent_bwd_impl(const float* rows, const int32_t* gidx, co
     }
     {
       molclr::TimerKindScope timed_as(molclr::kTimeNtxent);
-      // the columns' max slot and W's zeroed slot in one launch
-      hipLaunchKernelGGL(k_ntxent_absmax_plain, dim3(kMaxSlotParts), dim3(1024), 0, s, cols,
-                         ncols * C / 4, cmax, wmax);
+      // the columns' max slot and W's bound slot in one launch
+      hipLaunchKernelGGL(k_ntxent_absmax_bound, dim3(kMaxSlotParts), dim3(1024), 0, s, cols,
+                         ncols * C / 4, cmax, wmax, grad_loss, B, inv_t);
       molclr::launch_timed(molclr::kTimeNtxent, k_ntxent_weights_t,
                            dim3((unsigned)molclr::ceil_div(ncols * nrows / 4, 256)), dim3(256), 0, s,
-                           St, Wt, nrows, ncols, gidx, lse_cols, grad_loss, B, inv_t, wmax);
+                           St, Wt, nrows, ncols, gidx, lse_cols, grad_loss, B, inv_t);
       // dR[r][k] = Σ_c W^T[c][r] cols[c][k]: the weight-gradient product
       rc = molclr_linear_wgrad_h3(Wt, wmax, cols, cmax, drows, nullptr, ncols, nrows, C, nrows, C,
                                   0, g, gws, s);

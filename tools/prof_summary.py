@@ -3,7 +3,7 @@
     python tools/prof_summary.py gpurun_out/prof profiles/r1_bench_c2.md [steps]
 
 Reads the *kernel_stats.csv (per-kernel totals) and *kernel_trace.csv
-(per-dispatch) files, groups kernels by short name, and reports time per step
+(per-dispatch) files, or rocprofv3's default *results.db (rocpd SQLite), groups kernels by short name, and reports time per step
 and the average duration of the GIN scatter-add kernel (k_gine_agg_fwd), which
 bench.py's HIP-event roofline must agree with.
 """
@@ -30,6 +30,23 @@ def main():
     stats = sorted(src.rglob("*kernel_stats.csv"))
     trace = sorted(src.rglob("*kernel_trace.csv"))
     rows = []
+    agg_durs = []
+    dbs = sorted(src.rglob("*results.db"))
+    if not stats and dbs:
+        # rocprofv3's default rocpd (SQLite) output: one row per dispatch
+        import sqlite3
+        con = sqlite3.connect(str(dbs[0]))
+        per = defaultdict(list)
+        for name, t0, t1 in con.execute(
+                "select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d "
+                "join rocpd_info_kernel_symbol s on d.kernel_id = s.id"):
+            per[name].append(t1 - t0)
+        tot_all = sum(sum(v) for v in per.values()) or 1
+        for name, ds in per.items():
+            rows.append((short(name), len(ds), float(sum(ds)), sum(ds) / len(ds),
+                         100.0 * sum(ds) / tot_all))
+            if "k_gine_agg_fwd" in name:
+                agg_durs += ds
     if stats:
         with open(stats[0]) as f:
             for r in csv.DictReader(f):
@@ -41,6 +58,11 @@ def main():
         agg[n][1] += tot
     total = sum(v[1] for v in agg.values())
     lines = [f"# rocprofv3 kernel summary — {src}", ""]
+    if agg_durs:
+        lines.append(f"k_gine_agg_fwd: {len(agg_durs)} dispatches, average "
+                     f"{sum(agg_durs)/len(agg_durs)/1e3:.2f} us, min {min(agg_durs)/1e3:.2f} us, "
+                     f"max {max(agg_durs)/1e3:.2f} us")
+        lines.append("")
     if trace:
         durs = []
         with open(trace[0]) as f:
