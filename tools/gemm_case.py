@@ -60,7 +60,7 @@ def main():
         rdz = torch.empty(M, device=dev)
         rdz1 = torch.empty(M, device=dev)
         ragg = torch.empty(M, device=dev)
-        bits = torch.empty((H + 31) // 32, M, dtype=torch.int32, device=dev)
+        bits = torch.randint(-2**31, 2**31 - 1, ((H + 31) // 32, M), dtype=torch.int32, device=dev)
         smax = {n: torch.zeros(ops.MAX_SLOT, device=dev) for n in X}
         for n, r in (("dz", rdz), ("dz1", rdz1), ("agg", ragg)):
             lib.molclr_absmax_rows_f32(X[n].data_ptr(), M, X[n].shape[1], X[n].shape[1],
@@ -78,8 +78,11 @@ def main():
                  "q6_dz1": lambda: ops.gemm_w(X["dz"], W2, M, H, D, D, H, False, True,
                                               EPI_RELU_MASK, aux=X["a1"], tile=t),
                  "q6_dagg": lambda: ops.gemm_w(X["dz1"], W0, M, D, H, H, D, False, True, tile=t),
+                 # the step's dz1 takes its ReLU mask from lin1's bits (as it does there)
                  "h3_dz1": lambda: ops.gemm_h3(X["dz"], rdz, W2, H, D, H, 1, EPI_RELU_MASK,
-                                               aux=X["a1"], rowwise=1),
+                                               rowwise=1, mask_bits=bits),
+                 "h3_dz1_aux": lambda: ops.gemm_h3(X["dz"], rdz, W2, H, D, H, 1, EPI_RELU_MASK,
+                                                   aux=X["a1"], rowwise=1),
                  "h3_dagg": lambda: ops.gemm_h3(X["dz1"], rdz1, W0, D, H, D, 1, rowwise=1),
                  # the step's h3 forward products (row-scaled A)
                  "h3_lin1": lambda: ops.gemm_h3(X["agg"], ragg, W0, H, D, D, 0, EPI_BIAS_RELU,
