@@ -412,7 +412,9 @@ __device__ __forceinline__ float row_max_of_waves(const float2* __restrict__ wm,
   float m = 0.f;
   for (int64_t w = s >> 6; w <= (e >> 6); ++w) {
     const float2 v = wm[w];
-    m = fmaxf(m, (w << 6) / d4 == row ? v.x : v.y);
+    // w's first row is `row` iff the wave starts inside it: w's units begin at
+    // 64 w <= e (w <= e >> 6), so floor(64 w / d4) == row iff 64 w >= s
+    m = fmaxf(m, (w << 6) >= s ? v.x : v.y);
   }
   return m;
 }

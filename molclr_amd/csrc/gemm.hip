@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void k_gemm_p6(
 
   const int nsteps = kt_end - kt_beg;
   auto kof = [&](int step) { return (int64_t)(kt_beg + step) * BK; };
-  constexpr int CSN = CS ? SA::PER : 1;
+  constexpr int CSN = CS == 1 ? SA::PER : CS == 2 ? SB::PER : 1;
   float4 cs[CSN];
 #pragma unroll
   for (int j = 0; j < CSN; ++j) cs[j] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1759,7 +1759,8 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int64_t wi = (s0 >> 6) + q;
-        if (wi <= (e0 >> 6)) m = fmaxf(m, (wi << 6) / d4 == arow ? rw[2 * q] : rw[2 * q + 1]);
+        // wave wi's first row is arow iff it starts inside the row (no division)
+        if (wi <= (e0 >> 6)) m = fmaxf(m, (wi << 6) >= s0 ? rw[2 * q] : rw[2 * q + 1]);
       }
     } else {
 #pragma unroll
@@ -1899,6 +1900,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
     const int64_t m = mw_cur + li;
     const float sc = __builtin_ldexpf(1.f, -(sha_cur + shb));
     float rmax = 0.f;
+    int rmaxi = 0;  // the ReLU epilogue's maxima, as bits
 #pragma unroll
     for (int b = 0; b < kTN; ++b) {
       const int64_t nb = n0 + 32 * b;
@@ -1924,7 +1926,14 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
           }
           if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
           *reinterpret_cast<float4*>(o) = v;
-          rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          if (EPI == MOLCLR_EPI_BIAS_RELU && !accumulate) {
+            // v = max(., 0) >= 0 or -0: the maxima as integer maxima of the
+            // bits (no |.| and no NaN canonicalisation; -0 reads as < 0)
+            rmaxi = max(rmaxi, max(max(__float_as_int(v.x), __float_as_int(v.y)),
+                                   max(__float_as_int(v.z), __float_as_int(v.w))));
+          } else {
+            rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          }
           pos |= ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
                   (v.w > 0.f ? 8u : 0u)) << cb;
         }
@@ -1934,6 +1943,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
         if (lh == 0 && m < M) bits_out[(nb >> 5) * bits_ld + m] = pos;
       }
     }
+    rmax = fmaxf(rmax, __int_as_float(rmaxi));
     if (crow != nullptr) {
       const float v = fmaxf(rmax, __shfl_xor(rmax, 32, 64));
       if (lh == 0 && m < M) crow[(int64_t)tile * M + m] = v;
@@ -1970,7 +1980,9 @@ constexpr int kW6BM = 128;
 
 // H3: both operands scaled by their max slots and split into two fp16 parts
 // (mfma.h "h3"), three fp16 MFMAs per product, partials scaled back.
-template <int TN, bool CS, int KG, bool H3 = false>
+// CS: column sums of nothing (0), of A (1: the bias gradient when A = dY), or
+// of B (2: when the product runs transposed, B = dY -- w6_transposed).
+template <int TN, int CS, int KG, bool H3 = false>
 __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) void k_gemm_w6(
     const float* __restrict__ A, const float* __restrict__ B, float* __restrict__ part,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int ktiles_per_split, int splits,
@@ -2018,7 +2030,7 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
   SB sb;
   sa.init(A, lda, m0, M, gt);
   sb.init(B, ldb, n0, N, gt);
-  constexpr int CSN = CS ? SA::PER : 1;
+  constexpr int CSN = CS == 1 ? SA::PER : CS == 2 ? SB::PER : 1;
   float4 cs[CSN];
 #pragma unroll
   for (int j = 0; j < CSN; ++j) cs[j] = f4zero();
@@ -2089,7 +2101,8 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
     if (q >= 0 && q < 2 * ns) {
       const int i = q >> 1;
       if ((q & 1) == 0) {
-        if constexpr (CS) sa.colsum_add(cs, gt);
+        if constexpr (CS == 1) sa.colsum_add(cs, gt);
+        if constexpr (CS == 2) sb.colsum_add(cs, gt);
         sa.store(img, gt, sha);
         sb.store(img + AI, gt, shb);
       } else {
@@ -2103,7 +2116,31 @@ __global__ __launch_bounds__(256 * KG) __attribute__((amdgpu_waves_per_eu(2))) v
     __syncthreads();
   }
 
-  if constexpr (CS) {
+  if constexpr (CS == 2) {
+    if (m0 == 0 && cs_part != nullptr) {  // block-uniform
+      // B's column sums: every (group, unit u = k (BN/4) + rb) float4 through
+      // LDS, then thread rb < BN/4 adds its units in (group, k) order
+      constexpr int RB = BN / 4;
+      float4* red = reinterpret_cast<float4*>(lds);
+#pragma unroll
+      for (int j = 0; j < CSN; ++j) {
+        const int u = gt + j * T;
+        if (u < SB::UNITS) red[grp * SB::UNITS + u] = cs[j];
+      }
+      __syncthreads();
+      if (tid < RB) {
+        float4 t4 = f4zero();
+        for (int q = 0; q < KG * BK; ++q) t4 = f4add(t4, red[q * RB + tid]);
+        const float e[4] = {t4.x, t4.y, t4.z, t4.w};
+        for (int j = 0; j < 4; ++j) {
+          const int64_t n = n0 + 4 * tid + j;
+          if (n < N) cs_part[(int64_t)split * N + n] = e[j];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (CS == 1) {
     if (n0 == 0 && cs_part != nullptr) {  // block-uniform
       // a thread's units all share one 4-row group rb = tid % (BM/4): fold
       // them, then the KG*T/(BM/4) threads of each group in a fixed order
@@ -2433,6 +2470,8 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
 // Two weight gradients' ordered split-K reductions in ONE launch (the GIN
 // layer's dW2 and dW1: molclr_linear_wgrad_h3_pair).  Threads [0, M_a N_a)
 // reduce job a, the rest job b, each exactly as k_splitk_reduce<EPI_NONE>.
+// A transposed job (trans = 1: partials of C^T, [split][N][M]) reads its
+// partials along their rows and stores C transposed.
 struct ReduceJob {
   const float* partial;
   int splits;
@@ -2441,6 +2480,7 @@ struct ReduceJob {
   int64_t ldc;
   const float* cs_partial;
   float* colsum;
+  int trans = 0;
 };
 __global__ void k_splitk_reduce_pair(ReduceJob ja, ReduceJob jb, int accumulate) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2470,7 +2510,14 @@ __global__ void k_splitk_reduce_pair(ReduceJob ja, ReduceJob jb, int accumulate)
     j.colsum[t] = accumulate ? j.colsum[t] + c : c;
   }
   if (t >= j.M * j.N) return;
-  const int64_t m = t / j.N, n = t - m * j.N;
+  int64_t m, n;
+  if (j.trans) {
+    n = t / j.M;
+    m = t - n * j.M;
+  } else {
+    m = t / j.N;
+    n = t - m * j.N;
+  }
   float v = ordered_sum(j.partial + t, j.M * j.N, j.splits);
   if (accumulate) v += j.C[m * j.ldc + n];
   j.C[m * j.ldc + n] = v;
@@ -2859,32 +2906,38 @@ bool w6_shape_ok(int64_t M, int64_t N, int64_t K) {
 // takes either with the same workspace query)
 size_t w6_ws_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
   size_t need = 0;
-  for (int kg = 1; kg <= 2; ++kg) {
-    const W6Plan p = w6_plan(M, N, K, kg);
-    const size_t b = (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
-    need = b > need ? b : need;
-  }
+  for (int kg = 1; kg <= 2; ++kg)
+    for (int tr = 0; tr < 2; ++tr) {  // and the transposed plan (w6_transposed)
+      const W6Plan p = tr ? w6_plan(N, M, K, kg) : w6_plan(M, N, K, kg);
+      const size_t b = (size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float) + 256;
+      need = b > need ? b : need;
+    }
   return need;
 }
 
 template <int TN, int KG, bool H3>
 void launch_w6_kg(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
                   int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part,
-                  const float* amax, const float* bmax) {
+                  const float* amax, const float* bmax, bool cs_b) {
   const dim3 grid((unsigned)(p.ntiles * p.splits));
-  if (cs_part)
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, true, KG, H3>), grid, dim3(256 * KG), 0,
+  if (cs_part && cs_b)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, 2, KG, H3>), grid, dim3(256 * KG), 0,
+                         s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part, amax, bmax);
+  else if (cs_part)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, 1, KG, H3>), grid, dim3(256 * KG), 0,
                          s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part, amax, bmax);
   else
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, false, KG, H3>), grid, dim3(256 * KG),
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_w6<TN, 0, KG, H3>), grid, dim3(256 * KG),
                          0, s, A, B, part, M, N, K, lda, ldb, p.kps, p.splits, cs_part, amax, bmax);
 }
 template <int TN, bool H3>
 void launch_w6(const W6Plan& p, hipStream_t s, const float* A, const float* B, float* part,
                int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, float* cs_part,
-               const float* amax, const float* bmax) {
-  if (p.kg == 2) launch_w6_kg<TN, 2, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
-  else launch_w6_kg<TN, 1, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
+               const float* amax, const float* bmax, bool cs_b = false) {
+  if (p.kg == 2)
+    launch_w6_kg<TN, 2, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax, cs_b);
+  else
+    launch_w6_kg<TN, 1, H3>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax, cs_b);
 }
 
 // C (+)= A^T B over K-major A [K][M] (lda) and B [K][N] (ldb); colsum (+)= Σ_k A
@@ -3460,6 +3513,61 @@ MOLCLR_API int molclr_gemm_f32_h3_impl(const float* A, const float* amax, int a_
   return rc;
 }
 
+namespace {
+// the w6 launch of run_w6 without its reduction: partials (and the bias
+// partials) into `part`; returns the plan
+// cs_b: the column sums are B's (a transposed launch, B = dY)
+W6Plan launch_w6_h3(const float* A, const float* B, float* part, bool colsum, int64_t M, int64_t N,
+                    int64_t K, int64_t lda, int64_t ldb, hipStream_t s, const float* amax,
+                    const float* bmax, bool cs_b = false) {
+  const W6Plan p = w6_plan(M, N, K, 2);
+  float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
+  if (p.tn == 5) launch_w6<5, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax, cs_b);
+  else if (p.tn == 4)
+    launch_w6<4, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax, cs_b);
+  else launch_w6<2, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax, cs_b);
+  return p;
+}
+// dW = dY^T X as (X^T dY)^T when that pads less: w6 tiles are 128 along M and
+// 32 TN along N, so dW2 of the c2 layer (300 x 600) covers 384 x 640 and its
+// transpose 640 x 320 (0.73 -> 0.88 of the MFMA work useful; measured in
+// the c2 step 59.9 us against dW1's 52.3 us at the same FLOPs).
+// MOLCLR_W6_TRANSPOSE=0 keeps every product in its own orientation.
+int64_t w6_area(int64_t M, int64_t N) {
+  const int64_t bn = 32 * wide_tn(N);
+  return ((M + kW6BM - 1) / kW6BM * kW6BM) * ((N + bn - 1) / bn * bn);
+}
+bool w6_transposed(int64_t n_out, int64_t n_in) {
+  static const bool off = [] {
+    const char* e = getenv("MOLCLR_W6_TRANSPOSE");
+    return e != nullptr && e[0] == '0';
+  }();
+  return !off && w6_area(n_in, n_out) < w6_area(n_out, n_in);
+}
+// the w6 partial bytes of dW [n_out][n_in] (its chosen orientation)
+size_t w6_part_bytes(int64_t n_out, int64_t n_in, int64_t K, bool colsum) {
+  const bool tr = w6_transposed(n_out, n_in);
+  const W6Plan p = tr ? w6_plan(n_in, n_out, K, 2) : w6_plan(n_out, n_in, K, 2);
+  return molclr::align_up((size_t)p.splits * (n_out * n_in + (colsum ? n_out : 0)) * sizeof(float),
+                          256);
+}
+// one job of the pair: dW = dY^T X (+ db = Σ dY) as partials, in the
+// orientation w6_transposed picks; returns its reduce job
+ReduceJob launch_wgrad_job(const float* dy, const float* dymax, const float* x, const float* xmax,
+                           float* dW, float* db, int64_t n_out, int64_t n_in, int64_t rows,
+                           int64_t ld_dy, int64_t ld_x, float* part, hipStream_t s) {
+  const bool tr = w6_transposed(n_out, n_in);
+  const W6Plan q = tr ? launch_w6_h3(x, dy, part, db != nullptr, n_in, n_out, rows, ld_x, ld_dy, s,
+                                     xmax, dymax, true)
+                      : launch_w6_h3(dy, x, part, db != nullptr, n_out, n_in, rows, ld_dy, ld_x, s,
+                                     dymax, xmax);
+  ReduceJob j{part, q.splits, n_out, n_in, dW, n_in,
+              db ? part + (size_t)q.splits * n_out * n_in : nullptr, db};
+  j.trans = tr ? 1 : 0;
+  return j;
+}
+}  // namespace
+
 MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax, const float* x,
                                              const float* xmax, float* dW, float* db, int64_t rows,
                                              int64_t n_out, int64_t n_in, int64_t ld_dy,
@@ -3484,28 +3592,21 @@ MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax
     return MOLCLR_OK;
   }
   MOLCLR_REQUIRE_WS(workspace_bytes, w6_ws_bytes(n_out, n_in, rows, db != nullptr));
+  if (groups == 2 && w6_transposed(n_out, n_in)) {
+    // the orientation the pair takes (bit-identical to it)
+    const ReduceJob j = launch_wgrad_job(dy, dymax, x, xmax, dW, db, n_out, n_in, rows, ld_dy, ld_x,
+                                         static_cast<float*>(workspace), s);
+    ReduceJob none{nullptr, 0, 0, 0, nullptr, 0, nullptr, nullptr};
+    molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce_pair,
+                         dim3((unsigned)molclr::ceil_div(n_out * n_in, 256)), dim3(256), 0, s, j,
+                         none, accumulate);
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
   return run_w6(dy, x, dW, db, n_out, n_in, rows, ld_dy, ld_x, n_in, accumulate, workspace,
                 workspace_bytes, s, groups, dymax, xmax);
 }
 
-namespace {
-// the w6 launch of run_w6 without its reduction: partials (and the bias
-// partials) into `part`; returns the plan
-W6Plan launch_w6_h3(const float* A, const float* B, float* part, bool colsum, int64_t M, int64_t N,
-                    int64_t K, int64_t lda, int64_t ldb, hipStream_t s, const float* amax,
-                    const float* bmax) {
-  const W6Plan p = w6_plan(M, N, K, 2);
-  float* cs_part = colsum ? part + (size_t)p.splits * M * N : nullptr;
-  if (p.tn == 5) launch_w6<5, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
-  else if (p.tn == 4) launch_w6<4, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
-  else launch_w6<2, true>(p, s, A, B, part, M, N, K, lda, ldb, cs_part, amax, bmax);
-  return p;
-}
-size_t w6_part_bytes(int64_t M, int64_t N, int64_t K, bool colsum) {
-  const W6Plan p = w6_plan(M, N, K, 2);
-  return molclr::align_up((size_t)p.splits * (M * N + (colsum ? M : 0)) * sizeof(float), 256);
-}
-}  // namespace
 
 MOLCLR_API size_t molclr_linear_wgrad_h3_pair_workspace_bytes(int64_t rows, int64_t n_out_a,
                                                               int64_t n_in_a, int64_t n_out_b,
@@ -3538,14 +3639,10 @@ MOLCLR_API int molclr_linear_wgrad_h3_pair(
   float* pa = static_cast<float*>(workspace);
   float* pb = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                        w6_part_bytes(n_out_a, n_in_a, rows, true));
-  const W6Plan qa = launch_w6_h3(dy_a, x_a, pa, db_a != nullptr, n_out_a, n_in_a, rows, ld_dy_a,
-                                 ld_x_a, s, dymax_a, xmax_a);
-  const W6Plan qb = launch_w6_h3(dy_b, x_b, pb, db_b != nullptr, n_out_b, n_in_b, rows, ld_dy_b,
-                                 ld_x_b, s, dymax_b, xmax_b);
-  ReduceJob ja{pa, qa.splits, n_out_a, n_in_a, dW_a, n_in_a,
-               db_a ? pa + (size_t)qa.splits * n_out_a * n_in_a : nullptr, db_a};
-  ReduceJob jb{pb, qb.splits, n_out_b, n_in_b, dW_b, n_in_b,
-               db_b ? pb + (size_t)qb.splits * n_out_b * n_in_b : nullptr, db_b};
+  const ReduceJob ja = launch_wgrad_job(dy_a, dymax_a, x_a, xmax_a, dW_a, db_a, n_out_a, n_in_a,
+                                        rows, ld_dy_a, ld_x_a, pa, s);
+  const ReduceJob jb = launch_wgrad_job(dy_b, dymax_b, x_b, xmax_b, dW_b, db_b, n_out_b, n_in_b,
+                                        rows, ld_dy_b, ld_x_b, pb, s);
   const int64_t total = n_out_a * n_in_a + n_out_b * n_in_b;
   molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce_pair,
                        dim3((unsigned)molclr::ceil_div(total, 256)), dim3(256), 0, s, ja, jb,

@@ -1,6 +1,6 @@
 """Run one GEMM shape of the c2 / c5 step repeatedly (for rocprofv3 PMC passes).
 
-    python tools/gemm_case.py CASE [reps] [impl]
+    python tools/gemm_case.py CASE [reps] [impl] [--time]
 
 CASE: qb_lin1 qb_lin2 qb_dz1 qb_dagg wb_dW2 wb_dW0 (bf16, c5 shapes, 55k rows)
       q6_lin1 q6_lin2 q6_dz1 q6_dagg w6_dW2 w6_dW1 (fp32 split-bf16, c2, 30.5k rows)
@@ -94,6 +94,21 @@ def main():
                  "w6_dW2": lambda: ops.linear_bwd(X["dz"], X["a1"], W2, need_x=False),
                  "w6_dW1": lambda: ops.linear_bwd(X["dz1"], X["agg"], W0, need_x=False)}
         fn = cases[case]
+    if "--time" in sys.argv:  # median of 5 event-timed runs of `reps` calls
+        import statistics
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+        print(f"{case} {statistics.median(ts):.2f} us/call")
+        return
     for _ in range(reps):
         fn()
     torch.cuda.synchronize()
