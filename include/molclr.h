@@ -487,10 +487,12 @@ int molclr_gemm_f32_h3(const float* A, const float* amax, int a_row_parts, const
                        const uint32_t* mask_bits, float* cmax, float* crow, float* amax_out,
                        molclr_stream_t stream);
 /* molclr_gemm_f32_h3_bits with the kernel chosen per call (tests): impl 0 =
- * automatic, 1 = k_gemm_pp / k_gemm_q6, 2 = k_gemm_bs (K in (288, 304],
- * N > 320, C float4-aligned, ReLU mask as bits; MOLCLR_ERR_UNSUPPORTED
- * otherwise).  Every kernel gives bit-identical C, bits and maxima; the row
- * maxima (crow) are molclr_gemm_row_parts(N) arrays whatever the kernel. */
+ * automatic, 1 = k_gemm_pp / k_gemm_q6, 2 = k_gemm_bs, 3 = k_gemm_bs16 (both
+ * bs: K in (288, 304], N > 320, C float4-aligned, ReLU mask as bits;
+ * MOLCLR_ERR_UNSUPPORTED otherwise).  Kernels 1 and 2 give bit-identical C,
+ * bits and maxima; 3 (16 x 16 x 32 MFMAs) sums each product's k in another
+ * order, equal to fp32 rounding.  The row maxima (crow) are
+ * molclr_gemm_row_parts(N) arrays whatever the kernel. */
 int molclr_gemm_f32_h3_impl(const float* A, const float* amax, int a_row_parts,
                             const uint16_t* hplanes, float* C, int64_t M, int64_t N, int64_t K,
                             int64_t lda, int64_t ldc, int epilogue_flags, const float* bias,

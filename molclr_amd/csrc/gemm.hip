@@ -1954,6 +1954,308 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
   if (amax_out != nullptr) absmax_publish(ain, amax_out);
 }
 
+// "bs16": k_gemm_bs on the 16 x 16 x 32 fp16 MFMA.  The same B image and the
+// same pipeline, over 16-row slabs: a lane holds 8 consecutive k of its row
+// (one fragment per 32-k step) and, after the MFMAs, 4 consecutive columns of
+// its row per 16-column block, so an epilogue store instruction writes 16
+// rows x 64 B (k_gemm_bs: 32 rows x 32 B), a block's slabs split over its 8
+// waves in twice as many, finer rounds (c2: 4.7 slabs per wave against 2.3),
+// and half the accumulator registers.  The k order inside an MFMA differs
+// from the 32 x 32 x 16 form: results equal k_gemm_bs's to fp32 rounding,
+// not bit for bit.
+__device__ __forceinline__ f32x4 mfma16_h3_t(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah, acc, 0, 0, 0);
+}
+template <int EPI, int H3, int S, bool HALF, int W = 8>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4))) void k_gemm_bs16(
+    const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
+    int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
+    const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux, int accumulate,
+    const float* __restrict__ amax, const float* __restrict__ bmax, float* __restrict__ cmax,
+    float* __restrict__ crow, float* __restrict__ amax_out, int arow_parts,
+    uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in, int64_t bits_ld,
+    int ntn, int groups) {
+  static_assert(S % 2 == 0 && S >= 4, "two A register sets, steps in pairs");
+  constexpr int NFULL = HALF ? S - 1 : S;
+  constexpr int IMG = NFULL * kFullImg + (HALF ? kHalfImg : 0);
+  constexpr int NB = kBN / 16;  // 16-column blocks of the tile
+  __shared__ __attribute__((aligned(16))) uint16_t img[IMG];
+  __shared__ __attribute__((aligned(16))) float bsh[kBN];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = L % ntn, grp = L / ntn;
+  const int64_t n0 = (int64_t)tile * kBN;
+  const int64_t slabs = (M + 15) / 16;
+  const int64_t s_beg = slabs * grp / groups, s_end = slabs * (grp + 1) / groups;
+  constexpr bool HAS_BIAS = EPI == MOLCLR_EPI_BIAS || EPI == MOLCLR_EPI_BIAS_RELU;
+
+  // the B image: as k_gemm_bs
+  const __amdgpu_buffer_rsrc_t brsrc = make_rsrc(Bp, (int64_t)2 * npad * kp * 2);
+  {
+    constexpr int CHF = NFULL * 2 * (kBN / 16);
+    for (int q = w; q < CHF; q += W) {
+      const int st = q / (2 * (kBN / 16)), rem = q % (2 * (kBN / 16));
+      const int pl = rem / (kBN / 16), r0 = (rem % (kBN / 16)) * 16;
+      const int row = r0 + (lane >> 2), c = lane & 3;
+      int64_t gr = n0 + row;
+      gr = gr < npad ? gr : npad - 1;
+      const uint32_t voff = (uint32_t)(((pl * npad + gr) * kp + 32 * st + 8 * (c ^ ((row >> 2) & 3))) * 2);
+      buf_lds16(brsrc, img + st * kFullImg + pl * kBN * XK + r0 * XK, voff, 0);
+    }
+    if constexpr (HALF) {
+      constexpr int CHH = 2 * (kBN / 32);
+      for (int q = w; q < CHH; q += W) {
+        const int pl = q / (kBN / 32), r0 = (q % (kBN / 32)) * 32;
+        const int row = r0 + (lane >> 1), c = lane & 1;
+        int64_t gr = n0 + row;
+        gr = gr < npad ? gr : npad - 1;
+        const uint32_t voff =
+            (uint32_t)(((pl * npad + gr) * kp + 32 * (S - 1) + 8 * (c ^ ((row >> 2) & 1))) * 2);
+        buf_lds16(brsrc, img + NFULL * kFullImg + pl * kBN * 16 + r0 * 16, voff, 0);
+      }
+    }
+    if constexpr (HAS_BIAS) {
+      if (tid < kBN) bsh[tid] = n0 + tid < N ? bias[n0 + tid] : 0.f;
+    }
+  }
+  const __amdgpu_buffer_rsrc_t arsrc = make_rsrc(A, M * lda * 4);
+  float cm = 0.f, ain = 0.f;
+
+  int64_t arow = 0;
+  uint32_t avoff = 0;
+  float rw[8];
+  uint32_t mws[kTN];
+  auto meta_issue = [&](int64_t slab) {
+    arow = slab * 16 + r16;
+    arow = arow < M ? arow : M - 1;
+    avoff = (uint32_t)((arow * lda + 8 * q4) * 4);
+    if constexpr (H3 == 2) {
+      if (arow_parts < 0) {
+        const int d4 = -arow_parts;
+        const int64_t s0 = arow * d4, e0 = s0 + d4 - 1;
+        const float2* wm = reinterpret_cast<const float2*>(amax);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const int64_t wi = (s0 >> 6) + q;
+          const float2 v = wm[wi <= (e0 >> 6) ? wi : (s0 >> 6)];
+          rw[2 * q] = v.x;
+          rw[2 * q + 1] = v.y;
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) rw[p] = amax[(int64_t)(p < arow_parts ? p : 0) * M + arow];
+      }
+    }
+    if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+#pragma unroll
+      for (int g = 0; g < kTN; ++g) {
+        int64_t nb = n0 + 32 * g;
+        nb = nb < N ? nb : 0;
+        mws[g] = bits_in[(nb >> 5) * bits_ld + arow];
+      }
+    }
+  };
+  auto row_shift = [&]() -> int {
+    if constexpr (H3 == 1) return h3_shift(amax);
+    float m = 0.f;
+    if (arow_parts < 0) {
+      const int d4 = -arow_parts;
+      const int64_t s0 = arow * d4, e0 = s0 + d4 - 1;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int64_t wi = (s0 >> 6) + q;
+        if (wi <= (e0 >> 6)) m = fmaxf(m, (wi << 6) >= s0 ? rw[2 * q] : rw[2 * q + 1]);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 8; ++p)
+        if (p < arow_parts) m = fmaxf(m, rw[p]);
+    }
+    return h3_shift_of(m);
+  };
+  auto load_a = [&](int r, float4(&v)[2]) {
+    const uint32_t soff = (uint32_t)(r * BK * 4);
+    v[0] = buf_ld4(arsrc, avoff, soff);
+    v[1] = buf_ld4(arsrc, avoff + 16, soff);
+  };
+
+  float4 ar0[2], ar1[2];
+  u32x4 frh, frl;
+  f32x4 acc[NB];
+  auto compute = [&](const uint16_t* base) {
+    auto rd = [&](int b, u32x4(&f)[2]) {
+      const int row = 16 * b + r16;
+      f[0] = *reinterpret_cast<const u32x4*>(base + xoff(row, q4));
+      f[1] = *reinterpret_cast<const u32x4*>(base + kBN * XK + xoff(row, q4));
+    };
+    u32x4 q[2][2];
+    rd(0, q[0]);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b + 1 < NB) rd(b + 1, q[(b + 1) & 1]);
+      acc[b] = mfma16_h3_t(__builtin_bit_cast(f16x8, frh), __builtin_bit_cast(f16x8, frl),
+                           __builtin_bit_cast(f16x8, q[b & 1][0]),
+                           __builtin_bit_cast(f16x8, q[b & 1][1]), acc[b]);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int mm = 0; mm < 3; ++mm) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (b + 1 < NB && mm < 2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+  };
+  // the last step holds k0 .. k0+15 only: lanes q4 >= 2 (k0+16 ..) take zeros
+  auto compute_half = [&]() {
+    const uint16_t* base = img + NFULL * kFullImg;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    const int c = q4 & 1;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int row = 16 * b + r16;
+      const u32x4 h = *reinterpret_cast<const u32x4*>(base + hoff(row, c));
+      const u32x4 l = *reinterpret_cast<const u32x4*>(base + kBN * 16 + hoff(row, c));
+      acc[b] = mfma16_h3_t(__builtin_bit_cast(f16x8, frh), __builtin_bit_cast(f16x8, frl),
+                           __builtin_bit_cast(f16x8, q4 >= 2 ? z : h),
+                           __builtin_bit_cast(f16x8, q4 >= 2 ? z : l), acc[b]);
+    }
+  };
+  auto split = [&](float4(&a)[2], int r, int sha) {
+    if (amax_out != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        ain = fmaxf(ain, fmaxf(fmaxf(fabsf(a[j].x), fabsf(a[j].y)), fmaxf(fabsf(a[j].z), fabsf(a[j].w))));
+    }
+    if (r == S - 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if ((int64_t)r * BK + 8 * q4 + 4 * j >= K) a[j] = f4zero();
+    }
+    hsplit8(a[0], a[1], sha, frh, frl);
+  };
+
+  int64_t slab = s_beg + w;
+  if (slab < s_end) {
+    meta_issue(slab);
+    load_a(0, ar0);
+    load_a(1, ar1);
+  }
+  vm_wait<0>();  // B image, the first slab's row maxima and two A steps
+  __syncthreads();
+  const int shb = h3_shift(bmax);
+  int sha = slab < s_end ? row_shift() : 0;
+  int64_t mw = slab * 16;
+
+  for (; slab < s_end; slab += W) {
+    const int64_t next = slab + W;
+    const bool more = next < s_end;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[b][r] = 0.f;
+    uint32_t mcur[kTN];
+#pragma unroll
+    for (int g = 0; g < kTN; ++g) mcur[g] = mws[g];
+#pragma unroll 1
+    for (int r = 0; r < S - 2; r += 2) {
+      if (r > 0) vm_wait<2>();
+      split(ar0, r, sha);
+      load_a(r + 2, ar0);
+      compute(img + r * kFullImg);
+      if (r > 0) vm_wait<2>();
+      split(ar1, r + 1, sha);
+      load_a(r + 3, ar1);
+      compute(img + (r + 1) * kFullImg);
+    }
+    const int sha_cur = sha;
+    const int64_t mw_cur = mw;
+    {
+      vm_wait<2>();
+      split(ar0, S - 2, sha_cur);
+      if (more) {
+        meta_issue(next);
+        load_a(0, ar0);
+      }
+      compute(img + (S - 2) * kFullImg);
+      if (more) vm_wait<4>();
+      else vm_wait<0>();
+      split(ar1, S - 1, sha_cur);
+      if (more) load_a(1, ar1);
+      if (HALF) compute_half();
+      else compute(img + (S - 1) * kFullImg);
+    }
+    vm_wait<0>();  // the next slab's loads landed before any store is issued
+    if (more) {
+      sha = row_shift();
+      mw = next * 16;
+    }
+
+    // ---- epilogue: lane (r16, q4) holds columns 16 b + 4 q4 .. +3 of row r16
+    const int64_t m = mw_cur + r16;
+    const float sc = __builtin_ldexpf(1.f, -(sha_cur + shb));
+    float rmax = 0.f;
+    int rmaxi = 0;
+#pragma unroll
+    for (int g = 0; g < kTN; ++g) {  // 32-column groups (a ReLU-bit word each)
+      const int64_t ng = n0 + 32 * g;
+      if (ng >= N) break;
+      uint32_t pos = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int b = 2 * g + h;
+        const int cb = 16 * h + 4 * q4;  // column within the group
+        const int64_t n = ng + cb;
+        if (m < M && n < N) {
+          float* o = C + m * ldc + n;
+          float4 v = make_float4(acc[b][0] * sc, acc[b][1] * sc, acc[b][2] * sc, acc[b][3] * sc);
+          if constexpr (HAS_BIAS) {
+            v = f4add(v, *reinterpret_cast<const float4*>(bsh + 32 * g + cb));
+            if (EPI == MOLCLR_EPI_BIAS_RELU)
+              v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+          }
+          if constexpr (EPI == MOLCLR_EPI_RELU_MASK) {
+            const uint32_t mk = (mcur[g] >> cb) & 15u;
+            v = make_float4(mk & 1u ? v.x : 0.f, mk & 2u ? v.y : 0.f, mk & 4u ? v.z : 0.f,
+                            mk & 8u ? v.w : 0.f);
+          }
+          if (accumulate) v = f4add(v, *reinterpret_cast<const float4*>(o));
+          *reinterpret_cast<float4*>(o) = v;
+          if (EPI == MOLCLR_EPI_BIAS_RELU && !accumulate) {
+            rmaxi = max(rmaxi, max(max(__float_as_int(v.x), __float_as_int(v.y)),
+                                   max(__float_as_int(v.z), __float_as_int(v.w))));
+          } else {
+            rmax = fmaxf(rmax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+          }
+          pos |= ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+                  (v.w > 0.f ? 8u : 0u)) << cb;
+        }
+      }
+      if (bits_out != nullptr) {
+        pos |= __shfl_xor(pos, 16, 64);
+        pos |= __shfl_xor(pos, 32, 64);
+        if (q4 == 0 && m < M) bits_out[(ng >> 5) * bits_ld + m] = pos;
+      }
+    }
+    rmax = fmaxf(rmax, __int_as_float(rmaxi));
+    if (crow != nullptr) {
+      float v = fmaxf(rmax, __shfl_xor(rmax, 16, 64));
+      v = fmaxf(v, __shfl_xor(v, 32, 64));
+      if (q4 == 0 && m < M) crow[(int64_t)tile * M + m] = v;
+    }
+    cm = fmaxf(cm, rmax);
+  }
+  if (cmax != nullptr) absmax_publish(cm, cmax);
+  if (amax_out != nullptr) absmax_publish(ain, amax_out);
+}
+
 // ---------------------------------------------------------------------------
 // "w6": the weight gradient of a Linear, C[m][n] = Σ_k A[k][m] B[k][n] with
 // both operands K-major (K = rows: dW = dY^T X), optionally with the column
@@ -2800,7 +3102,7 @@ int dispatch_q6_tn(int epi, const Args& a, int64_t npad, hipStream_t s) {
 // The h3 products k_gemm_bs takes: K in (288, 304] (its LDS image), wide
 // (> 320 columns), float4-aligned C, ReLU masks as bits, row maxima as a slot,
 // <= 8 partial arrays or per-wave pairs.  MOLCLR_GEMM_BS=0 keeps pp / q6;
-// g_bs_force (molclr_gemm_f32_h3_impl): 1 never, 2 only bs.
+// g_bs_force (molclr_gemm_f32_h3_impl): 1 never, 2 bs, 3 bs16.
 int g_bs_force = 0;
 bool bs_shape_ok(const Args& a, int64_t npad, int epi, int h3) {
   if (h3 == 0 || a.N <= 320 || a.K <= 288 || a.K > 304 || a.ldb != 320) return false;
@@ -2815,18 +3117,48 @@ bool use_bs(const Args& a, int64_t npad, int epi, int h3) {
     const char* e = getenv("MOLCLR_GEMM_BS");
     return e != nullptr && e[0] == '0';
   }();
-  if (g_bs_force == 1 || (off && g_bs_force != 2)) return false;
+  if (g_bs_force == 1 || (off && g_bs_force < 2)) return false;
   return bs_shape_ok(a, npad, epi, h3);
+}
+// k_gemm_bs16 (default) or k_gemm_bs: MOLCLR_GEMM_BS16=0 or g_bs_force 2
+// (molclr_gemm_f32_h3_impl 2) takes the 32 x 32 x 16 form, g_bs_force 3 bs16
+bool use_bs16() {
+  static const bool off = [] {
+    const char* e = getenv("MOLCLR_GEMM_BS16");
+    return e != nullptr && e[0] == '0';
+  }();
+  return g_bs_force == 3 || (g_bs_force != 2 && !off);
 }
 template <int EPI, int H3>
 void launch_bs(const Args& a, int64_t npad, hipStream_t s) {
   const int ntn = (int)((a.N + kBN - 1) / kBN);
   int groups = molclr::cu_count() / ntn;
   groups = groups < 1 ? 1 : groups;
-  molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs<EPI, H3, 10, true>), dim3((unsigned)(ntn * groups)),
-                       dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N, a.K, a.lda, a.ldb, npad, a.ldc,
-                       a.bias, a.aux, a.ldaux, a.accumulate, a.amax, a.bmax, a.cmax, a.crow,
-                       a.amax_out, a.arow_parts, a.bits_out, a.bits_in, a.bits_ld, ntn, groups);
+  // three waves per SIMD (<= 168 VGPRs): the c2 step 187.1k molecules/s
+  // against 186.1k at two (MOLCLR_BS16_WAVES=8) and 180.8k on k_gemm_bs
+  // (same box, round 6)
+  static const int w16 = [] {
+    const char* e = getenv("MOLCLR_BS16_WAVES");
+    return e != nullptr && atoi(e) == 8 ? 8 : 12;
+  }();
+  if (use_bs16() && w16 == 12)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs16<EPI, H3, 10, true, 12>),
+                         dim3((unsigned)(ntn * groups)), dim3(768), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate, a.amax,
+                         a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out, a.bits_in,
+                         a.bits_ld, ntn, groups);
+  else if (use_bs16())
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs16<EPI, H3, 10, true>),
+                         dim3((unsigned)(ntn * groups)), dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate, a.amax,
+                         a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out, a.bits_in,
+                         a.bits_ld, ntn, groups);
+  else
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs<EPI, H3, 10, true>),
+                         dim3((unsigned)(ntn * groups)), dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate, a.amax,
+                         a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out, a.bits_in,
+                         a.bits_ld, ntn, groups);
 }
 template <int H3>
 int dispatch_bs(int epi, const Args& a, int64_t npad, hipStream_t s) {
@@ -2853,7 +3185,7 @@ int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, int h3 = 0) {
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;
   }
-  if (g_bs_force == 2) {
+  if (g_bs_force >= 2) {
     molclr::set_error("gemm_f32_h3_impl: the bs kernel does not take this product");
     return MOLCLR_ERR_UNSUPPORTED;
   }
@@ -3504,7 +3836,8 @@ MOLCLR_API int molclr_gemm_f32_h3_impl(const float* A, const float* amax, int a_
                                        const uint32_t* mask_bits, float* cmax, float* crow,
                                        float* amax_out, uint32_t* relu_bits,
                                        molclr_stream_t stream, int impl) {
-  MOLCLR_REQUIRE(impl >= 0 && impl <= 2, "gemm_f32_h3_impl: impl %d (0 auto, 1 pp / q6, 2 bs)", impl);
+  MOLCLR_REQUIRE(impl >= 0 && impl <= 3,
+                 "gemm_f32_h3_impl: impl %d (0 auto, 1 pp / q6, 2 bs, 3 bs16)", impl);
   g_bs_force = impl;
   const int rc = molclr_gemm_f32_h3_bits(A, amax, a_row_parts, hplanes, C, M, N, K, lda, ldc,
                                          epilogue_flags, bias, aux, ldaux, mask_bits, cmax, crow,

@@ -934,14 +934,26 @@ def test_gemm_h3(dev, M, N, K, rowwise, epi):
         mb = ((pos.view(M, words, 32).long() << torch.arange(32, device=dev)).sum(-1)
               .remainder(1 << 32).t().contiguous())
         mb = torch.where(mb >= (1 << 31), mb - (1 << 32), mb).to(torch.int32)
-        C2 = torch.empty_like(C)
-        rc = lib.molclr_gemm_f32_h3(Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(),
-                                    rowwise, planes.data_ptr(), C2.data_ptr(), M, N, K, K, N, epi,
-                                    None, None, 0, mb.data_ptr(), None, None, None,
-                                    ops._stream(Ad))
-        assert rc == 0, lib.molclr_last_error()
-        torch.cuda.synchronize()
-        assert torch.equal(C2, C)
+        # (on the kernel the aux form takes, impl 1; the automatic choice for
+        # bits may be k_gemm_bs16, whose k order differs: fp32 accuracy there)
+        for impl in (1, 0):
+            C2 = torch.empty_like(C)
+            rc = lib.molclr_gemm_f32_h3_impl(
+                Ad.data_ptr(), (rows[0] if rowwise else slots[0]).data_ptr(), rowwise,
+                planes.data_ptr(), C2.data_ptr(), M, N, K, K, N, epi, None, None, 0,
+                mb.data_ptr(), None, None, None, None, ops._stream(Ad), impl)
+            assert rc == 0, lib.molclr_last_error()
+            torch.cuda.synchronize()
+            if impl == 1:
+                assert torch.equal(C2, C)
+            else:
+                C2c = C2.double().cpu()
+                if rowwise:
+                    e2 = ((C2c - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))
+                    e2 = e2[ref.norm(dim=1) > 0].max().item()
+                else:
+                    e2 = rel(C2c, ref)
+                assert e2 < 2e-6, e2
 
 
 @pytest.mark.parametrize("rows,n_out,n_in", [(30556, 300, 600), (1500, 256, 128), (100, 64, 12),
@@ -1268,3 +1280,74 @@ def test_gemm_h3_bs_matches_pp(dev, M, N, K, scales, epi, acc):
         Cc = C.double().cpu()
         err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))[ref.norm(dim=1) > 0]
         assert err.max().item() < 2e-6 if scales != "tensor" else rel(Cc, ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(30556, 600, 300), (1000, 400, 292), (70, 600, 300),
+                                   (4099, 512, 300)])
+@pytest.mark.parametrize("scales", ["tensor", "rows", "pairs"])
+@pytest.mark.parametrize("epi,acc", [(0, 0), (1, 1), (2, 0), (3, 0)])
+def test_gemm_h3_bs16(dev, M, N, K, scales, epi, acc):
+    """k_gemm_bs16 (molclr_gemm_f32_h3_impl 3: the K = 300 products on the
+    16 x 16 x 32 MFMA): C against fp64 at the h3 kernels' accuracy (row-wise
+    2e-6), and its ReLU bits, row maxima, max |C| and max |A| consistent with
+    its own C, for every epilogue and A-scale form, accumulation, partial
+    tiles and mostly idle blocks."""
+    from molclr_amd import _lib
+    if scales == "pairs" and (K // 4 < 64 or M * (K // 4) > 400_000):
+        pytest.skip("pairs: a dense A of >= 64 float4s per row; host-built for small M")
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + epi + 1)
+    A = torch.randn(M, K, generator=g) * torch.pow(10.0, -6 * torch.rand(M, 1, generator=g))
+    W = (torch.rand(N, K, generator=g) * 2 - 1) / K ** 0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    mask = torch.rand(M, N, generator=g) > 0.4
+    words = (N + 31) // 32
+    pos = torch.zeros(M, words * 32, dtype=torch.bool)
+    pos[:, :N] = mask
+    mb = ((pos.view(M, words, 32).long() << torch.arange(32)).sum(-1).remainder(1 << 32).t()
+          .contiguous())
+    mb = torch.where(mb >= (1 << 31), mb - (1 << 32), mb).to(torch.int32).to(dev)
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    planes = _h3_planes(lib, Wd, N, K, 0, dev)
+    P = int(lib.molclr_gemm_row_parts(N))
+    if scales == "tensor":
+        amax, parts = torch.zeros(2048, device=dev), 0
+        assert lib.molclr_absmax_f32(Ad.data_ptr(), M, K, K, amax.data_ptr(), 0,
+                                     ops._stream(Ad)) == 0
+    elif scales == "rows":
+        amax, parts = Ad.abs().amax(1).contiguous(), 1
+    else:
+        amax, parts = _wave_pairs(A).to(dev), -(K // 4)
+    C0 = torch.randn(M, N, generator=g).to(dev)
+    C = C0.clone()
+    crow = torch.full((P, M), 7.0, device=dev)
+    cmax = torch.zeros(2048, device=dev)
+    aout = torch.zeros(2048, device=dev)
+    bits = torch.zeros(words, M, dtype=torch.int32, device=dev)
+    rc = lib.molclr_gemm_f32_h3_impl(
+        Ad.data_ptr(), amax.data_ptr(), parts, planes.data_ptr(), C.data_ptr(), M, N, K, K, N,
+        epi | (_lib.EPI_ACCUMULATE if acc else 0), bd.data_ptr(), None, 0,
+        mb.data_ptr() if epi == 3 else None, cmax.data_ptr(), crow.data_ptr(),
+        aout.data_ptr(), bits.data_ptr() if epi == 2 else None, ops._stream(Ad), 3)
+    assert rc == 0, lib.molclr_last_error()
+    torch.cuda.synchronize()
+    assert torch.equal(crow.amax(0), C.abs().amax(1))
+    assert cmax.max().item() == C.abs().max().item()
+    assert aout.max().item() == Ad.abs().max().item()
+    if epi == 2:
+        pos = torch.zeros(M, words * 32, dtype=torch.bool, device=dev)
+        pos[:, :N] = C > 0
+        want = ((pos.view(M, words, 32).long() << torch.arange(32, device=dev)).sum(-1)
+                .remainder(1 << 32).t())
+        want = torch.where(want >= (1 << 31), want - (1 << 32), want).to(torch.int32)
+        assert torch.equal(bits, want)
+    ref = C0.double().cpu() * acc + A.double() @ W.double().t()
+    if epi in (1, 2):
+        ref = ref + bias.double()
+    if epi == 2:
+        ref = ref.clamp_min(0)
+    if epi == 3:
+        ref = ref * mask
+    Cc = C.double().cpu()
+    err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))[ref.norm(dim=1) > 0]
+    assert err.max().item() < 2e-6 if scales != "tensor" else rel(Cc, ref) < 2e-6
