@@ -1968,8 +1968,11 @@ __device__ __forceinline__ f32x4 mfma16_h3_t(f16x8 ah, f16x8 al, f16x8 bh, f16x8
   acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, al, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah, acc, 0, 0, 0);
 }
-template <int EPI, int H3, int S, bool HALF, int W = 8>
-__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4))) void k_gemm_bs16(
+// k_gemm_bsn: the same kernel for any tile width BNT (128: the K = 300
+// products; 64: the K = 600 products lin2 and dagg, N = 300, whose whole-K
+// image of a 64-column tile is 19 full steps, 152 KB) and an odd step count.
+template <int EPI, int H3, int S, bool HALF, int W = 8, int BNT = kBN>
+__global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4))) void k_gemm_bsn(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
     int64_t M, int64_t N, int64_t K, int64_t lda, int64_t kp, int64_t npad, int64_t ldc,
     const float* __restrict__ bias, const float* __restrict__ aux, int64_t ldaux, int accumulate,
@@ -1977,7 +1980,9 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
     float* __restrict__ crow, float* __restrict__ amax_out, int arow_parts,
     uint32_t* __restrict__ bits_out, const uint32_t* __restrict__ bits_in, int64_t bits_ld,
     int ntn, int groups) {
-  static_assert(S % 2 == 0 && S >= 4, "two A register sets, steps in pairs");
+  static_assert(S >= 4 && (S % 2 == 0 || !HALF), "steps in pairs, or an odd count of full steps");
+  constexpr int kBN = BNT, kTN = BNT / 32;  // this tile (k_gemm_bs's constants shadowed)
+  constexpr int kFullImg = 2 * kBN * XK, kHalfImg = 2 * kBN * 16;
   constexpr int NFULL = HALF ? S - 1 : S;
   constexpr int IMG = NFULL * kFullImg + (HALF ? kHalfImg : 0);
   constexpr int NB = kBN / 16;  // 16-column blocks of the tile
@@ -2164,8 +2169,9 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
     uint32_t mcur[kTN];
 #pragma unroll
     for (int g = 0; g < kTN; ++g) mcur[g] = mws[g];
+    constexpr int SP = S % 2 ? S - 3 : S - 2;  // steps taken in pairs
 #pragma unroll 1
-    for (int r = 0; r < S - 2; r += 2) {
+    for (int r = 0; r < SP; r += 2) {
       if (r > 0) vm_wait<2>();
       split(ar0, r, sha);
       load_a(r + 2, ar0);
@@ -2177,7 +2183,33 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
     }
     const int sha_cur = sha;
     const int64_t mw_cur = mw;
-    {
+    if constexpr (S % 2) {
+      // three last steps (ar0, ar1, ar0); the next slab's A(0), A(1) land in
+      // ar1, ar0 and are swapped back
+      vm_wait<2>();
+      split(ar0, S - 3, sha_cur);
+      load_a(S - 1, ar0);
+      compute(img + (S - 3) * kFullImg);
+      vm_wait<2>();
+      split(ar1, S - 2, sha_cur);
+      if (more) {
+        meta_issue(next);
+        load_a(0, ar1);
+      }
+      compute(img + (S - 2) * kFullImg);
+      if (more) vm_wait<4>();
+      else vm_wait<0>();
+      split(ar0, S - 1, sha_cur);
+      if (more) load_a(1, ar0);  // split consumed ar0
+      compute(img + (S - 1) * kFullImg);
+      if (more) {
+        const float4 x0 = ar0[0], x1 = ar0[1];
+        ar0[0] = ar1[0];
+        ar0[1] = ar1[1];
+        ar1[0] = x0;
+        ar1[1] = x1;
+      }
+    } else {
       vm_wait<2>();
       split(ar0, S - 2, sha_cur);
       if (more) {
@@ -3142,13 +3174,13 @@ void launch_bs(const Args& a, int64_t npad, hipStream_t s) {
     return e != nullptr && atoi(e) == 8 ? 8 : 12;
   }();
   if (use_bs16() && w16 == 12)
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs16<EPI, H3, 10, true, 12>),
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 10, true, 12>),
                          dim3((unsigned)(ntn * groups)), dim3(768), 0, s, a.A, a.Bp, a.C, a.M, a.N,
                          a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate, a.amax,
                          a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out, a.bits_in,
                          a.bits_ld, ntn, groups);
   else if (use_bs16())
-    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bs16<EPI, H3, 10, true>),
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 10, true>),
                          dim3((unsigned)(ntn * groups)), dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N,
                          a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate, a.amax,
                          a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out, a.bits_in,
@@ -3170,6 +3202,59 @@ int dispatch_bs(int epi, const Args& a, int64_t npad, hipStream_t s) {
     default: return -1;
   }
 }
+// The K = 600 products (lin2 = a1 W2^T and dagg = dz1 W1 of the c2 layer,
+// N = 300) on k_gemm_bsn with 64-column tiles: K in (576, 608], N <= 320, no
+// row maxima or ReLU bits out (their partial layouts are q6's), the rest as
+// bs_shape_ok.  Opt-in (MOLCLR_GEMM_BS64=1; g_bs_force 3 takes it too): in the
+// c2 step it measured even with k_gemm_q6 (182.6k vs 182.4k molecules/s, same
+// box, round 6; 16 waves per block 181.2k), so q6 stays the default.
+bool use_bs64(const Args& a, int64_t npad, int epi, int h3) {
+  static const bool off = [] {
+    const char* e = getenv("MOLCLR_GEMM_BS64");
+    return e == nullptr || e[0] != '1';
+  }();
+  if (g_bs_force == 1 || g_bs_force == 2 || (off && g_bs_force != 3)) return false;
+  if (h3 == 0 || a.N > 320 || a.N <= 192 || a.K <= 576 || a.K > 608 || a.ldb != 608) return false;
+  if (a.crow != nullptr || a.bits_out != nullptr) return false;
+  if (a.lda % 4 || a.ldc % 4 || a.N % 4 || (reinterpret_cast<uintptr_t>(a.C) & 15)) return false;
+  if (a.M * a.lda * 4 >= (1ll << 31) || 2 * npad * a.ldb * 2 >= (1ll << 31)) return false;
+  if (epi == MOLCLR_EPI_RELU_MASK && a.bits_in == nullptr) return false;
+  if (h3 == 2 && (a.arow_parts > 8 || (a.arow_parts < 0 && -a.arow_parts < 64))) return false;
+  return true;
+}
+template <int EPI, int H3>
+void launch_bs64(const Args& a, int64_t npad, hipStream_t s) {
+  const int ntn = (int)((a.N + 63) / 64);
+  int groups = molclr::cu_count() / ntn;
+  groups = groups < 1 ? 1 : groups;
+  // MOLCLR_BS64_WAVES=16: four waves per SIMD (<= 128 VGPRs)
+  static const int wv = [] {
+    const char* e = getenv("MOLCLR_BS64_WAVES");
+    return e != nullptr && atoi(e) == 16 ? 16 : 12;
+  }();
+  if (wv == 16)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 19, false, 16, 64>),
+                         dim3((unsigned)(ntn * groups)), dim3(1024), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate,
+                         a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out,
+                         a.bits_in, a.bits_ld, ntn, groups);
+  else
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 19, false, 12, 64>),
+                         dim3((unsigned)(ntn * groups)), dim3(768), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate,
+                         a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out,
+                         a.bits_in, a.bits_ld, ntn, groups);
+}
+template <int H3>
+int dispatch_bs64(int epi, const Args& a, int64_t npad, hipStream_t s) {
+  switch (epi) {
+    case MOLCLR_EPI_NONE: launch_bs64<MOLCLR_EPI_NONE, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS: launch_bs64<MOLCLR_EPI_BIAS, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_BIAS_RELU: launch_bs64<MOLCLR_EPI_BIAS_RELU, H3>(a, npad, s); return 0;
+    case MOLCLR_EPI_RELU_MASK: launch_bs64<MOLCLR_EPI_RELU_MASK, H3>(a, npad, s); return 0;
+    default: return -1;
+  }
+}
 // partial row-max arrays of an h3 product's C (crow): one per 128 columns for
 // the wide products (k_gemm_bs's tiles); pp / q6, whose tiles may be 160
 // wide, zero the arrays they do not write
@@ -3180,6 +3265,15 @@ int run_q6(const Args& a, int64_t npad, int epi, hipStream_t s, int h3 = 0) {
     const int rc = h3 == 2 ? dispatch_bs<2>(epi, a, npad, s) : dispatch_bs<1>(epi, a, npad, s);
     if (rc) {
       molclr::set_error("gemm_f32_h3: no bs kernel for epilogue %d", epi);
+      return MOLCLR_ERR_UNSUPPORTED;
+    }
+    MOLCLR_LAUNCHED();
+    return MOLCLR_OK;
+  }
+  if (h3 != 0 && use_bs64(a, npad, epi, h3)) {
+    const int rc = h3 == 2 ? dispatch_bs64<2>(epi, a, npad, s) : dispatch_bs64<1>(epi, a, npad, s);
+    if (rc) {
+      molclr::set_error("gemm_f32_h3: no bs64 kernel for epilogue %d", epi);
       return MOLCLR_ERR_UNSUPPORTED;
     }
     MOLCLR_LAUNCHED();

@@ -1351,3 +1351,58 @@ def test_gemm_h3_bs16(dev, M, N, K, scales, epi, acc):
     Cc = C.double().cpu()
     err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))[ref.norm(dim=1) > 0]
     assert err.max().item() < 2e-6 if scales != "tensor" else rel(Cc, ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(30556, 300, 600), (1000, 256, 580), (70, 300, 600),
+                                   (4099, 320, 608)])
+@pytest.mark.parametrize("scales", ["tensor", "rows"])
+@pytest.mark.parametrize("epi,acc", [(0, 0), (1, 1), (2, 0), (3, 0)])
+def test_gemm_h3_bs64(dev, M, N, K, scales, epi, acc):
+    """The K = 600 products (lin2, dagg) on k_gemm_bsn with 64-column tiles
+    (molclr_gemm_f32_h3_impl 3, 19 whole-K steps, an odd count): C against
+    fp64 at the h3 kernels' accuracy, max |C| and max |A| consistent with it,
+    every epilogue (ReLU mask from bits), accumulation, partial tiles."""
+    from molclr_amd import _lib
+    lib = _lib.load()
+    g = torch.Generator().manual_seed(M + N + K + epi + 2)
+    A = torch.randn(M, K, generator=g) * torch.pow(10.0, -6 * torch.rand(M, 1, generator=g))
+    W = (torch.rand(N, K, generator=g) * 2 - 1) / K ** 0.5
+    bias = torch.randn(N, generator=g) * 0.1
+    mask = torch.rand(M, N, generator=g) > 0.4
+    words = (N + 31) // 32
+    pos = torch.zeros(M, words * 32, dtype=torch.bool)
+    pos[:, :N] = mask
+    mb = ((pos.view(M, words, 32).long() << torch.arange(32)).sum(-1).remainder(1 << 32).t()
+          .contiguous())
+    mb = torch.where(mb >= (1 << 31), mb - (1 << 32), mb).to(torch.int32).to(dev)
+    Ad, Wd, bd = A.to(dev), W.to(dev), bias.to(dev)
+    planes = _h3_planes(lib, Wd, N, K, 0, dev)
+    if scales == "tensor":
+        amax, parts = torch.zeros(2048, device=dev), 0
+        assert lib.molclr_absmax_f32(Ad.data_ptr(), M, K, K, amax.data_ptr(), 0,
+                                     ops._stream(Ad)) == 0
+    else:
+        amax, parts = Ad.abs().amax(1).contiguous(), 1
+    C0 = torch.randn(M, N, generator=g).to(dev)
+    C = C0.clone()
+    cmax = torch.zeros(2048, device=dev)
+    aout = torch.zeros(2048, device=dev)
+    rc = lib.molclr_gemm_f32_h3_impl(
+        Ad.data_ptr(), amax.data_ptr(), parts, planes.data_ptr(), C.data_ptr(), M, N, K, K, N,
+        epi | (_lib.EPI_ACCUMULATE if acc else 0), bd.data_ptr(), None, 0,
+        mb.data_ptr() if epi == 3 else None, cmax.data_ptr(), None, aout.data_ptr(), None,
+        ops._stream(Ad), 3)
+    assert rc == 0, lib.molclr_last_error()
+    torch.cuda.synchronize()
+    assert cmax.max().item() == C.abs().max().item()
+    assert aout.max().item() == Ad.abs().max().item()
+    ref = C0.double().cpu() * acc + A.double() @ W.double().t()
+    if epi in (1, 2):
+        ref = ref + bias.double()
+    if epi == 2:
+        ref = ref.clamp_min(0)
+    if epi == 3:
+        ref = ref * mask
+    Cc = C.double().cpu()
+    err = ((Cc - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-300))[ref.norm(dim=1) > 0]
+    assert err.max().item() < 2e-6 if scales != "tensor" else rel(Cc, ref) < 2e-6

@@ -4,7 +4,7 @@
 
 CASE: qb_lin1 qb_lin2 qb_dz1 qb_dagg wb_dW2 wb_dW0 (bf16, c5 shapes, 55k rows)
       q6_lin1 q6_lin2 q6_dz1 q6_dagg w6_dW2 w6_dW1 (fp32 split-bf16, c2, 30.5k rows)
-      h3_lin1 h3_dz1 h3_dagg w6h_dW2 w6h_dW1 (fp32 via three fp16 MFMAs: the c2 step)
+      h3_lin1 h3_dz1 h3_lin2 h3_dagg w6h_dW2 w6h_dW1 (fp32 via three fp16 MFMAs: the c2 step)
 """
 import sys
 from pathlib import Path
@@ -62,7 +62,8 @@ def main():
         ragg = torch.empty(M, device=dev)
         bits = torch.randint(-2**31, 2**31 - 1, ((H + 31) // 32, M), dtype=torch.int32, device=dev)
         smax = {n: torch.zeros(ops.MAX_SLOT, device=dev) for n in X}
-        for n, r in (("dz", rdz), ("dz1", rdz1), ("agg", ragg)):
+        ra1 = torch.empty(M, device=dev)
+        for n, r in (("dz", rdz), ("dz1", rdz1), ("agg", ragg), ("a1", ra1)):
             lib.molclr_absmax_rows_f32(X[n].data_ptr(), M, X[n].shape[1], X[n].shape[1],
                                        r.data_ptr(), smax[n].data_ptr(), 1, st)
         for n in ("agg", "a1"):
@@ -84,6 +85,8 @@ def main():
                  "h3_dz1_aux": lambda: ops.gemm_h3(X["dz"], rdz, W2, H, D, H, 1, EPI_RELU_MASK,
                                                    aux=X["a1"], rowwise=1),
                  "h3_dagg": lambda: ops.gemm_h3(X["dz1"], rdz1, W0, D, H, D, 1, rowwise=1),
+                 "h3_lin2": lambda: ops.gemm_h3(X["a1"], ra1, W2, D, H, H, 0, EPI_BIAS, bias=b2,
+                                                rowwise=1),
                  # the step's h3 forward products (row-scaled A)
                  "h3_lin1": lambda: ops.gemm_h3(X["agg"], ragg, W0, H, D, D, 0, EPI_BIAS_RELU,
                                                 bias=b0, rowwise=1, bits_out=bits),
