@@ -2804,8 +2804,10 @@ __global__ void k_splitk_reduce(const float* __restrict__ partial, int splits, i
 // Two weight gradients' ordered split-K reductions in ONE launch (the GIN
 // layer's dW2 and dW1: molclr_linear_wgrad_h3_pair).  Threads [0, M_a N_a)
 // reduce job a, the rest job b, each exactly as k_splitk_reduce<EPI_NONE>.
-// A transposed job (trans = 1: partials of C^T, [split][N][M]) reads its
-// partials along their rows and stores C transposed.
+// A transposed job (trans = 1: partials of C^T, [split][N][M]; N % 4 == 0,
+// ldc % 4 == 0) gives a thread four columns n0..n0+3 of one row m: it reads
+// each column's partials along their rows (consecutive threads, consecutive
+// m) and stores the four sums as one float4 of C's row m.
 struct ReduceJob {
   const float* partial;
   int splits;
@@ -2815,12 +2817,13 @@ struct ReduceJob {
   const float* cs_partial;
   float* colsum;
   int trans = 0;
+  __host__ __device__ int64_t threads() const { return trans ? M * N / 4 : M * N; }
 };
 __global__ void k_splitk_reduce_pair(ReduceJob ja, ReduceJob jb, int accumulate) {
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool second = t >= ja.M * ja.N;
+  const bool second = t >= ja.threads();
   const ReduceJob& j = second ? jb : ja;
-  if (second) t -= ja.M * ja.N;
+  if (second) t -= ja.threads();
   auto ordered_sum = [](const float* __restrict__ p, int64_t stride, int splits) {
     float v = 0.f;
     int z = 0;
@@ -2843,15 +2846,19 @@ __global__ void k_splitk_reduce_pair(ReduceJob ja, ReduceJob jb, int accumulate)
     const float c = ordered_sum(j.cs_partial + t, j.M, j.splits);
     j.colsum[t] = accumulate ? j.colsum[t] + c : c;
   }
-  if (t >= j.M * j.N) return;
-  int64_t m, n;
+  if (t >= j.threads()) return;
   if (j.trans) {
-    n = t / j.M;
-    m = t - n * j.M;
-  } else {
-    m = t / j.N;
-    n = t - m * j.N;
+    const int64_t n0 = 4 * (t / j.M), m = t - (n0 / 4) * j.M;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = ordered_sum(j.partial + (n0 + q) * j.M + m, j.M * j.N, j.splits);
+    float4* o = reinterpret_cast<float4*>(j.C + m * j.ldc + n0);
+    float4 r = make_float4(v[0], v[1], v[2], v[3]);
+    if (accumulate) r = f4add(r, *o);
+    *o = r;
+    return;
   }
+  const int64_t m = t / j.N, n = t - m * j.N;
   float v = ordered_sum(j.partial + t, j.M * j.N, j.splits);
   if (accumulate) v += j.C[m * j.ldc + n];
   j.C[m * j.ldc + n] = v;
@@ -3973,9 +3980,10 @@ bool w6_transposed(int64_t n_out, int64_t n_in) {
 }
 // the w6 partial bytes of dW [n_out][n_in] (its chosen orientation)
 size_t w6_part_bytes(int64_t n_out, int64_t n_in, int64_t K, bool colsum) {
-  const bool tr = w6_transposed(n_out, n_in);
-  const W6Plan p = tr ? w6_plan(n_in, n_out, K, 2) : w6_plan(n_out, n_in, K, 2);
-  return molclr::align_up((size_t)p.splits * (n_out * n_in + (colsum ? n_out : 0)) * sizeof(float),
+  // either orientation (launch_wgrad_job keeps dW's own for an unaligned dW)
+  const W6Plan p = w6_plan(n_out, n_in, K, 2), q = w6_plan(n_in, n_out, K, 2);
+  const int splits = p.splits > q.splits ? p.splits : q.splits;
+  return molclr::align_up((size_t)splits * (n_out * n_in + (colsum ? n_out : 0)) * sizeof(float),
                           256);
 }
 // one job of the pair: dW = dY^T X (+ db = Σ dY) as partials, in the
@@ -3983,7 +3991,8 @@ size_t w6_part_bytes(int64_t n_out, int64_t n_in, int64_t K, bool colsum) {
 ReduceJob launch_wgrad_job(const float* dy, const float* dymax, const float* x, const float* xmax,
                            float* dW, float* db, int64_t n_out, int64_t n_in, int64_t rows,
                            int64_t ld_dy, int64_t ld_x, float* part, hipStream_t s) {
-  const bool tr = w6_transposed(n_out, n_in);
+  // the transposed reduction stores float4 rows of dW
+  const bool tr = w6_transposed(n_out, n_in) && (reinterpret_cast<uintptr_t>(dW) & 15) == 0;
   const W6Plan q = tr ? launch_w6_h3(x, dy, part, db != nullptr, n_in, n_out, rows, ld_x, ld_dy, s,
                                      xmax, dymax, true)
                       : launch_w6_h3(dy, x, part, db != nullptr, n_out, n_in, rows, ld_dy, ld_x, s,
@@ -4025,7 +4034,7 @@ MOLCLR_API int molclr_linear_wgrad_h3_groups(const float* dy, const float* dymax
                                          static_cast<float*>(workspace), s);
     ReduceJob none{nullptr, 0, 0, 0, nullptr, 0, nullptr, nullptr};
     molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce_pair,
-                         dim3((unsigned)molclr::ceil_div(n_out * n_in, 256)), dim3(256), 0, s, j,
+                         dim3((unsigned)molclr::ceil_div(j.threads(), 256)), dim3(256), 0, s, j,
                          none, accumulate);
     MOLCLR_LAUNCHED();
     return MOLCLR_OK;
@@ -4070,7 +4079,7 @@ MOLCLR_API int molclr_linear_wgrad_h3_pair(
                                         rows, ld_dy_a, ld_x_a, pa, s);
   const ReduceJob jb = launch_wgrad_job(dy_b, dymax_b, x_b, xmax_b, dW_b, db_b, n_out_b, n_in_b,
                                         rows, ld_dy_b, ld_x_b, pb, s);
-  const int64_t total = n_out_a * n_in_a + n_out_b * n_in_b;
+  const int64_t total = ja.threads() + jb.threads();
   molclr::launch_timed(molclr::kTimeGemm, k_splitk_reduce_pair,
                        dim3((unsigned)molclr::ceil_div(total, 256)), dim3(256), 0, s, ja, jb,
                        accumulate);
