@@ -3212,13 +3212,14 @@ int dispatch_bs(int epi, const Args& a, int64_t npad, hipStream_t s) {
 // The K = 600 products (lin2 = a1 W2^T and dagg = dz1 W1 of the c2 layer,
 // N = 300) on k_gemm_bsn with 64-column tiles: K in (576, 608], N <= 320, no
 // row maxima or ReLU bits out (their partial layouts are q6's), the rest as
-// bs_shape_ok.  Opt-in (MOLCLR_GEMM_BS64=1; g_bs_force 3 takes it too): in the
-// c2 step it measured even with k_gemm_q6 (182.6k vs 182.4k molecules/s, same
-// box, round 6; 16 waves per block 181.2k), so q6 stays the default.
+// bs_shape_ok.  c2 step, same box, round 6: k_gemm_q6 185.1k / 185.2k
+// molecules/s, bsn-64 at 12 waves 185.4k / 185.6k, at 8 waves 186.2k / 186.0k
+// (16 waves measured slower on another box), so 8 waves is the default;
+// MOLCLR_GEMM_BS64=0 keeps q6.
 bool use_bs64(const Args& a, int64_t npad, int epi, int h3) {
   static const bool off = [] {
     const char* e = getenv("MOLCLR_GEMM_BS64");
-    return e == nullptr || e[0] != '1';
+    return e != nullptr && e[0] == '0';
   }();
   if (g_bs_force == 1 || g_bs_force == 2 || (off && g_bs_force != 3)) return false;
   if (h3 == 0 || a.N > 320 || a.N <= 192 || a.K <= 576 || a.K > 608 || a.ldb != 608) return false;
@@ -3234,12 +3235,19 @@ void launch_bs64(const Args& a, int64_t npad, hipStream_t s) {
   const int ntn = (int)((a.N + 63) / 64);
   int groups = molclr::cu_count() / ntn;
   groups = groups < 1 ? 1 : groups;
-  // MOLCLR_BS64_WAVES=16: four waves per SIMD (<= 128 VGPRs)
+  // MOLCLR_BS64_WAVES=12 / 16: three / four waves per SIMD (<= 128 VGPRs)
   static const int wv = [] {
     const char* e = getenv("MOLCLR_BS64_WAVES");
-    return e != nullptr && atoi(e) == 16 ? 16 : 12;
+    const int v = e != nullptr ? atoi(e) : 8;
+    return v == 16 || v == 12 ? v : 8;
   }();
-  if (wv == 16)
+  if (wv == 8)
+    molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 19, false, 8, 64>),
+                         dim3((unsigned)(ntn * groups)), dim3(512), 0, s, a.A, a.Bp, a.C, a.M, a.N,
+                         a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate,
+                         a.amax, a.bmax, a.cmax, a.crow, a.amax_out, a.arow_parts, a.bits_out,
+                         a.bits_in, a.bits_ld, ntn, groups);
+  else if (wv == 16)
     molclr::launch_timed(molclr::kTimeGemm, (k_gemm_bsn<EPI, H3, 19, false, 16, 64>),
                          dim3((unsigned)(ntn * groups)), dim3(1024), 0, s, a.A, a.Bp, a.C, a.M, a.N,
                          a.K, a.lda, a.ldb, npad, a.ldc, a.bias, a.aux, a.ldaux, a.accumulate,
