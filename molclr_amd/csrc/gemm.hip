@@ -1971,6 +1971,17 @@ __device__ __forceinline__ f32x4 mfma16_h3_t(f16x8 ah, f16x8 al, f16x8 bh, f16x8
 // k_gemm_bsn: the same kernel for any tile width BNT (128: the K = 300
 // products; 64: the K = 600 products lin2 and dagg, N = 300, whose whole-K
 // image of a 64-column tile is 19 full steps, 152 KB) and an odd step count.
+// bsn's image swizzle: chunk c of row r sits in 16-byte slot c ^ F[(r >> 2) & 3]
+// with F = {0, 2, 3, 1}.  A 16 x 16 x 32 fragment read (lane: row r16 of the
+// block, chunk lane >> 4) then touches 16 distinct 16-byte bank slots in each
+// of ds_read_b128's four lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31},
+// and the same + 32); xoff's F = {0, 1, 2, 3}, right for the 32 x 32 x 16
+// reads, gives these reads 2-way conflicts (PMC: SQ_LDS_BANK_CONFLICT 45 % of
+// the LDS cycles).
+__device__ __forceinline__ int bsn_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+__device__ __forceinline__ int bsn_off(int row, int chunk) {
+  return row * XK + ((chunk ^ bsn_swz(row)) << 3);
+}
 template <int EPI, int H3, int S, bool HALF, int W = 8, int BNT = kBN>
 __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4))) void k_gemm_bsn(
     const float* __restrict__ A, const uint16_t* __restrict__ Bp, float* __restrict__ C,
@@ -2010,7 +2021,7 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
       const int row = r0 + (lane >> 2), c = lane & 3;
       int64_t gr = n0 + row;
       gr = gr < npad ? gr : npad - 1;
-      const uint32_t voff = (uint32_t)(((pl * npad + gr) * kp + 32 * st + 8 * (c ^ ((row >> 2) & 3))) * 2);
+      const uint32_t voff = (uint32_t)(((pl * npad + gr) * kp + 32 * st + 8 * (c ^ bsn_swz(row))) * 2);
       buf_lds16(brsrc, img + st * kFullImg + pl * kBN * XK + r0 * XK, voff, 0);
     }
     if constexpr (HALF) {
@@ -2096,8 +2107,8 @@ __global__ __launch_bounds__(W * 64) __attribute__((amdgpu_waves_per_eu(W / 4)))
   auto compute = [&](const uint16_t* base) {
     auto rd = [&](int b, u32x4(&f)[2]) {
       const int row = 16 * b + r16;
-      f[0] = *reinterpret_cast<const u32x4*>(base + xoff(row, q4));
-      f[1] = *reinterpret_cast<const u32x4*>(base + kBN * XK + xoff(row, q4));
+      f[0] = *reinterpret_cast<const u32x4*>(base + bsn_off(row, q4));
+      f[1] = *reinterpret_cast<const u32x4*>(base + kBN * XK + bsn_off(row, q4));
     };
     u32x4 q[2][2];
     rd(0, q[0]);
